@@ -1,0 +1,304 @@
+"""ctypes binding of libdatago_hip.so (the C ABI in include/datago_hip.h).
+
+The product path: every call goes to the HIP library.  There is no CPU
+fallback — if the library is missing, importing this module raises.
+
+torch (when installed) is imported first so that the process holds exactly one
+HIP runtime: torch ships its own libamdhip64.so (soname libamdhip64.so.7) and
+loads it via DT_NEEDED "libamdhip64.so"; our library's DT_NEEDED
+"libamdhip64.so.7" then binds to that same copy instead of a second one.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+try:  # one HIP runtime per process (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdatago_hip.so")
+
+DG_OK, DG_ERR_UNSUPPORTED, DG_ERR_CORRUPT, DG_ERR_OOM, DG_ERR_BAD_BUCKET = 0, 1, 2, 3, 4
+DG_ERR_INVALID, DG_ERR_SMALL_BUFFER, DG_ERR_DEVICE, DG_ERR_NOT_READY = 5, 6, 7, 8
+STATUS_NAMES = {0: "OK", 1: "UNSUPPORTED", 2: "CORRUPT", 3: "OOM", 4: "BAD_BUCKET", 5: "INVALID",
+                6: "SMALL_BUFFER", 7: "DEVICE", 8: "NOT_READY"}
+DG_FMT_UNKNOWN, DG_FMT_JPEG, DG_FMT_PNG = 0, 1, 2
+
+# exported symbols (must match include/datago_hip.h; checked by tests)
+EXPORTS = [
+    "dg_bucket_table_build", "dg_bucket_table_free", "dg_bucket_count", "dg_bucket_get",
+    "dg_closest_bucket", "dg_bucket_find_key", "dg_aspect_ratio_to_str", "dg_probe",
+    "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_buckets", "dg_output_size", "dg_submit", "dg_wait",
+    "dg_poll", "dg_decode_one", "dg_submit_device", "dg_device_alloc", "dg_device_free",
+    "dg_memcpy_h2d", "dg_memcpy_d2h", "dg_synchronize", "dg_last_batch_timings",
+    "dg_ctx_set_option", "dg_ctx_get_stat", "dg_last_error", "dg_abi_version",
+]
+
+
+class DgError(RuntimeError):
+    def __init__(self, status: int, msg: str = ""):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class ImageConfig(ctypes.Structure):
+    _fields_ = [("crop_and_resize", ctypes.c_int32), ("default_image_size", ctypes.c_uint32),
+                ("downsampling_ratio", ctypes.c_uint32), ("min_aspect_ratio", ctypes.c_double),
+                ("max_aspect_ratio", ctypes.c_double), ("pre_encode_images", ctypes.c_int32),
+                ("image_to_rgb8", ctypes.c_int32), ("encode_format", ctypes.c_int32),
+                ("jpeg_quality", ctypes.c_int32)]
+
+
+class ProbeInfo(ctypes.Structure):
+    _fields_ = [("format", ctypes.c_int32), ("width", ctypes.c_uint32), ("height", ctypes.c_uint32),
+                ("components", ctypes.c_int32), ("bit_depth", ctypes.c_int32),
+                ("h_samp", ctypes.c_int32 * 4), ("v_samp", ctypes.c_int32 * 4),
+                ("progressive", ctypes.c_int32), ("arithmetic", ctypes.c_int32),
+                ("precision", ctypes.c_int32), ("restart_interval", ctypes.c_int32),
+                ("gpu_supported", ctypes.c_int32)]
+
+
+class PayloadMeta(ctypes.Structure):
+    _fields_ = [("original_width", ctypes.c_uint32), ("original_height", ctypes.c_uint32),
+                ("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("channels", ctypes.c_int32),
+                ("bit_depth", ctypes.c_int32), ("is_encoded", ctypes.c_int32), ("status", ctypes.c_int32),
+                ("bucket", ctypes.c_int32), ("nbytes", ctypes.c_uint64)]
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `python -m datago_amd.build` "
+                          "(the GPU path has no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u8pp = ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)
+    i32, u32, u64, dbl = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double
+    L.dg_bucket_table_build.argtypes = [u32, u32, dbl, dbl, ctypes.POINTER(vp)]
+    L.dg_bucket_table_free.argtypes = [vp]
+    L.dg_bucket_table_free.restype = None
+    L.dg_bucket_count.argtypes = [vp]
+    L.dg_bucket_get.argtypes = [vp, i32, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.c_char_p, sz]
+    L.dg_closest_bucket.argtypes = [vp, i32, i32]
+    L.dg_bucket_find_key.argtypes = [vp, ctypes.c_char_p]
+    L.dg_aspect_ratio_to_str.argtypes = [u32, u32, ctypes.c_char_p, sz]
+    L.dg_probe.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(ProbeInfo)]
+    L.dg_ctx_create.argtypes = [i32, ctypes.POINTER(ImageConfig), ctypes.POINTER(vp)]
+    L.dg_ctx_destroy.argtypes = [vp]
+    L.dg_ctx_destroy.restype = None
+    L.dg_ctx_buckets.argtypes = [vp]
+    L.dg_ctx_buckets.restype = vp
+    L.dg_output_size.argtypes = [vp, ctypes.c_char_p, sz, i32, ctypes.POINTER(u64)]
+    L.dg_submit.argtypes = [vp, i32, u8pp, ctypes.POINTER(sz), ctypes.POINTER(i32), u8pp,
+                            ctypes.POINTER(u64), ctypes.POINTER(PayloadMeta), ctypes.POINTER(u64)]
+    L.dg_submit_device.argtypes = [vp, i32, u8pp, u8pp, ctypes.POINTER(sz), ctypes.POINTER(i32), u8pp,
+                                   ctypes.POINTER(u64), ctypes.POINTER(PayloadMeta), ctypes.POINTER(u64)]
+    L.dg_wait.argtypes = [vp, u64]
+    L.dg_poll.argtypes = [vp, u64]
+    L.dg_decode_one.argtypes = [vp, ctypes.c_char_p, sz, i32, vp, u64, ctypes.POINTER(PayloadMeta)]
+    L.dg_device_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
+    L.dg_device_free.argtypes = [vp, vp]
+    L.dg_memcpy_h2d.argtypes = [vp, vp, vp, sz]
+    L.dg_memcpy_d2h.argtypes = [vp, vp, vp, sz]
+    L.dg_synchronize.argtypes = [vp]
+    L.dg_last_batch_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), i32]
+    L.dg_ctx_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
+    L.dg_ctx_get_stat.argtypes = [vp, ctypes.c_char_p]
+    L.dg_ctx_get_stat.restype = ctypes.c_int64
+    L.dg_last_error.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return load().dg_last_error().decode(errors="replace")
+
+
+def _check(st: int) -> None:
+    if st != DG_OK:
+        raise DgError(st, last_error())
+
+
+# ------------------------------------------------------------------ buckets
+
+class BucketTable:
+    """dg_bucket_table: ImageTransformConfig::get_ar_aware_transform."""
+
+    def __init__(self, default_image_size: int, downsampling_ratio: int, min_ar: float, max_ar: float,
+                 _borrowed: Optional[int] = None):
+        L = load()
+        self._owned = _borrowed is None
+        if _borrowed is not None:
+            self._h = ctypes.c_void_p(_borrowed)
+        else:
+            h = ctypes.c_void_p()
+            _check(L.dg_bucket_table_build(default_image_size, downsampling_ratio, min_ar, max_ar,
+                                           ctypes.byref(h)))
+            self._h = h
+
+    def __del__(self):
+        if getattr(self, "_owned", False) and self._h and _lib is not None:
+            _lib.dg_bucket_table_free(self._h)
+
+    def __len__(self) -> int:
+        return load().dg_bucket_count(self._h)
+
+    def get(self, i: int) -> Tuple[int, int, str]:
+        w, h = ctypes.c_uint32(), ctypes.c_uint32()
+        key = ctypes.create_string_buffer(32)
+        _check(load().dg_bucket_get(self._h, i, ctypes.byref(w), ctypes.byref(h), key, 32))
+        return w.value, h.value, key.value.decode()
+
+    def buckets(self) -> List[Tuple[int, int, str]]:
+        return [self.get(i) for i in range(len(self))]
+
+    def closest(self, w: int, h: int) -> int:
+        return load().dg_closest_bucket(self._h, w, h)
+
+    def find_key(self, key: str) -> int:
+        return load().dg_bucket_find_key(self._h, key.encode())
+
+
+def aspect_ratio_to_str(w: int, h: int) -> str:
+    buf = ctypes.create_string_buffer(64)
+    _check(load().dg_aspect_ratio_to_str(w, h, buf, 64))
+    return buf.value.decode()
+
+
+def probe(data: bytes) -> Tuple[int, ProbeInfo]:
+    info = ProbeInfo()
+    st = load().dg_probe(data, len(data), ctypes.byref(info))
+    return st, info
+
+
+# ------------------------------------------------------------------ context
+
+def _as_ptr_array(ptrs: Sequence[int]):
+    arr = (ctypes.c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr
+
+
+class Context:
+    """dg_ctx: one HIP stream + device arenas on one device (rank -> device)."""
+
+    def __init__(self, device: int = 0, crop_and_resize: bool = False, default_image_size: int = 0,
+                 downsampling_ratio: int = 0, min_aspect_ratio: float = 0.0, max_aspect_ratio: float = 0.0,
+                 image_to_rgb8: bool = False, pre_encode_images: bool = False, encode_format: int = 0,
+                 jpeg_quality: int = 92):
+        L = load()
+        cfg = ImageConfig(int(crop_and_resize), default_image_size, downsampling_ratio, min_aspect_ratio,
+                          max_aspect_ratio, int(pre_encode_images), int(image_to_rgb8), encode_format,
+                          jpeg_quality)
+        h = ctypes.c_void_p()
+        _check(L.dg_ctx_create(device, ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+        self.cfg = cfg
+        bt = L.dg_ctx_buckets(h)
+        self.buckets = BucketTable(0, 0, 0, 0, _borrowed=bt) if bt else None
+
+    def close(self) -> None:
+        if self._h and _lib is not None:
+            _lib.dg_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_option(self, key: str, value: int) -> None:
+        _check(load().dg_ctx_set_option(self._h, key.encode(), int(value)))
+
+    def stat(self, key: str) -> int:
+        return load().dg_ctx_get_stat(self._h, key.encode())
+
+    def timings(self) -> dict:
+        names = (ctypes.c_char_p * 32)()
+        ms = (ctypes.c_float * 32)()
+        n = load().dg_last_batch_timings(self._h, names, ms, 32)
+        return {names[i].decode(): ms[i] for i in range(n)}
+
+    def output_size(self, data: bytes, forced_bucket: int = -1) -> Tuple[int, int]:
+        n = ctypes.c_uint64()
+        st = load().dg_output_size(self._h, data, len(data), forced_bucket, ctypes.byref(n))
+        return st, n.value
+
+    # -- host memory in, host memory out (the Rust workers' path)
+    def decode_batch(self, datas: Sequence[bytes], forced: Optional[Sequence[int]] = None
+                     ) -> List[Tuple[int, Optional[np.ndarray], PayloadMeta]]:
+        n = len(datas)
+        L = load()
+        outs, caps = [], []
+        for i, d in enumerate(datas):
+            st, nb = self.output_size(d, forced[i] if forced else -1)
+            outs.append(np.empty(max(nb, 1), np.uint8))
+            caps.append(max(nb, 1))
+        bufs = [ctypes.create_string_buffer(d, len(d)) for d in datas]
+        srcs = _as_ptr_array([ctypes.addressof(b) for b in bufs])
+        lens = (ctypes.c_size_t * max(1, n))(*[len(d) for d in datas])
+        fb = (ctypes.c_int32 * max(1, n))(*(forced if forced else [-1] * n))
+        optrs = _as_ptr_array([o.ctypes.data for o in outs])
+        capa = (ctypes.c_uint64 * max(1, n))(*caps)
+        metas = (PayloadMeta * max(1, n))()
+        ticket = ctypes.c_uint64()
+        _check(L.dg_submit(self._h, n, srcs, lens, fb, optrs, capa, metas, ctypes.byref(ticket)))
+        _check(L.dg_wait(self._h, ticket.value))
+        res = []
+        for i in range(n):
+            m = metas[i]
+            if m.status != DG_OK:
+                res.append((m.status, None, m))
+                continue
+            c = int(m.nbytes // (m.width * m.height)) if m.width and m.height else 0
+            res.append((DG_OK, outs[i][: m.nbytes].reshape(m.height, m.width, c), m))
+        return res
+
+    def decode_one(self, data: bytes, forced_bucket: int = -1):
+        return self.decode_batch([data], [forced_bucket])[0]
+
+    # -- device-resident path (bench): coded bytes already in HBM
+    def alloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        _check(load().dg_device_alloc(self._h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def free(self, ptr: int) -> None:
+        _check(load().dg_device_free(self._h, ptr))
+
+    def h2d(self, dst: int, src: np.ndarray) -> None:
+        _check(load().dg_memcpy_h2d(self._h, dst, src.ctypes.data, src.nbytes))
+
+    def d2h(self, dst: np.ndarray, src: int) -> None:
+        _check(load().dg_memcpy_d2h(self._h, dst.ctypes.data, src, dst.nbytes))
+
+    def synchronize(self) -> None:
+        _check(load().dg_synchronize(self._h))
+
+    def submit_device(self, h_ptrs, d_ptrs, lens, d_outs, caps, forced=None):
+        """Asynchronous device-resident batch; returns (ticket, metas)."""
+        n = len(d_ptrs)
+        hp = _as_ptr_array(h_ptrs)
+        dp = _as_ptr_array(d_ptrs)
+        la = (ctypes.c_size_t * max(1, n))(*lens)
+        fb = (ctypes.c_int32 * max(1, n))(*(forced if forced is not None else [-1] * n))
+        op = _as_ptr_array(d_outs)
+        ca = (ctypes.c_uint64 * max(1, n))(*caps)
+        metas = (PayloadMeta * max(1, n))()
+        ticket = ctypes.c_uint64()
+        _check(load().dg_submit_device(self._h, n, hp, dp, la, fb, op, ca, metas, ctypes.byref(ticket)))
+        return ticket.value, metas
+
+    def wait(self, ticket: int) -> None:
+        _check(load().dg_wait(self._h, ticket))

@@ -1,0 +1,259 @@
+// dg_pixel.h — per-pixel arithmetic shared by the HIP kernels and the CPU
+// emulator: ISLOW IDCT, chroma upsampling, YCbCr->RGB, Lanczos3 coefficients.
+//
+// Semantics follow libjpeg-turbo (the decoder the oracle is pinned against:
+// tests/test_oracle_jpeg.py) and fast_image_resize 5.5.0's Convolution
+// (reference image_processing.rs:288-323), see oracle/*.c for the restatements
+// these kernels are checked against bit for bit.
+#pragma once
+#include "dg_types.h"
+
+namespace dg {
+
+// ---------------------------------------------------------------- ISLOW IDCT
+// T.81 A.3.3 inverse DCT in the fixed-point factorisation of libjpeg's
+// jidctint.c (CONST_BITS 13, PASS1_BITS 2).
+constexpr int32_t kConstBits = 13, kPass1Bits = 2;
+
+DG_HD void idct_1d(const int32_t i0, const int32_t i1, const int32_t i2, const int32_t i3,
+                   const int32_t i4, const int32_t i5, const int32_t i6, const int32_t i7,
+                   int32_t o[8]) {
+  int32_t z1, z2, z3, z4, z5, t0, t1, t2, t3, t10, t11, t12, t13;
+  z2 = i2;
+  z3 = i6;
+  z1 = (z2 + z3) * 4433;
+  t2 = z1 + z3 * (-15137);
+  t3 = z1 + z2 * 6270;
+  t0 = (int32_t)((uint32_t)(i0 + i4) << kConstBits);
+  t1 = (int32_t)((uint32_t)(i0 - i4) << kConstBits);
+  t10 = t0 + t3;
+  t13 = t0 - t3;
+  t11 = t1 + t2;
+  t12 = t1 - t2;
+  t0 = i7;
+  t1 = i5;
+  t2 = i3;
+  t3 = i1;
+  z1 = t0 + t3;
+  z2 = t1 + t2;
+  z3 = t0 + t2;
+  z4 = t1 + t3;
+  z5 = (z3 + z4) * 9633;
+  t0 = t0 * 2446;
+  t1 = t1 * 16819;
+  t2 = t2 * 25172;
+  t3 = t3 * 12299;
+  z1 = z1 * (-7373);
+  z2 = z2 * (-20995);
+  z3 = z3 * (-16069);
+  z4 = z4 * (-3196);
+  z3 += z5;
+  z4 += z5;
+  t0 += z1 + z3;
+  t1 += z2 + z4;
+  t2 += z2 + z3;
+  t3 += z1 + z4;
+  o[0] = t10 + t3;
+  o[7] = t10 - t3;
+  o[1] = t11 + t2;
+  o[6] = t11 - t2;
+  o[2] = t12 + t1;
+  o[5] = t12 - t1;
+  o[3] = t13 + t0;
+  o[4] = t13 - t0;
+}
+
+DG_HD int32_t descale(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
+
+DG_HD uint8_t idct_out(int32_t x) {
+  // libjpeg-turbo's SIMD IDCT output stage: saturate to int8, then +128
+  x = descale(x, kConstBits + kPass1Bits + 3);
+  x = x < -128 ? -128 : (x > 127 ? 127 : x);
+  return (uint8_t)(x + 128);
+}
+
+// zigzag index -> natural index
+#if defined(DG_DEVICE)
+__constant__
+#endif
+static const uint8_t kZigzagToNatural[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// --------------------------------------------------------- colour conversion
+// libjpeg jdcolor.c build_ycc_rgb_table, SCALEBITS 16, computed inline.
+DG_HD uint8_t clamp255(int32_t v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+DG_HD void ycc_to_rgb(int32_t y, int32_t cb, int32_t cr, uint8_t &r, uint8_t &g, uint8_t &b) {
+  const int32_t F140200 = 91881;  // (int)(1.40200 * 65536 + 0.5)
+  const int32_t F177200 = 116130;
+  const int32_t F071414 = 46802;
+  const int32_t F034414 = 22554;
+  int32_t xcr = cr - 128, xcb = cb - 128;
+  int32_t crr = (F140200 * xcr + 32768) >> 16;
+  int32_t cbb = (F177200 * xcb + 32768) >> 16;
+  int32_t g_ = (-F034414 * xcb + 32768 + -F071414 * xcr) >> 16;
+  r = clamp255(y + crr);
+  g = clamp255(y + g_);
+  b = clamp255(y + cbb);
+}
+
+// ----------------------------------------------------------- upsampling
+// Value of component `c` at full-resolution pixel (x, y) — libjpeg-turbo
+// jdsample.c: h2v1/h2v2 "fancy" triangle filters (box replication when
+// downsampled_width <= 2), edges replicated (jdmainct.c context rows).
+DG_HD uint32_t upsample_at(const uint8_t *pl, uint32_t stride, uint32_t hr, uint32_t vr,
+                           uint32_t dsw, uint32_t dsh, uint32_t x, uint32_t y) {
+  if (hr == 1 && vr == 1) return pl[(size_t)y * stride + x];
+  uint32_t c = x >> 1;
+  bool fancy = dsw > 2;
+  if (vr == 1) {  // h2v1
+    const uint8_t *in = pl + (size_t)y * stride;
+    if (!fancy) return in[c];
+    int32_t a = in[c] * 3;
+    if (x & 1) {
+      uint32_t n = c + 1 < dsw ? c + 1 : dsw - 1;
+      return (uint32_t)((a + in[n] + 2) >> 2);
+    }
+    uint32_t n = c > 0 ? c - 1 : 0;
+    return (uint32_t)((a + in[n] + 1) >> 2);
+  }
+  // h2v2
+  uint32_t r = y >> 1;
+  if (!fancy) return pl[(size_t)r * stride + c];
+  int32_t rn = (y & 1) ? (int32_t)r + 1 : (int32_t)r - 1;
+  if (rn < 0) rn = 0;
+  if (rn > (int32_t)dsh - 1) rn = (int32_t)dsh - 1;
+  const uint8_t *i0 = pl + (size_t)r * stride, *i1 = pl + (size_t)rn * stride;
+  int32_t cs = i0[c] * 3 + i1[c];
+  if (x & 1) {
+    uint32_t n = c + 1 < dsw ? c + 1 : dsw - 1;
+    int32_t ns = i0[n] * 3 + i1[n];
+    return (uint32_t)((cs * 3 + ns + 7) >> 4);
+  }
+  uint32_t n = c > 0 ? c - 1 : 0;
+  int32_t ps = i0[n] * 3 + i1[n];
+  return (uint32_t)((cs * 3 + ps + 8) >> 4);
+}
+
+// --------------------------------------------------------------- Lanczos3
+// Portable sin (fdlibm algorithm, < 1 ULP): identical on host and device so
+// coefficient tables are bit-reproducible; within 1 ULP of glibc's sin.
+// Callers compile with -ffp-contract=off.
+DG_HD double k_sin(double x, double y, int iy) {
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  double z = x * x, v = z * x;
+  double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  if (iy == 0) return x + v * (S1 + z * r);
+  return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+
+DG_HD double k_cos(double x, double y) {
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  double z = x * x;
+  double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+  double ax = x < 0 ? -x : x;
+  if (ax < 0.3) return 1.0 - (0.5 * z - (z * r - x * y));
+  double qx;
+  if (ax > 0.78125) {
+    qx = 0.28125;
+  } else {
+    uint64_t bits;
+    __builtin_memcpy(&bits, &ax, 8);
+    bits = (bits - 0x0020000000000000ULL) & 0xFFFFFFFF00000000ULL;
+    __builtin_memcpy(&qx, &bits, 8);
+  }
+  double hz = 0.5 * z - qx, a = 1.0 - qx;
+  return a - (hz - (z * r - x * y));
+}
+
+DG_HD double dg_sin(double x) {
+  const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+               pio2_1t = 6.07710050650619224932e-11;
+  double ax = x < 0 ? -x : x;
+  if (ax <= 0.785398163397448279) return k_sin(x, 0.0, 0);
+  double fn = __builtin_floor(ax * invpio2 + 0.5);
+  int n = (int)fn;
+  double r = ax - fn * pio2_1, w = fn * pio2_1t;
+  double y0 = r - w, y1 = (r - y0) - w;
+  double s;
+  switch (n & 3) {
+    case 0: s = k_sin(y0, y1, 1); break;
+    case 1: s = k_cos(y0, y1); break;
+    case 2: s = -k_sin(y0, y1, 1); break;
+    default: s = -k_cos(y0, y1); break;
+  }
+  return x < 0 ? -s : s;
+}
+
+DG_HD double sinc(double x) {
+  if (x == 0.0) return 1.0;
+  x *= 3.14159265358979323846;
+  return dg_sin(x) / x;
+}
+
+DG_HD double lanczos3(double x) { return (x >= -3.0 && x < 3.0) ? sinc(x) * sinc(x / 3.0) : 0.0; }
+
+// fast_image_resize precompute_coefficients for output index o.  Writes the
+// normalised f64 weights (n of them) into w[] and returns the bound.
+// ksize slots are enough by construction (ceil(support)*2+1).
+DG_HD void fir_weights(uint32_t in_size, double in0, double in1, uint32_t out_size, uint32_t o,
+                       double *w, int32_t &start, int32_t &n) {
+  double scale = (in1 - in0) / (double)out_size;
+  double filter_scale = scale > 1.0 ? scale : 1.0;
+  double support = 3.0 * filter_scale;
+  double recip = 1.0 / filter_scale;
+  double center = in0 + ((double)o + 0.5) * scale;
+  double fl = __builtin_floor(center - support);
+  double cl = __builtin_ceil(center + support);
+  int32_t xmin = fl < 0.0 ? 0 : (int32_t)fl;
+  int32_t xmax = cl > (double)in_size ? (int32_t)in_size : (int32_t)cl;
+  double c = center - 0.5;
+  int32_t st = xmin, cnt = 0;
+  double ww = 0.0;
+  for (int32_t x = xmin; x < xmax; x++) {
+    double v = lanczos3(((double)x - c) * recip);
+    if (x == st && v == 0.0) {
+      st++;
+    } else {
+      w[cnt++] = v;
+      ww += v;
+    }
+  }
+  while (cnt > 0 && w[cnt - 1] == 0.0) cnt--;
+  if (ww != 0.0)
+    for (int32_t i = 0; i < cnt; i++) w[i] /= ww;
+  start = st;
+  n = cnt;
+}
+
+DG_HD uint32_t fir_ksize(double in0, double in1, uint32_t out_size) {
+  double scale = (in1 - in0) / (double)out_size;
+  double filter_scale = scale > 1.0 ? scale : 1.0;
+  return (uint32_t)__builtin_ceil(3.0 * filter_scale) * 2 + 1;
+}
+
+// Pillow-SIMD / fast_image_resize Normalizer16 precision for max weight m.
+DG_HD int32_t fir_precision(double maxw) {
+  int32_t precision = 0;
+  for (int32_t p = 0; p < 22; p++) {
+    precision = p;
+    double nv = __builtin_round(maxw * (double)(1 << (p + 1)));
+    if ((int32_t)nv >= (1 << 15)) break;
+  }
+  return precision;
+}
+
+DG_HD int16_t fir_quant(double v, int32_t precision) {
+  double q = __builtin_round(v * (double)(1 << precision));
+  if (q > 32767.0) q = 32767.0;
+  if (q < -32768.0) q = -32768.0;
+  return (int16_t)q;
+}
+
+}  // namespace dg

@@ -1,0 +1,133 @@
+// dg_types.h — POD structures shared by the host planner and the HIP kernels.
+//
+// One batch = N images.  The host parses headers (host/jpeg_header.cpp),
+// chooses buckets (host/buckets.cpp), lays every per-image buffer out in one
+// device arena and uploads an array of ImageDesc + per-kernel workgroup lists
+// (WgItem).  All device addresses inside these structs are absolute.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIP__)
+#define DG_HD __host__ __device__ __forceinline__
+#define DG_DEVICE 1
+#else
+#define DG_HD static inline
+#endif
+
+namespace dg {
+
+constexpr int kLutBits = 9;          // Huffman fast-lookup width
+constexpr int kMaxSlots = 6;         // Huffman tables per image (DC/AC x 3 components)
+constexpr int kSubPerWg = 256;       // entropy subsequences per workgroup (= threads)
+constexpr int kDefaultSubBytes = 128;// raw coded bytes per subsequence
+constexpr uint32_t kInf = 0xFFFFFFFFu;
+
+// Canonical Huffman table for the GPU decoder (built on the host, pooled).
+struct HuffTable {
+  uint16_t lut[1 << kLutBits];  // (len << 8) | symbol for codes of length <= kLutBits; 0 = longer
+  uint32_t lim[17];             // lim[l]: exclusive bound on the left-justified 16-bit peek for length l
+  int32_t valoff[17];           // symbol = vals[valoff[l] + (peek16 >> (16 - l))]
+  uint8_t vals[256];
+};
+
+struct QuantTable {
+  uint16_t q[64];  // natural (row-major) order
+};
+
+// Entropy-decoder state at a subsequence boundary:
+//   bit 31 valid | bits 16..23 rel (destuffed bits past the anchor) | 8..15 r (block in MCU) | 0..7 z
+DG_HD uint32_t pack_state(uint32_t rel, uint32_t r, uint32_t z) {
+  return 0x80000000u | (rel << 16) | (r << 8) | z;
+}
+DG_HD uint32_t st_rel(uint32_t s) { return (s >> 16) & 0xFFu; }
+DG_HD uint32_t st_r(uint32_t s) { return (s >> 8) & 0xFFu; }
+DG_HD uint32_t st_z(uint32_t s) { return s & 0xFFu; }
+
+// Per-subsequence record (64 bytes).
+struct SubState {
+  uint32_t in;      // state used at the subsequence start
+  uint32_t out;     // state at the first symbol boundary at/after the next anchor
+  uint32_t m;       // RST markers owned (FF byte inside this subsequence)
+  uint32_t n;       // blocks started after the last owned marker (or the start)
+  int32_t dc[3];    // DC differences summed after the last owned marker, per component
+  uint32_t seg;     // exclusive segmented scan: restart segment at start
+  uint32_t nin;     //   blocks already started in that segment
+  int32_t dcin[3];  //   DC predictors at start
+  uint32_t pad[2];
+};
+
+enum Colorspace : uint32_t { CS_YCC = 0, CS_RGB = 1, CS_GRAY = 2 };
+
+// Resize pass along one axis (one half of a fast_image_resize `resize` call).
+struct ResizePass {
+  uint64_t src, dst;        // device addresses
+  uint64_t coef;            // int16 [out_size * ksize]   (written by k_coeffs)
+  uint64_t bounds;          // int32 {start, size} [out_size] (written by k_coeffs)
+  double in0, in1;          // source box along the axis
+  uint32_t in_size, out_size;
+  uint32_t ksize;           // coefficient slots per output
+  int32_t precision;        // written by k_coeffs
+  uint32_t src_stride, dst_stride;  // bytes per row
+  uint32_t width, rows;     // output extent of this pass (pixels, rows)
+  uint32_t row0;            // H pass: first source row; V pass: source row of temp row 0
+  uint32_t C;               // channels
+  uint32_t kind;            // 0 none, 1 horizontal, 2 vertical
+  uint32_t pad;
+};
+
+constexpr int kStages = 4;  // R1.H, R1.V, R2.H, R2.V
+
+struct ImageDesc {
+  // ---- entropy stream
+  uint64_t scan;            // device address of the first entropy-coded byte
+  uint32_t scan_len;        // bytes of entropy-coded data (up to the end of data)
+  uint32_t nsub;            // subsequences
+  uint32_t sub_base;        // first SubState index
+  uint32_t sub_bytes;       // bytes per subsequence
+  uint32_t restart;         // restart interval (MCUs), 0 = none
+  uint32_t blocks_per_seg;  // restart * bpm, 0 = unlimited
+  uint32_t total_blocks;
+  uint32_t bpm;             // blocks per MCU
+  uint8_t blk_comp[12];     // component of block k within an MCU
+  uint16_t hslot[kMaxSlots];  // pool index of Huffman slot s
+  uint8_t dc_slot[3], ac_slot[3];
+  uint8_t ncomp, colorspace, dec_c, nslots;  // dec_c: channels of the decoded image
+  uint16_t qpool[3];
+  uint16_t pad1;
+  uint64_t coef;            // device address of block 0 (int16 zigzag[64] per block, decode order)
+  // ---- geometry
+  uint32_t width, height;
+  uint32_t mcux, mcuy;
+  uint32_t hmax, vmax;
+  uint32_t ch[3], cv[3];    // sampling factors
+  uint32_t cfirst[3];       // first block of component c within an MCU
+  uint32_t cbw[3], cbh[3];  // plane size in blocks
+  uint32_t cdsw[3], cdsh[3];// downsampled width/height (libjpeg downsampled_width)
+  uint64_t plane[3];        // device address of component planes (stride cbw*8)
+  uint64_t pix;             // decoded interleaved image (stride pix_stride), 0 for gray
+  uint32_t pix_stride;
+  int32_t status;           // set by kernels on corruption
+  // ---- resize plan
+  ResizePass pass[kStages];
+  uint64_t out;             // final output (tight rows)
+  uint32_t out_w, out_h, out_c, out_stride;
+  uint64_t final_src;       // copy-kernel source (no pass runs, or gray->RGB expansion)
+  uint32_t final_src_stride, copy_needed;
+  uint32_t final_src_c, pad2;
+};
+
+// One workgroup's work: an image and the first item it handles.
+struct WgItem {
+  uint32_t image;
+  uint32_t item0;
+};
+
+// Batch-wide flags written by kernels (zeroed before each batch).
+struct BatchFlags {
+  uint32_t chain_changed;   // k_huff_fix changed a workgroup's last exit state
+  uint32_t fix_count;       // workgroups k_huff_fix had to re-run
+  uint32_t write_mismatch;  // k_huff_write exit != next subsequence's input
+  uint32_t sync_iters_max;  // longest intra-workgroup sync loop
+};
+
+}  // namespace dg

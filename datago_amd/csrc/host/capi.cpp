@@ -1,0 +1,228 @@
+// capi.cpp — extern "C" entry points declared in include/datago_hip.h.
+#include <string.h>
+
+#include <new>
+#include <string>
+
+#include "../../../include/datago_hip.h"
+#include "buckets.h"
+#include "jpeg_header.h"
+#include "pipeline.h"
+
+namespace dg {
+extern thread_local std::string g_last_error;
+void set_error(const std::string &s);
+}  // namespace dg
+
+struct dg_bucket_table {
+  dg::BucketTable t;
+  dg_bucket_table(uint32_t a, uint32_t b, double c, double d) : t(a, b, c, d) {}
+};
+
+struct dg_ctx {
+  dg::Context c;
+  dg_bucket_table view;
+  dg_ctx(int dev, const dg_image_config *cfg)
+      : c(dev, cfg),
+        view(cfg && cfg->crop_and_resize && cfg->default_image_size && cfg->downsampling_ratio
+                 ? cfg->default_image_size
+                 : 224,
+             cfg && cfg->crop_and_resize && cfg->default_image_size && cfg->downsampling_ratio
+                 ? cfg->downsampling_ratio
+                 : 16,
+             cfg && cfg->crop_and_resize ? cfg->min_aspect_ratio : 0.5,
+             cfg && cfg->crop_and_resize ? cfg->max_aspect_ratio : 2.0) {}
+};
+
+extern "C" {
+
+const char *dg_last_error(void) { return dg::g_last_error.c_str(); }
+int32_t dg_abi_version(void) { return DG_ABI_VERSION; }
+
+dg_status dg_bucket_table_build(uint32_t size, uint32_t ratio, double min_ar, double max_ar,
+                                dg_bucket_table **out) {
+  if (!out) return DG_ERR_INVALID;
+  *out = nullptr;
+  // assert!s of image_processing.rs:78-93, reported instead of aborting
+  if (size == 0 || ratio == 0 || !(min_ar > 0.0) || !(max_ar >= min_ar)) {
+    dg::set_error("invalid bucket parameters");
+    return DG_ERR_INVALID;
+  }
+  dg_bucket_table *t = new (std::nothrow) dg_bucket_table(size, ratio, min_ar, max_ar);
+  if (!t) return DG_ERR_OOM;
+  *out = t;
+  return DG_OK;
+}
+
+void dg_bucket_table_free(dg_bucket_table *t) { delete t; }
+
+int32_t dg_bucket_count(const dg_bucket_table *t) { return t ? (int32_t)t->t.buckets().size() : 0; }
+
+dg_status dg_bucket_get(const dg_bucket_table *t, int32_t i, uint32_t *w, uint32_t *h, char *key, size_t cap) {
+  if (!t || i < 0 || i >= (int32_t)t->t.buckets().size()) return DG_ERR_BAD_BUCKET;
+  const dg::Bucket &b = t->t.buckets()[i];
+  if (w) *w = b.w;
+  if (h) *h = b.h;
+  if (key && cap) {
+    strncpy(key, b.key.c_str(), cap - 1);
+    key[cap - 1] = 0;
+  }
+  return DG_OK;
+}
+
+int32_t dg_closest_bucket(const dg_bucket_table *t, int32_t w, int32_t h) {
+  if (!t || w <= 0 || h <= 0) return -1;
+  return t->t.closest(w, h);
+}
+
+int32_t dg_bucket_find_key(const dg_bucket_table *t, const char *key) {
+  if (!t || !key) return -1;
+  return t->t.find_key(key);
+}
+
+dg_status dg_aspect_ratio_to_str(uint32_t w, uint32_t h, char *out, size_t cap) {
+  if (!out || !cap || h == 0) return DG_ERR_INVALID;
+  std::string s = dg::aspect_ratio_to_str(w, h);
+  strncpy(out, s.c_str(), cap - 1);
+  out[cap - 1] = 0;
+  return DG_OK;
+}
+
+dg_status dg_probe(const uint8_t *bytes, size_t len, dg_probe_info *out) {
+  if (!out) return DG_ERR_INVALID;
+  memset(out, 0, sizeof(*out));
+  if (!bytes || !len) return DG_ERR_CORRUPT;
+  if (dg::is_png(bytes, len)) {
+    out->format = DG_FMT_PNG;
+    if (len >= 24) {
+      out->width = (uint32_t)bytes[16] << 24 | (uint32_t)bytes[17] << 16 | (uint32_t)bytes[18] << 8 | bytes[19];
+      out->height = (uint32_t)bytes[20] << 24 | (uint32_t)bytes[21] << 16 | (uint32_t)bytes[22] << 8 | bytes[23];
+      if (len >= 26) out->bit_depth = bytes[24];
+    }
+    out->gpu_supported = 0;
+    return DG_OK;
+  }
+  if (!dg::is_jpeg(bytes, len)) {
+    dg::set_error("unknown image format");
+    return DG_ERR_CORRUPT;
+  }
+  dg::JpegHeader h;
+  dg::parse_jpeg_header(bytes, len, h);
+  out->format = DG_FMT_JPEG;
+  out->width = h.width;
+  out->height = h.height;
+  out->components = h.ncomp;
+  out->bit_depth = h.precision;
+  for (int c = 0; c < h.ncomp && c < 4; c++) {
+    out->h_samp[c] = h.comp[c].h;
+    out->v_samp[c] = h.comp[c].v;
+  }
+  out->progressive = h.progressive;
+  out->arithmetic = h.arithmetic;
+  out->precision = h.precision;
+  out->restart_interval = h.restart;
+  out->gpu_supported = h.status == dg::JH_OK;
+  if (h.status == dg::JH_CORRUPT) {
+    dg::set_error(h.why);
+    return DG_ERR_CORRUPT;
+  }
+  return DG_OK;
+}
+
+dg_status dg_ctx_create(int32_t device, const dg_image_config *cfg, dg_ctx **out) {
+  if (!out) return DG_ERR_INVALID;
+  *out = nullptr;
+  dg_ctx *c = new (std::nothrow) dg_ctx(device, cfg);
+  if (!c) return DG_ERR_OOM;
+  dg_status st = c->c.init();
+  if (st) {
+    delete c;
+    return st;
+  }
+  *out = c;
+  return DG_OK;
+}
+
+void dg_ctx_destroy(dg_ctx *ctx) { delete ctx; }
+
+const dg_bucket_table *dg_ctx_buckets(const dg_ctx *ctx) {
+  if (!ctx || !ctx->c.buckets()) return nullptr;
+  return &ctx->view;
+}
+
+dg_status dg_output_size(dg_ctx *ctx, const uint8_t *bytes, size_t len, int32_t forced, uint64_t *nbytes) {
+  if (!ctx || !nbytes) return DG_ERR_INVALID;
+  return ctx->c.output_size(bytes, len, forced, nbytes);
+}
+
+dg_status dg_submit(dg_ctx *ctx, int32_t n, const uint8_t *const *srcs, const size_t *lens, const int32_t *forced,
+                    uint8_t *const *outs, const uint64_t *caps, dg_payload_meta *metas, uint64_t *ticket) {
+  if (!ctx || !ticket) return DG_ERR_INVALID;
+  return ctx->c.submit(n, srcs, nullptr, lens, forced, outs, caps, metas, true, ticket);
+}
+
+dg_status dg_submit_device(dg_ctx *ctx, int32_t n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs,
+                           const size_t *lens, const int32_t *forced, uint8_t *const *d_outs,
+                           const uint64_t *caps, dg_payload_meta *metas, uint64_t *ticket) {
+  if (!ctx || !ticket || (n > 0 && !d_srcs)) return DG_ERR_INVALID;
+  return ctx->c.submit(n, h_srcs, d_srcs, lens, forced, d_outs, caps, metas, false, ticket);
+}
+
+dg_status dg_wait(dg_ctx *ctx, uint64_t ticket) { return ctx ? ctx->c.wait(ticket) : DG_ERR_INVALID; }
+dg_status dg_poll(dg_ctx *ctx, uint64_t ticket) { return ctx ? ctx->c.poll(ticket) : DG_ERR_INVALID; }
+
+dg_status dg_decode_one(dg_ctx *ctx, const uint8_t *src, size_t len, int32_t forced, uint8_t *out, uint64_t cap,
+                        dg_payload_meta *meta) {
+  if (!ctx || !meta) return DG_ERR_INVALID;
+  uint64_t t = 0;
+  const uint8_t *srcs[1] = {src};
+  size_t lens[1] = {len};
+  int32_t f[1] = {forced};
+  uint8_t *outs[1] = {out};
+  uint64_t caps[1] = {cap};
+  dg_status st = ctx->c.submit(1, srcs, nullptr, lens, f, outs, caps, meta, true, &t);
+  if (st) return st;
+  st = ctx->c.wait(t);
+  if (st) return st;
+  return (dg_status)meta->status;
+}
+
+dg_status dg_device_alloc(dg_ctx *ctx, size_t bytes, void **dptr) {
+  if (!ctx || !dptr) return DG_ERR_INVALID;
+  hipSetDevice(ctx->c.device());
+  if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess) return DG_ERR_OOM;
+  return DG_OK;
+}
+dg_status dg_device_free(dg_ctx *ctx, void *dptr) {
+  if (!ctx) return DG_ERR_INVALID;
+  hipSetDevice(ctx->c.device());
+  return hipFree(dptr) == hipSuccess ? DG_OK : DG_ERR_DEVICE;
+}
+dg_status dg_memcpy_h2d(dg_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  if (!ctx) return DG_ERR_INVALID;
+  hipSetDevice(ctx->c.device());
+  return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? DG_OK : DG_ERR_DEVICE;
+}
+dg_status dg_memcpy_d2h(dg_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  if (!ctx) return DG_ERR_INVALID;
+  hipSetDevice(ctx->c.device());
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? DG_OK : DG_ERR_DEVICE;
+}
+dg_status dg_synchronize(dg_ctx *ctx) {
+  if (!ctx) return DG_ERR_INVALID;
+  hipSetDevice(ctx->c.device());
+  return hipStreamSynchronize(ctx->c.stream()) == hipSuccess ? DG_OK : DG_ERR_DEVICE;
+}
+
+int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_t cap) {
+  return ctx ? ctx->c.timings(names, ms, cap) : 0;
+}
+
+dg_status dg_ctx_set_option(dg_ctx *ctx, const char *key, int64_t value) {
+  if (!ctx || !key) return DG_ERR_INVALID;
+  return ctx->c.set_option(key, value);
+}
+
+int64_t dg_ctx_get_stat(dg_ctx *ctx, const char *key) { return ctx && key ? ctx->c.get_stat(key) : -1; }
+
+}  // extern "C"

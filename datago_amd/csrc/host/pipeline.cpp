@@ -1,0 +1,734 @@
+// pipeline.cpp — batch planner + runtime for the decode/bucket-resize stage.
+//
+// Host work per image is header-only (parse + bucket + buffer layout); all
+// pixel and coefficient arithmetic runs in kernels.hip.  A batch is laid out
+// in one device scratch arena, its descriptors and workgroup lists go up in
+// one H2D copy, and every kernel of the batch is launched on the context's
+// stream back to back.  The reference equivalent is one tokio task per sample
+// (worker_files.rs:32-72 -> image_processing.rs:341-431).
+#include "pipeline.h"
+
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "../dg_pixel.h"
+#include "../kernels.h"
+
+namespace dg {
+
+thread_local std::string g_last_error;
+void set_error(const std::string &s) { g_last_error = s; }
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      set_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x);          \
+      return DG_ERR_DEVICE;                                                                \
+    }                                                                                      \
+  } while (0)
+
+static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+Context::Context(int device, const dg_image_config *cfg) : device_(device) {
+  if (cfg && cfg->crop_and_resize) {
+    has_cfg_ = true;
+    cfg_ = *cfg;
+  } else if (cfg) {
+    cfg_ = *cfg;
+  }
+}
+
+Context::~Context() {
+  hipSetDevice(device_);
+  if (stream_) hipStreamSynchronize(stream_);
+  for (auto e : events_) hipEventDestroy(e);
+  for (DevBuf *b : {&d_hpool_, &d_qpool_, &d_scratch_, &d_meta_, &d_input_})
+    if (b->p) hipFree(b->p);
+  for (PinBuf *b : {&h_stage_, &h_out_})
+    if (b->p) hipHostFree(b->p);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+dg_status Context::init() {
+  if (has_cfg_) {
+    // ImageTransformConfig::get_ar_aware_transform asserts (image_processing.rs:78-93)
+    if (cfg_.default_image_size == 0 || cfg_.downsampling_ratio == 0 || !(cfg_.min_aspect_ratio > 0.0) ||
+        !(cfg_.max_aspect_ratio >= cfg_.min_aspect_ratio)) {
+      set_error("invalid image_config (default_image_size/downsampling_ratio/aspect ratios)");
+      return DG_ERR_INVALID;
+    }
+    buckets_.reset(new BucketTable(cfg_.default_image_size, cfg_.downsampling_ratio, cfg_.min_aspect_ratio,
+                                   cfg_.max_aspect_ratio));
+    if (buckets_->buckets().empty()) {
+      set_error("empty bucket table");
+      return DG_ERR_INVALID;
+    }
+  }
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device_ < 0 || device_ >= ndev) {
+    set_error("device ordinal out of range");
+    return DG_ERR_INVALID;
+  }
+  HIPCHK(hipSetDevice(device_));
+  HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  events_.resize(16);
+  for (auto &e : events_) HIPCHK(hipEventCreate(&e));
+  return DG_OK;
+}
+
+dg_status Context::set_option(const std::string &k, int64_t v) {
+  if (k == "sub_bytes") {
+    if (v < 16 || v > 4096 || (v & 3)) return DG_ERR_INVALID;
+    sub_bytes_ = (uint32_t)v;
+    return DG_OK;
+  }
+  if (k == "timing") {
+    timing_ = v != 0;
+    return DG_OK;
+  }
+  return DG_ERR_INVALID;
+}
+
+int64_t Context::get_stat(const std::string &k) {
+  if (k == "batches") return stat_batches_;
+  if (k == "resync_rounds") return stat_resync_;
+  if (k == "fix_workgroups") return stat_fix_;
+  if (k == "write_mismatch") return stat_mismatch_;
+  if (k == "sync_iters_max") return stat_iters_;
+  if (k == "sub_bytes") return sub_bytes_;
+  if (k == "hpool") return (int64_t)hpool_.size();
+  if (k == "qpool") return (int64_t)qpool_.size();
+  return -1;
+}
+
+static const char *kStageNames[] = {"upload", "huff_sync", "huff_fix", "huff_scan", "huff_write", "coeffs",
+                                    "idct", "color", "resize_h1", "resize_v1", "resize_h2", "resize_v2",
+                                    "copy", "download"};
+
+int Context::timings(const char **names, float *ms, int cap) {
+  int n = (int)last_ms_.size();
+  for (int i = 0; i < n && i < cap; i++) {
+    if (names) names[i] = kStageNames[i];
+    if (ms) ms[i] = last_ms_[i];
+  }
+  return n;
+}
+
+dg_status Context::ensure(DevBuf &b, size_t bytes) {
+  if (b.cap >= bytes) return DG_OK;
+  if (b.p) {
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  size_t cap = align_up(std::max(bytes, (size_t)1 << 20) + bytes / 4, 1 << 20);
+  hipError_t e = hipMalloc(&b.p, cap);
+  if (e != hipSuccess) {
+    set_error("device allocation failed");
+    b.p = nullptr;
+    return DG_ERR_OOM;
+  }
+  b.cap = cap;
+  return DG_OK;
+}
+
+dg_status Context::ensure_pinned(PinBuf &b, size_t bytes) {
+  if (b.cap >= bytes) return DG_OK;
+  if (b.p) {
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(hipHostFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  size_t cap = align_up(std::max(bytes, (size_t)1 << 20) + bytes / 4, 1 << 20);
+  if (hipHostMalloc(&b.p, cap, hipHostMallocDefault) != hipSuccess) {
+    set_error("pinned host allocation failed");
+    b.p = nullptr;
+    return DG_ERR_OOM;
+  }
+  b.cap = cap;
+  return DG_OK;
+}
+
+int Context::pool_huff(const HuffSpec &s) {
+  std::string key((const char *)s.bits, 17);
+  key.append((const char *)s.vals, (size_t)s.nvals);
+  auto it = hpool_idx_.find(key);
+  if (it != hpool_idx_.end()) return it->second;
+  HuffTable t;
+  if (!build_huff_table(s, t)) return -1;
+  if (hpool_.size() >= 65535) return -1;
+  hpool_.push_back(t);
+  int idx = (int)hpool_.size() - 1;
+  hpool_idx_[key] = idx;
+  return idx;
+}
+
+int Context::pool_quant(const uint16_t *q) {
+  std::string key((const char *)q, 128);
+  auto it = qpool_idx_.find(key);
+  if (it != qpool_idx_.end()) return it->second;
+  QuantTable t;
+  memcpy(t.q, q, 128);
+  if (qpool_.size() >= 65535) return -1;
+  qpool_.push_back(t);
+  int idx = (int)qpool_.size() - 1;
+  qpool_idx_[key] = idx;
+  return idx;
+}
+
+dg_status Context::upload_pools() {
+  if (hpool_.size() != hpool_uploaded_) {
+    size_t bytes = hpool_.size() * sizeof(HuffTable);
+    if (d_hpool_.cap < bytes) {
+      dg_status st = ensure(d_hpool_, bytes * 2);
+      if (st) return st;
+      hpool_uploaded_ = 0;
+    }
+    HIPCHK(hipMemcpyAsync((char *)d_hpool_.p + hpool_uploaded_ * sizeof(HuffTable), &hpool_[hpool_uploaded_],
+                          (hpool_.size() - hpool_uploaded_) * sizeof(HuffTable), hipMemcpyHostToDevice, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));  // the host vector may reallocate later
+    hpool_uploaded_ = hpool_.size();
+  }
+  if (qpool_.size() != qpool_uploaded_) {
+    size_t bytes = qpool_.size() * sizeof(QuantTable);
+    if (d_qpool_.cap < bytes) {
+      dg_status st = ensure(d_qpool_, bytes * 2);
+      if (st) return st;
+      qpool_uploaded_ = 0;
+    }
+    HIPCHK(hipMemcpyAsync((char *)d_qpool_.p + qpool_uploaded_ * sizeof(QuantTable), &qpool_[qpool_uploaded_],
+                          (qpool_.size() - qpool_uploaded_) * sizeof(QuantTable), hipMemcpyHostToDevice, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    qpool_uploaded_ = qpool_.size();
+  }
+  return DG_OK;
+}
+
+// Decide what the GPU will do with one image: header, bucket, output size.
+dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, ImagePlan &p) {
+  p = ImagePlan();
+  if (!h || len == 0) {
+    p.status = DG_ERR_CORRUPT;
+    return DG_OK;
+  }
+  if (!is_jpeg(h, len)) {
+    p.status = is_png(h, len) ? DG_ERR_UNSUPPORTED : DG_ERR_CORRUPT;
+    return DG_OK;
+  }
+  parse_jpeg_header(h, len, p.hdr);
+  if (p.hdr.status != JH_OK) {
+    p.status = p.hdr.status == JH_UNSUPPORTED ? DG_ERR_UNSUPPORTED : DG_ERR_CORRUPT;
+    return DG_OK;
+  }
+  const uint32_t W = p.hdr.width, H = p.hdr.height;
+  const uint32_t C = p.hdr.ncomp == 1 ? 1 : 3;
+  p.channels = (int32_t)C;  // pre-transform (image_processing.rs:349-351)
+  p.bit_depth = 8;
+  uint32_t ow = W, oh = H;
+  if (has_cfg_) {
+    int b = forced;
+    if (b < 0) {
+      b = buckets_->closest((int32_t)W, (int32_t)H);
+    } else if (b >= (int)buckets_->buckets().size()) {
+      p.status = DG_ERR_BAD_BUCKET;
+      return DG_OK;
+    }
+    p.bucket = b;
+    ow = buckets_->buckets()[b].w;
+    oh = buckets_->buckets()[b].h;
+  }
+  p.out_w = ow;
+  p.out_h = oh;
+  p.out_c = (cfg_.image_to_rgb8 && C == 1) ? 3 : C;
+  if (cfg_.image_to_rgb8) p.channels = 3;  // image_processing.rs:367-372
+  p.out_bytes = (uint64_t)ow * oh * p.out_c;
+  if (cfg_.pre_encode_images) p.status = DG_ERR_UNSUPPORTED;
+  return DG_OK;
+}
+
+dg_status Context::output_size(const uint8_t *bytes, size_t len, int32_t forced, uint64_t *nbytes) {
+  ImagePlan p;
+  plan_image(bytes, len, forced, p);
+  *nbytes = p.out_bytes;
+  if (p.status) set_error(p.hdr.why ? p.hdr.why : "unsupported");
+  return (dg_status)p.status;
+}
+
+namespace {
+struct Layout {
+  size_t off = 0;
+  size_t take(size_t bytes, size_t align = 256) {
+    off = align_up(off, align);
+    size_t o = off;
+    off += bytes;
+    return o;
+  }
+};
+}  // namespace
+
+dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
+                          const int32_t *forced, uint8_t *const *outs, const uint64_t *caps,
+                          dg_payload_meta *metas, bool host_io, uint64_t *ticket) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (n < 0 || (n > 0 && (!h_srcs || !lens || !outs || !caps || !metas))) {
+    set_error("null argument");
+    return DG_ERR_INVALID;
+  }
+  HIPCHK(hipSetDevice(device_));
+  if (cur_ && !cur_->done) {
+    dg_status st = finish(*cur_);
+    if (st) return st;
+  }
+  std::unique_ptr<Batch> bp(new Batch());
+  Batch &b = *bp;
+  b.ticket = next_ticket_++;
+  b.n = n;
+  b.host_io = host_io;
+  b.metas = metas;
+  b.plans.resize(n);
+  b.desc_of.assign(n, -1);
+  // ---- 1. plan every image (host, header only)
+  for (int i = 0; i < n; i++) {
+    plan_image(h_srcs[i], lens[i], forced ? forced[i] : -1, b.plans[i]);
+    ImagePlan &p = b.plans[i];
+    dg_payload_meta &m = metas[i];
+    memset(&m, 0, sizeof(m));
+    m.status = p.status;
+    m.bucket = p.bucket;
+    if (p.hdr.status == JH_OK) {
+      m.original_width = p.hdr.width;
+      m.original_height = p.hdr.height;
+    }
+    m.width = p.out_w;
+    m.height = p.out_h;
+    m.channels = p.channels;
+    m.bit_depth = p.bit_depth;
+    m.is_encoded = 0;
+    m.nbytes = p.out_bytes;
+    if (p.status == DG_OK && caps[i] < p.out_bytes) {
+      p.status = DG_ERR_SMALL_BUFFER;
+      m.status = DG_ERR_SMALL_BUFFER;
+    }
+    if (p.status == DG_OK && !outs[i]) {
+      p.status = DG_ERR_INVALID;
+      m.status = DG_ERR_INVALID;
+    }
+  }
+  // ---- 2. table pools
+  for (int i = 0; i < n; i++) {
+    ImagePlan &p = b.plans[i];
+    if (p.status) continue;
+    bool ok = true;
+    for (int c = 0; c < p.hdr.ncomp; c++) {
+      if (pool_huff(p.hdr.dc[p.hdr.comp[c].td]) < 0 || pool_huff(p.hdr.ac[p.hdr.comp[c].ta]) < 0 ||
+          pool_quant(p.hdr.q[p.hdr.comp[c].tq]) < 0)
+        ok = false;
+    }
+    if (!ok) {
+      p.status = DG_ERR_CORRUPT;
+      metas[i].status = DG_ERR_CORRUPT;
+    }
+  }
+  dg_status st = upload_pools();
+  if (st) return st;
+
+  // ---- 3. layout
+  Layout L;        // scratch arena
+  Layout IN;       // input arena (host path)
+  std::vector<size_t> in_off(n, 0);
+  size_t out_total = 0;
+  b.out_dev_off.assign(n, 0);
+  uint32_t sub_base = 0;
+  b.descs.reserve(n);
+  // first pass: sizes only (pointers are patched after allocation)
+  struct Offs {
+    size_t coef, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], tmp, out;
+  };
+  std::vector<Offs> offs;
+  for (int i = 0; i < n; i++) {
+    ImagePlan &p = b.plans[i];
+    if (p.status) continue;
+    const JpegHeader &h = p.hdr;
+    ImageDesc d;
+    memset(&d, 0, sizeof(d));
+    Offs o;
+    memset(&o, 0, sizeof(o));
+    const uint32_t W = h.width, H = h.height;
+    d.width = W;
+    d.height = H;
+    d.ncomp = (uint8_t)h.ncomp;
+    d.colorspace = (uint8_t)h.colorspace;
+    d.dec_c = h.ncomp == 1 ? 1 : 3;
+    d.hmax = (uint32_t)h.hmax;
+    d.vmax = (uint32_t)h.vmax;
+    d.mcux = (W + 8 * d.hmax - 1) / (8 * d.hmax);
+    d.mcuy = (H + 8 * d.vmax - 1) / (8 * d.vmax);
+    uint32_t bpm = 0;
+    for (int c = 0; c < h.ncomp; c++) {
+      const JpegComponent &k = h.comp[c];
+      d.ch[c] = (uint32_t)k.h;
+      d.cv[c] = (uint32_t)k.v;
+      d.cdsw[c] = (uint32_t)(((uint64_t)W * k.h + d.hmax - 1) / d.hmax);
+      d.cdsh[c] = (uint32_t)(((uint64_t)H * k.v + d.vmax - 1) / d.vmax);
+      if (h.ncomp == 1) {
+        d.cbw[c] = (d.cdsw[c] + 7) / 8;
+        d.cbh[c] = (d.cdsh[c] + 7) / 8;
+        d.cfirst[c] = 0;
+        d.blk_comp[0] = 0;
+        bpm = 1;
+      } else {
+        d.cbw[c] = d.mcux * k.h;
+        d.cbh[c] = d.mcuy * k.v;
+        d.cfirst[c] = bpm;
+        for (int j = 0; j < k.h * k.v; j++) d.blk_comp[bpm + j] = (uint8_t)c;
+        bpm += (uint32_t)(k.h * k.v);
+      }
+    }
+    d.bpm = bpm;
+    d.total_blocks = h.ncomp == 1 ? d.cbw[0] * d.cbh[0] : d.mcux * d.mcuy * bpm;
+    d.restart = (uint32_t)h.restart;
+    d.blocks_per_seg = d.restart * bpm;
+    // Huffman slots: unique pool indices per image
+    int nslots = 0;
+    auto slot_of = [&](int pidx) {
+      for (int s = 0; s < nslots; s++)
+        if (d.hslot[s] == pidx) return s;
+      d.hslot[nslots] = (uint16_t)pidx;
+      return nslots++;
+    };
+    for (int c = 0; c < h.ncomp; c++) {
+      d.dc_slot[c] = (uint8_t)slot_of(pool_huff(h.dc[h.comp[c].td]));
+      d.ac_slot[c] = (uint8_t)slot_of(pool_huff(h.ac[h.comp[c].ta]));
+      d.qpool[c] = (uint16_t)pool_quant(h.q[h.comp[c].tq]);
+    }
+    d.nslots = (uint8_t)nslots;
+    // entropy data
+    d.scan_len = (uint32_t)(h.scan_end - h.scan_off);
+    d.sub_bytes = sub_bytes_;
+    d.nsub = std::max<uint32_t>(1, (d.scan_len + sub_bytes_ - 1) / sub_bytes_);
+    d.sub_base = sub_base;
+    sub_base += d.nsub;
+    if (host_io) in_off[i] = IN.take(lens[i] + 16, 16);
+    // buffers
+    o.coef = L.take((size_t)d.total_blocks * 128);
+    for (int c = 0; c < h.ncomp; c++) o.plane[c] = L.take((size_t)d.cbw[c] * 8 * d.cbh[c] * 8);
+    const uint32_t C = d.dec_c;
+    size_t cur_stride;
+    if (h.ncomp == 3) {
+      d.pix_stride = (uint32_t)align_up((size_t)W * 3, 16);
+      o.pix = L.take((size_t)d.pix_stride * H);
+      cur_stride = d.pix_stride;
+    } else {
+      cur_stride = (size_t)d.cbw[0] * 8;
+    }
+    // resize plan (image_processing.rs:264-325)
+    d.out_w = p.out_w;
+    d.out_h = p.out_h;
+    d.out_c = p.out_c;
+    d.out_stride = p.out_w * p.out_c;
+    uint32_t cw = W, chh = H;
+    int nst = 0;
+    int last_stage = -1;
+    if (has_cfg_ && !(W == p.out_w && H == p.out_h)) {
+      uint32_t nw, nh;
+      scaled_size(W, H, p.out_w, p.out_h, nw, nh);
+      double l, t, bw, bh;
+      fit_crop_box(nw, nh, p.out_w, p.out_h, l, t, bw, bh);
+      struct Call {
+        uint32_t dw, dh;
+        double x0, y0, x1, y1;
+      } calls[2] = {{nw, nh, 0.0, 0.0, (double)W, (double)H}, {p.out_w, p.out_h, l, t, l + bw, t + bh}};
+      for (int r = 0; r < 2; r++) {
+        const Call &k = calls[r];
+        bool need_h = k.dw != cw || k.x0 != 0.0 || k.x1 != (double)k.dw;
+        bool need_v = k.dh != chh || k.y0 != 0.0 || k.y1 != (double)k.dh;
+        if (need_h) {
+          ResizePass &ps = d.pass[2 * r];
+          ps.kind = 1;
+          ps.in0 = k.x0;
+          ps.in1 = k.x1;
+          ps.in_size = cw;
+          ps.out_size = k.dw;
+          ps.ksize = fir_ksize(k.x0, k.x1, k.dw);
+          ps.src_stride = (uint32_t)cur_stride;
+          ps.width = k.dw;
+          ps.rows = chh;
+          ps.row0 = 0;
+          ps.C = C;
+          ps.dst_stride = (uint32_t)align_up((size_t)k.dw * C, 16);
+          o.pass_dst[2 * r] = L.take((size_t)ps.dst_stride * ps.rows);
+          o.pass_coef[2 * r] = L.take((size_t)ps.out_size * ps.ksize * 2);
+          o.pass_bounds[2 * r] = L.take((size_t)ps.out_size * 8);
+          cw = k.dw;
+          cur_stride = ps.dst_stride;
+          last_stage = 2 * r;
+          nst++;
+        }
+        if (need_v) {
+          ResizePass &ps = d.pass[2 * r + 1];
+          ps.kind = 2;
+          ps.in0 = k.y0;
+          ps.in1 = k.y1;
+          ps.in_size = chh;
+          ps.out_size = k.dh;
+          ps.ksize = fir_ksize(k.y0, k.y1, k.dh);
+          ps.src_stride = (uint32_t)cur_stride;
+          ps.width = cw;
+          ps.rows = k.dh;
+          ps.row0 = 0;
+          ps.C = C;
+          ps.dst_stride = (uint32_t)align_up((size_t)cw * C, 16);
+          o.pass_dst[2 * r + 1] = L.take((size_t)ps.dst_stride * ps.rows);
+          o.pass_coef[2 * r + 1] = L.take((size_t)ps.out_size * ps.ksize * 2);
+          o.pass_bounds[2 * r + 1] = L.take((size_t)ps.out_size * 8);
+          chh = k.dh;
+          cur_stride = ps.dst_stride;
+          last_stage = 2 * r + 1;
+          nst++;
+        }
+      }
+    }
+    // final write: the last pass writes straight into the output when the
+    // channel count is unchanged; otherwise (or with no pass) k_copy runs.
+    if (last_stage >= 0 && d.out_c == C) {
+      d.pass[last_stage].dst_stride = d.out_stride;
+      o.pass_dst[last_stage] = (size_t)-1;  // -> out
+      d.copy_needed = 0;
+    } else {
+      d.copy_needed = 1;
+      d.final_src_c = C;
+      d.final_src_stride = (uint32_t)cur_stride;
+    }
+    (void)nst;
+    if (host_io) {
+      o.out = L.take(p.out_bytes, 16);
+      b.out_dev_off[i] = o.out;
+      out_total += p.out_bytes;
+    }
+    b.desc_of[i] = (int)b.descs.size();
+    b.descs.push_back(d);
+    offs.push_back(o);
+    (void)last_stage;
+  }
+  b.total_subs = sub_base;
+  const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
+  st = ensure(d_scratch_, L.off + 256);
+  if (st) return st;
+  if (host_io) {
+    st = ensure(d_input_, IN.off + 64);
+    if (st) return st;
+  }
+  // ---- 4. patch device addresses
+  char *S = (char *)d_scratch_.p;
+  int k = 0;
+  for (int i = 0; i < n; i++) {
+    if (b.desc_of[i] < 0) continue;
+    ImageDesc &d = b.descs[b.desc_of[i]];
+    const Offs &o = offs[k++];
+    const JpegHeader &h = b.plans[i].hdr;
+    const uint8_t *src = host_io ? (const uint8_t *)d_input_.p + in_off[i] : d_srcs[i];
+    d.scan = (uint64_t)(uintptr_t)(src + h.scan_off);
+    d.coef = (uint64_t)(uintptr_t)(S + o.coef);
+    for (int c = 0; c < h.ncomp; c++) d.plane[c] = (uint64_t)(uintptr_t)(S + o.plane[c]);
+    d.pix = h.ncomp == 3 ? (uint64_t)(uintptr_t)(S + o.pix) : 0;
+    uint64_t out = host_io ? (uint64_t)(uintptr_t)(S + o.out) : (uint64_t)(uintptr_t)outs[i];
+    d.out = out;
+    uint64_t cur = h.ncomp == 3 ? d.pix : d.plane[0];
+    for (int s = 0; s < kStages; s++) {
+      ResizePass &ps = d.pass[s];
+      if (!ps.kind) continue;
+      ps.src = cur;
+      ps.dst = o.pass_dst[s] == (size_t)-1 ? out : (uint64_t)(uintptr_t)(S + o.pass_dst[s]);
+      ps.coef = (uint64_t)(uintptr_t)(S + o.pass_coef[s]);
+      ps.bounds = (uint64_t)(uintptr_t)(S + o.pass_bounds[s]);
+      cur = ps.dst;
+    }
+    d.final_src = cur;
+    (void)subs_off;
+  }
+  // ---- 5. workgroup lists
+  for (auto &l : b.lists) l.clear();
+  for (int di = 0; di < (int)b.descs.size(); di++) {
+    const ImageDesc &d = b.descs[di];
+    const uint32_t I = (uint32_t)di;
+    for (uint32_t w = 0; w < d.nsub; w += kSubPerWg) b.lists[L_HUFF].push_back({I, w});
+    b.lists[L_SCAN].push_back({I, 0});
+    uint32_t items = 0;
+    for (uint32_t c = 0; c < d.ncomp; c++) items += d.cbh[c] * ((d.cbw[c] + 31) / 32);
+    for (uint32_t it = 0; it < items; it++) b.lists[L_IDCT].push_back({I, it});
+    if (d.ncomp == 3) {
+      uint32_t q = (d.width + 3) / 4 * d.height;
+      for (uint32_t it = 0; it < q; it += 256) b.lists[L_COLOR].push_back({I, it});
+    }
+    for (int s = 0; s < kStages; s++) {
+      const ResizePass &ps = d.pass[s];
+      if (!ps.kind) continue;
+      b.lists[L_COEF].push_back({I, (uint32_t)s});
+      uint32_t cnt = ps.kind == 1 ? ps.width * ps.rows : (ps.width * ps.C + 3) / 4 * ps.rows;
+      for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_RH0 + s].push_back({I, it});
+    }
+    if (d.copy_needed) {
+      uint32_t cnt = d.out_w * d.out_h;
+      for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_COPY].push_back({I, it});
+    }
+  }
+  // ---- 6. meta buffer: [flags][descs][lists...]
+  Layout M;
+  b.flags_off = M.take(sizeof(BatchFlags));
+  b.desc_off = M.take(b.descs.size() * sizeof(ImageDesc));
+  for (int l = 0; l < L_COUNT; l++) b.list_off[l] = M.take(b.lists[l].size() * sizeof(WgItem));
+  b.meta_bytes = M.off;
+  st = ensure(d_meta_, b.meta_bytes + 256);
+  if (st) return st;
+  size_t stage_bytes = b.meta_bytes + (host_io ? IN.off : 0);
+  st = ensure_pinned(h_stage_, stage_bytes + 256);
+  if (st) return st;
+  char *P = (char *)h_stage_.p;
+  memset(P + b.flags_off, 0, sizeof(BatchFlags));
+  memcpy(P + b.desc_off, b.descs.data(), b.descs.size() * sizeof(ImageDesc));
+  for (int l = 0; l < L_COUNT; l++)
+    if (!b.lists[l].empty()) memcpy(P + b.list_off[l], b.lists[l].data(), b.lists[l].size() * sizeof(WgItem));
+  if (host_io) {
+    for (int i = 0; i < n; i++)
+      if (b.desc_of[i] >= 0) memcpy(P + b.meta_bytes + in_off[i], h_srcs[i], lens[i]);
+  }
+  if (timing_) HIPCHK(hipEventRecord(events_[0], stream_));
+  HIPCHK(hipMemcpyAsync(d_meta_.p, P, b.meta_bytes, hipMemcpyHostToDevice, stream_));
+  if (host_io && IN.off) HIPCHK(hipMemcpyAsync(d_input_.p, P + b.meta_bytes, IN.off, hipMemcpyHostToDevice, stream_));
+  b.stage_ms.clear();
+  subs_off_ = subs_off;  // SubStates live in the scratch arena
+  if (host_io) {
+    b.host_outs.assign(outs, outs + n);
+    b.host_caps.assign(caps, caps + n);
+  }
+  st = launch_all(b, false);
+  if (st) return st;
+  stat_batches_++;
+  *ticket = b.ticket;
+  cur_ = std::move(bp);
+  return DG_OK;
+}
+
+dg_status Context::launch_all(Batch &b, bool from_fix) {
+  char *M = (char *)d_meta_.p;
+  const ImageDesc *dd = (const ImageDesc *)(M + b.desc_off);
+  ImageDesc *dm = (ImageDesc *)(M + b.desc_off);
+  BatchFlags *fl = (BatchFlags *)(M + b.flags_off);
+  SubState *subs = (SubState *)((char *)d_scratch_.p + subs_off_);
+  const HuffTable *hp = (const HuffTable *)d_hpool_.p;
+  const QuantTable *qp = (const QuantTable *)d_qpool_.p;
+  auto lst = [&](int l) { return (const WgItem *)(M + b.list_off[l]); };
+  auto cnt = [&](int l) { return (uint32_t)b.lists[l].size(); };
+  auto ev = [&](int i) -> dg_status {
+    if (timing_) HIPCHK(hipEventRecord(events_[i], stream_));
+    return DG_OK;
+  };
+  if (from_fix) HIPCHK(hipMemsetAsync(fl, 0, sizeof(BatchFlags), stream_));
+  if (ev(1)) return DG_ERR_DEVICE;
+  if (!from_fix) launch_huff_sync(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+  if (ev(2)) return DG_ERR_DEVICE;
+  launch_huff_fix(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+  if (ev(3)) return DG_ERR_DEVICE;
+  launch_huff_scan(stream_, dm, lst(L_SCAN), cnt(L_SCAN), subs);
+  if (ev(4)) return DG_ERR_DEVICE;
+  launch_huff_write(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+  if (ev(5)) return DG_ERR_DEVICE;
+  if (!from_fix) launch_coeffs(stream_, dm, lst(L_COEF), cnt(L_COEF));
+  if (ev(6)) return DG_ERR_DEVICE;
+  launch_idct(stream_, dd, lst(L_IDCT), cnt(L_IDCT), qp);
+  if (ev(7)) return DG_ERR_DEVICE;
+  launch_color(stream_, dd, lst(L_COLOR), cnt(L_COLOR));
+  if (ev(8)) return DG_ERR_DEVICE;
+  launch_resize_h(stream_, dd, lst(L_RH0), cnt(L_RH0), 0);
+  if (ev(9)) return DG_ERR_DEVICE;
+  launch_resize_v(stream_, dd, lst(L_RV1), cnt(L_RV1), 1);
+  if (ev(10)) return DG_ERR_DEVICE;
+  launch_resize_h(stream_, dd, lst(L_RH2), cnt(L_RH2), 2);
+  if (ev(11)) return DG_ERR_DEVICE;
+  launch_resize_v(stream_, dd, lst(L_RV3), cnt(L_RV3), 3);
+  if (ev(12)) return DG_ERR_DEVICE;
+  launch_copy(stream_, dd, lst(L_COPY), cnt(L_COPY));
+  if (ev(13)) return DG_ERR_DEVICE;
+  HIPCHK(hipGetLastError());
+  // read back flags + per-image status (descs) for finish(), then outputs (host path)
+  size_t back = b.desc_off + b.descs.size() * sizeof(ImageDesc);
+  size_t total = align_up(back, 256);
+  if (b.host_io)
+    for (int i = 0; i < b.n; i++)
+      if (b.desc_of[i] >= 0) total += align_up(b.plans[i].out_bytes, 16);
+  dg_status st = ensure_pinned(h_out_, total + 256);
+  if (st) return st;
+  HIPCHK(hipMemcpyAsync(h_out_.p, M, back, hipMemcpyDeviceToHost, stream_));
+  if (b.host_io) {
+    size_t off = align_up(back, 256);
+    for (int i = 0; i < b.n; i++) {
+      if (b.desc_of[i] < 0) continue;
+      HIPCHK(hipMemcpyAsync((char *)h_out_.p + off, (char *)d_scratch_.p + b.out_dev_off[i], b.plans[i].out_bytes,
+                            hipMemcpyDeviceToHost, stream_));
+      off += align_up(b.plans[i].out_bytes, 16);
+    }
+  }
+  if (ev(14)) return DG_ERR_DEVICE;
+  return DG_OK;
+}
+
+dg_status Context::finish(Batch &b) {
+  for (;;) {
+    HIPCHK(hipStreamSynchronize(stream_));
+    memcpy(&b.flags, (char *)h_out_.p + b.flags_off, sizeof(BatchFlags));
+    stat_fix_ += b.flags.fix_count;
+    stat_mismatch_ += b.flags.write_mismatch;
+    stat_iters_ = std::max<int64_t>(stat_iters_, b.flags.sync_iters_max);
+    if (b.flags.chain_changed == 0 || b.resync_rounds >= 64) break;
+    // a workgroup's last exit state changed during the boundary repair: repeat
+    // repair + everything downstream until the chain is stable
+    b.resync_rounds++;
+    stat_resync_++;
+    dg_status st = launch_all(b, true);
+    if (st) return st;
+  }
+  if (timing_) {
+    last_ms_.assign(14, 0.f);
+    for (int i = 0; i < 14; i++) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, events_[i], events_[i + 1]) == hipSuccess) last_ms_[i] = ms;
+    }
+  }
+  const ImageDesc *back = (const ImageDesc *)((char *)h_out_.p + b.desc_off);
+  size_t off = align_up(b.desc_off + b.descs.size() * sizeof(ImageDesc), 256);
+  for (int i = 0; i < b.n; i++) {
+    if (b.desc_of[i] < 0) continue;
+    int status = back[b.desc_of[i]].status;
+    if (status) b.metas[i].status = status;
+    if (b.host_io) {
+      if (!status) memcpy(b.host_outs[i], (char *)h_out_.p + off, b.plans[i].out_bytes);
+      off += align_up(b.plans[i].out_bytes, 16);
+    }
+  }
+  b.done = true;
+  return DG_OK;
+}
+
+dg_status Context::wait(uint64_t ticket) {
+  std::lock_guard<std::mutex> lk(mu_);
+  HIPCHK(hipSetDevice(device_));
+  if (!cur_ || cur_->ticket != ticket) return ticket < next_ticket_ ? DG_OK : DG_ERR_INVALID;
+  if (cur_->done) return DG_OK;
+  return finish(*cur_);
+}
+
+dg_status Context::poll(uint64_t ticket) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!cur_ || cur_->ticket != ticket || cur_->done) return DG_OK;
+  hipError_t e = hipStreamQuery(stream_);
+  if (e == hipErrorNotReady) return DG_ERR_NOT_READY;
+  return DG_OK;
+}
+
+}  // namespace dg

@@ -1,0 +1,122 @@
+// pipeline.h — per-device context and batch runtime behind the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../../include/datago_hip.h"
+#include "../dg_types.h"
+#include "buckets.h"
+#include "jpeg_header.h"
+
+namespace dg {
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+};
+
+struct PinBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+};
+
+// Per-image host-side plan (what the host knows before the GPU runs).
+struct ImagePlan {
+  int status = DG_OK;
+  JpegHeader hdr;
+  int bucket = -1;
+  uint32_t out_w = 0, out_h = 0, out_c = 0;
+  uint64_t out_bytes = 0;
+  int32_t channels = 0, bit_depth = 8;
+};
+
+struct Batch {
+  uint64_t ticket = 0;
+  int n = 0;
+  bool host_io = false;
+  std::vector<ImagePlan> plans;
+  std::vector<ImageDesc> descs;
+  std::vector<int> desc_of;           // image -> desc index or -1
+  // workgroup lists (host copies) and their offsets in the device meta buffer
+  std::vector<WgItem> lists[12];
+  size_t list_off[12] = {0};
+  size_t desc_off = 0, flags_off = 0;
+  size_t meta_bytes = 0;
+  size_t total_subs = 0;
+  // host outputs
+  std::vector<uint8_t *> host_outs;
+  std::vector<uint64_t> host_caps;
+  std::vector<size_t> out_dev_off;    // offset of each output in the scratch arena (host path)
+  dg_payload_meta *metas = nullptr;
+  bool done = false;
+  int resync_rounds = 0;
+  BatchFlags flags = {0, 0, 0, 0};
+  std::vector<float> stage_ms;
+};
+
+enum ListId { L_HUFF = 0, L_SCAN, L_IDCT, L_COLOR, L_COEF, L_RH0, L_RV1, L_RH2, L_RV3, L_COPY, L_COUNT };
+
+class Context {
+ public:
+  Context(int device, const dg_image_config *cfg);
+  ~Context();
+  dg_status init();
+
+  dg_status submit(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
+                   const int32_t *forced, uint8_t *const *outs, const uint64_t *caps, dg_payload_meta *metas,
+                   bool host_io, uint64_t *ticket);
+  dg_status wait(uint64_t ticket);
+  dg_status poll(uint64_t ticket);
+  dg_status output_size(const uint8_t *bytes, size_t len, int32_t forced, uint64_t *nbytes);
+
+  const BucketTable *buckets() const { return buckets_.get(); }
+  int device() const { return device_; }
+  hipStream_t stream() const { return stream_; }
+  dg_status set_option(const std::string &k, int64_t v);
+  int64_t get_stat(const std::string &k);
+  int timings(const char **names, float *ms, int cap);
+
+ private:
+  dg_status plan_image(const uint8_t *h, size_t len, int32_t forced, ImagePlan &p);
+  int pool_huff(const HuffSpec &s);
+  int pool_quant(const uint16_t *q);
+  dg_status ensure(DevBuf &b, size_t bytes);
+  dg_status ensure_pinned(PinBuf &b, size_t bytes);
+  dg_status upload_pools();
+  dg_status launch_all(Batch &b, bool from_fix);
+  dg_status finish(Batch &b);
+
+  int device_;
+  bool has_cfg_ = false;
+  dg_image_config cfg_{};
+  std::unique_ptr<BucketTable> buckets_;
+  hipStream_t stream_ = nullptr;
+  std::mutex mu_;
+
+  std::vector<HuffTable> hpool_;
+  std::unordered_map<std::string, int> hpool_idx_;
+  std::vector<QuantTable> qpool_;
+  std::unordered_map<std::string, int> qpool_idx_;
+  size_t hpool_uploaded_ = 0, qpool_uploaded_ = 0;
+  DevBuf d_hpool_, d_qpool_;
+
+  DevBuf d_scratch_, d_meta_, d_input_;
+  PinBuf h_stage_, h_out_;
+  std::unique_ptr<Batch> cur_;
+  size_t subs_off_ = 0;
+  uint64_t next_ticket_ = 1;
+
+  uint32_t sub_bytes_ = kDefaultSubBytes;
+  bool timing_ = false;
+  std::vector<hipEvent_t> events_;
+  // stats
+  int64_t stat_batches_ = 0, stat_resync_ = 0, stat_fix_ = 0, stat_mismatch_ = 0, stat_iters_ = 0;
+  std::vector<float> last_ms_;
+};
+
+}  // namespace dg

@@ -1,0 +1,31 @@
+// kernels.h — launchers for the HIP kernels in kernels.hip (host-callable).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dg_types.h"
+
+namespace dg {
+
+// Entropy decode (one 256-thread workgroup per 256 subsequences of one image)
+void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+                      const HuffTable *pool, SubState *subs, BatchFlags *flags);
+void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+                     const HuffTable *pool, SubState *subs, BatchFlags *flags);
+// one workgroup per image
+void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs);
+void launch_huff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+                       const HuffTable *pool, const SubState *subs, BatchFlags *flags);
+// dequant + IDCT: 32 blocks of one block row per workgroup
+void launch_idct(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+                 const QuantTable *qpool);
+// upsample + colour convert: 256 x 4-pixel quads per workgroup
+void launch_color(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+// Lanczos coefficient tables: one workgroup per (image, stage)
+void launch_coeffs(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+// resize passes of one stage: 256 output pixels (H) / 4-byte units (V) per workgroup
+void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage);
+void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage);
+// final copy / gray->RGB expansion: 256 output pixels per workgroup
+void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+
+}  // namespace dg

@@ -1,0 +1,533 @@
+// kernels.hip — CDNA4 (gfx950) kernels of the decode + bucket-resize stage.
+//
+// Pipeline for one batch (all images at once, one HIP stream):
+//   k_huff_sync   entropy decode, intra-workgroup self-synchronisation
+//   k_huff_fix    cross-workgroup boundary repair (usually a no-op)
+//   k_huff_scan   per-image segmented prefix of block counts / DC predictors
+//   k_huff_write  final decode writing int16 zigzag coefficient blocks
+//   k_coeffs      Lanczos3 i16 coefficient tables (fast_image_resize semantics)
+//   k_idct        dequant + ISLOW IDCT -> component planes
+//   k_color       fancy upsampling + YCbCr->RGB -> interleaved image
+//   k_resize_h/v  separable convolution passes (R1.H, R1.V, R2.H, R2.V)
+//   k_copy        exact-size images / gray->RGB expansion
+// Everything is integer or byte work, so nothing here is MFMA-shaped; the
+// design points are wave64 occupancy for the latency-bound entropy decoder,
+// LDS-resident Huffman tables and coefficient blocks, coalesced row stores.
+#include <hip/hip_runtime.h>
+
+#include "dg_entropy.h"
+#include "dg_pixel.h"
+#include "kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace dg {
+
+// ------------------------------------------------------------------ helpers
+
+__device__ __forceinline__ void load_tables(HuffTable *tabs, const HuffTable *pool, const ImageDesc &im) {
+  const int words = (int)(sizeof(HuffTable) / 4);
+  const int ns = im.nslots;
+  for (int i = threadIdx.x; i < ns * words; i += blockDim.x) {
+    int s = i / words, w = i - s * words;
+    ((uint32_t *)&tabs[s])[w] = ((const uint32_t *)&pool[im.hslot[s]])[w];
+  }
+}
+
+// ------------------------------------------------------------ entropy decode
+
+__global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__ imgs,
+                                                   const WgItem *__restrict__ list,
+                                                   const HuffTable *__restrict__ pool,
+                                                   SubState *__restrict__ subs, BatchFlags *flags) {
+  __shared__ HuffTable tabs[kMaxSlots];
+  __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  load_tables(tabs, pool, im);
+  __syncthreads();
+  const int t = threadIdx.x;
+  const uint32_t s = it.item0 + t;
+  const bool active = s < im.nsub;
+  const uint8_t *scan = (const uint8_t *)im.scan;
+  RangeAcc acc = {0, 0, 0, {0, 0, 0}};
+  uint32_t in = pack_state(0, 0, 0);  // exact for s == 0, a guess otherwise
+  if (active) decode_range<false>(im, tabs, scan, s, in, acc, nullptr);
+  ex[t] = active ? acc.out : 0u;
+  ins[t] = in;
+  __syncthreads();
+  uint32_t iters = 0;
+  for (;;) {
+    bool redo = active && t > 0 && ins[t] != ex[t - 1];
+    uint32_t pin = redo ? ex[t - 1] : 0u;
+    __syncthreads();
+    if (redo) {
+      decode_range<false>(im, tabs, scan, s, pin, acc, nullptr);
+      ex[t] = acc.out;
+      ins[t] = pin;
+    }
+    iters++;
+    if (!__syncthreads_or(redo)) break;
+  }
+  if (active) {
+    SubState &o = subs[im.sub_base + s];
+    o.in = ins[t];
+    o.out = ex[t];
+    o.m = acc.m;
+    o.n = acc.n;
+    o.dc[0] = acc.dc[0];
+    o.dc[1] = acc.dc[1];
+    o.dc[2] = acc.dc[2];
+  }
+  if (t == 0) atomicMax(&flags->sync_iters_max, iters);
+}
+
+__global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ imgs,
+                                                  const WgItem *__restrict__ list,
+                                                  const HuffTable *__restrict__ pool,
+                                                  SubState *__restrict__ subs, BatchFlags *flags) {
+  __shared__ HuffTable tabs[kMaxSlots];
+  __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
+  const WgItem it = list[blockIdx.x];
+  if (it.item0 == 0) return;
+  const ImageDesc &im = imgs[it.image];
+  SubState *base = subs + im.sub_base;
+  const uint32_t first_in = base[it.item0 - 1].out;
+  if (base[it.item0].in == first_in) return;  // boundary already consistent (uniform branch)
+  load_tables(tabs, pool, im);
+  const int t = threadIdx.x;
+  const uint32_t s = it.item0 + t;
+  const bool active = s < im.nsub;
+  const uint8_t *scan = (const uint8_t *)im.scan;
+  const uint32_t orig_out = active ? base[s].out : 0u;
+  ex[t] = orig_out;
+  ins[t] = active ? base[s].in : 0u;
+  __syncthreads();
+  RangeAcc acc = {0, 0, 0, {0, 0, 0}};
+  bool mine = false;
+  for (;;) {
+    bool redo = active && (t == 0 ? ins[0] != first_in : ins[t] != ex[t - 1]);
+    uint32_t pin = redo ? (t == 0 ? first_in : ex[t - 1]) : 0u;
+    __syncthreads();
+    if (redo) {
+      decode_range<false>(im, tabs, scan, s, pin, acc, nullptr);
+      ex[t] = acc.out;
+      ins[t] = pin;
+      mine = true;
+    }
+    if (!__syncthreads_or(redo)) break;
+  }
+  if (active && mine) {
+    SubState &o = base[s];
+    o.in = ins[t];
+    o.out = ex[t];
+    o.m = acc.m;
+    o.n = acc.n;
+    o.dc[0] = acc.dc[0];
+    o.dc[1] = acc.dc[1];
+    o.dc[2] = acc.dc[2];
+    bool last = (t == kSubPerWg - 1) && (s + 1 < im.nsub);
+    if (last && ex[t] != orig_out) atomicAdd(&flags->chain_changed, 1u);
+  }
+  if (t == 0) atomicAdd(&flags->fix_count, 1u);
+}
+
+// segmented scan element
+struct SegAcc {
+  uint32_t m, n;
+  int32_t d0, d1, d2;
+};
+__device__ __forceinline__ SegAcc seg_combine(const SegAcc &a, const SegAcc &b) {
+  if (b.m) return SegAcc{a.m + b.m, b.n, b.d0, b.d1, b.d2};
+  return SegAcc{a.m, a.n + b.n, a.d0 + b.d0, a.d1 + b.d1, a.d2 + b.d2};
+}
+
+__global__ __launch_bounds__(256) void k_huff_scan(ImageDesc *__restrict__ imgs,
+                                                   const WgItem *__restrict__ list,
+                                                   SubState *__restrict__ subs) {
+  __shared__ SegAcc sh[kSubPerWg];
+  const WgItem it = list[blockIdx.x];
+  ImageDesc &im = imgs[it.image];
+  SubState *base = subs + im.sub_base;
+  const int t = threadIdx.x;
+  SegAcc carry = {0, 0, 0, 0, 0};
+  for (uint32_t c0 = 0; c0 < im.nsub; c0 += kSubPerWg) {
+    uint32_t i = c0 + t;
+    SegAcc v = {0, 0, 0, 0, 0};
+    if (i < im.nsub) v = SegAcc{base[i].m, base[i].n, base[i].dc[0], base[i].dc[1], base[i].dc[2]};
+    sh[t] = v;
+    __syncthreads();
+    for (int off = 1; off < kSubPerWg; off <<= 1) {
+      SegAcc prev = (t >= off) ? sh[t - off] : SegAcc{0, 0, 0, 0, 0};
+      __syncthreads();
+      if (t >= off) sh[t] = seg_combine(prev, sh[t]);
+      __syncthreads();
+    }
+    SegAcc ex = (t == 0) ? SegAcc{0, 0, 0, 0, 0} : sh[t - 1];
+    SegAcc r = seg_combine(carry, ex);
+    if (i < im.nsub) {
+      base[i].seg = r.m;
+      base[i].nin = r.n;
+      base[i].dcin[0] = r.d0;
+      base[i].dcin[1] = r.d1;
+      base[i].dcin[2] = r.d2;
+    }
+    carry = seg_combine(carry, sh[kSubPerWg - 1]);
+    __syncthreads();
+  }
+  if (t == 0) {
+    uint64_t decoded = im.blocks_per_seg ? (uint64_t)carry.m * im.blocks_per_seg + carry.n : carry.n;
+    if (decoded < im.total_blocks) im.status = 2;  // DG_ERR_CORRUPT: truncated entropy data
+  }
+}
+
+__global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict__ imgs,
+                                                    const WgItem *__restrict__ list,
+                                                    const HuffTable *__restrict__ pool,
+                                                    const SubState *__restrict__ subs, BatchFlags *flags) {
+  __shared__ HuffTable tabs[kMaxSlots];
+  __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][64];
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  load_tables(tabs, pool, im);
+  __syncthreads();
+  const int t = threadIdx.x;
+  const uint32_t s = it.item0 + t;
+  if (s >= im.nsub) return;
+  const SubState ss = subs[im.sub_base + s];
+  WriteCtx w;
+  w.blk = blk[t];
+  w.coef = (int16_t *)im.coef;
+  w.seg = ss.seg;
+  w.nin = ss.nin;
+  w.pred[0] = ss.dcin[0];
+  w.pred[1] = ss.dcin[1];
+  w.pred[2] = ss.dcin[2];
+  w.blocks_per_seg = im.blocks_per_seg;
+  w.total_blocks = im.total_blocks;
+  w.cur = -1;
+  w.zs = 0;
+  RangeAcc acc;
+  decode_range<true>(im, tabs, (const uint8_t *)im.scan, s, ss.in, acc, &w);
+  if (acc.out != ss.out) atomicAdd(&flags->write_mismatch, 1u);
+}
+
+// ------------------------------------------------------------ IDCT
+
+__global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
+                                              const QuantTable *__restrict__ qpool) {
+  constexpr int LD = 65;  // padded block stride (dwords): breaks the 64-dword bank period
+  __shared__ int32_t blkv[32 * LD];
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  // item -> (component, block row, chunk of 32 blocks)
+  uint32_t item = it.item0, c = 0;
+  for (; c < im.ncomp; c++) {
+    uint32_t ck = (im.cbw[c] + 31) / 32;
+    uint32_t n = im.cbh[c] * ck;
+    if (item < n) break;
+    item -= n;
+  }
+  const uint32_t ck = (im.cbw[c] + 31) / 32;
+  const uint32_t by = item / ck, chunk = item - by * ck;
+  const int t = threadIdx.x, slot = t >> 3, lane = t & 7;
+  const uint32_t bx = chunk * 32 + slot;
+  const bool valid = bx < im.cbw[c];
+  const uint16_t *q = qpool[im.qpool[c]].q;
+  int32_t *bv = blkv + slot * LD;
+  if (valid) {
+    uint32_t b;
+    if (im.ncomp == 1) {
+      b = by * im.cbw[0] + bx;
+    } else {
+      uint32_t my = by / im.cv[c], vy = by - my * im.cv[c];
+      uint32_t mx = bx / im.ch[c], hx = bx - mx * im.ch[c];
+      b = (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * im.ch[c] + hx;
+    }
+    const int16_t *src = (const int16_t *)im.coef + (size_t)b * 64 + lane * 8;
+    uint4 raw = *(const uint4 *)src;
+    int16_t v[8];
+    __builtin_memcpy(v, &raw, 16);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      int n = kZigzagToNatural[lane * 8 + i];
+      bv[n] = (int32_t)v[i] * (int32_t)q[n];
+    }
+  }
+  __syncthreads();
+  int32_t o[8];
+  if (valid) {  // pass 1: column `lane`
+    idct_1d(bv[0 * 8 + lane], bv[1 * 8 + lane], bv[2 * 8 + lane], bv[3 * 8 + lane], bv[4 * 8 + lane],
+            bv[5 * 8 + lane], bv[6 * 8 + lane], bv[7 * 8 + lane], o);
+  }
+  __syncthreads();
+  if (valid) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) bv[r * 8 + lane] = descale(o[r], kConstBits - kPass1Bits);
+  }
+  __syncthreads();
+  if (valid) {  // pass 2: row `lane`
+    const int32_t *w = bv + lane * 8;
+    idct_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      lo |= (uint32_t)idct_out(o[i]) << (8 * i);
+      hi |= (uint32_t)idct_out(o[i + 4]) << (8 * i);
+    }
+    uint8_t *dst = (uint8_t *)im.plane[c] + (size_t)(by * 8 + lane) * (im.cbw[c] * 8) + bx * 8;
+    *(uint2 *)dst = make_uint2(lo, hi);
+  }
+}
+
+// ------------------------------------------------------------ colour
+
+__global__ __launch_bounds__(256) void k_color(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  const uint32_t qw = (im.width + 3) / 4;
+  const uint32_t q = it.item0 + threadIdx.x;
+  if (q >= qw * im.height) return;
+  const uint32_t y = q / qw, x0 = (q - y * qw) * 4;
+  const uint8_t *p0 = (const uint8_t *)im.plane[0];
+  const uint8_t *p1 = (const uint8_t *)im.plane[1];
+  const uint8_t *p2 = (const uint8_t *)im.plane[2];
+  const uint32_t s0 = im.cbw[0] * 8, s1 = im.cbw[1] * 8, s2 = im.cbw[2] * 8;
+  const uint32_t hr1 = im.hmax / im.ch[1], vr1 = im.vmax / im.cv[1];
+  const uint32_t hr2 = im.hmax / im.ch[2], vr2 = im.vmax / im.cv[2];
+  const uint32_t hr0 = im.hmax / im.ch[0], vr0 = im.vmax / im.cv[0];
+  uint8_t px[12];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t x = x0 + k;
+    if (x >= im.width) x = im.width - 1;
+    uint32_t Y = upsample_at(p0, s0, hr0, vr0, im.cdsw[0], im.cdsh[0], x, y);
+    uint32_t cb = upsample_at(p1, s1, hr1, vr1, im.cdsw[1], im.cdsh[1], x, y);
+    uint32_t cr = upsample_at(p2, s2, hr2, vr2, im.cdsw[2], im.cdsh[2], x, y);
+    if (im.colorspace == CS_RGB) {
+      px[3 * k] = (uint8_t)Y;
+      px[3 * k + 1] = (uint8_t)cb;
+      px[3 * k + 2] = (uint8_t)cr;
+    } else {
+      ycc_to_rgb((int32_t)Y, (int32_t)cb, (int32_t)cr, px[3 * k], px[3 * k + 1], px[3 * k + 2]);
+    }
+  }
+  uint8_t *dst = (uint8_t *)im.pix + (size_t)y * im.pix_stride + x0 * 3;
+  if (x0 + 4 <= im.width) {
+    uint32_t w[3];
+    __builtin_memcpy(w, px, 12);
+    uint32_t *d = (uint32_t *)dst;  // x0*3 is a multiple of 12, pix_stride of 16
+    d[0] = w[0];
+    d[1] = w[1];
+    d[2] = w[2];
+  } else {
+    uint32_t n = (im.width - x0) * 3;
+    for (uint32_t i = 0; i < n; i++) dst[i] = px[i];
+  }
+}
+
+// ------------------------------------------------------------ resize
+
+__global__ __launch_bounds__(256) void k_coeffs(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
+  __shared__ double red[256];
+  const WgItem it = list[blockIdx.x];
+  ResizePass &ps = imgs[it.image].pass[it.item0];
+  const int t = threadIdx.x;
+  const double in0 = ps.in0, in1 = ps.in1;
+  const uint32_t out_size = ps.out_size, in_size = ps.in_size, ksize = ps.ksize;
+  const double scale = (in1 - in0) / (double)out_size;
+  const double filter_scale = scale > 1.0 ? scale : 1.0;
+  const double support = 3.0 * filter_scale;
+  const double recip = 1.0 / filter_scale;
+  int2 *bounds = (int2 *)ps.bounds;
+  int16_t *coef = (int16_t *)ps.coef;
+  double maxw = 0.0;
+  for (uint32_t o = t; o < out_size; o += 256) {
+    // fast_image_resize precompute_coefficients for output o (see fir_weights)
+    double center = in0 + ((double)o + 0.5) * scale;
+    double fl = floor(center - support), cl = ceil(center + support);
+    int32_t xmin = fl < 0.0 ? 0 : (int32_t)fl;
+    int32_t xmax = cl > (double)in_size ? (int32_t)in_size : (int32_t)cl;
+    double c = center - 0.5, ww = 0.0;
+    int32_t first = -1, last = -1;
+    for (int32_t x = xmin; x < xmax; x++) {
+      double v = lanczos3(((double)x - c) * recip);
+      if (v != 0.0) {
+        if (first < 0) first = x;
+        last = x;
+      }
+      ww += v;
+    }
+    int32_t st = first < 0 ? xmax : first;
+    int32_t n = first < 0 ? 0 : last - first + 1;
+    bounds[o] = make_int2(st, n);
+    for (int32_t i = 0; i < n; i++) {
+      double v = lanczos3(((double)(st + i) - c) * recip);
+      if (ww != 0.0) v /= ww;
+      if (v > maxw) maxw = v;
+    }
+  }
+  red[t] = maxw;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) red[t] = red[t] > red[t + off] ? red[t] : red[t + off];
+    __syncthreads();
+  }
+  const int32_t precision = fir_precision(red[0]);
+  if (t == 0) ps.precision = precision;
+  for (uint32_t o = t; o < out_size; o += 256) {
+    double center = in0 + ((double)o + 0.5) * scale;
+    double fl = floor(center - support), cl = ceil(center + support);
+    int32_t xmin = fl < 0.0 ? 0 : (int32_t)fl;
+    int32_t xmax = cl > (double)in_size ? (int32_t)in_size : (int32_t)cl;
+    double c = center - 0.5, ww = 0.0;
+    for (int32_t x = xmin; x < xmax; x++) ww += lanczos3(((double)x - c) * recip);
+    int2 bd = bounds[o];
+    int16_t *k = coef + (size_t)o * ksize;
+    for (int32_t i = 0; i < bd.y; i++) {
+      double v = lanczos3(((double)(bd.x + i) - c) * recip);
+      if (ww != 0.0) v /= ww;
+      k[i] = fir_quant(v, precision);
+    }
+  }
+}
+
+__device__ __forceinline__ uint8_t clip_shift(int32_t acc, int32_t prec) {
+  int32_t v = acc >> prec;
+  return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+__global__ __launch_bounds__(256) void k_resize_h(const ImageDesc *__restrict__ imgs,
+                                                  const WgItem *__restrict__ list, int stage) {
+  const WgItem it = list[blockIdx.x];
+  const ResizePass &ps = imgs[it.image].pass[stage];
+  const uint32_t idx = it.item0 + threadIdx.x;
+  if (idx >= ps.width * ps.rows) return;
+  const uint32_t y = idx / ps.width, x = idx - y * ps.width;
+  const int2 bd = ((const int2 *)ps.bounds)[x];
+  const int16_t *k = (const int16_t *)ps.coef + (size_t)x * ps.ksize;
+  const uint8_t *src = (const uint8_t *)ps.src + (size_t)(ps.row0 + y) * ps.src_stride;
+  uint8_t *dst = (uint8_t *)ps.dst + (size_t)y * ps.dst_stride + (size_t)x * ps.C;
+  const int32_t prec = ps.precision, bias = 1 << (prec - 1);
+  if (ps.C == 3) {
+    int32_t a0 = bias, a1 = bias, a2 = bias;
+    const uint8_t *s = src + (size_t)bd.x * 3;
+    for (int32_t i = 0; i < bd.y; i++) {
+      int32_t w = k[i];
+      a0 += (int32_t)s[3 * i] * w;
+      a1 += (int32_t)s[3 * i + 1] * w;
+      a2 += (int32_t)s[3 * i + 2] * w;
+    }
+    dst[0] = clip_shift(a0, prec);
+    dst[1] = clip_shift(a1, prec);
+    dst[2] = clip_shift(a2, prec);
+  } else {
+    for (uint32_t ch = 0; ch < ps.C; ch++) {
+      int32_t a = bias;
+      const uint8_t *s = src + (size_t)bd.x * ps.C + ch;
+      for (int32_t i = 0; i < bd.y; i++) a += (int32_t)s[(size_t)i * ps.C] * (int32_t)k[i];
+      dst[ch] = clip_shift(a, prec);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ imgs,
+                                                  const WgItem *__restrict__ list, int stage) {
+  const WgItem it = list[blockIdx.x];
+  const ResizePass &ps = imgs[it.image].pass[stage];
+  const uint32_t rowbytes = ps.width * ps.C;
+  const uint32_t units = (rowbytes + 3) / 4;
+  const uint32_t idx = it.item0 + threadIdx.x;
+  if (idx >= units * ps.rows) return;
+  const uint32_t y = idx / units, u = idx - y * units;
+  const uint32_t b0 = u * 4;
+  const uint32_t nb = rowbytes - b0 < 4 ? rowbytes - b0 : 4;
+  const int2 bd = ((const int2 *)ps.bounds)[y];
+  const int16_t *k = (const int16_t *)ps.coef + (size_t)y * ps.ksize;
+  const int32_t prec = ps.precision, bias = 1 << (prec - 1);
+  int32_t a0 = bias, a1 = bias, a2 = bias, a3 = bias;
+  const uint8_t *src = (const uint8_t *)ps.src + (size_t)(bd.x - (int32_t)ps.row0) * ps.src_stride + b0;
+  const bool aligned = ((ps.src_stride & 3) == 0) && nb == 4;
+  for (int32_t i = 0; i < bd.y; i++) {
+    int32_t w = k[i];
+    const uint8_t *s = src + (size_t)i * ps.src_stride;
+    if (aligned) {
+      uint32_t v = *(const uint32_t *)s;
+      a0 += (int32_t)(v & 0xFF) * w;
+      a1 += (int32_t)((v >> 8) & 0xFF) * w;
+      a2 += (int32_t)((v >> 16) & 0xFF) * w;
+      a3 += (int32_t)(v >> 24) * w;
+    } else {
+      a0 += (int32_t)s[0] * w;
+      if (nb > 1) a1 += (int32_t)s[1] * w;
+      if (nb > 2) a2 += (int32_t)s[2] * w;
+      if (nb > 3) a3 += (int32_t)s[3] * w;
+    }
+  }
+  uint8_t *dst = (uint8_t *)ps.dst + (size_t)y * ps.dst_stride + b0;
+  uint32_t o = (uint32_t)clip_shift(a0, prec) | ((uint32_t)clip_shift(a1, prec) << 8) |
+               ((uint32_t)clip_shift(a2, prec) << 16) | ((uint32_t)clip_shift(a3, prec) << 24);
+  if (nb == 4 && ((ps.dst_stride & 3) == 0)) {
+    *(uint32_t *)dst = o;
+  } else {
+    for (uint32_t i = 0; i < nb; i++) dst[i] = (uint8_t)(o >> (8 * i));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_copy(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  const uint32_t idx = it.item0 + threadIdx.x;
+  if (idx >= im.out_w * im.out_h) return;
+  const uint32_t y = idx / im.out_w, x = idx - y * im.out_w;
+  const uint8_t *s = (const uint8_t *)im.final_src + (size_t)y * im.final_src_stride + (size_t)x * im.final_src_c;
+  uint8_t *d = (uint8_t *)im.out + (size_t)y * im.out_stride + (size_t)x * im.out_c;
+  if (im.final_src_c == im.out_c) {
+    for (uint32_t c = 0; c < im.out_c; c++) d[c] = s[c];
+  } else {  // L8 -> RGB8 (image::DynamicImage::to_rgb8 replicates luma)
+    d[0] = d[1] = d[2] = s[0];
+  }
+}
+
+// ------------------------------------------------------------ launchers
+
+#define DG_LAUNCH(kern, nwg, st, ...)                                              \
+  do {                                                                            \
+    if (nwg) hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), 0, st, __VA_ARGS__); \
+  } while (0)
+
+void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+                      const HuffTable *pool, SubState *subs, BatchFlags *flags) {
+  DG_LAUNCH(k_huff_sync, nwg, st, imgs, list, pool, subs, flags);
+}
+void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+                     const HuffTable *pool, SubState *subs, BatchFlags *flags) {
+  DG_LAUNCH(k_huff_fix, nwg, st, imgs, list, pool, subs, flags);
+}
+void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs) {
+  DG_LAUNCH(k_huff_scan, nwg, st, imgs, list, subs);
+}
+void launch_huff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+                       const HuffTable *pool, const SubState *subs, BatchFlags *flags) {
+  DG_LAUNCH(k_huff_write, nwg, st, imgs, list, pool, subs, flags);
+}
+void launch_idct(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, const QuantTable *qpool) {
+  DG_LAUNCH(k_idct, nwg, st, imgs, list, qpool);
+}
+void launch_color(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
+  DG_LAUNCH(k_color, nwg, st, imgs, list);
+}
+void launch_coeffs(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
+  DG_LAUNCH(k_coeffs, nwg, st, imgs, list);
+}
+void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
+  DG_LAUNCH(k_resize_h, nwg, st, imgs, list, stage);
+}
+void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
+  DG_LAUNCH(k_resize_v, nwg, st, imgs, list, stage);
+}
+void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
+  DG_LAUNCH(k_copy, nwg, st, imgs, list);
+}
+
+}  // namespace dg

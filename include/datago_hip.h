@@ -1,0 +1,186 @@
+/*
+ * datago_hip.h — C ABI of the MI355X decode + aspect-ratio-bucket resize stage.
+ *
+ * Drop-in boundary for datago's CPU hot path.  The Rust workers call these
+ * entry points at the places where the reference decodes and transforms a
+ * sample (see INTEGRATION.md for the Rust `extern "C"` block):
+ *
+ *   reference (Rust, /root/reference/src)                   replaced by
+ *   -----------------------------------------------------   ---------------------------------
+ *   ImageTransformConfig::get_ar_aware_transform             dg_bucket_table_build
+ *       image_processing.rs:77-121 (+ build_image_size_list :188-219)
+ *   aspect_ratio_to_str            image_processing.rs:130-133   dg_bucket_key / dg_aspect_ratio_to_str
+ *   ARAwareTransform::get_closest_aspect_ratio  :222-252      dg_closest_bucket
+ *   aspect_ratio_to_size.get(key)  :264, panic :334-336       dg_bucket_find_key (-1 = not found)
+ *   ImageReader::with_guessed_format (header sniff)
+ *       worker_files.rs:14-16                                dg_probe
+ *   image_from_path + image_to_payload
+ *       worker_files.rs:8-30, image_processing.rs:341-431    dg_decode_one (sync)
+ *   image::load_from_memory + image_to_payload (per member)
+ *       worker_wds.rs:45-66, worker_http.rs:64,129-137       dg_submit / dg_wait (batched)
+ *   ImagePayload {data, original_*, height, width, channels, bit_depth, is_encoded}
+ *       structs.rs:52-71                                     dg_payload_meta (+ caller-owned data buffer)
+ *   ImageError -> sample dropped (worker_files.rs:63-70)     DG_ERR_CORRUPT
+ *   panic!/assert! (Cargo.toml:54 panic="abort")             DG_ERR_BAD_BUCKET / DG_ERR_INVALID (never abort)
+ *
+ * Conventions: every function returns a dg_status (0 = OK) unless stated;
+ * plain pointers and sizes only; the caller owns every buffer it passes;
+ * dg_last_error() returns a thread-local message for the last failure on the
+ * calling thread.  All entry points are reentrant; one dg_ctx may be shared
+ * by many host threads (submissions are serialised on its HIP stream).
+ */
+#ifndef DATAGO_HIP_H
+#define DATAGO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DG_ABI_VERSION 1
+
+typedef enum dg_status {
+  DG_OK = 0,
+  DG_ERR_UNSUPPORTED = 1, /* valid image the GPU path does not decode (progressive,
+                             arithmetic, 12-bit, CMYK, non-JPEG...): caller keeps its CPU path */
+  DG_ERR_CORRUPT = 2,     /* maps to image::ImageError::Decoding: drop the sample */
+  DG_ERR_OOM = 3,         /* device or host allocation failed */
+  DG_ERR_BAD_BUCKET = 4,  /* forced aspect-ratio key/index not in the table (the reference panics) */
+  DG_ERR_INVALID = 5,     /* invalid argument / config (the reference asserts) */
+  DG_ERR_SMALL_BUFFER = 6,/* caller's output buffer is too small; meta holds the size needed */
+  DG_ERR_DEVICE = 7,      /* HIP runtime error */
+  DG_ERR_NOT_READY = 8    /* dg_poll: batch still running */
+} dg_status;
+
+/* Image formats reported by dg_probe. */
+enum { DG_FMT_UNKNOWN = 0, DG_FMT_JPEG = 1, DG_FMT_PNG = 2 };
+
+/* Mirrors ImageTransformConfig (image_processing.rs:43-70) + ImageEncoding (:24-30). */
+typedef struct dg_image_config {
+  int32_t crop_and_resize;      /* required true when an image_config is given */
+  uint32_t default_image_size;  /* e.g. 1024 */
+  uint32_t downsampling_ratio;  /* e.g. 32 */
+  double min_aspect_ratio;      /* e.g. 0.5 */
+  double max_aspect_ratio;      /* e.g. 2.0 */
+  int32_t pre_encode_images;    /* not yet supported on the GPU path: DG_ERR_UNSUPPORTED */
+  int32_t image_to_rgb8;        /* gray -> RGB expansion after resize (:367-372) */
+  int32_t encode_format;        /* 0 = PNG, 1 = JPEG (EncodeFormat, :16-22) */
+  int32_t jpeg_quality;         /* default 92 (:14) */
+} dg_image_config;
+
+/* ------------------------------------------------------------ buckets */
+
+typedef struct dg_bucket_table dg_bucket_table;
+
+/* ImageTransformConfig::get_ar_aware_transform: builds the bucket list, the
+ * "%.3f" key -> (w,h) map (last insert wins) and the keys sorted by value. */
+dg_status dg_bucket_table_build(uint32_t default_image_size, uint32_t downsampling_ratio,
+                                double min_aspect_ratio, double max_aspect_ratio,
+                                dg_bucket_table **out);
+void dg_bucket_table_free(dg_bucket_table *t);
+/* Number of distinct keys (buckets), sorted ascending by aspect ratio. */
+int32_t dg_bucket_count(const dg_bucket_table *t);
+/* Bucket i: width, height and its "%.3f" key (key buffer >= 16 bytes). */
+dg_status dg_bucket_get(const dg_bucket_table *t, int32_t i, uint32_t *w, uint32_t *h, char *key,
+                        size_t key_cap);
+/* get_closest_aspect_ratio(width, height) -> bucket index (ties go right). */
+int32_t dg_closest_bucket(const dg_bucket_table *t, int32_t width, int32_t height);
+/* aspect_ratio_to_size lookup by key string; -1 if absent. */
+int32_t dg_bucket_find_key(const dg_bucket_table *t, const char *key);
+/* aspect_ratio_to_str((w,h)) -> "%.3f" of w/h (buffer >= 32 bytes). */
+dg_status dg_aspect_ratio_to_str(uint32_t w, uint32_t h, char *out, size_t cap);
+
+/* ------------------------------------------------------------ probe */
+
+typedef struct dg_probe_info {
+  int32_t format;         /* DG_FMT_* */
+  uint32_t width, height;
+  int32_t components;     /* 1 (L8) or 3 (RGB8) for JPEG */
+  int32_t bit_depth;      /* bits per channel (8) */
+  int32_t h_samp[4], v_samp[4];
+  int32_t progressive, arithmetic, precision, restart_interval;
+  int32_t gpu_supported;  /* 1 if dg_submit would decode it on the GPU */
+} dg_probe_info;
+
+/* Header-only: lets the caller compute the bucket and size the output before
+ * any GPU work.  Returns DG_ERR_CORRUPT for unparseable data. */
+dg_status dg_probe(const uint8_t *bytes, size_t len, dg_probe_info *out);
+
+/* ------------------------------------------------------------ context */
+
+typedef struct dg_ctx dg_ctx;
+
+/* device: HIP device ordinal (rank -> device).  cfg may be NULL (no resize:
+ * image_config absent -> decode only, like img_tfm = None). */
+dg_status dg_ctx_create(int32_t device, const dg_image_config *cfg, dg_ctx **out);
+void dg_ctx_destroy(dg_ctx *ctx);
+const dg_bucket_table *dg_ctx_buckets(const dg_ctx *ctx);
+
+/* Output metadata, mirrors ImagePayload (structs.rs:52-71).  channels and
+ * bit_depth are the decoded image's (pre-transform, image_processing.rs:347-351)
+ * unless image_to_rgb8 converted it (then 3 / 8). */
+typedef struct dg_payload_meta {
+  uint32_t original_width, original_height;
+  uint32_t width, height;
+  int32_t channels;       /* -1 when encoded */
+  int32_t bit_depth;
+  int32_t is_encoded;
+  int32_t status;         /* dg_status of this image */
+  int32_t bucket;         /* bucket index used, -1 without transform */
+  uint64_t nbytes;        /* bytes written (or needed) in the output buffer */
+} dg_payload_meta;
+
+/* Bytes needed for image `bytes` (after probe + bucket choice). */
+dg_status dg_output_size(dg_ctx *ctx, const uint8_t *bytes, size_t len, int32_t forced_bucket,
+                         uint64_t *nbytes);
+
+/* Batched decode + transform from HOST memory to HOST memory (the path the
+ * Rust workers take).  forced_bucket[i] = -1 selects the closest bucket
+ * (aspect_ratio "" in image_to_payload), otherwise that bucket index is used
+ * (the WebDataset / DB alignment of worker_wds.rs:68-76).  forced_bucket may
+ * be NULL.  outs[i] must hold out_caps[i] bytes.  Inputs are copied before
+ * return; outputs and metas are valid after dg_wait(ticket). */
+dg_status dg_submit(dg_ctx *ctx, int32_t n, const uint8_t *const *srcs, const size_t *lens,
+                    const int32_t *forced_bucket, uint8_t *const *outs, const uint64_t *out_caps,
+                    dg_payload_meta *metas, uint64_t *ticket);
+dg_status dg_wait(dg_ctx *ctx, uint64_t ticket);
+dg_status dg_poll(dg_ctx *ctx, uint64_t ticket);
+
+/* Synchronous single-image convenience (image_payload_from_path equivalent). */
+dg_status dg_decode_one(dg_ctx *ctx, const uint8_t *src, size_t len, int32_t forced_bucket,
+                        uint8_t *out, uint64_t out_cap, dg_payload_meta *meta);
+
+/* Device-resident batch: coded bytes already in HBM (d_srcs[i], device
+ * pointers); h_srcs[i] is a host copy the header parser reads (only the bytes
+ * up to the start of scan are touched).  Outputs are written to device
+ * pointers d_outs[i] (capacity out_caps[i]).  Asynchronous on the context's
+ * stream; dg_wait(ticket) completes it. */
+dg_status dg_submit_device(dg_ctx *ctx, int32_t n, const uint8_t *const *h_srcs,
+                           const uint8_t *const *d_srcs, const size_t *lens,
+                           const int32_t *forced_bucket, uint8_t *const *d_outs,
+                           const uint64_t *out_caps, dg_payload_meta *metas, uint64_t *ticket);
+
+/* Device memory helpers for callers without a GPU runtime of their own. */
+dg_status dg_device_alloc(dg_ctx *ctx, size_t bytes, void **dptr);
+dg_status dg_device_free(dg_ctx *ctx, void *dptr);
+dg_status dg_memcpy_h2d(dg_ctx *ctx, void *dst, const void *src, size_t bytes);
+dg_status dg_memcpy_d2h(dg_ctx *ctx, void *dst, const void *src, size_t bytes);
+dg_status dg_synchronize(dg_ctx *ctx);
+
+/* Per-kernel timing of the last completed batch (HIP events on the context's
+ * stream).  names[i] points to static strings; returns the number of stages. */
+int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_t cap);
+
+/* Tuning knobs (testing): subsequence size in bytes for the entropy decoder. */
+dg_status dg_ctx_set_option(dg_ctx *ctx, const char *key, int64_t value);
+int64_t dg_ctx_get_stat(dg_ctx *ctx, const char *key);
+
+const char *dg_last_error(void);
+int32_t dg_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DATAGO_HIP_H */

@@ -1,0 +1,175 @@
+// CPU emulation of the GPU entropy-decoding pipeline (test infrastructure).
+// Runs the product's own dg_entropy.h decode_range() with the exact phase
+// structure of k_huff_sync / k_huff_fix / k_huff_scan / k_huff_write
+// (sequential over the threads of a workgroup, same read-then-write
+// iteration semantics), so the parallel algorithm's logic can be checked
+// against the oracle without a GPU.
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "dg_entropy.h"
+#include "host/jpeg_header.h"
+
+using namespace dg;
+
+extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bytes, int16_t *out,
+                                size_t cap_blocks, size_t *nblocks, int64_t *stats) {
+  JpegHeader h;
+  parse_jpeg_header(data, len, h);
+  if (h.status != JH_OK) return h.status;
+  ImageDesc d;
+  memset(&d, 0, sizeof(d));
+  const uint32_t W = h.width, H = h.height;
+  d.ncomp = (uint8_t)h.ncomp;
+  d.hmax = h.hmax;
+  d.vmax = h.vmax;
+  d.mcux = (W + 8 * d.hmax - 1) / (8 * d.hmax);
+  d.mcuy = (H + 8 * d.vmax - 1) / (8 * d.vmax);
+  uint32_t bpm = 0, cbw0 = 0, cbh0 = 0;
+  for (int c = 0; c < h.ncomp; c++) {
+    if (h.ncomp == 1) {
+      uint32_t dsw = (W * h.comp[c].h + d.hmax - 1) / d.hmax, dsh = (H * h.comp[c].v + d.vmax - 1) / d.vmax;
+      cbw0 = (dsw + 7) / 8;
+      cbh0 = (dsh + 7) / 8;
+      d.blk_comp[0] = 0;
+      bpm = 1;
+    } else {
+      for (int j = 0; j < h.comp[c].h * h.comp[c].v; j++) d.blk_comp[bpm + j] = (uint8_t)c;
+      bpm += h.comp[c].h * h.comp[c].v;
+    }
+  }
+  d.bpm = bpm;
+  d.total_blocks = h.ncomp == 1 ? cbw0 * cbh0 : d.mcux * d.mcuy * bpm;
+  d.restart = h.restart;
+  d.blocks_per_seg = d.restart * bpm;
+  std::vector<HuffTable> tabs;
+  for (int c = 0; c < h.ncomp; c++) {
+    HuffTable t;
+    build_huff_table(h.dc[h.comp[c].td], t);
+    d.dc_slot[c] = (uint8_t)tabs.size();
+    tabs.push_back(t);
+    build_huff_table(h.ac[h.comp[c].ta], t);
+    d.ac_slot[c] = (uint8_t)tabs.size();
+    tabs.push_back(t);
+  }
+  d.scan_len = (uint32_t)(h.scan_end - h.scan_off);
+  d.sub_bytes = sub_bytes;
+  d.nsub = d.scan_len ? (d.scan_len + sub_bytes - 1) / sub_bytes : 1;
+  const uint8_t *scan = data + h.scan_off;
+  std::vector<SubState> subs(d.nsub);
+  const uint32_t NW = (d.nsub + kSubPerWg - 1) / kSubPerWg;
+  int64_t redo_total = 0, iters_max = 0, fix_wgs = 0, rounds = 0;
+  // ---- k_huff_sync
+  for (uint32_t wg = 0; wg < NW; wg++) {
+    uint32_t s0 = wg * kSubPerWg;
+    uint32_t n = d.nsub - s0 < (uint32_t)kSubPerWg ? d.nsub - s0 : kSubPerWg;
+    std::vector<uint32_t> ex(n), ins(n);
+    std::vector<RangeAcc> acc(n);
+    for (uint32_t t = 0; t < n; t++) {
+      ins[t] = pack_state(0, 0, 0);
+      decode_range<false>(d, tabs.data(), scan, s0 + t, ins[t], acc[t], nullptr);
+      ex[t] = acc[t].out;
+    }
+    int64_t it = 0;
+    for (;;) {
+      std::vector<uint32_t> pin(n, 0);
+      std::vector<char> redo(n, 0);
+      bool any = false;
+      for (uint32_t t = 1; t < n; t++)
+        if (ins[t] != ex[t - 1]) { redo[t] = 1; pin[t] = ex[t - 1]; any = true; }
+      for (uint32_t t = 1; t < n; t++)
+        if (redo[t]) {
+          decode_range<false>(d, tabs.data(), scan, s0 + t, pin[t], acc[t], nullptr);
+          ex[t] = acc[t].out;
+          ins[t] = pin[t];
+          redo_total++;
+        }
+      it++;
+      if (!any) break;
+    }
+    if (it > iters_max) iters_max = it;
+    for (uint32_t t = 0; t < n; t++) {
+      SubState &o = subs[s0 + t];
+      o.in = ins[t]; o.out = ex[t]; o.m = acc[t].m; o.n = acc[t].n;
+      o.dc[0] = acc[t].dc[0]; o.dc[1] = acc[t].dc[1]; o.dc[2] = acc[t].dc[2];
+    }
+  }
+  // ---- k_huff_fix until no workgroup's last exit changes
+  for (;;) {
+    rounds++;
+    bool chain = false;
+    std::vector<SubState> snap = subs;  // all workgroups read the launch-start values
+    for (uint32_t wg = 1; wg < NW; wg++) {
+      uint32_t s0 = wg * kSubPerWg;
+      uint32_t n = d.nsub - s0 < (uint32_t)kSubPerWg ? d.nsub - s0 : kSubPerWg;
+      uint32_t first_in = snap[s0 - 1].out;
+      if (subs[s0].in == first_in) continue;
+      fix_wgs++;
+      std::vector<uint32_t> ex(n), ins(n);
+      std::vector<RangeAcc> acc(n);
+      std::vector<char> mine(n, 0);
+      for (uint32_t t = 0; t < n; t++) { ex[t] = subs[s0 + t].out; ins[t] = subs[s0 + t].in; }
+      uint32_t orig_last = ex[n - 1];
+      for (;;) {
+        std::vector<uint32_t> pin(n, 0);
+        std::vector<char> redo(n, 0);
+        bool any = false;
+        for (uint32_t t = 0; t < n; t++) {
+          uint32_t want = t == 0 ? first_in : ex[t - 1];
+          if (ins[t] != want) { redo[t] = 1; pin[t] = want; any = true; }
+        }
+        for (uint32_t t = 0; t < n; t++)
+          if (redo[t]) {
+            decode_range<false>(d, tabs.data(), scan, s0 + t, pin[t], acc[t], nullptr);
+            ex[t] = acc[t].out; ins[t] = pin[t]; mine[t] = 1; redo_total++;
+          }
+        if (!any) break;
+      }
+      for (uint32_t t = 0; t < n; t++)
+        if (mine[t]) {
+          SubState &o = subs[s0 + t];
+          o.in = ins[t]; o.out = ex[t]; o.m = acc[t].m; o.n = acc[t].n;
+          o.dc[0] = acc[t].dc[0]; o.dc[1] = acc[t].dc[1]; o.dc[2] = acc[t].dc[2];
+        }
+      if (n == (uint32_t)kSubPerWg && s0 + n < d.nsub && ex[n - 1] != orig_last) chain = true;
+    }
+    if (!chain || rounds > 64) break;
+  }
+  // ---- k_huff_scan (segmented exclusive scan)
+  uint32_t cm = 0, cn = 0;
+  int32_t cd[3] = {0, 0, 0};
+  for (uint32_t i = 0; i < d.nsub; i++) {
+    subs[i].seg = cm; subs[i].nin = cn;
+    subs[i].dcin[0] = cd[0]; subs[i].dcin[1] = cd[1]; subs[i].dcin[2] = cd[2];
+    if (subs[i].m) { cm += subs[i].m; cn = subs[i].n; for (int c = 0; c < 3; c++) cd[c] = subs[i].dc[c]; }
+    else { cn += subs[i].n; for (int c = 0; c < 3; c++) cd[c] += subs[i].dc[c]; }
+  }
+  uint64_t decoded = d.blocks_per_seg ? (uint64_t)cm * d.blocks_per_seg + cn : cn;
+  // ---- k_huff_write
+  std::vector<int16_t> coef((size_t)d.total_blocks * 64, (int16_t)0x7777);  // poison: every slot must be written
+  int64_t mismatch = 0;
+  int16_t blk[64];
+  for (uint32_t s = 0; s < d.nsub; s++) {
+    WriteCtx w;
+    w.blk = blk; w.coef = coef.data(); w.seg = subs[s].seg; w.nin = subs[s].nin;
+    for (int c = 0; c < 3; c++) w.pred[c] = subs[s].dcin[c];
+    w.blocks_per_seg = d.blocks_per_seg; w.total_blocks = d.total_blocks; w.cur = -1; w.zs = 0;
+    RangeAcc acc;
+    decode_range<true>(d, tabs.data(), scan, s, subs[s].in, acc, &w);
+    if (acc.out != subs[s].out) mismatch++;
+  }
+  // zigzag -> natural
+  static const int nat[64] = {0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48,
+                              41, 34, 27, 20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+                              30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+  *nblocks = d.total_blocks;
+  for (size_t b = 0; b < d.total_blocks && b < cap_blocks; b++)
+    for (int k = 0; k < 64; k++) out[b * 64 + nat[k]] = coef[b * 64 + k];
+  if (stats) {
+    stats[0] = d.nsub; stats[1] = redo_total; stats[2] = iters_max; stats[3] = fix_wgs;
+    stats[4] = rounds; stats[5] = mismatch; stats[6] = (int64_t)decoded; stats[7] = d.total_blocks;
+  }
+  return 0;
+}

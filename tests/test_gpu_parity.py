@@ -1,0 +1,221 @@
+"""GPU parity: the HIP path (through the C ABI) vs the oracle, bit-exact.
+
+Decode: libjpeg-turbo semantics (oracle pinned against PIL).  Resize: the
+oracle's MODE_FIR restatement of fast_image_resize (tolerance 0: the kernels
+use the same f64 coefficient math and i16 quantisation).  Sizes are small
+enough for the scalar oracle to finish in seconds.
+"""
+import hashlib
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from datago_amd import synth
+from oracle import buckets as B
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+
+def _lib():
+    from datago_amd import _lib as L
+    return L
+
+
+@pytest.fixture(scope="module")
+def ctx_dec():
+    return _lib().Context(0)
+
+
+@pytest.fixture(scope="module")
+def ctx512():
+    return _lib().Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+                          min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+
+
+@pytest.fixture(scope="module")
+def ctx1024():
+    return _lib().Context(0, crop_and_resize=True, default_image_size=1024, downsampling_ratio=32,
+                          min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+
+
+def _golden_files():
+    with open(os.path.join(GOLD, "jpeg_expected.json")) as f:
+        names = sorted(json.load(f).keys())
+    return [(n, open(os.path.join(GOLD, "jpeg", n + ".jpg"), "rb").read()) for n in names]
+
+
+def _oracle_resized(data, tw, th):
+    st, dec = O.jpeg_decode(data)
+    assert st == 0
+    return O.crop_and_resize(dec, tw, th, O.MODE_FIR)
+
+
+def _rand_jpegs(seed, n, maxdim=700, rst=False):
+    out = []
+    for i in range(n):
+        rng = np.random.default_rng(seed * 1000 + i)
+        w, h = int(rng.integers(1, maxdim)), int(rng.integers(1, maxdim))
+        ss = ["4:2:0", "4:2:2", "4:4:4"][i % 3]
+        r = ([0, 1, 2][i % 3] if rst else 0)
+        out.append(synth.encode_jpeg(synth.synth_pixels(rng, w, h, i % 9 == 4), int(rng.integers(40, 101)), ss,
+                                     restart_marker_rows=r))
+    return out
+
+
+def test_decode_only_golden_bit_exact(ctx_dec):
+    files = _golden_files()
+    res = ctx_dec.decode_batch([d for _, d in files])
+    exp = json.load(open(os.path.join(GOLD, "jpeg_expected.json")))
+    for (name, data), (st, arr, meta) in zip(files, res):
+        assert st == 0, (name, st)
+        a = arr[:, :, 0] if exp[name]["mode"] == "L" else arr
+        assert list(a.shape) == exp[name]["shape"], name
+        assert hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest() == exp[name]["sha256"], name
+    assert ctx_dec.stat("write_mismatch") == 0
+
+
+def test_decode_only_random_bit_exact_vs_oracle(ctx_dec):
+    datas = _rand_jpegs(1, 24, rst=True)
+    res = ctx_dec.decode_batch(datas)
+    for i, (d, (st, arr, meta)) in enumerate(zip(datas, res)):
+        ost, ref = O.jpeg_decode(d)
+        assert st == 0 and ost == 0
+        assert arr.shape == ref.shape, i
+        assert np.array_equal(arr, ref), (i, int((arr != ref).sum()))
+        assert (meta.original_width, meta.original_height) == (ref.shape[1], ref.shape[0])
+
+
+def test_crop_resize_golden_bit_exact(ctx512):
+    files = _golden_files()
+    res = ctx512.decode_batch([d for _, d in files])
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    for (name, data), (st, arr, meta) in zip(files, res):
+        assert st == 0, name
+        w, h = O.jpeg_info(data)[1:3]
+        tw, th = t.target_size(w, h)
+        assert (meta.width, meta.height) == (tw, th)
+        ref = _oracle_resized(data, tw, th)
+        assert arr.shape == ref.shape, name
+        d = np.abs(arr.astype(int) - ref.astype(int))
+        assert d.max() == 0, (name, int(d.max()), int((d > 0).sum()))
+
+
+def test_crop_resize_random_1024(ctx1024):
+    datas = _rand_jpegs(2, 16, maxdim=1400)
+    res = ctx1024.decode_batch(datas)
+    t = B.ARAwareTransform(1024, 32, 0.5, 2.0)
+    for i, (data, (st, arr, meta)) in enumerate(zip(datas, res)):
+        assert st == 0
+        w, h = O.jpeg_info(data)[1:3]
+        tw, th = t.target_size(w, h)
+        ref = _oracle_resized(data, tw, th)
+        assert arr.shape == ref.shape
+        assert np.array_equal(arr, ref), (i, (w, h), (tw, th))
+    assert ctx1024.stat("write_mismatch") == 0
+
+
+def test_fractional_crop_case(ctx512):
+    # 640x480 into 512/32 buckets: 597x448 then crop left 10.5
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=32,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+    data = synth.make_jpeg(9, 640, 480, 90)
+    st, arr, meta = ctx.decode_one(data)
+    assert st == 0 and (meta.width, meta.height) == (576, 448)
+    assert np.array_equal(arr, _oracle_resized(data, 576, 448))
+
+
+def test_subsequence_sizes_agree(ctx_dec):
+    datas = _rand_jpegs(3, 6, maxdim=900)
+    L = _lib()
+    base = [a for _, a, _ in ctx_dec.decode_batch(datas)]
+    for sb in (16, 64, 512, 2048):
+        ctx = L.Context(0)
+        ctx.set_option("sub_bytes", sb)
+        for (st, a, _), b in zip(ctx.decode_batch(datas), base):
+            assert st == 0 and np.array_equal(a, b), sb
+        assert ctx.stat("write_mismatch") == 0
+
+
+def test_forced_bucket_alignment(ctx512):
+    # worker_wds.rs:68-76: later members are forced into the first image's bucket
+    t = ctx512.buckets
+    k = t.find_key("1.000")
+    data = synth.make_jpeg(11, 300, 200, 90)
+    st, arr, meta = ctx512.decode_one(data, forced_bucket=k)
+    assert st == 0 and (meta.width, meta.height) == (512, 512) and meta.bucket == k
+    assert np.array_equal(arr, _oracle_resized(data, 512, 512))
+
+
+def test_exact_size_is_a_copy(ctx512):
+    data = synth.make_jpeg(12, 512, 512, 90)
+    st, arr, meta = ctx512.decode_one(data)
+    assert st == 0
+    assert np.array_equal(arr, O.jpeg_decode(data)[1])
+
+
+def test_status_codes(ctx512):
+    import io as _io
+    L = _lib()
+    good = synth.make_jpeg(13, 64, 64, 90)
+    buf = _io.BytesIO()
+    Image.fromarray(synth.synth_pixels(np.random.default_rng(0), 64, 64)).save(buf, format="JPEG", progressive=True)
+    prog = buf.getvalue()
+    png = _io.BytesIO()
+    Image.new("RGB", (8, 8)).save(png, format="PNG")
+    trunc = synth.make_jpeg(14, 300, 300, 90)[:1500]
+    res = ctx512.decode_batch([good, b"This is not a valid image file", prog, png.getvalue(), trunc, good])
+    sts = [r[0] for r in res]
+    assert sts == [L.DG_OK, L.DG_ERR_CORRUPT, L.DG_ERR_UNSUPPORTED, L.DG_ERR_UNSUPPORTED, L.DG_ERR_CORRUPT, L.DG_OK]
+    assert np.array_equal(res[0][1], res[5][1])
+
+
+def test_tiny_and_extreme_images(ctx512):
+    # test_datago_edge_cases.py:100-172 (1x1, 1000x10, 10x1000)
+    datas = [synth.make_jpeg(20, 1, 1, 90), synth.make_jpeg(21, 1000, 10, 90), synth.make_jpeg(22, 10, 1000, 90)]
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    for data, (st, arr, meta) in zip(datas, ctx512.decode_batch(datas)):
+        assert st == 0
+        w, h = O.jpeg_info(data)[1:3]
+        tw, th = t.target_size(w, h)
+        assert 0.5 <= meta.width / meta.height <= 2.1
+        assert np.array_equal(arr, _oracle_resized(data, tw, th))
+
+
+def test_gray_to_rgb8():
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=256, downsampling_ratio=16,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0, image_to_rgb8=True)
+    data = synth.make_jpeg(23, 333, 250, 90, gray=True)
+    st, arr, meta = ctx.decode_one(data)
+    assert st == 0 and meta.channels == 3 and arr.shape[2] == 3
+    t = B.ARAwareTransform(256, 16, 0.5, 2.0)
+    tw, th = t.target_size(333, 250)
+    ref = _oracle_resized(data, tw, th)
+    assert np.array_equal(arr, np.repeat(ref, 3, axis=2))
+
+
+def test_large_full_size_properties(ctx1024):
+    # BASELINE configs[1] sizes (short side up to 2048): size-independent checks
+    datas = [synth.make_jpeg(30 + i, w, h, 85, ss) for i, (w, h, ss) in
+             enumerate([(2048, 1536, "4:2:0"), (1600, 2600, "4:2:2"), (2300, 1100, "4:4:4")])]
+    res = ctx1024.decode_batch(datas)
+    res2 = ctx1024.decode_batch(datas)
+    t = B.ARAwareTransform(1024, 32, 0.5, 2.0)
+    for data, (st, arr, meta), (st2, arr2, _) in zip(datas, res, res2):
+        assert st == 0 and st2 == 0
+        assert np.array_equal(arr, arr2)  # deterministic
+        w, h = O.jpeg_info(data)[1:3]
+        assert (meta.width, meta.height) == t.target_size(w, h)
+        # the decode stage against PIL directly (libjpeg-turbo) via the oracle-equivalent resize
+        pil = np.asarray(Image.open(io.BytesIO(data)))
+        ref = O.crop_and_resize(pil, meta.width, meta.height, O.MODE_FIR)
+        assert np.array_equal(arr, ref)
