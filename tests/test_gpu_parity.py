@@ -178,15 +178,18 @@ def test_status_codes(ctx512):
     assert np.array_equal(res[0][1], res[5][1])
 
 
-def test_tiny_and_extreme_images(ctx512):
-    # test_datago_edge_cases.py:100-172 (1x1, 1000x10, 10x1000)
+def test_tiny_and_extreme_images():
+    # test_datago_edge_cases.py:100-172 (1x1, 1000x10, 10x1000 at 224/16 buckets)
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=224, downsampling_ratio=16,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
     datas = [synth.make_jpeg(20, 1, 1, 90), synth.make_jpeg(21, 1000, 10, 90), synth.make_jpeg(22, 10, 1000, 90)]
-    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
-    for data, (st, arr, meta) in zip(datas, ctx512.decode_batch(datas)):
+    t = B.ARAwareTransform(224, 16, 0.5, 2.0)
+    for data, (st, arr, meta) in zip(datas, ctx.decode_batch(datas)):
         assert st == 0
         w, h = O.jpeg_info(data)[1:3]
         tw, th = t.target_size(w, h)
-        assert 0.5 <= meta.width / meta.height <= 2.1
+        assert 0.5 <= meta.width / meta.height <= 2.0
         assert np.array_equal(arr, _oracle_resized(data, tw, th))
 
 
