@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--short-max", type=int, default=2048)
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--ratio", type=int, default=32)
-    ap.add_argument("--sub-bytes", type=int, default=0)
+    ap.add_argument("--sub-bits", type=int, default=0)
     ap.add_argument("--workers", type=int, default=0, help="corpus generation processes")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -130,8 +130,8 @@ def main() -> int:
 
     ctx = L.Context(local, crop_and_resize=True, default_image_size=a.size, downsampling_ratio=a.ratio,
                     min_aspect_ratio=0.5, max_aspect_ratio=2.0)
-    if a.sub_bytes:
-        ctx.set_option("sub_bytes", a.sub_bytes)
+    if a.sub_bits:
+        ctx.set_option("sub_bits", a.sub_bits)
     # ---- pool -> HBM (one arena, 16-byte aligned entries)
     offs, o = [], 0
     for d in pool:
@@ -289,7 +289,7 @@ def main() -> int:
             "corpus_gen_s": round(t_gen, 1),
             "stats": {"resync_rounds": ctx.stat("resync_rounds"), "fix_workgroups": ctx.stat("fix_workgroups"),
                       "write_mismatch": ctx.stat("write_mismatch"), "sync_iters_max": ctx.stat("sync_iters_max"),
-                      "sub_bytes": ctx.stat("sub_bytes")},
+                      "sub_bits": ctx.stat("sub_bits")},
         }
         if world == 1 and not a.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(pool, targets, a.cpu_seconds)

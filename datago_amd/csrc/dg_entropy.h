@@ -1,20 +1,21 @@
-// dg_entropy.h — self-synchronising parallel Huffman decoding of one JPEG
-// entropy-coded segment range (host+device code; the kernels in kernels.hip
-// and the CPU emulator in tests/native/ both include it).
+// dg_entropy.h — self-synchronising parallel Huffman decoding of a JPEG scan
+// (host+device code: the kernels in kernels.hip and the CPU emulator in
+// tests/native/ both include it).
 //
-// A scan is cut into fixed raw-byte subsequences [a_i, a_{i+1}).  The thread
-// of subsequence i decodes every symbol whose first bit lies in its range.
-// Its entry state (bits to skip past a_i, block-in-MCU r, zigzag index z)
-// comes from the exit state of subsequence i-1 ("the first symbol boundary at
-// or after a_i"); with a guessed entry it usually falls into step with the
-// true decode within a few symbols (Huffman self-synchronisation), so the
-// workgroup iterates "re-decode from the predecessor's exit" until no exit
-// changes.  Byte stuffing (FF 00) is removed while reading; an RST marker
-// (FF D0..D7) is a hard sync point: at the first symbol boundary past it the
-// state resets to (r=0, z=0) and the DC predictors reset (T.81 F.2.1.3.1).
-// Positions are destuffed bit counts relative to the reader's own start, and
-// states cross the boundary relative to the anchor a_{i+1}, which both
-// neighbours can locate.
+// Input is the *destuffed* entropy-coded stream of one image (FF00 -> FF,
+// RST markers removed, their bit positions listed separately; produced by
+// k_destuff_*).  The stream is cut into fixed bit ranges (subsequences)
+// [i*S, (i+1)*S).  The decoder of subsequence i decodes every symbol whose
+// first bit lies in its range.  Its entry state (bit position of its first
+// symbol boundary, block-in-MCU r, zigzag index z) is the exit state of
+// subsequence i-1 ("the first symbol boundary at or after i*S").  Started
+// from a guessed state, a Huffman decoder falls into step with the true
+// decode within a few hundred bits (self-synchronisation; measured in
+// DESIGN.md), so a workgroup iterates "re-decode from the predecessor's exit"
+// until no exit changes.  An RST marker is a hard sync point: at the first
+// symbol boundary at/after it the state resets to (r=0, z=0) and the DC
+// predictors reset (T.81 F.2.1.3.1); the marker belongs to the subsequence
+// whose range contains its position.
 #pragma once
 #include "dg_types.h"
 
@@ -22,143 +23,55 @@ namespace dg {
 
 DG_HD int32_t huff_extend(int32_t v, int32_t s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
-struct BitReader {
-  const uint8_t *d;
-  uint32_t p, end, anchor;
-  uint32_t anchor_bits;  // destuffed position of the anchor, kInf until the refill passes it
-  uint32_t loaded;       // destuffed bits loaded
-  uint32_t consumed;     // destuffed bits consumed
-  uint32_t mpos, mraw;   // pending RST marker: destuffed position and raw index of its FF
-  uint64_t buf;          // left-aligned
-  int32_t nb;
-  int32_t stop;
+DG_HD uint32_t bswap32(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
+}
+
+// 64-bit window over a big-endian bit stream stored as bytes (the stream base
+// is 4-byte aligned and zero-padded by >= 16 bytes past its end).
+struct BitWin {
+  const uint32_t *w;  // stream as little-endian words (byte-swapped on load)
+  uint64_t win;       // bits [base, base + 64)
+  uint32_t base;      // bit position of win's MSB (multiple of 32)
+  uint32_t next;      // prefetched word at base + 64
+  uint32_t nidx;      // index of `next`
 };
 
-// Start reading at raw index a (the second byte of a pair that began before a
-// belongs to the previous range).
-DG_HD void br_init(BitReader &b, const uint8_t *d, uint32_t a, uint32_t end, uint32_t anchor) {
-  b.d = d;
-  b.p = a;
-  if (a > 0 && a < end && d[a - 1] == 0xFF && d[a] != 0xFF) b.p = a + 1;
-  b.end = end;
-  b.anchor = anchor;
-  b.anchor_bits = kInf;
-  b.loaded = 0;
-  b.consumed = 0;
-  b.mpos = kInf;
-  b.mraw = kInf;
-  b.buf = 0;
-  b.nb = 0;
-  b.stop = 0;
+DG_HD void bw_init(BitWin &b, const uint8_t *stream, uint32_t pos) {
+  b.w = (const uint32_t *)stream;
+  uint32_t i = pos >> 5;
+  b.base = i << 5;
+  b.win = ((uint64_t)bswap32(b.w[i]) << 32) | bswap32(b.w[i + 1]);
+  b.nidx = i + 2;
+  b.next = bswap32(b.w[b.nidx]);
 }
 
-// 8 bytes at an arbitrary address.  Device: two/three aligned dword loads
-// (callers guarantee 12 readable bytes past the address and that the buffer
-// start is 16-byte aligned); host: memcpy.
-DG_HD uint64_t load8(const uint8_t *p) {
-#if defined(DG_DEVICE)
-  uintptr_t a = (uintptr_t)p;
-  const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
-  uint32_t sh = (uint32_t)(a & 3) * 8;
-  uint64_t lo = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-  return sh ? ((lo >> sh) | ((uint64_t)w[2] << (64 - sh))) : lo;
-#else
-  uint64_t v;
-  __builtin_memcpy(&v, p, 8);
-  return v;
-#endif
-}
+// 32 bits starting at pos (requires base <= pos < base + 32).
+DG_HD uint32_t bw_peek(const BitWin &b, uint32_t pos) { return (uint32_t)((b.win << (pos - b.base)) >> 32); }
 
-DG_HD void br_refill(BitReader &b) {
-  while (b.nb <= 56) {
-    if (b.anchor_bits == kInf && b.p >= b.anchor) b.anchor_bits = b.loaded;
-    if (b.stop || b.mpos != kInf) {  // feed zero bits past a marker / the end (libjpeg)
-      b.nb += 8;
-      continue;
-    }
-    if (b.p >= b.end) {
-      b.stop = 1;
-      if (b.anchor_bits == kInf) b.anchor_bits = b.loaded;
-      continue;
-    }
-    // fast path: next 8 bytes hold no 0xFF -> append up to 4 at once
-    if (b.nb <= 24 && b.p + 12 <= b.end) {
-      uint64_t v = load8(b.d + b.p);  // little-endian bytes p..p+7
-      uint64_t nv = ~v;
-      uint64_t hasff = (nv - 0x0101010101010101ull) & ~nv & 0x8080808080808080ull;
-      if (!hasff) {
-        uint32_t take = 4;  // nb <= 24 leaves room for 32 bits
-        if (b.anchor_bits == kInf && b.anchor > b.p && b.anchor - b.p < take) take = b.anchor - b.p;
-        for (uint32_t k = 0; k < take; k++) {
-          b.buf |= (uint64_t)((v >> (8 * k)) & 0xFF) << (56 - b.nb);
-          b.nb += 8;
-        }
-        b.loaded += 8 * take;
-        b.p += take;
-        continue;
-      }
-    }
-    uint32_t c = b.d[b.p];
-    if (c != 0xFF) {
-      b.buf |= (uint64_t)c << (56 - b.nb);
-      b.nb += 8;
-      b.loaded += 8;
-      b.p += 1;
-      continue;
-    }
-    uint32_t nx = (b.p + 1 < b.end) ? b.d[b.p + 1] : 0xD9u;
-    if (nx == 0x00) {
-      b.buf |= (uint64_t)0xFF << (56 - b.nb);
-      b.nb += 8;
-      b.loaded += 8;
-      b.p += 2;
-    } else if (nx == 0xFF) {
-      b.p += 1;  // fill byte
-    } else if (nx >= 0xD0 && nx <= 0xD7) {
-      b.mpos = b.loaded;
-      b.mraw = b.p;
-      b.p += 2;
-    } else {
-      b.stop = 1;  // EOI or another marker: end of entropy data
-      if (b.anchor_bits == kInf) b.anchor_bits = b.loaded;
-    }
+DG_HD void bw_advance(BitWin &b, uint32_t pos) {
+  while (pos - b.base >= 32) {
+    b.win = (b.win << 32) | b.next;
+    b.base += 32;
+    b.nidx++;
+    b.next = bswap32(b.w[b.nidx]);
   }
 }
 
-DG_HD void br_skip(BitReader &b, int32_t k) {
-  b.buf <<= k;
-  b.nb -= k;
-  b.consumed += (uint32_t)k;
+DG_HD void bw_seek(BitWin &b, uint32_t pos) {
+  if (pos - b.base >= 64u) bw_init(b, (const uint8_t *)b.w, pos);
+  else bw_advance(b, pos);
 }
 
-DG_HD int32_t br_get(BitReader &b, int32_t k) {
-  if (k == 0) return 0;
-  int32_t v = (int32_t)(b.buf >> (64 - k));
-  br_skip(b, k);
-  return v;
-}
-
+// Decode one Huffman code from the top bits of `bits`; returns (len << 8) | sym.
 template <class T>
-DG_HD int32_t huff_decode(BitReader &b, const T &t) {
-  uint32_t pk = (uint32_t)(b.buf >> 48);
-  uint32_t e = t.lut[pk >> (16 - kLutBits)];
-  int32_t len, sym;
-  if (e) {
-    len = (int32_t)(e >> 8);
-    sym = (int32_t)(e & 0xFF);
-  } else {
-    len = 16;
-    sym = 0;  // invalid code: consume 16 bits (only reachable off-sync / past the data)
-    for (int32_t l = kLutBits + 1; l <= 16; l++) {
-      if (pk < t.lim[l]) {
-        len = l;
-        sym = t.vals[(t.valoff[l] + (int32_t)(pk >> (16 - l))) & 255];
-        break;
-      }
-    }
-  }
-  br_skip(b, len);
-  return sym;
+DG_HD uint32_t huff_lookup(const T &t, uint32_t bits) {
+  uint32_t e = t.lut[bits >> (32 - kLutBits)];
+  if (e) return e;
+  uint32_t pk = bits >> 16;
+  for (int32_t l = kLutBits + 1; l <= 16; l++)
+    if (pk < t.lim[l]) return ((uint32_t)l << 8) | t.vals[(t.valoff[l] + (int32_t)(pk >> (16 - l))) & 255];
+  return 16u << 8;  // invalid code: consume 16 bits (only off-sync / past the data)
 }
 
 // Accumulators of one subsequence decode.
@@ -168,16 +81,16 @@ struct RangeAcc {
   int32_t dc[3];
 };
 
-// Write-side context (only used when WRITE): coefficient block buffer of this
-// thread (64 int16, zigzag order), global coefficient base, prefix values.
+// Write-side context: coefficient block buffer of this thread (64 int16,
+// zigzag order), global coefficient base, prefix values.
 struct WriteCtx {
-  int16_t *blk;      // thread-private 64-entry buffer
-  int16_t *coef;     // image block 0
+  int16_t *blk;
+  int16_t *coef;
   uint32_t seg, nin;
   int32_t pred[3];
   uint32_t blocks_per_seg, total_blocks;
-  int32_t cur;       // global block index of the block being filled (-1 = none/invalid)
-  uint32_t zs;       // first zigzag index this thread owns in the current block
+  int32_t cur;   // global index of the block being filled (-1 = none / dropped)
+  uint32_t zs;   // first zigzag index this thread owns in the current block
 };
 
 DG_HD int32_t wc_index(const WriteCtx &w, uint32_t in_seg) {
@@ -189,7 +102,13 @@ DG_HD int32_t wc_index(const WriteCtx &w, uint32_t in_seg) {
 DG_HD void wc_begin(WriteCtx &w, int32_t idx, uint32_t zs) {
   w.cur = idx;
   w.zs = zs;
+#if defined(DG_DEVICE)
+  uint4 *p = (uint4 *)w.blk;
+#pragma unroll
+  for (int i = 0; i < 8; i++) p[i] = make_uint4(0, 0, 0, 0);
+#else
   for (int i = 0; i < 64; i++) w.blk[i] = 0;
+#endif
 }
 
 DG_HD void wc_flush(WriteCtx &w, uint32_t ze) {
@@ -210,35 +129,52 @@ DG_HD void wc_flush(WriteCtx &w, uint32_t ze) {
   w.cur = -1;
 }
 
-// Decode the symbols of subsequence `s` of image `im` starting from `in`.
-// tabs: Huffman tables indexed by slot (dc_slot/ac_slot of the image).
+// Position of the first RST marker >= pos in the image's sorted marker list.
+DG_HD uint32_t first_marker(const uint32_t *mk, uint32_t nmk, uint32_t pos, uint32_t &idx) {
+  uint32_t lo = 0, hi = nmk;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (mk[mid] < pos) lo = mid + 1;
+    else hi = mid;
+  }
+  idx = lo;
+  return lo < nmk ? mk[lo] : kInf;
+}
+
+// Decode the symbols of subsequence s of image im from entry state `in`.
+//   stream: destuffed bytes (4-byte aligned, zero padded); mk: marker bit positions
+//   tabs: Huffman tables indexed by slot (im.dc_slot / im.ac_slot)
 template <bool WRITE, class TAB>
-DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const uint8_t *scan, uint32_t s,
-                        uint32_t in, RangeAcc &acc, WriteCtx *w) {
-  uint32_t a0 = s * im.sub_bytes;
-  uint32_t a1 = (s + 1 == im.nsub) ? im.scan_len : a0 + im.sub_bytes;
-  BitReader b;
-  br_init(b, scan, a0, im.scan_len, a1);
+DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const uint8_t *stream, const uint32_t *mk,
+                        uint32_t s, uint32_t in, RangeAcc &acc, WriteCtx *w) {
+  const uint32_t S = im.sub_bits, total = im.ds_bits;
+  const uint32_t a0 = s * S;
+  const uint32_t a1 = (a0 + S < total) ? a0 + S : total;
   uint32_t r = st_r(in), z = st_z(in);
-  const uint32_t bpm = im.bpm;
+  uint32_t pos = a0 + st_rel(in);
   acc.m = 0;
   acc.n = 0;
   acc.dc[0] = acc.dc[1] = acc.dc[2] = 0;
-  br_refill(b);
-  br_skip(b, (int32_t)st_rel(in));
+  if (a0 >= total) {  // empty trailing subsequence (sized from the raw length)
+    acc.out = in;
+    return;
+  }
+  uint32_t midx;
+  uint32_t mpos = im.nmk ? first_marker(mk, im.nmk, a0, midx) : kInf;
+  const uint32_t bpm = im.bpm;
+  const uint32_t slotmap = im.slotmap;  // 4 bits per (component, dc/ac)
+  BitWin b;
+  bw_init(b, stream, pos < a1 ? pos : a0);
   uint32_t comp = im.blk_comp[r];
   if (WRITE) {
     w->cur = -1;
     if (z > 0) wc_begin(*w, w->nin > 0 ? wc_index(*w, w->nin - 1) : -1, z);
   }
   for (;;) {
-    if (b.consumed >= b.mpos) {  // restart marker reached: hard resync
-      bool owned = b.mraw < a1;
+    if (pos >= mpos) {  // restart marker: hard resync
+      bool owned = mpos < a1;
       if (WRITE && z > 0) wc_flush(*w, z);
-      b.consumed = b.mpos;
-      b.buf = 0;
-      b.nb = 0;
-      b.mpos = kInf;
+      pos = mpos;
       r = 0;
       z = 0;
       comp = im.blk_comp[0];
@@ -252,47 +188,67 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const uint8_t *sca
           w->pred[0] = w->pred[1] = w->pred[2] = 0;
         }
       }
+      midx++;
+      mpos = midx < im.nmk ? mk[midx] : kInf;
+      bw_seek(b, pos);
     }
-    br_refill(b);
-    if (b.anchor_bits != kInf && b.consumed >= b.anchor_bits) break;
-    if (z == 0) {
-      const TAB &t = tabs[im.dc_slot[comp]];
-      int32_t sc = huff_decode(b, t) & 15;
-      int32_t diff = sc ? huff_extend(br_get(b, sc), sc) : 0;
+    if (pos >= a1) break;
+    const uint32_t bits = bw_peek(b, pos);
+    const bool isdc = (z == 0);
+    const uint32_t slot = (slotmap >> (((comp << 1) | (isdc ? 0u : 1u)) << 2)) & 15u;
+    const uint32_t e = huff_lookup(tabs[slot], bits);
+    const uint32_t len = e >> 8, sym = e & 0xFFu;
+    const uint32_t size = sym & 15u;
+    const uint32_t run = isdc ? 0u : (sym >> 4);
+    int32_t v = 0;
+    if (size) v = huff_extend((int32_t)((bits << len) >> (32 - size)), (int32_t)size);
+    pos += len + size;
+    bw_advance(b, pos);
+    if (isdc) {
       acc.n++;
-      acc.dc[comp] += diff;
-      z = 1;
+      acc.dc[comp] += v;
       if (WRITE) {
-        w->pred[comp] += diff;
+        w->pred[comp] += v;
         wc_begin(*w, wc_index(*w, w->nin), 0);
         w->nin++;
         w->blk[0] = (int16_t)w->pred[comp];
       }
+      z = 1;
     } else {
-      const TAB &t = tabs[im.ac_slot[comp]];
-      int32_t rs = huff_decode(b, t);
-      int32_t run = rs >> 4, sz = rs & 15;
-      if (sz) {
-        z += (uint32_t)run;
-        int32_t v = huff_extend(br_get(b, sz), sz);
-        if (WRITE && z < 64) w->blk[z] = (int16_t)v;
-        z++;
-      } else if (run == 15) {
-        z += 16;
-      } else {
-        z = 64;
+      const bool eob = (size == 0) && (run != 15u);
+      if (WRITE && size) {
+        uint32_t zz = z + run;
+        if (zz < 64) w->blk[zz] = (int16_t)v;
       }
-      if (z >= 64) {
-        if (WRITE) wc_flush(*w, 64);
-        z = 0;
-        r = (r + 1 == bpm) ? 0 : r + 1;
-        comp = im.blk_comp[r];
-      }
+      z = eob ? 64u : z + run + 1u;
+    }
+    if (z >= 64) {
+      if (WRITE) wc_flush(*w, 64);
+      z = 0;
+      r = (r + 1 == bpm) ? 0 : r + 1;
+      comp = im.blk_comp[r];
     }
   }
   if (WRITE && z > 0) wc_flush(*w, z);
-  uint32_t rel = b.consumed - b.anchor_bits;
+  uint32_t rel = pos - a1;
   acc.out = pack_state(rel > 255 ? 255 : rel, r, z);
+}
+
+// ------------------------------------------------------------ destuffing
+
+// Classify raw byte i of a scan: returns 1 if it carries entropy-coded data,
+// sets *marker when it is the FF of an RST marker (FF D0..D7).
+//   FF 00 -> FF kept, 00 dropped; FF FF -> first FF is fill (dropped);
+//   FF Dn -> both dropped, marker recorded at the FF.
+DG_HD uint32_t destuff_keep(uint32_t prev, uint32_t cur, uint32_t next, bool first, uint32_t *marker) {
+  *marker = 0;
+  if (!first && prev == 0xFF && cur != 0xFF) return 0;  // 00 of a stuffed pair, or the code of a marker
+  if (cur == 0xFF) {
+    if (next == 0x00) return 1;
+    if (next >= 0xD0 && next <= 0xD7) *marker = 1;
+    return 0;  // fill byte or marker prefix
+  }
+  return 1;
 }
 
 }  // namespace dg

@@ -19,7 +19,8 @@ namespace dg {
 constexpr int kLutBits = 9;          // Huffman fast-lookup width
 constexpr int kMaxSlots = 6;         // Huffman tables per image (DC/AC x 3 components)
 constexpr int kSubPerWg = 256;       // entropy subsequences per workgroup (= threads)
-constexpr int kDefaultSubBytes = 128;// raw coded bytes per subsequence
+constexpr int kDefaultSubBits = 2048; // destuffed bits per subsequence
+constexpr int kDestuffChunk = 4096;   // raw bytes per destuff workgroup (256 x 16)
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 
 // Canonical Huffman table for the GPU decoder (built on the host, pooled).
@@ -79,18 +80,25 @@ constexpr int kStages = 4;  // R1.H, R1.V, R2.H, R2.V
 
 struct ImageDesc {
   // ---- entropy stream
-  uint64_t scan;            // device address of the first entropy-coded byte
-  uint32_t scan_len;        // bytes of entropy-coded data (up to the end of data)
-  uint32_t nsub;            // subsequences
+  uint64_t scan;            // device address of the first raw entropy-coded byte
+  uint32_t scan_len;        // raw bytes of entropy-coded data (EOI excluded)
+  uint32_t nsub;            // subsequences (sized from the raw length)
   uint32_t sub_base;        // first SubState index
-  uint32_t sub_bytes;       // bytes per subsequence
+  uint32_t sub_bits;        // bits per subsequence
+  uint64_t ds;              // destuffed stream (4-byte aligned, >= 32 zero bytes of padding)
+  uint64_t mk;              // RST marker positions in ds (bits), ascending
+  uint64_t chunk;           // destuff per-chunk records: uint32 {cnt, mkc, off, mkoff}
+  uint32_t nchunk;          // raw chunks of kDestuffChunk bytes
+  uint32_t ds_bits;         // destuffed length in bits (written by k_destuff_scan)
+  uint32_t nmk;             // RST markers (written by k_destuff_scan)
+  uint32_t slotmap;         // Huffman slot of (component c, dc=0/ac=1) at nibble 2c+ac
+  uint32_t mk_cap, pad_mk;  // capacity of the marker list
   uint32_t restart;         // restart interval (MCUs), 0 = none
   uint32_t blocks_per_seg;  // restart * bpm, 0 = unlimited
   uint32_t total_blocks;
   uint32_t bpm;             // blocks per MCU
   uint8_t blk_comp[12];     // component of block k within an MCU
   uint16_t hslot[kMaxSlots];  // pool index of Huffman slot s
-  uint8_t dc_slot[3], ac_slot[3];
   uint8_t ncomp, colorspace, dec_c, nslots;  // dec_c: channels of the decoded image
   uint16_t qpool[3];
   uint16_t pad1;

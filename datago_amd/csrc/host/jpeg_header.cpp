@@ -119,7 +119,16 @@ void parse_jpeg_header(const uint8_t *d, size_t n, JpegHeader &h) {
       }
       h.scan_off = p + (size_t)L;
       h.scan_end = n;
-      if (n >= 2 && d[n - 2] == 0xFF && d[n - 1] == 0xD9) h.scan_end = n - 2;
+      if (n >= 2 && d[n - 2] == 0xFF && d[n - 1] == 0xD9) {
+        h.scan_end = n - 2;
+      } else {  // trailing data / truncated file: entropy data ends at the first non-RST marker
+        for (size_t q = h.scan_off; q + 1 < n; q++) {
+          if (d[q] == 0xFF && d[q + 1] != 0x00 && d[q + 1] != 0xFF && !(d[q + 1] >= 0xD0 && d[q + 1] <= 0xD7)) {
+            h.scan_end = q;
+            break;
+          }
+        }
+      }
       if (h.scan_end < h.scan_off) return fail(h, JH_CORRUPT, "empty scan");
       break;
     }

@@ -75,15 +75,15 @@ dg_status Context::init() {
   }
   HIPCHK(hipSetDevice(device_));
   HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  events_.resize(16);
+  events_.resize(17);
   for (auto &e : events_) HIPCHK(hipEventCreate(&e));
   return DG_OK;
 }
 
 dg_status Context::set_option(const std::string &k, int64_t v) {
-  if (k == "sub_bytes") {
-    if (v < 16 || v > 4096 || (v & 3)) return DG_ERR_INVALID;
-    sub_bytes_ = (uint32_t)v;
+  if (k == "sub_bits") {
+    if (v < 64 || v > 65536 || (v & 31)) return DG_ERR_INVALID;
+    sub_bits_ = (uint32_t)v;
     return DG_OK;
   }
   if (k == "timing") {
@@ -99,15 +99,16 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "fix_workgroups") return stat_fix_;
   if (k == "write_mismatch") return stat_mismatch_;
   if (k == "sync_iters_max") return stat_iters_;
-  if (k == "sub_bytes") return sub_bytes_;
+  if (k == "sub_bits") return sub_bits_;
   if (k == "hpool") return (int64_t)hpool_.size();
   if (k == "qpool") return (int64_t)qpool_.size();
   return -1;
 }
 
-static const char *kStageNames[] = {"upload", "huff_sync", "huff_fix", "huff_scan", "huff_write", "coeffs",
-                                    "idct", "color", "resize_h1", "resize_v1", "resize_h2", "resize_v2",
-                                    "copy", "download"};
+static const char *kStageNames[] = {"upload",    "destuff",   "huff_sync", "huff_fix",  "huff_scan",
+                                    "huff_write", "coeffs",   "idct",      "color",     "resize_h1",
+                                    "resize_v1", "resize_h2", "resize_v2", "copy",      "download"};
+static const int kNumStages = 15;
 
 int Context::timings(const char **names, float *ms, int cap) {
   int n = (int)last_ms_.size();
@@ -348,7 +349,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.descs.reserve(n);
   // first pass: sizes only (pointers are patched after allocation)
   struct Offs {
-    size_t coef, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], tmp, out;
+    size_t coef, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], tmp, out, ds, mk, chunk;
   };
   std::vector<Offs> offs;
   for (int i = 0; i < n; i++) {
@@ -402,18 +403,25 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       d.hslot[nslots] = (uint16_t)pidx;
       return nslots++;
     };
+    d.slotmap = 0;
     for (int c = 0; c < h.ncomp; c++) {
-      d.dc_slot[c] = (uint8_t)slot_of(pool_huff(h.dc[h.comp[c].td]));
-      d.ac_slot[c] = (uint8_t)slot_of(pool_huff(h.ac[h.comp[c].ta]));
+      d.slotmap |= (uint32_t)slot_of(pool_huff(h.dc[h.comp[c].td])) << ((2 * c) * 4);
+      d.slotmap |= (uint32_t)slot_of(pool_huff(h.ac[h.comp[c].ta])) << ((2 * c + 1) * 4);
       d.qpool[c] = (uint16_t)pool_quant(h.q[h.comp[c].tq]);
     }
     d.nslots = (uint8_t)nslots;
     // entropy data
     d.scan_len = (uint32_t)(h.scan_end - h.scan_off);
-    d.sub_bytes = sub_bytes_;
-    d.nsub = std::max<uint32_t>(1, (d.scan_len + sub_bytes_ - 1) / sub_bytes_);
+    d.sub_bits = sub_bits_;
+    d.nsub = std::max<uint32_t>(1, (uint32_t)(((uint64_t)d.scan_len * 8 + sub_bits_ - 1) / sub_bits_));
     d.sub_base = sub_base;
     sub_base += d.nsub;
+    d.nchunk = std::max<uint32_t>(1, (d.scan_len + kDestuffChunk - 1) / kDestuffChunk);
+    uint32_t mcus = h.ncomp == 1 ? d.total_blocks : d.mcux * d.mcuy;
+    d.mk_cap = (d.restart ? mcus / d.restart + 2 : 0) + 64;
+    o.ds = L.take((size_t)d.scan_len + 64, 16);
+    o.mk = L.take((size_t)d.mk_cap * 4, 16);
+    o.chunk = L.take((size_t)d.nchunk * 16, 16);
     if (host_io) in_off[i] = IN.take(lens[i] + 16, 16);
     // buffers
     o.coef = L.take((size_t)d.total_blocks * 128);
@@ -535,6 +543,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     const uint8_t *src = host_io ? (const uint8_t *)d_input_.p + in_off[i] : d_srcs[i];
     d.scan = (uint64_t)(uintptr_t)(src + h.scan_off);
     d.coef = (uint64_t)(uintptr_t)(S + o.coef);
+    d.ds = (uint64_t)(uintptr_t)(S + o.ds);
+    d.mk = (uint64_t)(uintptr_t)(S + o.mk);
+    d.chunk = (uint64_t)(uintptr_t)(S + o.chunk);
     for (int c = 0; c < h.ncomp; c++) d.plane[c] = (uint64_t)(uintptr_t)(S + o.plane[c]);
     d.pix = h.ncomp == 3 ? (uint64_t)(uintptr_t)(S + o.pix) : 0;
     uint64_t out = host_io ? (uint64_t)(uintptr_t)(S + o.out) : (uint64_t)(uintptr_t)outs[i];
@@ -558,6 +569,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     const ImageDesc &d = b.descs[di];
     const uint32_t I = (uint32_t)di;
     for (uint32_t w = 0; w < d.nsub; w += kSubPerWg) b.lists[L_HUFF].push_back({I, w});
+    for (uint32_t c = 0; c < d.nchunk; c++) b.lists[L_DESTUFF].push_back({I, c});
     b.lists[L_SCAN].push_back({I, 0});
     uint32_t items = 0;
     for (uint32_t c = 0; c < d.ncomp; c++) items += d.cbh[c] * ((d.cbw[c] + 31) / 32);
@@ -631,30 +643,36 @@ dg_status Context::launch_all(Batch &b, bool from_fix) {
   };
   if (from_fix) HIPCHK(hipMemsetAsync(fl, 0, sizeof(BatchFlags), stream_));
   if (ev(1)) return DG_ERR_DEVICE;
-  if (!from_fix) launch_huff_sync(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+  if (!from_fix) {
+    launch_destuff_count(stream_, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
+    launch_destuff_scan(stream_, dm, lst(L_SCAN), cnt(L_SCAN));
+    launch_destuff_write(stream_, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
+  }
   if (ev(2)) return DG_ERR_DEVICE;
-  launch_huff_fix(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+  if (!from_fix) launch_huff_sync(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
   if (ev(3)) return DG_ERR_DEVICE;
-  launch_huff_scan(stream_, dm, lst(L_SCAN), cnt(L_SCAN), subs);
+  launch_huff_fix(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
   if (ev(4)) return DG_ERR_DEVICE;
-  launch_huff_write(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+  launch_huff_scan(stream_, dm, lst(L_SCAN), cnt(L_SCAN), subs);
   if (ev(5)) return DG_ERR_DEVICE;
-  if (!from_fix) launch_coeffs(stream_, dm, lst(L_COEF), cnt(L_COEF));
+  launch_huff_write(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
   if (ev(6)) return DG_ERR_DEVICE;
-  launch_idct(stream_, dd, lst(L_IDCT), cnt(L_IDCT), qp);
+  if (!from_fix) launch_coeffs(stream_, dm, lst(L_COEF), cnt(L_COEF));
   if (ev(7)) return DG_ERR_DEVICE;
-  launch_color(stream_, dd, lst(L_COLOR), cnt(L_COLOR));
+  launch_idct(stream_, dd, lst(L_IDCT), cnt(L_IDCT), qp);
   if (ev(8)) return DG_ERR_DEVICE;
-  launch_resize_h(stream_, dd, lst(L_RH0), cnt(L_RH0), 0);
+  launch_color(stream_, dd, lst(L_COLOR), cnt(L_COLOR));
   if (ev(9)) return DG_ERR_DEVICE;
-  launch_resize_v(stream_, dd, lst(L_RV1), cnt(L_RV1), 1);
+  launch_resize_h(stream_, dd, lst(L_RH0), cnt(L_RH0), 0);
   if (ev(10)) return DG_ERR_DEVICE;
-  launch_resize_h(stream_, dd, lst(L_RH2), cnt(L_RH2), 2);
+  launch_resize_v(stream_, dd, lst(L_RV1), cnt(L_RV1), 1);
   if (ev(11)) return DG_ERR_DEVICE;
-  launch_resize_v(stream_, dd, lst(L_RV3), cnt(L_RV3), 3);
+  launch_resize_h(stream_, dd, lst(L_RH2), cnt(L_RH2), 2);
   if (ev(12)) return DG_ERR_DEVICE;
-  launch_copy(stream_, dd, lst(L_COPY), cnt(L_COPY));
+  launch_resize_v(stream_, dd, lst(L_RV3), cnt(L_RV3), 3);
   if (ev(13)) return DG_ERR_DEVICE;
+  launch_copy(stream_, dd, lst(L_COPY), cnt(L_COPY));
+  if (ev(14)) return DG_ERR_DEVICE;
   HIPCHK(hipGetLastError());
   // read back flags + per-image status (descs) for finish(), then outputs (host path)
   size_t back = b.desc_off + b.descs.size() * sizeof(ImageDesc);
@@ -674,7 +692,7 @@ dg_status Context::launch_all(Batch &b, bool from_fix) {
       off += align_up(b.plans[i].out_bytes, 16);
     }
   }
-  if (ev(14)) return DG_ERR_DEVICE;
+  if (ev(15)) return DG_ERR_DEVICE;
   return DG_OK;
 }
 
@@ -694,8 +712,8 @@ dg_status Context::finish(Batch &b) {
     if (st) return st;
   }
   if (timing_) {
-    last_ms_.assign(14, 0.f);
-    for (int i = 0; i < 14; i++) {
+    last_ms_.assign(kNumStages, 0.f);
+    for (int i = 0; i < kNumStages; i++) {
       float ms = 0.f;
       if (hipEventElapsedTime(&ms, events_[i], events_[i + 1]) == hipSuccess) last_ms_[i] = ms;
     }

@@ -43,8 +43,8 @@ struct Batch {
   std::vector<ImageDesc> descs;
   std::vector<int> desc_of;           // image -> desc index or -1
   // workgroup lists (host copies) and their offsets in the device meta buffer
-  std::vector<WgItem> lists[12];
-  size_t list_off[12] = {0};
+  std::vector<WgItem> lists[16];
+  size_t list_off[16] = {0};
   size_t desc_off = 0, flags_off = 0;
   size_t meta_bytes = 0;
   size_t total_subs = 0;
@@ -59,7 +59,7 @@ struct Batch {
   std::vector<float> stage_ms;
 };
 
-enum ListId { L_HUFF = 0, L_SCAN, L_IDCT, L_COLOR, L_COEF, L_RH0, L_RV1, L_RH2, L_RV3, L_COPY, L_COUNT };
+enum ListId { L_HUFF = 0, L_DESTUFF, L_SCAN, L_IDCT, L_COLOR, L_COEF, L_RH0, L_RV1, L_RH2, L_RV3, L_COPY, L_COUNT };
 
 class Context {
  public:
@@ -111,7 +111,7 @@ class Context {
   size_t subs_off_ = 0;
   uint64_t next_ticket_ = 1;
 
-  uint32_t sub_bytes_ = kDefaultSubBytes;
+  uint32_t sub_bits_ = kDefaultSubBits;
   bool timing_ = false;
   std::vector<hipEvent_t> events_;
   // stats

@@ -6,6 +6,10 @@
 
 namespace dg {
 
+// Destuffing: raw scan -> clean bit stream + RST marker positions
+void launch_destuff_count(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_destuff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 // Entropy decode (one 256-thread workgroup per 256 subsequences of one image)
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                       const HuffTable *pool, SubState *subs, BatchFlags *flags);

@@ -34,6 +34,130 @@ __device__ __forceinline__ void load_tables(HuffTable *tabs, const HuffTable *po
   }
 }
 
+// ------------------------------------------------------------ destuffing
+// Raw scan -> destuffed stream + RST marker positions, in three passes over
+// 4 KiB raw chunks (count / per-image scan / write).  The coded data is a few
+// percent of the pixel traffic, so plain byte loads are fine here.
+
+__device__ __forceinline__ void destuff_thread(const uint8_t *raw, uint32_t n, uint32_t i0, uint32_t &kept,
+                                               uint32_t &mks, uint32_t keepmask[1], uint32_t &mkmask) {
+  kept = 0;
+  mks = 0;
+  keepmask[0] = 0;
+  mkmask = 0;
+  uint32_t prev = i0 ? raw[i0 - 1] : 0u;
+  uint32_t cur = i0 < n ? raw[i0] : 0u;
+#pragma unroll 4
+  for (uint32_t j = 0; j < 16; j++) {
+    uint32_t i = i0 + j;
+    if (i >= n) break;
+    uint32_t next = i + 1 < n ? raw[i + 1] : 0xD9u;
+    uint32_t m;
+    uint32_t k = destuff_keep(prev, cur, next, i == 0, &m);
+    keepmask[0] |= k << j;
+    mkmask |= m << j;
+    kept += k;
+    mks += m;
+    prev = cur;
+    cur = next;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_destuff_count(const ImageDesc *__restrict__ imgs,
+                                                       const WgItem *__restrict__ list) {
+  __shared__ uint32_t rk[256], rm[256];
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  const int t = threadIdx.x;
+  uint32_t kept, mks, km[1], mm;
+  destuff_thread((const uint8_t *)im.scan, im.scan_len, it.item0 * kDestuffChunk + t * 16, kept, mks, km, mm);
+  rk[t] = kept;
+  rm[t] = mks;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) {
+      rk[t] += rk[t + off];
+      rm[t] += rm[t + off];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    uint32_t *ch = (uint32_t *)im.chunk + it.item0 * 4;
+    ch[0] = rk[0];
+    ch[1] = rm[0];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_destuff_scan(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
+  __shared__ uint32_t sk[256], sm[256];
+  const WgItem it = list[blockIdx.x];
+  ImageDesc &im = imgs[it.image];
+  const int t = threadIdx.x;
+  uint32_t *ch = (uint32_t *)im.chunk;
+  uint32_t ck = 0, cm = 0;
+  for (uint32_t c0 = 0; c0 < im.nchunk; c0 += 256) {
+    uint32_t c = c0 + t;
+    uint32_t k = c < im.nchunk ? ch[c * 4] : 0u, m = c < im.nchunk ? ch[c * 4 + 1] : 0u;
+    sk[t] = k;
+    sm[t] = m;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+      uint32_t a = t >= off ? sk[t - off] : 0u, b = t >= off ? sm[t - off] : 0u;
+      __syncthreads();
+      sk[t] += a;
+      sm[t] += b;
+      __syncthreads();
+    }
+    if (c < im.nchunk) {
+      ch[c * 4 + 2] = ck + sk[t] - k;
+      ch[c * 4 + 3] = cm + sm[t] - m;
+    }
+    ck += sk[255];
+    cm += sm[255];
+    __syncthreads();
+  }
+  if (t == 0) {
+    im.ds_bits = ck * 8;
+    im.nmk = cm < im.mk_cap ? cm : im.mk_cap;
+  }
+  uint8_t *ds = (uint8_t *)im.ds;
+  if (t < 48) ds[ck + t] = 0;  // zero padding for the bit-window reader
+}
+
+__global__ __launch_bounds__(256) void k_destuff_write(const ImageDesc *__restrict__ imgs,
+                                                       const WgItem *__restrict__ list) {
+  __shared__ uint32_t sk[256], sm[256];
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  const int t = threadIdx.x;
+  const uint8_t *raw = (const uint8_t *)im.scan;
+  const uint32_t i0 = it.item0 * kDestuffChunk + t * 16;
+  uint32_t kept, mks, km[1], mm;
+  destuff_thread(raw, im.scan_len, i0, kept, mks, km, mm);
+  sk[t] = kept;
+  sm[t] = mks;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    uint32_t a = t >= off ? sk[t - off] : 0u, b = t >= off ? sm[t - off] : 0u;
+    __syncthreads();
+    sk[t] += a;
+    sm[t] += b;
+    __syncthreads();
+  }
+  const uint32_t *ch = (const uint32_t *)im.chunk + it.item0 * 4;
+  uint32_t o = ch[2] + sk[t] - kept;
+  uint32_t mo = ch[3] + sm[t] - mks;
+  uint8_t *ds = (uint8_t *)im.ds;
+  uint32_t *mk = (uint32_t *)im.mk;
+  for (uint32_t j = 0; j < 16; j++) {
+    if ((mm >> j) & 1u) {
+      if (mo < im.mk_cap) mk[mo] = o * 8;
+      mo++;
+    }
+    if ((km[0] >> j) & 1u) ds[o++] = raw[i0 + j];
+  }
+}
+
 // ------------------------------------------------------------ entropy decode
 
 __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__ imgs,
@@ -49,10 +173,11 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   const int t = threadIdx.x;
   const uint32_t s = it.item0 + t;
   const bool active = s < im.nsub;
-  const uint8_t *scan = (const uint8_t *)im.scan;
+  const uint8_t *scan = (const uint8_t *)im.ds;
+  const uint32_t *mkp = (const uint32_t *)im.mk;
   RangeAcc acc = {0, 0, 0, {0, 0, 0}};
   uint32_t in = pack_state(0, 0, 0);  // exact for s == 0, a guess otherwise
-  if (active) decode_range<false>(im, tabs, scan, s, in, acc, nullptr);
+  if (active) decode_range<false>(im, tabs, scan, mkp, s, in, acc, nullptr);
   ex[t] = active ? acc.out : 0u;
   ins[t] = in;
   __syncthreads();
@@ -62,7 +187,7 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
     uint32_t pin = redo ? ex[t - 1] : 0u;
     __syncthreads();
     if (redo) {
-      decode_range<false>(im, tabs, scan, s, pin, acc, nullptr);
+      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr);
       ex[t] = acc.out;
       ins[t] = pin;
     }
@@ -98,7 +223,8 @@ __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ 
   const int t = threadIdx.x;
   const uint32_t s = it.item0 + t;
   const bool active = s < im.nsub;
-  const uint8_t *scan = (const uint8_t *)im.scan;
+  const uint8_t *scan = (const uint8_t *)im.ds;
+  const uint32_t *mkp = (const uint32_t *)im.mk;
   const uint32_t orig_out = active ? base[s].out : 0u;
   ex[t] = orig_out;
   ins[t] = active ? base[s].in : 0u;
@@ -110,7 +236,7 @@ __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ 
     uint32_t pin = redo ? (t == 0 ? first_in : ex[t - 1]) : 0u;
     __syncthreads();
     if (redo) {
-      decode_range<false>(im, tabs, scan, s, pin, acc, nullptr);
+      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr);
       ex[t] = acc.out;
       ins[t] = pin;
       mine = true;
@@ -208,7 +334,7 @@ __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict_
   w.cur = -1;
   w.zs = 0;
   RangeAcc acc;
-  decode_range<true>(im, tabs, (const uint8_t *)im.scan, s, ss.in, acc, &w);
+  decode_range<true>(im, tabs, (const uint8_t *)im.ds, (const uint32_t *)im.mk, s, ss.in, acc, &w);
   if (acc.out != ss.out) atomicAdd(&flags->write_mismatch, 1u);
 }
 
@@ -496,6 +622,15 @@ __global__ __launch_bounds__(256) void k_copy(const ImageDesc *__restrict__ imgs
     if (nwg) hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), 0, st, __VA_ARGS__); \
   } while (0)
 
+void launch_destuff_count(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
+  DG_LAUNCH(k_destuff_count, nwg, st, imgs, list);
+}
+void launch_destuff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
+  DG_LAUNCH(k_destuff_scan, nwg, st, imgs, list);
+}
+void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
+  DG_LAUNCH(k_destuff_write, nwg, st, imgs, list);
+}
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                       const HuffTable *pool, SubState *subs, BatchFlags *flags) {
   DG_LAUNCH(k_huff_sync, nwg, st, imgs, list, pool, subs, flags);

@@ -14,7 +14,7 @@
 
 using namespace dg;
 
-extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bytes, int16_t *out,
+extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bits, int16_t *out,
                                 size_t cap_blocks, size_t *nblocks, int64_t *stats) {
   JpegHeader h;
   parse_jpeg_header(data, len, h);
@@ -45,19 +45,34 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_by
   d.restart = h.restart;
   d.blocks_per_seg = d.restart * bpm;
   std::vector<HuffTable> tabs;
+  d.slotmap = 0;
   for (int c = 0; c < h.ncomp; c++) {
     HuffTable t;
     build_huff_table(h.dc[h.comp[c].td], t);
-    d.dc_slot[c] = (uint8_t)tabs.size();
+    d.slotmap |= (uint32_t)tabs.size() << ((2 * c) * 4);
     tabs.push_back(t);
     build_huff_table(h.ac[h.comp[c].ta], t);
-    d.ac_slot[c] = (uint8_t)tabs.size();
+    d.slotmap |= (uint32_t)tabs.size() << ((2 * c + 1) * 4);
     tabs.push_back(t);
   }
   d.scan_len = (uint32_t)(h.scan_end - h.scan_off);
-  d.sub_bytes = sub_bytes;
-  d.nsub = d.scan_len ? (d.scan_len + sub_bytes - 1) / sub_bytes : 1;
-  const uint8_t *scan = data + h.scan_off;
+  const uint8_t *raw = data + h.scan_off;
+  // destuff exactly as k_destuff_* do (per byte, same classification function)
+  std::vector<uint8_t> ds;
+  std::vector<uint32_t> mk;
+  for (uint32_t i = 0; i < d.scan_len; i++) {
+    uint32_t prev = i ? raw[i - 1] : 0, next = i + 1 < d.scan_len ? raw[i + 1] : 0xD9, m;
+    uint32_t keep = destuff_keep(prev, raw[i], next, i == 0, &m);
+    if (m) mk.push_back((uint32_t)ds.size() * 8);
+    if (keep) ds.push_back(raw[i]);
+  }
+  d.ds_bits = (uint32_t)ds.size() * 8;
+  d.nmk = (uint32_t)mk.size();
+  ds.resize(((ds.size() + 3) & ~(size_t)3) + 32, 0);
+  d.sub_bits = sub_bits;
+  d.nsub = d.scan_len ? (uint32_t)(((uint64_t)d.scan_len * 8 + sub_bits - 1) / sub_bits) : 1;
+  const uint8_t *scan = ds.data();
+  const uint32_t *mkp = mk.data();
   std::vector<SubState> subs(d.nsub);
   const uint32_t NW = (d.nsub + kSubPerWg - 1) / kSubPerWg;
   int64_t redo_total = 0, iters_max = 0, fix_wgs = 0, rounds = 0;
@@ -69,7 +84,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_by
     std::vector<RangeAcc> acc(n);
     for (uint32_t t = 0; t < n; t++) {
       ins[t] = pack_state(0, 0, 0);
-      decode_range<false>(d, tabs.data(), scan, s0 + t, ins[t], acc[t], nullptr);
+      decode_range<false>(d, tabs.data(), scan, mkp, s0 + t, ins[t], acc[t], nullptr);
       ex[t] = acc[t].out;
     }
     int64_t it = 0;
@@ -81,7 +96,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_by
         if (ins[t] != ex[t - 1]) { redo[t] = 1; pin[t] = ex[t - 1]; any = true; }
       for (uint32_t t = 1; t < n; t++)
         if (redo[t]) {
-          decode_range<false>(d, tabs.data(), scan, s0 + t, pin[t], acc[t], nullptr);
+          decode_range<false>(d, tabs.data(), scan, mkp, s0 + t, pin[t], acc[t], nullptr);
           ex[t] = acc[t].out;
           ins[t] = pin[t];
           redo_total++;
@@ -122,7 +137,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_by
         }
         for (uint32_t t = 0; t < n; t++)
           if (redo[t]) {
-            decode_range<false>(d, tabs.data(), scan, s0 + t, pin[t], acc[t], nullptr);
+            decode_range<false>(d, tabs.data(), scan, mkp, s0 + t, pin[t], acc[t], nullptr);
             ex[t] = acc[t].out; ins[t] = pin[t]; mine[t] = 1; redo_total++;
           }
         if (!any) break;
@@ -157,7 +172,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_by
     for (int c = 0; c < 3; c++) w.pred[c] = subs[s].dcin[c];
     w.blocks_per_seg = d.blocks_per_seg; w.total_blocks = d.total_blocks; w.cur = -1; w.zs = 0;
     RangeAcc acc;
-    decode_range<true>(d, tabs.data(), scan, s, subs[s].in, acc, &w);
+    decode_range<true>(d, tabs.data(), scan, mkp, s, subs[s].in, acc, &w);
     if (acc.out != subs[s].out) mismatch++;
   }
   // zigzag -> natural

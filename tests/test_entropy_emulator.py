@@ -30,20 +30,20 @@ def emu():
                                    ctypes.POINTER(ctypes.c_int16), ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int64)]
 
-    def run(data, sub_bytes):
+    def run(data, sub_bits):
         cap = 1 << 18
         out = np.zeros((cap, 64), np.int16)
         nb = ctypes.c_size_t()
         st = (ctypes.c_int64 * 8)()
-        r = E.emu_decode_coefs(data, len(data), sub_bytes, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),
+        r = E.emu_decode_coefs(data, len(data), sub_bits, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),
                                cap, ctypes.byref(nb), st)
         return r, out[: nb.value], list(st)
     return run
 
 
 @pytest.mark.parametrize("seed", range(24))
-@pytest.mark.parametrize("sub_bytes", [16, 128, 512])
-def test_emulated_parallel_decode_matches_oracle(emu, seed, sub_bytes):
+@pytest.mark.parametrize("sub_bits", [128, 1024, 4096])
+def test_emulated_parallel_decode_matches_oracle(emu, seed, sub_bits):
     rng = np.random.default_rng(seed)
     w, h = int(rng.integers(1, 700)), int(rng.integers(1, 700))
     ss = ["4:2:0", "4:2:2", "4:4:4"][seed % 3]
@@ -51,7 +51,7 @@ def test_emulated_parallel_decode_matches_oracle(emu, seed, sub_bytes):
     data = synth.encode_jpeg(synth.synth_pixels(rng, w, h, seed % 7 == 0), int(rng.integers(30, 101)), ss,
                              restart_marker_rows=rst)
     st, ref = O.jpeg_coefs(data)
-    r, co, stats = emu(data, sub_bytes)
+    r, co, stats = emu(data, sub_bits)
     assert r == 0 and st == 0
     assert co.shape == ref.shape
     assert np.array_equal(co, ref)
@@ -61,5 +61,5 @@ def test_emulated_parallel_decode_matches_oracle(emu, seed, sub_bytes):
 def test_truncated_stream_is_detected(emu):
     data = synth.make_jpeg(3, 300, 200, 90, "4:2:0")
     cut = data[: len(data) * 2 // 3]
-    r, co, stats = emu(cut, 128)
+    r, co, stats = emu(cut, 1024)
     assert stats[6] < stats[7]  # decoded blocks < total blocks -> CORRUPT on the GPU path
