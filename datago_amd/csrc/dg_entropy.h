@@ -30,15 +30,15 @@ DG_HD uint32_t bswap32(uint32_t x) {
 // 64-bit window over a big-endian bit stream stored as bytes (the stream base
 // is 4-byte aligned and zero-padded by >= 16 bytes past its end).
 struct BitWin {
-  const uint32_t *w;  // stream as little-endian words (byte-swapped on load)
+  const DG_GLOBAL uint32_t *w;  // stream as little-endian words (byte-swapped on load)
   uint64_t win;       // bits [base, base + 64)
   uint32_t base;      // bit position of win's MSB (multiple of 32)
   uint32_t next;      // prefetched word at base + 64
   uint32_t nidx;      // index of `next`
 };
 
-DG_HD void bw_init(BitWin &b, const uint8_t *stream, uint32_t pos) {
-  b.w = (const uint32_t *)stream;
+DG_HD void bw_init(BitWin &b, const DG_GLOBAL uint8_t *stream, uint32_t pos) {
+  b.w = (const DG_GLOBAL uint32_t *)stream;
   uint32_t i = pos >> 5;
   b.base = i << 5;
   b.win = ((uint64_t)bswap32(b.w[i]) << 32) | bswap32(b.w[i + 1]);
@@ -59,7 +59,7 @@ DG_HD void bw_advance(BitWin &b, uint32_t pos) {
 }
 
 DG_HD void bw_seek(BitWin &b, uint32_t pos) {
-  if (pos - b.base >= 64u) bw_init(b, (const uint8_t *)b.w, pos);
+  if (pos - b.base >= 64u) bw_init(b, (const DG_GLOBAL uint8_t *)b.w, pos);
   else bw_advance(b, pos);
 }
 
@@ -85,7 +85,7 @@ struct RangeAcc {
 // zigzag order), global coefficient base, prefix values.
 struct WriteCtx {
   int16_t *blk;
-  int16_t *coef;
+  DG_GLOBAL int16_t *coef;
   uint32_t seg, nin;
   int32_t pred[3];
   uint32_t blocks_per_seg, total_blocks;
@@ -103,9 +103,10 @@ DG_HD void wc_begin(WriteCtx &w, int32_t idx, uint32_t zs) {
   w.cur = idx;
   w.zs = zs;
 #if defined(DG_DEVICE)
-  uint4 *p = (uint4 *)w.blk;
+  u32x4 *p = (u32x4 *)w.blk;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int i = 0; i < 8; i++) p[i] = make_uint4(0, 0, 0, 0);
+  for (int i = 0; i < 8; i++) p[i] = zero;
 #else
   for (int i = 0; i < 64; i++) w.blk[i] = 0;
 #endif
@@ -113,11 +114,11 @@ DG_HD void wc_begin(WriteCtx &w, int32_t idx, uint32_t zs) {
 
 DG_HD void wc_flush(WriteCtx &w, uint32_t ze) {
   if (w.cur < 0) return;
-  int16_t *dst = w.coef + (size_t)w.cur * 64;
+  DG_GLOBAL int16_t *dst = w.coef + (size_t)w.cur * 64;
   if (w.zs == 0 && ze == 64) {
 #if defined(DG_DEVICE)
-    const uint4 *s4 = (const uint4 *)w.blk;
-    uint4 *d4 = (uint4 *)dst;
+    const u32x4 *s4 = (const u32x4 *)w.blk;
+    DG_GLOBAL u32x4 *d4 = (DG_GLOBAL u32x4 *)dst;
 #pragma unroll
     for (int i = 0; i < 8; i++) d4[i] = s4[i];
 #else
@@ -129,8 +130,28 @@ DG_HD void wc_flush(WriteCtx &w, uint32_t ze) {
   w.cur = -1;
 }
 
+// Checkpoints for early merging.  A decode records, at the first symbol
+// boundary at/after every kCkptBits-th bit of its range, the state there and
+// the accumulator *tail* from that point to the end of the range.  A later
+// re-decode of the same range from a different entry state compares states at
+// each checkpoint: once they agree the two paths coincide to the end, so it
+// stops and completes its totals with the stored tail.  This cuts a re-decode
+// from a full range to about the self-synchronisation distance.
+constexpr uint32_t kCkptBits = 256;
+constexpr uint32_t kMaxCkpt = 15;  // enough for sub_bits <= 4096
+struct Ckpt {
+  uint32_t st;   // packed state (rel past the checkpoint position, r, z)
+  uint32_t m, n; // tail (segmented: m > 0 means the tail contains a reset)
+  int32_t dc[3];
+};
+
+DG_HD uint32_t num_ckpt(uint32_t sub_bits) {
+  uint32_t k = (sub_bits - 1) / kCkptBits;
+  return k > kMaxCkpt ? kMaxCkpt : k;
+}
+
 // Position of the first RST marker >= pos in the image's sorted marker list.
-DG_HD uint32_t first_marker(const uint32_t *mk, uint32_t nmk, uint32_t pos, uint32_t &idx) {
+DG_HD uint32_t first_marker(const DG_GLOBAL uint32_t *mk, uint32_t nmk, uint32_t pos, uint32_t &idx) {
   uint32_t lo = 0, hi = nmk;
   while (lo < hi) {
     uint32_t mid = (lo + hi) >> 1;
@@ -144,9 +165,13 @@ DG_HD uint32_t first_marker(const uint32_t *mk, uint32_t nmk, uint32_t pos, uint
 // Decode the symbols of subsequence s of image im from entry state `in`.
 //   stream: destuffed bytes (4-byte aligned, zero padded); mk: marker bit positions
 //   tabs: Huffman tables indexed by slot (im.dc_slot / im.ac_slot)
+//   ck: this subsequence's checkpoint records (nullptr: none); merge: the
+//   records hold a previous decode of this range whose exit state was old_out.
 template <bool WRITE, class TAB>
-DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const uint8_t *stream, const uint32_t *mk,
-                        uint32_t s, uint32_t in, RangeAcc &acc, WriteCtx *w) {
+DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uint8_t *stream,
+                        const DG_GLOBAL uint32_t *mk,
+                        uint32_t s, uint32_t in, RangeAcc &acc, WriteCtx *w, DG_GLOBAL Ckpt *ck = nullptr,
+                        bool merge = false, uint32_t old_out = 0) {
   const uint32_t S = im.sub_bits, total = im.ds_bits;
   const uint32_t a0 = s * S;
   const uint32_t a1 = (a0 + S < total) ? a0 + S : total;
@@ -155,8 +180,8 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const uint8_t *str
   acc.m = 0;
   acc.n = 0;
   acc.dc[0] = acc.dc[1] = acc.dc[2] = 0;
-  if (a0 >= total) {  // empty trailing subsequence (sized from the raw length)
-    acc.out = in;
+  if (a0 >= total) {  // empty trailing subsequence (nsub is sized from the raw length):
+    acc.out = pack_state(0, 0, 0);  // constant exit, so state changes do not ripple through it
     return;
   }
   uint32_t midx;
@@ -166,6 +191,9 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const uint8_t *str
   BitWin b;
   bw_init(b, stream, pos < a1 ? pos : a0);
   uint32_t comp = im.blk_comp[r];
+  const uint32_t nck = ck ? num_ckpt(S) : 0;
+  uint32_t k = 0, cpos = a0 + kCkptBits;
+  bool merged = false;
   if (WRITE) {
     w->cur = -1;
     if (z > 0) wc_begin(*w, w->nin > 0 ? wc_index(*w, w->nin - 1) : -1, z);
@@ -192,6 +220,36 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const uint8_t *str
       mpos = midx < im.nmk ? mk[midx] : kInf;
       bw_seek(b, pos);
     }
+    if (k < nck && cpos < a1 && pos >= cpos) {  // first boundary at/after checkpoint k
+      uint32_t rel = pos - cpos;
+      uint32_t st = pack_state(rel > 255 ? 255 : rel, r, z);
+      DG_GLOBAL Ckpt &c = ck[k];
+      if (merge && c.st == st) {  // rejoined the previous decode: acc (+) tail_k
+        if (c.m) {
+          acc.m += c.m;
+          acc.n = c.n;
+          acc.dc[0] = c.dc[0];
+          acc.dc[1] = c.dc[1];
+          acc.dc[2] = c.dc[2];
+        } else {
+          acc.n += c.n;
+          acc.dc[0] += c.dc[0];
+          acc.dc[1] += c.dc[1];
+          acc.dc[2] += c.dc[2];
+        }
+        acc.out = old_out;
+        merged = true;
+        break;
+      }
+      c.st = st;  // record the prefix for now; turned into a tail at the end
+      c.m = acc.m;
+      c.n = acc.n;
+      c.dc[0] = acc.dc[0];
+      c.dc[1] = acc.dc[1];
+      c.dc[2] = acc.dc[2];
+      k++;
+      cpos += kCkptBits;
+    }
     if (pos >= a1) break;
     const uint32_t bits = bw_peek(b, pos);
     const bool isdc = (z == 0);
@@ -206,12 +264,12 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const uint8_t *str
     bw_advance(b, pos);
     if (isdc) {
       acc.n++;
-      acc.dc[comp] += v;
+      add3(acc.dc, comp, v);
       if (WRITE) {
-        w->pred[comp] += v;
+        add3(w->pred, comp, v);
         wc_begin(*w, wc_index(*w, w->nin), 0);
         w->nin++;
-        w->blk[0] = (int16_t)w->pred[comp];
+        w->blk[0] = (int16_t)sel3(w->pred, comp);
       }
       z = 1;
     } else {
@@ -230,8 +288,26 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const uint8_t *str
     }
   }
   if (WRITE && z > 0) wc_flush(*w, z);
-  uint32_t rel = pos - a1;
-  acc.out = pack_state(rel > 255 ? 255 : rel, r, z);
+  if (!merged) {
+    uint32_t rel = pos - a1;
+    acc.out = pack_state(rel > 255 ? 255 : rel, r, z);
+  }
+  for (uint32_t j = 0; j < k; j++) {  // prefixes written this time -> tails
+    DG_GLOBAL Ckpt &c = ck[j];
+    if (acc.m > c.m) {
+      c.m = acc.m - c.m;
+      c.n = acc.n;
+      c.dc[0] = acc.dc[0];
+      c.dc[1] = acc.dc[1];
+      c.dc[2] = acc.dc[2];
+    } else {
+      c.m = 0;
+      c.n = acc.n - c.n;
+      c.dc[0] = acc.dc[0] - c.dc[0];
+      c.dc[1] = acc.dc[1] - c.dc[1];
+      c.dc[2] = acc.dc[2] - c.dc[2];
+    }
+  }
 }
 
 // ------------------------------------------------------------ destuffing

@@ -10,11 +10,30 @@
 #if defined(__HIP__)
 #define DG_HD __host__ __device__ __forceinline__
 #define DG_DEVICE 1
+#define DG_GLOBAL __attribute__((address_space(1)))  // global memory: global_load/store, not flat
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #else
 #define DG_HD static inline
+#define DG_GLOBAL
 #endif
 
 namespace dg {
+
+// Typed pointer to device memory from an address held in a descriptor.
+template <class T>
+DG_HD DG_GLOBAL T *gp(uint64_t a) {
+  return (DG_GLOBAL T *)(uintptr_t)a;
+}
+
+// Three per-component counters without dynamic register indexing (which would
+// spill to scratch): c in {0,1,2}.
+DG_HD int32_t sel3(const int32_t v[3], uint32_t c) { return c == 0 ? v[0] : (c == 1 ? v[1] : v[2]); }
+DG_HD void add3(int32_t v[3], uint32_t c, int32_t d) {
+  v[0] += c == 0 ? d : 0;
+  v[1] += c == 1 ? d : 0;
+  v[2] += c == 2 ? d : 0;
+}
 
 constexpr int kLutBits = 9;          // Huffman fast-lookup width
 constexpr int kMaxSlots = 6;         // Huffman tables per image (DC/AC x 3 components)

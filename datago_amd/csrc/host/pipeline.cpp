@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 
+#include "../dg_entropy.h"
 #include "../dg_pixel.h"
 #include "../kernels.h"
 
@@ -49,6 +50,10 @@ Context::~Context() {
     if (b->p) hipFree(b->p);
   for (PinBuf *b : {&h_stage_, &h_out_})
     if (b->p) hipHostFree(b->p);
+  if (side_) hipStreamSynchronize(side_);
+  if (ev_meta_) hipEventDestroy(ev_meta_);
+  if (ev_coef_) hipEventDestroy(ev_coef_);
+  if (side_) hipStreamDestroy(side_);
   if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -75,6 +80,9 @@ dg_status Context::init() {
   }
   HIPCHK(hipSetDevice(device_));
   HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&ev_meta_, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&ev_coef_, hipEventDisableTiming));
   events_.resize(17);
   for (auto &e : events_) HIPCHK(hipEventCreate(&e));
   return DG_OK;
@@ -526,6 +534,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   b.total_subs = sub_base;
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
+  ckpt_off_ = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits_)) * sizeof(Ckpt));
   st = ensure(d_scratch_, L.off + 256);
   if (st) return st;
   if (host_io) {
@@ -569,21 +578,27 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     const ImageDesc &d = b.descs[di];
     const uint32_t I = (uint32_t)di;
     for (uint32_t w = 0; w < d.nsub; w += kSubPerWg) b.lists[L_HUFF].push_back({I, w});
+    for (uint32_t w = 0; w < d.nsub; w += kSubPerWg - 1) b.lists[L_SYNC].push_back({I, w});
     for (uint32_t c = 0; c < d.nchunk; c++) b.lists[L_DESTUFF].push_back({I, c});
     b.lists[L_SCAN].push_back({I, 0});
     uint32_t items = 0;
     for (uint32_t c = 0; c < d.ncomp; c++) items += d.cbh[c] * ((d.cbw[c] + 31) / 32);
     for (uint32_t it = 0; it < items; it++) b.lists[L_IDCT].push_back({I, it});
     if (d.ncomp == 3) {
-      uint32_t q = (d.width + 3) / 4 * d.height;
+      uint32_t q = (d.width + 7) / 8 * d.height;
       for (uint32_t it = 0; it < q; it += 256) b.lists[L_COLOR].push_back({I, it});
     }
     for (int s = 0; s < kStages; s++) {
       const ResizePass &ps = d.pass[s];
       if (!ps.kind) continue;
       b.lists[L_COEF].push_back({I, (uint32_t)s});
-      uint32_t cnt = ps.kind == 1 ? ps.width * ps.rows : (ps.width * ps.C + 3) / 4 * ps.rows;
-      for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_RH0 + s].push_back({I, it});
+      if (ps.kind == 1) {  // one workgroup per (row, 512-column tile)
+        uint32_t cnt = ps.rows * ((ps.width + 511) / 512);
+        for (uint32_t it = 0; it < cnt; it++) b.lists[L_RH0 + s].push_back({I, it});
+      } else {
+        uint32_t cnt = (ps.width * ps.C + 15) / 16 * ps.rows;
+        for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_RH0 + s].push_back({I, it});
+      }
     }
     if (d.copy_needed) {
       uint32_t cnt = d.out_w * d.out_h;
@@ -644,25 +659,32 @@ dg_status Context::launch_all(Batch &b, bool from_fix) {
   if (from_fix) HIPCHK(hipMemsetAsync(fl, 0, sizeof(BatchFlags), stream_));
   if (ev(1)) return DG_ERR_DEVICE;
   if (!from_fix) {
+    // Lanczos coefficient tables depend only on the plan: compute them on a
+    // side stream, overlapped with the entropy decode.
+    HIPCHK(hipEventRecord(ev_meta_, stream_));
+    HIPCHK(hipStreamWaitEvent(side_, ev_meta_, 0));
+    launch_coeffs(side_, dm, lst(L_COEF), cnt(L_COEF));
+    HIPCHK(hipEventRecord(ev_coef_, side_));
     launch_destuff_count(stream_, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
     launch_destuff_scan(stream_, dm, lst(L_SCAN), cnt(L_SCAN));
     launch_destuff_write(stream_, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
   }
   if (ev(2)) return DG_ERR_DEVICE;
-  if (!from_fix) launch_huff_sync(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+  Ckpt *ck = (Ckpt *)((char *)d_scratch_.p + ckpt_off_);
+  if (!from_fix) launch_huff_sync(stream_, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
   if (ev(3)) return DG_ERR_DEVICE;
-  launch_huff_fix(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+  launch_huff_fix(stream_, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
   if (ev(4)) return DG_ERR_DEVICE;
   launch_huff_scan(stream_, dm, lst(L_SCAN), cnt(L_SCAN), subs);
   if (ev(5)) return DG_ERR_DEVICE;
   launch_huff_write(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
   if (ev(6)) return DG_ERR_DEVICE;
-  if (!from_fix) launch_coeffs(stream_, dm, lst(L_COEF), cnt(L_COEF));
   if (ev(7)) return DG_ERR_DEVICE;
   launch_idct(stream_, dd, lst(L_IDCT), cnt(L_IDCT), qp);
   if (ev(8)) return DG_ERR_DEVICE;
   launch_color(stream_, dd, lst(L_COLOR), cnt(L_COLOR));
   if (ev(9)) return DG_ERR_DEVICE;
+  HIPCHK(hipStreamWaitEvent(stream_, ev_coef_, 0));
   launch_resize_h(stream_, dd, lst(L_RH0), cnt(L_RH0), 0);
   if (ev(10)) return DG_ERR_DEVICE;
   launch_resize_v(stream_, dd, lst(L_RV1), cnt(L_RV1), 1);

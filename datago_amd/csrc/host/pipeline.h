@@ -59,7 +59,7 @@ struct Batch {
   std::vector<float> stage_ms;
 };
 
-enum ListId { L_HUFF = 0, L_DESTUFF, L_SCAN, L_IDCT, L_COLOR, L_COEF, L_RH0, L_RV1, L_RH2, L_RV3, L_COPY, L_COUNT };
+enum ListId { L_HUFF = 0, L_SYNC, L_DESTUFF, L_SCAN, L_IDCT, L_COLOR, L_COEF, L_RH0, L_RV1, L_RH2, L_RV3, L_COPY, L_COUNT };
 
 class Context {
  public:
@@ -95,7 +95,8 @@ class Context {
   bool has_cfg_ = false;
   dg_image_config cfg_{};
   std::unique_ptr<BucketTable> buckets_;
-  hipStream_t stream_ = nullptr;
+  hipStream_t stream_ = nullptr, side_ = nullptr;
+  hipEvent_t ev_meta_ = nullptr, ev_coef_ = nullptr;
   std::mutex mu_;
 
   std::vector<HuffTable> hpool_;
@@ -108,7 +109,7 @@ class Context {
   DevBuf d_scratch_, d_meta_, d_input_;
   PinBuf h_stage_, h_out_;
   std::unique_ptr<Batch> cur_;
-  size_t subs_off_ = 0;
+  size_t subs_off_ = 0, ckpt_off_ = 0;
   uint64_t next_ticket_ = 1;
 
   uint32_t sub_bits_ = kDefaultSubBits;

@@ -11,10 +11,12 @@ void launch_destuff_count(hipStream_t st, const ImageDesc *imgs, const WgItem *l
 void launch_destuff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 // Entropy decode (one 256-thread workgroup per 256 subsequences of one image)
+// (sync/fix: 255 useful subsequences per workgroup, see kernels.hip)
+struct Ckpt;
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                      const HuffTable *pool, SubState *subs, BatchFlags *flags);
+                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags);
 void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                     const HuffTable *pool, SubState *subs, BatchFlags *flags);
+                     const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags);
 // one workgroup per image
 void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs);
 void launch_huff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,

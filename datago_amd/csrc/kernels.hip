@@ -39,7 +39,8 @@ __device__ __forceinline__ void load_tables(HuffTable *tabs, const HuffTable *po
 // 4 KiB raw chunks (count / per-image scan / write).  The coded data is a few
 // percent of the pixel traffic, so plain byte loads are fine here.
 
-__device__ __forceinline__ void destuff_thread(const uint8_t *raw, uint32_t n, uint32_t i0, uint32_t &kept,
+template <class P>
+__device__ __forceinline__ void destuff_thread(P raw, uint32_t n, uint32_t i0, uint32_t &kept,
                                                uint32_t &mks, uint32_t keepmask[1], uint32_t &mkmask) {
   kept = 0;
   mks = 0;
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(256) void k_destuff_count(const ImageDesc *__restri
   const ImageDesc &im = imgs[it.image];
   const int t = threadIdx.x;
   uint32_t kept, mks, km[1], mm;
-  destuff_thread((const uint8_t *)im.scan, im.scan_len, it.item0 * kDestuffChunk + t * 16, kept, mks, km, mm);
+  destuff_thread(gp<const uint8_t>(im.scan), im.scan_len, it.item0 * kDestuffChunk + t * 16, kept, mks, km, mm);
   rk[t] = kept;
   rm[t] = mks;
   __syncthreads();
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(256) void k_destuff_count(const ImageDesc *__restri
     __syncthreads();
   }
   if (t == 0) {
-    uint32_t *ch = (uint32_t *)im.chunk + it.item0 * 4;
+    DG_GLOBAL uint32_t *ch = gp<uint32_t>(im.chunk) + it.item0 * 4;
     ch[0] = rk[0];
     ch[1] = rm[0];
   }
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(256) void k_destuff_scan(ImageDesc *__restrict__ im
   const WgItem it = list[blockIdx.x];
   ImageDesc &im = imgs[it.image];
   const int t = threadIdx.x;
-  uint32_t *ch = (uint32_t *)im.chunk;
+  DG_GLOBAL uint32_t *ch = gp<uint32_t>(im.chunk);
   uint32_t ck = 0, cm = 0;
   for (uint32_t c0 = 0; c0 < im.nchunk; c0 += 256) {
     uint32_t c = c0 + t;
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(256) void k_destuff_scan(ImageDesc *__restrict__ im
     im.ds_bits = ck * 8;
     im.nmk = cm < im.mk_cap ? cm : im.mk_cap;
   }
-  uint8_t *ds = (uint8_t *)im.ds;
+  DG_GLOBAL uint8_t *ds = gp<uint8_t>(im.ds);
   if (t < 48) ds[ck + t] = 0;  // zero padding for the bit-window reader
 }
 
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(256) void k_destuff_write(const ImageDesc *__restri
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
   const int t = threadIdx.x;
-  const uint8_t *raw = (const uint8_t *)im.scan;
+  const DG_GLOBAL uint8_t *raw = gp<const uint8_t>(im.scan);
   const uint32_t i0 = it.item0 * kDestuffChunk + t * 16;
   uint32_t kept, mks, km[1], mm;
   destuff_thread(raw, im.scan_len, i0, kept, mks, km, mm);
@@ -144,11 +145,11 @@ __global__ __launch_bounds__(256) void k_destuff_write(const ImageDesc *__restri
     sm[t] += b;
     __syncthreads();
   }
-  const uint32_t *ch = (const uint32_t *)im.chunk + it.item0 * 4;
+  const DG_GLOBAL uint32_t *ch = gp<const uint32_t>(im.chunk) + it.item0 * 4;
   uint32_t o = ch[2] + sk[t] - kept;
   uint32_t mo = ch[3] + sm[t] - mks;
-  uint8_t *ds = (uint8_t *)im.ds;
-  uint32_t *mk = (uint32_t *)im.mk;
+  DG_GLOBAL uint8_t *ds = gp<uint8_t>(im.ds);
+  DG_GLOBAL uint32_t *mk = gp<uint32_t>(im.mk);
   for (uint32_t j = 0; j < 16; j++) {
     if ((mm >> j) & 1u) {
       if (mo < im.mk_cap) mk[mo] = o * 8;
@@ -160,10 +161,27 @@ __global__ __launch_bounds__(256) void k_destuff_write(const ImageDesc *__restri
 
 // ------------------------------------------------------------ entropy decode
 
+// Workgroup layout for sync/fix: 255 useful subsequences per workgroup.
+// Thread 0 is a lead-in: it decodes the previous workgroup's last subsequence
+// from a guessed state (writing nothing) so that thread 1 usually starts in
+// step with the true decode and k_huff_fix finds nothing to repair.
+constexpr uint32_t kUseful = kSubPerWg - 1;
+
+__device__ __forceinline__ void store_sub(SubState &o, uint32_t in, uint32_t out, const RangeAcc &a) {
+  o.in = in;
+  o.out = out;
+  o.m = a.m;
+  o.n = a.n;
+  o.dc[0] = a.dc[0];
+  o.dc[1] = a.dc[1];
+  o.dc[2] = a.dc[2];
+}
+
 __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__ imgs,
                                                    const WgItem *__restrict__ list,
                                                    const HuffTable *__restrict__ pool,
-                                                   SubState *__restrict__ subs, BatchFlags *flags) {
+                                                   SubState *__restrict__ subs, Ckpt *__restrict__ ckpt,
+                                                   BatchFlags *flags) {
   __shared__ HuffTable tabs[kMaxSlots];
   __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
   const WgItem it = list[blockIdx.x];
@@ -171,72 +189,84 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   load_tables(tabs, pool, im);
   __syncthreads();
   const int t = threadIdx.x;
-  const uint32_t s = it.item0 + t;
-  const bool active = s < im.nsub;
-  const uint8_t *scan = (const uint8_t *)im.ds;
-  const uint32_t *mkp = (const uint32_t *)im.mk;
+  const uint32_t s0 = it.item0;                  // first useful subsequence
+  const int64_t si = (int64_t)s0 + t - 1;        // this thread's subsequence (t = 0: lead-in)
+  const bool active = si >= 0 && si < (int64_t)im.nsub;
+  const bool head = (t == 0) || (s0 == 0 && t == 1);
+  const uint32_t s = active ? (uint32_t)si : 0u;
+  const uint32_t nck = num_ckpt(im.sub_bits);
+  DG_GLOBAL Ckpt *ck = (t > 0 && active && nck) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck : nullptr;
+  const DG_GLOBAL uint8_t *scan = gp<const uint8_t>(im.ds);
+  const DG_GLOBAL uint32_t *mkp = gp<const uint32_t>(im.mk);
   RangeAcc acc = {0, 0, 0, {0, 0, 0}};
   uint32_t in = pack_state(0, 0, 0);  // exact for s == 0, a guess otherwise
-  if (active) decode_range<false>(im, tabs, scan, mkp, s, in, acc, nullptr);
+  if (active) decode_range<false>(im, tabs, scan, mkp, s, in, acc, nullptr, ck);
   ex[t] = active ? acc.out : 0u;
   ins[t] = in;
   __syncthreads();
   uint32_t iters = 0;
   for (;;) {
-    bool redo = active && t > 0 && ins[t] != ex[t - 1];
+    bool redo = active && !head && ins[t] != ex[t - 1];
     uint32_t pin = redo ? ex[t - 1] : 0u;
     __syncthreads();
     if (redo) {
-      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr);
+      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr, ck, true, ex[t]);
       ex[t] = acc.out;
       ins[t] = pin;
     }
     iters++;
     if (!__syncthreads_or(redo)) break;
   }
-  if (active) {
-    SubState &o = subs[im.sub_base + s];
-    o.in = ins[t];
-    o.out = ex[t];
-    o.m = acc.m;
-    o.n = acc.n;
-    o.dc[0] = acc.dc[0];
-    o.dc[1] = acc.dc[1];
-    o.dc[2] = acc.dc[2];
-  }
+  if (active && t > 0) store_sub(subs[im.sub_base + s], ins[t], ex[t], acc);
   if (t == 0) atomicMax(&flags->sync_iters_max, iters);
 }
 
 __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ imgs,
                                                   const WgItem *__restrict__ list,
                                                   const HuffTable *__restrict__ pool,
-                                                  SubState *__restrict__ subs, BatchFlags *flags) {
+                                                  SubState *__restrict__ subs, Ckpt *__restrict__ ckpt,
+                                                  BatchFlags *flags) {
   __shared__ HuffTable tabs[kMaxSlots];
   __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
   const WgItem it = list[blockIdx.x];
-  if (it.item0 == 0) return;
+  const uint32_t s0 = it.item0;
+  if (s0 == 0) return;
   const ImageDesc &im = imgs[it.image];
   SubState *base = subs + im.sub_base;
-  const uint32_t first_in = base[it.item0 - 1].out;
-  if (base[it.item0].in == first_in) return;  // boundary already consistent (uniform branch)
+  const uint32_t first_in = base[s0 - 1].out;
+  if (base[s0].in == first_in) return;  // boundary already consistent (uniform branch)
   load_tables(tabs, pool, im);
-  const int t = threadIdx.x;
-  const uint32_t s = it.item0 + t;
-  const bool active = s < im.nsub;
-  const uint8_t *scan = (const uint8_t *)im.ds;
-  const uint32_t *mkp = (const uint32_t *)im.mk;
-  const uint32_t orig_out = active ? base[s].out : 0u;
-  ex[t] = orig_out;
-  ins[t] = active ? base[s].in : 0u;
-  __syncthreads();
+  const int t = threadIdx.x;  // thread t handles s0 + t (t < kUseful)
+  const uint32_t s = s0 + t;
+  const bool active = t < (int)kUseful && s < im.nsub;
+  const uint32_t nck = num_ckpt(im.sub_bits);
+  DG_GLOBAL Ckpt *ck = (active && nck) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck : nullptr;
+  const DG_GLOBAL uint8_t *scan = gp<const uint8_t>(im.ds);
+  const DG_GLOBAL uint32_t *mkp = gp<const uint32_t>(im.mk);
   RangeAcc acc = {0, 0, 0, {0, 0, 0}};
+  uint32_t orig_out = 0;
+  if (active) {
+    const SubState &o = base[s];
+    orig_out = o.out;
+    acc.m = o.m;
+    acc.n = o.n;
+    acc.dc[0] = o.dc[0];
+    acc.dc[1] = o.dc[1];
+    acc.dc[2] = o.dc[2];
+    ex[t] = o.out;
+    ins[t] = o.in;
+  } else {
+    ex[t] = 0u;
+    ins[t] = 0u;
+  }
+  __syncthreads();
   bool mine = false;
   for (;;) {
     bool redo = active && (t == 0 ? ins[0] != first_in : ins[t] != ex[t - 1]);
     uint32_t pin = redo ? (t == 0 ? first_in : ex[t - 1]) : 0u;
     __syncthreads();
     if (redo) {
-      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr);
+      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr, ck, true, ex[t]);
       ex[t] = acc.out;
       ins[t] = pin;
       mine = true;
@@ -244,15 +274,8 @@ __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ 
     if (!__syncthreads_or(redo)) break;
   }
   if (active && mine) {
-    SubState &o = base[s];
-    o.in = ins[t];
-    o.out = ex[t];
-    o.m = acc.m;
-    o.n = acc.n;
-    o.dc[0] = acc.dc[0];
-    o.dc[1] = acc.dc[1];
-    o.dc[2] = acc.dc[2];
-    bool last = (t == kSubPerWg - 1) && (s + 1 < im.nsub);
+    store_sub(base[s], ins[t], ex[t], acc);
+    bool last = (t == (int)kUseful - 1) && (s + 1 < im.nsub);
     if (last && ex[t] != orig_out) atomicAdd(&flags->chain_changed, 1u);
   }
   if (t == 0) atomicAdd(&flags->fix_count, 1u);
@@ -323,7 +346,7 @@ __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict_
   const SubState ss = subs[im.sub_base + s];
   WriteCtx w;
   w.blk = blk[t];
-  w.coef = (int16_t *)im.coef;
+  w.coef = gp<int16_t>(im.coef);
   w.seg = ss.seg;
   w.nin = ss.nin;
   w.pred[0] = ss.dcin[0];
@@ -334,7 +357,7 @@ __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict_
   w.cur = -1;
   w.zs = 0;
   RangeAcc acc;
-  decode_range<true>(im, tabs, (const uint8_t *)im.ds, (const uint32_t *)im.mk, s, ss.in, acc, &w);
+  decode_range<true>(im, tabs, gp<const uint8_t>(im.ds), gp<const uint32_t>(im.mk), s, ss.in, acc, &w);
   if (acc.out != ss.out) atomicAdd(&flags->write_mismatch, 1u);
 }
 
@@ -370,8 +393,8 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
       uint32_t mx = bx / im.ch[c], hx = bx - mx * im.ch[c];
       b = (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * im.ch[c] + hx;
     }
-    const int16_t *src = (const int16_t *)im.coef + (size_t)b * 64 + lane * 8;
-    uint4 raw = *(const uint4 *)src;
+    const DG_GLOBAL int16_t *src = gp<const int16_t>(im.coef) + (size_t)b * 64 + lane * 8;
+    u32x4 raw = *(const DG_GLOBAL u32x4 *)src;
     int16_t v[8];
     __builtin_memcpy(v, &raw, 16);
 #pragma unroll
@@ -401,58 +424,139 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
       lo |= (uint32_t)idct_out(o[i]) << (8 * i);
       hi |= (uint32_t)idct_out(o[i + 4]) << (8 * i);
     }
-    uint8_t *dst = (uint8_t *)im.plane[c] + (size_t)(by * 8 + lane) * (im.cbw[c] * 8) + bx * 8;
-    *(uint2 *)dst = make_uint2(lo, hi);
+    DG_GLOBAL uint8_t *dst = gp<uint8_t>(im.plane[c]) + (size_t)(by * 8 + lane) * (im.cbw[c] * 8) + bx * 8;
+    u32x2 v2 = {lo, hi};
+    *(DG_GLOBAL u32x2 *)dst = v2;
   }
 }
 
 // ------------------------------------------------------------ colour
 
+// 8 consecutive upsampled samples of component plane `pl` at row y, columns
+// x0..x0+7 (x0 a multiple of 8), with libjpeg's fancy filters (see
+// upsample_at, which this vectorises: one aligned load per source row plus
+// the two edge samples instead of four byte loads per pixel).
+template <class P>
+__device__ __forceinline__ void upsample8(P pl, uint32_t stride, uint32_t hr, uint32_t vr,
+                                          uint32_t dsw, uint32_t dsh, uint32_t x0, uint32_t y, int32_t o[8]) {
+  if (hr == 1) {  // 4:4:4 component (vr is 1 too for the supported samplings)
+    u32x2 v = *(const DG_GLOBAL u32x2 *)(pl + (size_t)y * stride + x0);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      o[k] = (v.x >> (8 * k)) & 0xFF;
+      o[k + 4] = (v.y >> (8 * k)) & 0xFF;
+    }
+    return;
+  }
+  const uint32_t c0 = x0 >> 1;  // multiple of 4
+  const bool fancy = dsw > 2;
+  int32_t cs[6];                // column sums (or plain samples for h2v1) at c0-1 .. c0+4
+  const uint32_t cl = c0 > 0 ? c0 - 1 : 0, cr = c0 + 4 < dsw ? c0 + 4 : dsw - 1;
+  if (vr == 1) {
+    P in = pl + (size_t)y * stride;
+    uint32_t v = *(const DG_GLOBAL uint32_t *)(in + c0);
+    cs[0] = in[cl];
+#pragma unroll
+    for (int k = 0; k < 4; k++) cs[k + 1] = (v >> (8 * k)) & 0xFF;
+    cs[5] = in[cr];
+    // clamp interior samples past the downsampled width (replicate the edge)
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (c0 + k >= dsw) cs[k + 1] = cs[dsw - c0];
+    if (!fancy) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) o[k] = cs[1 + (k >> 1)];
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int32_t a = cs[k + 1] * 3;
+      int32_t nl = (c0 + k + 1 < dsw) ? cs[k + 2] : cs[k + 1];
+      o[2 * k] = (a + cs[k] + 1) >> 2;
+      o[2 * k + 1] = (a + nl + 2) >> 2;
+    }
+    if (c0 == 0) o[0] = (cs[1] * 3 + cs[1] + 1) >> 2;
+    return;
+  }
+  // h2v2
+  const uint32_t r = y >> 1;
+  if (!fancy) {
+    P in = pl + (size_t)r * stride;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      uint32_t c = c0 + (k >> 1);
+      o[k] = in[c < dsw ? c : dsw - 1];
+    }
+    return;
+  }
+  int32_t rn = (y & 1) ? (int32_t)r + 1 : (int32_t)r - 1;
+  rn = rn < 0 ? 0 : (rn > (int32_t)dsh - 1 ? (int32_t)dsh - 1 : rn);
+  P i0 = pl + (size_t)r * stride;
+  P i1 = pl + (size_t)rn * stride;
+  uint32_t v0 = *(const DG_GLOBAL uint32_t *)(i0 + c0), v1 = *(const DG_GLOBAL uint32_t *)(i1 + c0);
+  cs[0] = i0[cl] * 3 + i1[cl];
+#pragma unroll
+  for (int k = 0; k < 4; k++) cs[k + 1] = (int32_t)((v0 >> (8 * k)) & 0xFF) * 3 + (int32_t)((v1 >> (8 * k)) & 0xFF);
+  cs[5] = i0[cr] * 3 + i1[cr];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (c0 + k >= dsw) cs[k + 1] = cs[dsw - c0];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    int32_t nl = (c0 + k + 1 < dsw) ? cs[k + 2] : cs[k + 1];
+    o[2 * k] = (cs[k + 1] * 3 + cs[k] + 8) >> 4;
+    o[2 * k + 1] = (cs[k + 1] * 3 + nl + 7) >> 4;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_color(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
-  const uint32_t qw = (im.width + 3) / 4;
+  const uint32_t ow = (im.width + 7) / 8;  // octets per row
   const uint32_t q = it.item0 + threadIdx.x;
-  if (q >= qw * im.height) return;
-  const uint32_t y = q / qw, x0 = (q - y * qw) * 4;
-  const uint8_t *p0 = (const uint8_t *)im.plane[0];
-  const uint8_t *p1 = (const uint8_t *)im.plane[1];
-  const uint8_t *p2 = (const uint8_t *)im.plane[2];
-  const uint32_t s0 = im.cbw[0] * 8, s1 = im.cbw[1] * 8, s2 = im.cbw[2] * 8;
-  const uint32_t hr1 = im.hmax / im.ch[1], vr1 = im.vmax / im.cv[1];
-  const uint32_t hr2 = im.hmax / im.ch[2], vr2 = im.vmax / im.cv[2];
-  const uint32_t hr0 = im.hmax / im.ch[0], vr0 = im.vmax / im.cv[0];
-  uint8_t px[12];
+  if (q >= ow * im.height) return;
+  const uint32_t y = q / ow, x0 = (q - y * ow) * 8;
+  int32_t Y[8], Cb[8], Cr[8];
+  upsample8(gp<const uint8_t>(im.plane[0]), im.cbw[0] * 8, im.hmax / im.ch[0], im.vmax / im.cv[0], im.cdsw[0],
+            im.cdsh[0], x0, y, Y);
+  upsample8(gp<const uint8_t>(im.plane[1]), im.cbw[1] * 8, im.hmax / im.ch[1], im.vmax / im.cv[1], im.cdsw[1],
+            im.cdsh[1], x0, y, Cb);
+  upsample8(gp<const uint8_t>(im.plane[2]), im.cbw[2] * 8, im.hmax / im.ch[2], im.vmax / im.cv[2], im.cdsw[2],
+            im.cdsh[2], x0, y, Cr);
+  uint32_t w[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    uint32_t x = x0 + k;
-    if (x >= im.width) x = im.width - 1;
-    uint32_t Y = upsample_at(p0, s0, hr0, vr0, im.cdsw[0], im.cdsh[0], x, y);
-    uint32_t cb = upsample_at(p1, s1, hr1, vr1, im.cdsw[1], im.cdsh[1], x, y);
-    uint32_t cr = upsample_at(p2, s2, hr2, vr2, im.cdsw[2], im.cdsh[2], x, y);
+  for (int k = 0; k < 8; k++) {
+    uint8_t r, g, b;
     if (im.colorspace == CS_RGB) {
-      px[3 * k] = (uint8_t)Y;
-      px[3 * k + 1] = (uint8_t)cb;
-      px[3 * k + 2] = (uint8_t)cr;
+      r = (uint8_t)Y[k];
+      g = (uint8_t)Cb[k];
+      b = (uint8_t)Cr[k];
     } else {
-      ycc_to_rgb((int32_t)Y, (int32_t)cb, (int32_t)cr, px[3 * k], px[3 * k + 1], px[3 * k + 2]);
+      ycc_to_rgb(Y[k], Cb[k], Cr[k], r, g, b);
     }
+    const int o = 3 * k;
+    w[o >> 2] |= (uint32_t)r << (8 * (o & 3));
+    w[(o + 1) >> 2] |= (uint32_t)g << (8 * ((o + 1) & 3));
+    w[(o + 2) >> 2] |= (uint32_t)b << (8 * ((o + 2) & 3));
   }
-  uint8_t *dst = (uint8_t *)im.pix + (size_t)y * im.pix_stride + x0 * 3;
-  if (x0 + 4 <= im.width) {
-    uint32_t w[3];
-    __builtin_memcpy(w, px, 12);
-    uint32_t *d = (uint32_t *)dst;  // x0*3 is a multiple of 12, pix_stride of 16
-    d[0] = w[0];
-    d[1] = w[1];
-    d[2] = w[2];
+  DG_GLOBAL uint8_t *dst = gp<uint8_t>(im.pix) + (size_t)y * im.pix_stride + x0 * 3;
+  if (x0 + 8 <= im.width) {
+    DG_GLOBAL u32x2 *d = (DG_GLOBAL u32x2 *)dst;  // x0*3 is a multiple of 24, pix_stride of 16
+    d[0] = u32x2{w[0], w[1]};
+    d[1] = u32x2{w[2], w[3]};
+    d[2] = u32x2{w[4], w[5]};
   } else {
-    uint32_t n = (im.width - x0) * 3;
-    for (uint32_t i = 0; i < n; i++) dst[i] = px[i];
+    const uint32_t n = (im.width - x0) * 3;
+    for (uint32_t i = 0; i < n; i++) dst[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
   }
 }
 
 // ------------------------------------------------------------ resize
+
+__device__ __forceinline__ uint8_t clip_shift(int32_t acc, int32_t prec) {
+  int32_t v = acc >> prec;
+  return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
 
 __global__ __launch_bounds__(256) void k_coeffs(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
   __shared__ double red[256];
@@ -465,8 +569,8 @@ __global__ __launch_bounds__(256) void k_coeffs(ImageDesc *__restrict__ imgs, co
   const double filter_scale = scale > 1.0 ? scale : 1.0;
   const double support = 3.0 * filter_scale;
   const double recip = 1.0 / filter_scale;
-  int2 *bounds = (int2 *)ps.bounds;
-  int16_t *coef = (int16_t *)ps.coef;
+  DG_GLOBAL int32_t *bounds = gp<int32_t>(ps.bounds);  // {start, size} per output
+  DG_GLOBAL int16_t *coef = gp<int16_t>(ps.coef);
   double maxw = 0.0;
   for (uint32_t o = t; o < out_size; o += 256) {
     // fast_image_resize precompute_coefficients for output o (see fir_weights)
@@ -486,7 +590,8 @@ __global__ __launch_bounds__(256) void k_coeffs(ImageDesc *__restrict__ imgs, co
     }
     int32_t st = first < 0 ? xmax : first;
     int32_t n = first < 0 ? 0 : last - first + 1;
-    bounds[o] = make_int2(st, n);
+    bounds[2 * o] = st;
+    bounds[2 * o + 1] = n;
     for (int32_t i = 0; i < n; i++) {
       double v = lanczos3(((double)(st + i) - c) * recip);
       if (ww != 0.0) v /= ww;
@@ -508,95 +613,145 @@ __global__ __launch_bounds__(256) void k_coeffs(ImageDesc *__restrict__ imgs, co
     int32_t xmax = cl > (double)in_size ? (int32_t)in_size : (int32_t)cl;
     double c = center - 0.5, ww = 0.0;
     for (int32_t x = xmin; x < xmax; x++) ww += lanczos3(((double)x - c) * recip);
-    int2 bd = bounds[o];
-    int16_t *k = coef + (size_t)o * ksize;
-    for (int32_t i = 0; i < bd.y; i++) {
-      double v = lanczos3(((double)(bd.x + i) - c) * recip);
+    const int32_t st = bounds[2 * o], n = bounds[2 * o + 1];
+    DG_GLOBAL int16_t *k = coef + (size_t)o * ksize;
+    for (int32_t i = 0; i < n; i++) {
+      double v = lanczos3(((double)(st + i) - c) * recip);
       if (ww != 0.0) v /= ww;
       k[i] = fir_quant(v, precision);
     }
   }
 }
 
-__device__ __forceinline__ uint8_t clip_shift(int32_t acc, int32_t prec) {
-  int32_t v = acc >> prec;
-  return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
-}
 
-__global__ __launch_bounds__(256) void k_resize_h(const ImageDesc *__restrict__ imgs,
-                                                  const WgItem *__restrict__ list, int stage) {
-  const WgItem it = list[blockIdx.x];
-  const ResizePass &ps = imgs[it.image].pass[stage];
-  const uint32_t idx = it.item0 + threadIdx.x;
-  if (idx >= ps.width * ps.rows) return;
-  const uint32_t y = idx / ps.width, x = idx - y * ps.width;
-  const int2 bd = ((const int2 *)ps.bounds)[x];
-  const int16_t *k = (const int16_t *)ps.coef + (size_t)x * ps.ksize;
-  const uint8_t *src = (const uint8_t *)ps.src + (size_t)(ps.row0 + y) * ps.src_stride;
-  uint8_t *dst = (uint8_t *)ps.dst + (size_t)y * ps.dst_stride + (size_t)x * ps.C;
-  const int32_t prec = ps.precision, bias = 1 << (prec - 1);
-  if (ps.C == 3) {
+// Horizontal pass: one workgroup = one output row x kResizeTile output
+// columns.  The source row segment those columns read is staged in LDS with
+// coalesced dword loads, then each thread convolves 2 output pixels from LDS.
+constexpr uint32_t kResizeTile = 512;
+
+// One output pixel of a horizontal pass: C channels, n taps from s[off...].
+template <class P>
+__device__ __forceinline__ void hconv(P s, uint32_t off, int32_t n, const DG_GLOBAL int16_t *k, uint32_t C,
+                                      int32_t prec, DG_GLOBAL uint8_t *dst) {
+  const int32_t bias = 1 << (prec - 1);
+  if (C == 3) {
     int32_t a0 = bias, a1 = bias, a2 = bias;
-    const uint8_t *s = src + (size_t)bd.x * 3;
-    for (int32_t i = 0; i < bd.y; i++) {
-      int32_t w = k[i];
-      a0 += (int32_t)s[3 * i] * w;
-      a1 += (int32_t)s[3 * i + 1] * w;
-      a2 += (int32_t)s[3 * i + 2] * w;
+    for (int32_t i = 0; i < n; i++) {
+      const int32_t w = k[i];
+      const uint32_t o = off + 3 * (uint32_t)i;
+      a0 += (int32_t)s[o] * w;
+      a1 += (int32_t)s[o + 1] * w;
+      a2 += (int32_t)s[o + 2] * w;
     }
     dst[0] = clip_shift(a0, prec);
     dst[1] = clip_shift(a1, prec);
     dst[2] = clip_shift(a2, prec);
   } else {
-    for (uint32_t ch = 0; ch < ps.C; ch++) {
+    for (uint32_t ch = 0; ch < C; ch++) {
       int32_t a = bias;
-      const uint8_t *s = src + (size_t)bd.x * ps.C + ch;
-      for (int32_t i = 0; i < bd.y; i++) a += (int32_t)s[(size_t)i * ps.C] * (int32_t)k[i];
+      for (int32_t i = 0; i < n; i++) a += (int32_t)s[off + (uint32_t)i * C + ch] * (int32_t)k[i];
       dst[ch] = clip_shift(a, prec);
     }
   }
 }
+constexpr uint32_t kResizeSeg = 24576;  // LDS bytes for the staged source segment
 
+__global__ __launch_bounds__(256) void k_resize_h(const ImageDesc *__restrict__ imgs,
+                                                  const WgItem *__restrict__ list, int stage) {
+  __shared__ __attribute__((aligned(16))) uint8_t seg[kResizeSeg + 16];
+  const WgItem it = list[blockIdx.x];
+  const ResizePass &ps = imgs[it.image].pass[stage];
+  const uint32_t tiles = (ps.width + kResizeTile - 1) / kResizeTile;
+  const uint32_t y = it.item0 / tiles, tile = it.item0 - y * tiles;
+  if (y >= ps.rows) return;
+  const uint32_t x0 = tile * kResizeTile;
+  const uint32_t x1 = x0 + kResizeTile < ps.width ? x0 + kResizeTile : ps.width;
+  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds);  // {start, size} per output
+  const uint32_t C = ps.C;
+  const uint32_t sb = (uint32_t)bounds[2 * x0] * C;
+  const uint32_t se = (uint32_t)(bounds[2 * (x1 - 1)] + bounds[2 * (x1 - 1) + 1]) * C;  // source bytes [sb, se)
+  const DG_GLOBAL uint8_t *srow = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y) * ps.src_stride;
+  const bool staged = se - sb + 8 <= kResizeSeg;
+  const uint32_t a0 = sb & ~3u;  // dword-aligned start (src_stride is a multiple of 4)
+  if (staged) {
+    const uint32_t nw = (se - a0 + 3) >> 2;
+    const DG_GLOBAL uint32_t *s4 = (const DG_GLOBAL uint32_t *)(srow + a0);
+    uint32_t *d4 = (uint32_t *)seg;
+    for (uint32_t i = threadIdx.x; i < nw; i += 256) d4[i] = s4[i];
+  }
+  __syncthreads();
+  DG_GLOBAL uint8_t *drow = gp<uint8_t>(ps.dst) + (size_t)y * ps.dst_stride;
+  const DG_GLOBAL int16_t *coef = gp<const int16_t>(ps.coef);
+  const int32_t prec = ps.precision;
+  if (staged) {
+    for (uint32_t x = x0 + threadIdx.x; x < x1; x += 256)
+      hconv(seg, (uint32_t)bounds[2 * x] * C - a0, bounds[2 * x + 1], coef + (size_t)x * ps.ksize, C,
+            prec, drow + (size_t)x * C);
+  } else {  // extreme downscale: segment larger than LDS, read the row directly
+    for (uint32_t x = x0 + threadIdx.x; x < x1; x += 256)
+      hconv(srow, (uint32_t)bounds[2 * x] * C, bounds[2 * x + 1], coef + (size_t)x * ps.ksize, C,
+            prec, drow + (size_t)x * C);
+  }
+}
+
+// Vertical pass: each thread produces 16 consecutive bytes of one output row
+// (channel-agnostic), one 16-byte load per tap: a wave streams 1 KiB of a
+// source row per tap.
 __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ imgs,
                                                   const WgItem *__restrict__ list, int stage) {
   const WgItem it = list[blockIdx.x];
   const ResizePass &ps = imgs[it.image].pass[stage];
   const uint32_t rowbytes = ps.width * ps.C;
-  const uint32_t units = (rowbytes + 3) / 4;
+  const uint32_t units = (rowbytes + 15) / 16;
   const uint32_t idx = it.item0 + threadIdx.x;
   if (idx >= units * ps.rows) return;
   const uint32_t y = idx / units, u = idx - y * units;
-  const uint32_t b0 = u * 4;
-  const uint32_t nb = rowbytes - b0 < 4 ? rowbytes - b0 : 4;
-  const int2 bd = ((const int2 *)ps.bounds)[y];
-  const int16_t *k = (const int16_t *)ps.coef + (size_t)y * ps.ksize;
+  const uint32_t b0 = u * 16;
+  const uint32_t nb = rowbytes - b0 < 16 ? rowbytes - b0 : 16;
+  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds);
+  const int32_t start = bounds[2 * y], n = bounds[2 * y + 1];
+  const DG_GLOBAL int16_t *k = gp<const int16_t>(ps.coef) + (size_t)y * ps.ksize;
   const int32_t prec = ps.precision, bias = 1 << (prec - 1);
-  int32_t a0 = bias, a1 = bias, a2 = bias, a3 = bias;
-  const uint8_t *src = (const uint8_t *)ps.src + (size_t)(bd.x - (int32_t)ps.row0) * ps.src_stride + b0;
-  const bool aligned = ((ps.src_stride & 3) == 0) && nb == 4;
-  for (int32_t i = 0; i < bd.y; i++) {
-    int32_t w = k[i];
-    const uint8_t *s = src + (size_t)i * ps.src_stride;
-    if (aligned) {
-      uint32_t v = *(const uint32_t *)s;
-      a0 += (int32_t)(v & 0xFF) * w;
-      a1 += (int32_t)((v >> 8) & 0xFF) * w;
-      a2 += (int32_t)((v >> 16) & 0xFF) * w;
-      a3 += (int32_t)(v >> 24) * w;
-    } else {
-      a0 += (int32_t)s[0] * w;
-      if (nb > 1) a1 += (int32_t)s[1] * w;
-      if (nb > 2) a2 += (int32_t)s[2] * w;
-      if (nb > 3) a3 += (int32_t)s[3] * w;
+  int32_t a[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) a[j] = bias;
+  const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(start - (int32_t)ps.row0) * ps.src_stride + b0;
+  if (nb == 16 && (ps.src_stride & 15) == 0) {
+    for (int32_t i = 0; i < n; i++) {
+      const int32_t w = k[i];
+      const u32x4 v = *(const DG_GLOBAL u32x4 *)(src + (size_t)i * ps.src_stride);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t x = v[j];
+        a[4 * j] += (int32_t)(x & 0xFF) * w;
+        a[4 * j + 1] += (int32_t)((x >> 8) & 0xFF) * w;
+        a[4 * j + 2] += (int32_t)((x >> 16) & 0xFF) * w;
+        a[4 * j + 3] += (int32_t)(x >> 24) * w;
+      }
+    }
+  } else {
+    for (int32_t i = 0; i < n; i++) {
+      const int32_t w = k[i];
+      const DG_GLOBAL uint8_t *sr = src + (size_t)i * ps.src_stride;
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if ((uint32_t)j < nb) a[j] += (int32_t)sr[j] * w;
     }
   }
-  uint8_t *dst = (uint8_t *)ps.dst + (size_t)y * ps.dst_stride + b0;
-  uint32_t o = (uint32_t)clip_shift(a0, prec) | ((uint32_t)clip_shift(a1, prec) << 8) |
-               ((uint32_t)clip_shift(a2, prec) << 16) | ((uint32_t)clip_shift(a3, prec) << 24);
-  if (nb == 4 && ((ps.dst_stride & 3) == 0)) {
-    *(uint32_t *)dst = o;
+  uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 16; j++) o[j >> 2] |= (uint32_t)clip_shift(a[j], prec) << (8 * (j & 3));
+  DG_GLOBAL uint8_t *dst = gp<uint8_t>(ps.dst) + (size_t)y * ps.dst_stride + b0;
+  if (nb == 16 && (ps.dst_stride & 15) == 0) {
+    *(DG_GLOBAL u32x4 *)dst = u32x4{o[0], o[1], o[2], o[3]};
+  } else if (nb == 16 && (ps.dst_stride & 3) == 0) {
+    DG_GLOBAL uint32_t *d = (DG_GLOBAL uint32_t *)dst;
+    d[0] = o[0];
+    d[1] = o[1];
+    d[2] = o[2];
+    d[3] = o[3];
   } else {
-    for (uint32_t i = 0; i < nb; i++) dst[i] = (uint8_t)(o >> (8 * i));
+    for (uint32_t j = 0; j < nb; j++) dst[j] = (uint8_t)(o[j >> 2] >> (8 * (j & 3)));
   }
 }
 
@@ -606,8 +761,8 @@ __global__ __launch_bounds__(256) void k_copy(const ImageDesc *__restrict__ imgs
   const uint32_t idx = it.item0 + threadIdx.x;
   if (idx >= im.out_w * im.out_h) return;
   const uint32_t y = idx / im.out_w, x = idx - y * im.out_w;
-  const uint8_t *s = (const uint8_t *)im.final_src + (size_t)y * im.final_src_stride + (size_t)x * im.final_src_c;
-  uint8_t *d = (uint8_t *)im.out + (size_t)y * im.out_stride + (size_t)x * im.out_c;
+  const DG_GLOBAL uint8_t *s = gp<const uint8_t>(im.final_src) + (size_t)y * im.final_src_stride + (size_t)x * im.final_src_c;
+  DG_GLOBAL uint8_t *d = gp<uint8_t>(im.out) + (size_t)y * im.out_stride + (size_t)x * im.out_c;
   if (im.final_src_c == im.out_c) {
     for (uint32_t c = 0; c < im.out_c; c++) d[c] = s[c];
   } else {  // L8 -> RGB8 (image::DynamicImage::to_rgb8 replicates luma)
@@ -632,12 +787,12 @@ void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *l
   DG_LAUNCH(k_destuff_write, nwg, st, imgs, list);
 }
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                      const HuffTable *pool, SubState *subs, BatchFlags *flags) {
-  DG_LAUNCH(k_huff_sync, nwg, st, imgs, list, pool, subs, flags);
+                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags) {
+  DG_LAUNCH(k_huff_sync, nwg, st, imgs, list, pool, subs, ck, flags);
 }
 void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                     const HuffTable *pool, SubState *subs, BatchFlags *flags) {
-  DG_LAUNCH(k_huff_fix, nwg, st, imgs, list, pool, subs, flags);
+                     const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags) {
+  DG_LAUNCH(k_huff_fix, nwg, st, imgs, list, pool, subs, ck, flags);
 }
 void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs) {
   DG_LAUNCH(k_huff_scan, nwg, st, imgs, list, subs);

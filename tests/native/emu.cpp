@@ -74,29 +74,38 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
   const uint8_t *scan = ds.data();
   const uint32_t *mkp = mk.data();
   std::vector<SubState> subs(d.nsub);
-  const uint32_t NW = (d.nsub + kSubPerWg - 1) / kSubPerWg;
+  const uint32_t NCK = num_ckpt(d.sub_bits);
+  std::vector<Ckpt> ck((size_t)d.nsub * (NCK ? NCK : 1));
+  const uint32_t U = kSubPerWg - 1;  // useful subsequences per workgroup (thread 0 = lead-in)
+  const uint32_t NW = (d.nsub + U - 1) / U;
   int64_t redo_total = 0, iters_max = 0, fix_wgs = 0, rounds = 0;
-  // ---- k_huff_sync
+  auto ckp = [&](uint32_t s) { return NCK ? &ck[(size_t)s * NCK] : (Ckpt *)nullptr; };
+  // ---- k_huff_sync (mirrors the kernel: threads in lockstep phases)
   for (uint32_t wg = 0; wg < NW; wg++) {
-    uint32_t s0 = wg * kSubPerWg;
-    uint32_t n = d.nsub - s0 < (uint32_t)kSubPerWg ? d.nsub - s0 : kSubPerWg;
-    std::vector<uint32_t> ex(n), ins(n);
-    std::vector<RangeAcc> acc(n);
-    for (uint32_t t = 0; t < n; t++) {
+    const uint32_t s0 = wg * U;
+    std::vector<uint32_t> ex(kSubPerWg, 0), ins(kSubPerWg, 0);
+    std::vector<RangeAcc> acc(kSubPerWg);
+    std::vector<char> active(kSubPerWg, 0), head(kSubPerWg, 0);
+    for (uint32_t t = 0; t < (uint32_t)kSubPerWg; t++) {
+      int64_t si = (int64_t)s0 + t - 1;
+      active[t] = si >= 0 && si < (int64_t)d.nsub;
+      head[t] = (t == 0) || (s0 == 0 && t == 1);
+      if (!active[t]) continue;
       ins[t] = pack_state(0, 0, 0);
-      decode_range<false>(d, tabs.data(), scan, mkp, s0 + t, ins[t], acc[t], nullptr);
+      decode_range<false>(d, tabs.data(), scan, mkp, (uint32_t)si, ins[t], acc[t], nullptr, t ? ckp((uint32_t)si) : nullptr);
       ex[t] = acc[t].out;
     }
     int64_t it = 0;
     for (;;) {
-      std::vector<uint32_t> pin(n, 0);
-      std::vector<char> redo(n, 0);
+      std::vector<uint32_t> pin(kSubPerWg, 0);
+      std::vector<char> redo(kSubPerWg, 0);
       bool any = false;
-      for (uint32_t t = 1; t < n; t++)
-        if (ins[t] != ex[t - 1]) { redo[t] = 1; pin[t] = ex[t - 1]; any = true; }
-      for (uint32_t t = 1; t < n; t++)
+      for (uint32_t t = 1; t < (uint32_t)kSubPerWg; t++)
+        if (active[t] && !head[t] && ins[t] != ex[t - 1]) { redo[t] = 1; pin[t] = ex[t - 1]; any = true; }
+      for (uint32_t t = 1; t < (uint32_t)kSubPerWg; t++)
         if (redo[t]) {
-          decode_range<false>(d, tabs.data(), scan, mkp, s0 + t, pin[t], acc[t], nullptr);
+          uint32_t si = s0 + t - 1;
+          decode_range<false>(d, tabs.data(), scan, mkp, si, pin[t], acc[t], nullptr, ckp(si), true, ex[t]);
           ex[t] = acc[t].out;
           ins[t] = pin[t];
           redo_total++;
@@ -105,8 +114,9 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
       if (!any) break;
     }
     if (it > iters_max) iters_max = it;
-    for (uint32_t t = 0; t < n; t++) {
-      SubState &o = subs[s0 + t];
+    for (uint32_t t = 1; t < (uint32_t)kSubPerWg; t++) {
+      if (!active[t]) continue;
+      SubState &o = subs[s0 + t - 1];
       o.in = ins[t]; o.out = ex[t]; o.m = acc[t].m; o.n = acc[t].n;
       o.dc[0] = acc[t].dc[0]; o.dc[1] = acc[t].dc[1]; o.dc[2] = acc[t].dc[2];
     }
@@ -117,15 +127,19 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
     bool chain = false;
     std::vector<SubState> snap = subs;  // all workgroups read the launch-start values
     for (uint32_t wg = 1; wg < NW; wg++) {
-      uint32_t s0 = wg * kSubPerWg;
-      uint32_t n = d.nsub - s0 < (uint32_t)kSubPerWg ? d.nsub - s0 : kSubPerWg;
+      const uint32_t s0 = wg * U;
+      const uint32_t n = d.nsub - s0 < U ? d.nsub - s0 : U;
       uint32_t first_in = snap[s0 - 1].out;
       if (subs[s0].in == first_in) continue;
       fix_wgs++;
       std::vector<uint32_t> ex(n), ins(n);
       std::vector<RangeAcc> acc(n);
       std::vector<char> mine(n, 0);
-      for (uint32_t t = 0; t < n; t++) { ex[t] = subs[s0 + t].out; ins[t] = subs[s0 + t].in; }
+      for (uint32_t t = 0; t < n; t++) {
+        ex[t] = subs[s0 + t].out; ins[t] = subs[s0 + t].in;
+        acc[t].m = subs[s0 + t].m; acc[t].n = subs[s0 + t].n;
+        for (int c = 0; c < 3; c++) acc[t].dc[c] = subs[s0 + t].dc[c];
+      }
       uint32_t orig_last = ex[n - 1];
       for (;;) {
         std::vector<uint32_t> pin(n, 0);
@@ -137,7 +151,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
         }
         for (uint32_t t = 0; t < n; t++)
           if (redo[t]) {
-            decode_range<false>(d, tabs.data(), scan, mkp, s0 + t, pin[t], acc[t], nullptr);
+            decode_range<false>(d, tabs.data(), scan, mkp, s0 + t, pin[t], acc[t], nullptr, ckp(s0 + t), true, ex[t]);
             ex[t] = acc[t].out; ins[t] = pin[t]; mine[t] = 1; redo_total++;
           }
         if (!any) break;
@@ -148,7 +162,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
           o.in = ins[t]; o.out = ex[t]; o.m = acc[t].m; o.n = acc[t].n;
           o.dc[0] = acc[t].dc[0]; o.dc[1] = acc[t].dc[1]; o.dc[2] = acc[t].dc[2];
         }
-      if (n == (uint32_t)kSubPerWg && s0 + n < d.nsub && ex[n - 1] != orig_last) chain = true;
+      if (n == U && s0 + n < d.nsub && ex[n - 1] != orig_last) chain = true;
     }
     if (!chain || rounds > 64) break;
   }

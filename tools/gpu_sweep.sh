@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/sweep
 mkdir -p $OUT
-for cfg in ${SWEEP:-"1024:64 2048:64 4096:64 2048:256"}; do
+for cfg in ${SWEEP:-1024:64 2048:64 4096:64 2048:256}; do
   sb=${cfg%%:*}; bt=${cfg##*:}
   echo "=== sub_bits=$sb batch=$bt"
   timeout -k 10 300 python bench.py --steps ${STEPS:-8} --warmup 2 --batch $bt --pool ${POOL:-256} --sub-bits $sb \
