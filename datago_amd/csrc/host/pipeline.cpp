@@ -98,6 +98,14 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     timing_ = v != 0;
     return DG_OK;
   }
+  if (k == "side_stream") {
+    side_stream_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "debug_flags") {
+    debug_flags_ = (int)v;
+    return DG_OK;
+  }
   return DG_ERR_INVALID;
 }
 
@@ -661,10 +669,11 @@ dg_status Context::launch_all(Batch &b, bool from_fix) {
   if (!from_fix) {
     // Lanczos coefficient tables depend only on the plan: compute them on a
     // side stream, overlapped with the entropy decode.
+    hipStream_t cs = side_stream_ ? side_ : stream_;
     HIPCHK(hipEventRecord(ev_meta_, stream_));
-    HIPCHK(hipStreamWaitEvent(side_, ev_meta_, 0));
-    launch_coeffs(side_, dm, lst(L_COEF), cnt(L_COEF));
-    HIPCHK(hipEventRecord(ev_coef_, side_));
+    HIPCHK(hipStreamWaitEvent(cs, ev_meta_, 0));
+    launch_coeffs(cs, dm, lst(L_COEF), cnt(L_COEF));
+    HIPCHK(hipEventRecord(ev_coef_, cs));
     launch_destuff_count(stream_, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
     launch_destuff_scan(stream_, dm, lst(L_SCAN), cnt(L_SCAN));
     launch_destuff_write(stream_, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
@@ -685,11 +694,11 @@ dg_status Context::launch_all(Batch &b, bool from_fix) {
   launch_color(stream_, dd, lst(L_COLOR), cnt(L_COLOR));
   if (ev(9)) return DG_ERR_DEVICE;
   HIPCHK(hipStreamWaitEvent(stream_, ev_coef_, 0));
-  launch_resize_h(stream_, dd, lst(L_RH0), cnt(L_RH0), 0);
+  launch_resize_h(stream_, dd, lst(L_RH0), cnt(L_RH0), 0 | (debug_flags_ << 8));
   if (ev(10)) return DG_ERR_DEVICE;
   launch_resize_v(stream_, dd, lst(L_RV1), cnt(L_RV1), 1);
   if (ev(11)) return DG_ERR_DEVICE;
-  launch_resize_h(stream_, dd, lst(L_RH2), cnt(L_RH2), 2);
+  launch_resize_h(stream_, dd, lst(L_RH2), cnt(L_RH2), 2 | (debug_flags_ << 8));
   if (ev(12)) return DG_ERR_DEVICE;
   launch_resize_v(stream_, dd, lst(L_RV3), cnt(L_RV3), 3);
   if (ev(13)) return DG_ERR_DEVICE;

@@ -114,6 +114,8 @@ class Context {
 
   uint32_t sub_bits_ = kDefaultSubBits;
   bool timing_ = false;
+  bool side_stream_ = true;
+  int debug_flags_ = 0;
   std::vector<hipEvent_t> events_;
   // stats
   int64_t stat_batches_ = 0, stat_resync_ = 0, stat_fix_ = 0, stat_mismatch_ = 0, stat_iters_ = 0;

@@ -553,6 +553,18 @@ __global__ __launch_bounds__(256) void k_color(const ImageDesc *__restrict__ img
 
 // ------------------------------------------------------------ resize
 
+// Pack the low bytes of four values into one dword with explicit v_perm byte
+// selects.  Plain shift/or packing of clamped values lets hipcc (ROCm 7.2,
+// gfx950) fuse pairs into v_ashr_pk_u8_i32 and then OR the next byte into
+// bits 16..23 of that register, whose upper half still holds the old
+// accumulator bits: byte 2 of every 4 came out corrupted.  v_perm only takes
+// the selected bytes.
+__device__ __forceinline__ uint32_t pack4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+  const uint32_t lo = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u);  // [b0, b1, 0, 0]
+  const uint32_t hi = __builtin_amdgcn_perm(b3, b2, 0x0c0c0400u);  // [b2, b3, 0, 0]
+  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);               // [b0, b1, b2, b3]
+}
+
 __device__ __forceinline__ uint8_t clip_shift(int32_t acc, int32_t prec) {
   int32_t v = acc >> prec;
   return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
@@ -657,8 +669,9 @@ __device__ __forceinline__ void hconv(P s, uint32_t off, int32_t n, const DG_GLO
 constexpr uint32_t kResizeSeg = 24576;  // LDS bytes for the staged source segment
 
 __global__ __launch_bounds__(256) void k_resize_h(const ImageDesc *__restrict__ imgs,
-                                                  const WgItem *__restrict__ list, int stage) {
+                                                  const WgItem *__restrict__ list, int stage_flags) {
   __shared__ __attribute__((aligned(16))) uint8_t seg[kResizeSeg + 16];
+  const int stage = stage_flags & 0xFF;
   const WgItem it = list[blockIdx.x];
   const ResizePass &ps = imgs[it.image].pass[stage];
   const uint32_t tiles = (ps.width + kResizeTile - 1) / kResizeTile;
@@ -671,7 +684,7 @@ __global__ __launch_bounds__(256) void k_resize_h(const ImageDesc *__restrict__ 
   const uint32_t sb = (uint32_t)bounds[2 * x0] * C;
   const uint32_t se = (uint32_t)(bounds[2 * (x1 - 1)] + bounds[2 * (x1 - 1) + 1]) * C;  // source bytes [sb, se)
   const DG_GLOBAL uint8_t *srow = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y) * ps.src_stride;
-  const bool staged = se - sb + 8 <= kResizeSeg;
+  const bool staged = se - sb + 8 <= kResizeSeg && !(stage_flags & 0x100);
   const uint32_t a0 = sb & ~3u;  // dword-aligned start (src_stride is a multiple of 4)
   if (staged) {
     const uint32_t nw = (se - a0 + 3) >> 2;
@@ -738,9 +751,11 @@ __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ 
         if ((uint32_t)j < nb) a[j] += (int32_t)sr[j] * w;
     }
   }
-  uint32_t o[4] = {0, 0, 0, 0};
+  uint32_t o[4];
 #pragma unroll
-  for (int j = 0; j < 16; j++) o[j >> 2] |= (uint32_t)clip_shift(a[j], prec) << (8 * (j & 3));
+  for (int j = 0; j < 4; j++)
+    o[j] = pack4(clip_shift(a[4 * j], prec), clip_shift(a[4 * j + 1], prec), clip_shift(a[4 * j + 2], prec),
+                 clip_shift(a[4 * j + 3], prec));
   DG_GLOBAL uint8_t *dst = gp<uint8_t>(ps.dst) + (size_t)y * ps.dst_stride + b0;
   if (nb == 16 && (ps.dst_stride & 15) == 0) {
     *(DG_GLOBAL u32x4 *)dst = u32x4{o[0], o[1], o[2], o[3]};
