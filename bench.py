@@ -96,6 +96,43 @@ def cpu_baseline(pool, targets, seconds: float):
                       f"decode + FIR-mode Lanczos3 crop_and_resize), {cores} processes, {wall:.1f} s"}
 
 
+# ------------------------------------------------------------- roofline
+
+def stage_bytes(L, data: bytes, dim, target) -> dict:
+    """Algorithmic bytes each kernel stage must move for one image (DESIGN.md
+    §Roofline): its minimal input + output, intermediates counted once."""
+    from oracle import buckets as B
+    w, h, nc = dim
+    tw, th = target
+    st, info = L.probe(data)
+    S = len(data)
+    if nc == 1:
+        nblk = ((w + 7) // 8) * ((h + 7) // 8)
+    else:
+        hm = max(info.h_samp[:3]); vm = max(info.v_samp[:3])
+        mcus = -(-w // (8 * hm)) * -(-h // (8 * vm))
+        nblk = mcus * sum(info.h_samp[c] * info.v_samp[c] for c in range(3))
+    b = {"destuff": 2 * S, "huff_sync": S, "huff_fix": 0.0, "huff_scan": 0.0,
+         "huff_write": S + 128 * nblk, "idct": 128 * nblk + 64 * nblk,
+         "color": (64 * nblk + 3 * w * h) if nc == 3 else 0.0, "coeffs": 0.0,
+         "resize_h1": 0.0, "resize_v1": 0.0, "resize_h2": 0.0, "resize_v2": 0.0, "copy": 0.0}
+    if (w, h) != (tw, th):
+        nw, nh = B.scaled_size(w, h, tw, th)
+        cw = w
+        if nw != w:
+            b["resize_h1"] = nc * (w * h + nw * h)
+            cw = nw
+        if nh != h:
+            b["resize_v1"] = nc * (cw * h + cw * nh)
+        if tw != nw:
+            b["resize_h2"] = nc * (nw * nh + tw * nh)
+        if th != nh:
+            b["resize_v2"] = nc * (tw * nh + tw * th)
+    else:
+        b["copy"] = 2 * nc * w * h
+    return b
+
+
 # ------------------------------------------------------------------- main
 
 def main() -> int:
@@ -144,60 +181,78 @@ def main() -> int:
     ctx.h2d(d_arena, host_arena)
     h_base = host_arena.ctypes.data
     out_bytes = [tw * th * nc for (tw, th), (_, _, nc) in zip(targets, dims)]
+    img_stage_bytes = [stage_bytes(L, d, dim, tgt) for d, dim, tgt in zip(pool, dims, targets)]
     B_ = min(a.batch, 1 << 16)
     # output arena for one step (reused), sized for the largest B_ outputs
     out_cap = sum(sorted(out_bytes)[-B_:]) + 16 * B_
-    d_out = ctx.alloc(out_cap)
+    d_out = [ctx.alloc(out_cap), ctx.alloc(out_cap)]
 
-    def step(k: int):
+    def submit(k: int):
         idx = [(k * B_ + j) % len(pool) for j in range(B_)]
         hp = [h_base + offs[i] for i in idx]
         dp = [d_arena + offs[i] for i in idx]
         lens = [len(pool[i]) for i in idx]
         outs, caps, oo = [], [], 0
+        slot = k & 1  # two output arenas: batch k+1 is planned while batch k runs
         for i in idx:
-            outs.append(d_out + oo)
+            outs.append(d_out[slot] + oo)
             caps.append(out_bytes[i])
             oo += (out_bytes[i] + 15) // 16 * 16
         ticket, metas = ctx.submit_device(hp, dp, lens, outs, caps)
+        return ticket, metas, idx
+
+    def complete(pend):
+        ticket, metas, idx = pend
         ctx.wait(ticket)
-        px = 0
         for j, i in enumerate(idx):
             if metas[j].status != 0:
                 raise RuntimeError(f"image {i} status {metas[j].status}: {L.last_error()}")
-            px += dims[i][0] * dims[i][1]
-        return px, sum(dims[i][0] * dims[i][1] for i in idx), idx
+        return idx
 
-    for k in range(a.warmup):
-        step(k)
+    def run(k0: int, n: int, on_done=None):
+        pend = submit(k0)
+        for k in range(k0 + 1, k0 + n):
+            nxt = submit(k)
+            idx = complete(pend)
+            if on_done:
+                on_done(idx)
+            pend = nxt
+        idx = complete(pend)
+        if on_done:
+            on_done(idx)
+
+    run(0, max(1, a.warmup))
     # ---- timed region
     ctx.set_option("timing", 1)
     stage_tot = {}
+    stage_alg = {}
+    acc = {"px": 0, "alg": 0.0, "coded": 0, "outpx": 0}
+
+    def on_done(idx):
+        for i in idx:
+            for kk, vv in img_stage_bytes[i].items():
+                stage_alg[kk] = stage_alg.get(kk, 0.0) + vv
+            w, h, nc = dims[i]
+            tw, th = targets[i]
+            acc["px"] += w * h
+            acc["coded"] += len(pool[i])
+            acc["alg"] += len(pool[i]) + nc * w * h + nc * tw * th  # SURVEY §8(d) B_alg
+            acc["outpx"] += tw * th
+        for name, ms in ctx.timings().items():
+            stage_tot[name] = stage_tot.get(name, 0.0) + ms
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ctx.synchronize()
     t0 = time.perf_counter()
-    px_total = 0
-    alg_bytes = 0.0
-    coded_bytes = 0
-    out_px = 0
-    for k in range(a.steps):
-        px, _, idx = step(a.warmup + k)
-        px_total += px
-        for i in idx:
-            w, h, nc = dims[i]
-            tw, th = targets[i]
-            coded_bytes += len(pool[i])
-            alg_bytes += len(pool[i]) + nc * w * h + nc * tw * th  # SURVEY §8(d) B_alg
-            out_px += tw * th
-        for name, ms in ctx.timings().items():
-            stage_tot[name] = stage_tot.get(name, 0.0) + ms
+    run(max(1, a.warmup), a.steps, on_done)
     ctx.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    px_total, alg_bytes, coded_bytes, out_px = acc["px"], acc["alg"], acc["coded"], acc["outpx"]
     ctx.set_option("timing", 0)
     # max over ranks; totals over ranks
     vals = torch.tensor([dt, float(px_total), alg_bytes, float(out_px)], dtype=torch.float64)
@@ -229,33 +284,8 @@ def main() -> int:
         kern = {k: v for k, v in stage_tot.items() if k not in ("upload", "download")}
         dom = max(kern, key=kern.get)
         dom_ms = kern[dom] / steps
-        nblk_bytes = 0
-        for k in range(a.steps):
-            for j in range(B_):
-                i = (a.warmup + k) * B_ + j
-                i %= len(pool)
         per_step_alg = alg_bytes / steps
-        # algorithmic bytes of the dominant stage per launch
-        coded_step = coded_bytes / steps
-        dom_alg = {
-            "huff_sync": coded_step, "huff_fix": coded_step, "huff_write": None, "idct": None,
-        }.get(dom, None)
-        pix_step = px_total / steps
-        outpx_step = out_px / steps
-        mean_c = np.mean([c for (_, _, c) in dims])
-        blk_per_px = 1.5  # 4:2:0-dominated mix (6 blocks / 256 px); exact count in DESIGN.md
-        if dom == "huff_write":
-            dom_alg = coded_step + 128.0 * blk_per_px * pix_step / 64.0
-        elif dom == "huff_sync" or dom == "huff_fix":
-            dom_alg = coded_step
-        elif dom == "idct":
-            dom_alg = 192.0 * blk_per_px * pix_step / 64.0
-        elif dom == "color":
-            dom_alg = (1.5 + 3.0) * pix_step
-        elif dom.startswith("resize"):
-            dom_alg = mean_c * (pix_step + outpx_step)
-        elif dom == "coeffs":
-            dom_alg = 0.0
+        dom_alg = stage_alg[dom] / steps if dom in stage_alg else 0.0
         achieved = dom_alg / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
         gpu_ms = sum(kern.values()) / steps
         result = {
@@ -301,7 +331,8 @@ def main() -> int:
             with open(a.out, "w") as f:
                 f.write(line + "\n")
     ctx.free(d_arena)
-    ctx.free(d_out)
+    for p_ in d_out:
+        ctx.free(p_)
     ctx.close()
     if world > 1:
         dist.barrier()

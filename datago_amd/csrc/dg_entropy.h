@@ -67,8 +67,12 @@ DG_HD void bw_seek(BitWin &b, uint32_t pos) {
 template <class T>
 DG_HD uint32_t huff_lookup(const T &t, uint32_t bits) {
   uint32_t e = t.lut[bits >> (32 - kLutBits)];
-  if (e) return e;
-  uint32_t pk = bits >> 16;
+  if (!(e & 0x8000u) && e) return e;
+  if (e & 0x8000u) {
+    uint32_t e2 = t.sub[e & (kMaxSubTables - 1)][(bits >> (32 - 16)) & ((1u << kSubBits) - 1)];
+    return e2 ? e2 : (16u << 8);
+  }
+  uint32_t pk = bits >> 16;  // fallback for tables with many long prefixes
   for (int32_t l = kLutBits + 1; l <= 16; l++)
     if (pk < t.lim[l]) return ((uint32_t)l << 8) | t.vals[(t.valoff[l] + (int32_t)(pk >> (16 - l))) & 255];
   return 16u << 8;  // invalid code: consume 16 bits (only off-sync / past the data)
@@ -190,7 +194,8 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
   const uint32_t slotmap = im.slotmap;  // 4 bits per (component, dc/ac)
   BitWin b;
   bw_init(b, stream, pos < a1 ? pos : a0);
-  uint32_t comp = im.blk_comp[r];
+  const uint32_t cbits = im.comp_bits;
+  uint32_t comp = (cbits >> (2 * r)) & 3u;
   const uint32_t nck = ck ? num_ckpt(S) : 0;
   uint32_t k = 0, cpos = a0 + kCkptBits;
   bool merged = false;
@@ -205,7 +210,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       pos = mpos;
       r = 0;
       z = 0;
-      comp = im.blk_comp[0];
+      comp = cbits & 3u;
       if (owned) {
         acc.m++;
         acc.n = 0;
@@ -284,7 +289,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       if (WRITE) wc_flush(*w, 64);
       z = 0;
       r = (r + 1 == bpm) ? 0 : r + 1;
-      comp = im.blk_comp[r];
+      comp = (cbits >> (2 * r)) & 3u;
     }
   }
   if (WRITE && z > 0) wc_flush(*w, z);

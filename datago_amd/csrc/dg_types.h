@@ -35,7 +35,7 @@ DG_HD void add3(int32_t v[3], uint32_t c, int32_t d) {
   v[2] += c == 2 ? d : 0;
 }
 
-constexpr int kLutBits = 9;          // Huffman fast-lookup width
+constexpr int kLutBits = 9;          // Huffman first-level lookup width
 constexpr int kMaxSlots = 6;         // Huffman tables per image (DC/AC x 3 components)
 constexpr int kSubPerWg = 256;       // entropy subsequences per workgroup (= threads)
 constexpr int kDefaultSubBits = 2048; // destuffed bits per subsequence
@@ -43,10 +43,18 @@ constexpr int kDestuffChunk = 4096;   // raw bytes per destuff workgroup (256 x 
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 
 // Canonical Huffman table for the GPU decoder (built on the host, pooled).
+// Two-level lookup: the first kLutBits bits index lut[]; codes longer than
+// that (JPEG allows 16) continue in a 7-bit subtable selected by the entry.
+//   lut entry: (len << 8) | symbol          for codes of length <= kLutBits
+//              0x8000 | subtable index      when the prefix starts a long code
+//              0                            invalid prefix / fallback below
+constexpr int kSubBits = 16 - kLutBits;   // 7
+constexpr int kMaxSubTables = 8;
 struct HuffTable {
-  uint16_t lut[1 << kLutBits];  // (len << 8) | symbol for codes of length <= kLutBits; 0 = longer
-  uint32_t lim[17];             // lim[l]: exclusive bound on the left-justified 16-bit peek for length l
-  int32_t valoff[17];           // symbol = vals[valoff[l] + (peek16 >> (16 - l))]
+  uint16_t lut[1 << kLutBits];
+  uint16_t sub[kMaxSubTables][1 << kSubBits];  // (len << 8) | symbol, 0 = invalid
+  uint32_t lim[17];             // fallback (more long prefixes than subtables)
+  int32_t valoff[17];
   uint8_t vals[256];
 };
 
@@ -116,7 +124,8 @@ struct ImageDesc {
   uint32_t blocks_per_seg;  // restart * bpm, 0 = unlimited
   uint32_t total_blocks;
   uint32_t bpm;             // blocks per MCU
-  uint8_t blk_comp[12];     // component of block k within an MCU
+  uint32_t comp_bits;       // component of block k within an MCU at bits 2k..2k+1
+  uint8_t blk_comp[12];     // same, unpacked (host side / IDCT)
   uint16_t hslot[kMaxSlots];  // pool index of Huffman slot s
   uint8_t ncomp, colorspace, dec_c, nslots;  // dec_c: channels of the decoded image
   uint16_t qpool[3];

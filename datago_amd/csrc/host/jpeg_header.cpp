@@ -200,6 +200,7 @@ bool build_huff_table(const HuffSpec &spec, HuffTable &out) {
     out.valoff[l] = valptr[l] - mincode[l];
   }
   memcpy(out.vals, spec.vals, 256);
+  // first level: codes of length <= kLutBits
   for (uint32_t pfx = 0; pfx < (1u << kLutBits); pfx++) {
     for (int l = 1; l <= kLutBits; l++) {
       int32_t c = (int32_t)(pfx >> (kLutBits - l));
@@ -209,6 +210,36 @@ bool build_huff_table(const HuffSpec &spec, HuffTable &out) {
       }
     }
   }
+  // second level: every 16-bit peek whose first kLutBits bits are not a
+  // complete code; subtables are allocated per such prefix (up to kMaxSubTables)
+  int nsub = 0;
+  bool overflow = false;
+  for (uint32_t pfx = 0; pfx < (1u << kLutBits); pfx++) {
+    if (out.lut[pfx]) continue;
+    uint16_t tmp[1 << kSubBits];
+    bool any = false;
+    for (uint32_t lo = 0; lo < (1u << kSubBits); lo++) {
+      uint32_t pk = (pfx << kSubBits) | lo;  // 16-bit peek
+      tmp[lo] = 0;
+      for (int l = kLutBits + 1; l <= 16; l++) {
+        int32_t c = (int32_t)(pk >> (16 - l));
+        if (spec.bits[l] && c <= maxcode[l]) {
+          if (c >= mincode[l]) tmp[lo] = (uint16_t)((l << 8) | spec.vals[(valptr[l] + c - mincode[l]) & 255]);
+          break;
+        }
+      }
+      any |= tmp[lo] != 0;
+    }
+    if (!any) continue;  // invalid prefix: stays 0 (fallback returns "invalid" too)
+    if (nsub == kMaxSubTables) {
+      overflow = true;
+      continue;
+    }
+    memcpy(out.sub[nsub], tmp, sizeof(tmp));
+    out.lut[pfx] = (uint16_t)(0x8000u | (uint32_t)nsub);
+    nsub++;
+  }
+  (void)overflow;  // prefixes beyond kMaxSubTables keep lut = 0 and use the lim[] fallback
   return true;
 }
 

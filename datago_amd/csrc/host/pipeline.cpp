@@ -45,11 +45,16 @@ Context::Context(int device, const dg_image_config *cfg) : device_(device) {
 Context::~Context() {
   hipSetDevice(device_);
   if (stream_) hipStreamSynchronize(stream_);
-  for (auto e : events_) hipEventDestroy(e);
-  for (DevBuf *b : {&d_hpool_, &d_qpool_, &d_scratch_, &d_meta_, &d_input_})
+  for (DevBuf *b : {&d_hpool_, &d_qpool_})
     if (b->p) hipFree(b->p);
-  for (PinBuf *b : {&h_stage_, &h_out_})
-    if (b->p) hipHostFree(b->p);
+  for (Slot &sl : slots_) {
+    for (auto e : sl.ev) hipEventDestroy(e);
+    if (sl.done) hipEventDestroy(sl.done);
+    for (DevBuf *b : {&sl.scratch, &sl.meta, &sl.input})
+      if (b->p) hipFree(b->p);
+    for (PinBuf *b : {&sl.stage, &sl.out})
+      if (b->p) hipHostFree(b->p);
+  }
   if (side_) hipStreamSynchronize(side_);
   if (ev_meta_) hipEventDestroy(ev_meta_);
   if (ev_coef_) hipEventDestroy(ev_coef_);
@@ -83,8 +88,11 @@ dg_status Context::init() {
   HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&ev_meta_, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&ev_coef_, hipEventDisableTiming));
-  events_.resize(17);
-  for (auto &e : events_) HIPCHK(hipEventCreate(&e));
+  for (Slot &sl : slots_) {
+    sl.ev.resize(17);
+    for (auto &e : sl.ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  }
   return DG_OK;
 }
 
@@ -298,8 +306,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     return DG_ERR_INVALID;
   }
   HIPCHK(hipSetDevice(device_));
-  if (cur_ && !cur_->done) {
-    dg_status st = finish(*cur_);
+  Slot &sl = slots_[next_slot_];
+  if (sl.batch && !sl.batch->done) {  // this slot's previous batch must complete first
+    dg_status st = finish(sl);
     if (st) return st;
   }
   std::unique_ptr<Batch> bp(new Batch());
@@ -408,6 +417,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       }
     }
     d.bpm = bpm;
+    d.comp_bits = 0;
+    for (uint32_t k = 0; k < bpm; k++) d.comp_bits |= (uint32_t)d.blk_comp[k] << (2 * k);
     d.total_blocks = h.ncomp == 1 ? d.cbw[0] * d.cbh[0] : d.mcux * d.mcuy * bpm;
     d.restart = (uint32_t)h.restart;
     d.blocks_per_seg = d.restart * bpm;
@@ -542,22 +553,22 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   b.total_subs = sub_base;
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
-  ckpt_off_ = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits_)) * sizeof(Ckpt));
-  st = ensure(d_scratch_, L.off + 256);
+  const size_t ckpt_off = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits_)) * sizeof(Ckpt));
+  st = ensure(sl.scratch, L.off + 256);
   if (st) return st;
   if (host_io) {
-    st = ensure(d_input_, IN.off + 64);
+    st = ensure(sl.input, IN.off + 64);
     if (st) return st;
   }
   // ---- 4. patch device addresses
-  char *S = (char *)d_scratch_.p;
+  char *S = (char *)sl.scratch.p;
   int k = 0;
   for (int i = 0; i < n; i++) {
     if (b.desc_of[i] < 0) continue;
     ImageDesc &d = b.descs[b.desc_of[i]];
     const Offs &o = offs[k++];
     const JpegHeader &h = b.plans[i].hdr;
-    const uint8_t *src = host_io ? (const uint8_t *)d_input_.p + in_off[i] : d_srcs[i];
+    const uint8_t *src = host_io ? (const uint8_t *)sl.input.p + in_off[i] : d_srcs[i];
     d.scan = (uint64_t)(uintptr_t)(src + h.scan_off);
     d.coef = (uint64_t)(uintptr_t)(S + o.coef);
     d.ds = (uint64_t)(uintptr_t)(S + o.ds);
@@ -619,12 +630,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.desc_off = M.take(b.descs.size() * sizeof(ImageDesc));
   for (int l = 0; l < L_COUNT; l++) b.list_off[l] = M.take(b.lists[l].size() * sizeof(WgItem));
   b.meta_bytes = M.off;
-  st = ensure(d_meta_, b.meta_bytes + 256);
+  st = ensure(sl.meta, b.meta_bytes + 256);
   if (st) return st;
   size_t stage_bytes = b.meta_bytes + (host_io ? IN.off : 0);
-  st = ensure_pinned(h_stage_, stage_bytes + 256);
+  st = ensure_pinned(sl.stage, stage_bytes + 256);
   if (st) return st;
-  char *P = (char *)h_stage_.p;
+  char *P = (char *)sl.stage.p;
   memset(P + b.flags_off, 0, sizeof(BatchFlags));
   memcpy(P + b.desc_off, b.descs.data(), b.descs.size() * sizeof(ImageDesc));
   for (int l = 0; l < L_COUNT; l++)
@@ -633,35 +644,38 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     for (int i = 0; i < n; i++)
       if (b.desc_of[i] >= 0) memcpy(P + b.meta_bytes + in_off[i], h_srcs[i], lens[i]);
   }
-  if (timing_) HIPCHK(hipEventRecord(events_[0], stream_));
-  HIPCHK(hipMemcpyAsync(d_meta_.p, P, b.meta_bytes, hipMemcpyHostToDevice, stream_));
-  if (host_io && IN.off) HIPCHK(hipMemcpyAsync(d_input_.p, P + b.meta_bytes, IN.off, hipMemcpyHostToDevice, stream_));
+  if (timing_) HIPCHK(hipEventRecord(sl.ev[0], stream_));
+  HIPCHK(hipMemcpyAsync(sl.meta.p, P, b.meta_bytes, hipMemcpyHostToDevice, stream_));
+  if (host_io && IN.off) HIPCHK(hipMemcpyAsync(sl.input.p, P + b.meta_bytes, IN.off, hipMemcpyHostToDevice, stream_));
   b.stage_ms.clear();
-  subs_off_ = subs_off;  // SubStates live in the scratch arena
+  sl.subs_off = subs_off;  // SubStates and checkpoints live in the scratch arena
+  sl.ckpt_off = ckpt_off;
   if (host_io) {
     b.host_outs.assign(outs, outs + n);
     b.host_caps.assign(caps, caps + n);
   }
-  st = launch_all(b, false);
+  sl.batch = std::move(bp);
+  st = launch_all(sl, false);
   if (st) return st;
   stat_batches_++;
-  *ticket = b.ticket;
-  cur_ = std::move(bp);
+  *ticket = sl.batch->ticket;
+  next_slot_ ^= 1;
   return DG_OK;
 }
 
-dg_status Context::launch_all(Batch &b, bool from_fix) {
-  char *M = (char *)d_meta_.p;
+dg_status Context::launch_all(Slot &sl, bool from_fix) {
+  Batch &b = *sl.batch;
+  char *M = (char *)sl.meta.p;
   const ImageDesc *dd = (const ImageDesc *)(M + b.desc_off);
   ImageDesc *dm = (ImageDesc *)(M + b.desc_off);
   BatchFlags *fl = (BatchFlags *)(M + b.flags_off);
-  SubState *subs = (SubState *)((char *)d_scratch_.p + subs_off_);
+  SubState *subs = (SubState *)((char *)sl.scratch.p + sl.subs_off);
   const HuffTable *hp = (const HuffTable *)d_hpool_.p;
   const QuantTable *qp = (const QuantTable *)d_qpool_.p;
   auto lst = [&](int l) { return (const WgItem *)(M + b.list_off[l]); };
   auto cnt = [&](int l) { return (uint32_t)b.lists[l].size(); };
   auto ev = [&](int i) -> dg_status {
-    if (timing_) HIPCHK(hipEventRecord(events_[i], stream_));
+    if (timing_) HIPCHK(hipEventRecord(sl.ev[i], stream_));
     return DG_OK;
   };
   if (from_fix) HIPCHK(hipMemsetAsync(fl, 0, sizeof(BatchFlags), stream_));
@@ -679,7 +693,7 @@ dg_status Context::launch_all(Batch &b, bool from_fix) {
     launch_destuff_write(stream_, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
   }
   if (ev(2)) return DG_ERR_DEVICE;
-  Ckpt *ck = (Ckpt *)((char *)d_scratch_.p + ckpt_off_);
+  Ckpt *ck = (Ckpt *)((char *)sl.scratch.p + sl.ckpt_off);
   if (!from_fix) launch_huff_sync(stream_, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
   if (ev(3)) return DG_ERR_DEVICE;
   launch_huff_fix(stream_, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
@@ -711,26 +725,28 @@ dg_status Context::launch_all(Batch &b, bool from_fix) {
   if (b.host_io)
     for (int i = 0; i < b.n; i++)
       if (b.desc_of[i] >= 0) total += align_up(b.plans[i].out_bytes, 16);
-  dg_status st = ensure_pinned(h_out_, total + 256);
+  dg_status st = ensure_pinned(sl.out, total + 256);
   if (st) return st;
-  HIPCHK(hipMemcpyAsync(h_out_.p, M, back, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipMemcpyAsync(sl.out.p, M, back, hipMemcpyDeviceToHost, stream_));
   if (b.host_io) {
     size_t off = align_up(back, 256);
     for (int i = 0; i < b.n; i++) {
       if (b.desc_of[i] < 0) continue;
-      HIPCHK(hipMemcpyAsync((char *)h_out_.p + off, (char *)d_scratch_.p + b.out_dev_off[i], b.plans[i].out_bytes,
+      HIPCHK(hipMemcpyAsync((char *)sl.out.p + off, (char *)sl.scratch.p + b.out_dev_off[i], b.plans[i].out_bytes,
                             hipMemcpyDeviceToHost, stream_));
       off += align_up(b.plans[i].out_bytes, 16);
     }
   }
   if (ev(15)) return DG_ERR_DEVICE;
+  HIPCHK(hipEventRecord(sl.done, stream_));
   return DG_OK;
 }
 
-dg_status Context::finish(Batch &b) {
+dg_status Context::finish(Slot &sl) {
+  Batch &b = *sl.batch;
   for (;;) {
-    HIPCHK(hipStreamSynchronize(stream_));
-    memcpy(&b.flags, (char *)h_out_.p + b.flags_off, sizeof(BatchFlags));
+    HIPCHK(hipEventSynchronize(sl.done));
+    memcpy(&b.flags, (char *)sl.out.p + b.flags_off, sizeof(BatchFlags));
     stat_fix_ += b.flags.fix_count;
     stat_mismatch_ += b.flags.write_mismatch;
     stat_iters_ = std::max<int64_t>(stat_iters_, b.flags.sync_iters_max);
@@ -739,24 +755,24 @@ dg_status Context::finish(Batch &b) {
     // repair + everything downstream until the chain is stable
     b.resync_rounds++;
     stat_resync_++;
-    dg_status st = launch_all(b, true);
+    dg_status st = launch_all(sl, true);
     if (st) return st;
   }
   if (timing_) {
     last_ms_.assign(kNumStages, 0.f);
     for (int i = 0; i < kNumStages; i++) {
       float ms = 0.f;
-      if (hipEventElapsedTime(&ms, events_[i], events_[i + 1]) == hipSuccess) last_ms_[i] = ms;
+      if (hipEventElapsedTime(&ms, sl.ev[i], sl.ev[i + 1]) == hipSuccess) last_ms_[i] = ms;
     }
   }
-  const ImageDesc *back = (const ImageDesc *)((char *)h_out_.p + b.desc_off);
+  const ImageDesc *back = (const ImageDesc *)((char *)sl.out.p + b.desc_off);
   size_t off = align_up(b.desc_off + b.descs.size() * sizeof(ImageDesc), 256);
   for (int i = 0; i < b.n; i++) {
     if (b.desc_of[i] < 0) continue;
     int status = back[b.desc_of[i]].status;
     if (status) b.metas[i].status = status;
     if (b.host_io) {
-      if (!status) memcpy(b.host_outs[i], (char *)h_out_.p + off, b.plans[i].out_bytes);
+      if (!status) memcpy(b.host_outs[i], (char *)sl.out.p + off, b.plans[i].out_bytes);
       off += align_up(b.plans[i].out_bytes, 16);
     }
   }
@@ -764,18 +780,26 @@ dg_status Context::finish(Batch &b) {
   return DG_OK;
 }
 
+Slot *Context::find(uint64_t ticket) {
+  for (Slot &sl : slots_)
+    if (sl.batch && sl.batch->ticket == ticket) return &sl;
+  return nullptr;
+}
+
 dg_status Context::wait(uint64_t ticket) {
   std::lock_guard<std::mutex> lk(mu_);
   HIPCHK(hipSetDevice(device_));
-  if (!cur_ || cur_->ticket != ticket) return ticket < next_ticket_ ? DG_OK : DG_ERR_INVALID;
-  if (cur_->done) return DG_OK;
-  return finish(*cur_);
+  Slot *sl = find(ticket);
+  if (!sl) return ticket < next_ticket_ ? DG_OK : DG_ERR_INVALID;  // already recycled => completed
+  if (sl->batch->done) return DG_OK;
+  return finish(*sl);
 }
 
 dg_status Context::poll(uint64_t ticket) {
   std::lock_guard<std::mutex> lk(mu_);
-  if (!cur_ || cur_->ticket != ticket || cur_->done) return DG_OK;
-  hipError_t e = hipStreamQuery(stream_);
+  Slot *sl = find(ticket);
+  if (!sl || sl->batch->done) return DG_OK;
+  hipError_t e = hipEventQuery(sl->done);
   if (e == hipErrorNotReady) return DG_ERR_NOT_READY;
   return DG_OK;
 }

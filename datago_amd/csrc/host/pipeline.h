@@ -59,6 +59,17 @@ struct Batch {
   std::vector<float> stage_ms;
 };
 
+// One in-flight batch's device/pinned buffers.  Two slots let the host plan
+// and upload batch k+1 while the GPU still runs batch k.
+struct Slot {
+  DevBuf scratch, meta, input;
+  PinBuf stage, out;
+  std::vector<hipEvent_t> ev;  // per-stage timing events
+  hipEvent_t done = nullptr;   // recorded after the batch's last copy
+  std::unique_ptr<Batch> batch;
+  size_t subs_off = 0, ckpt_off = 0;
+};
+
 enum ListId { L_HUFF = 0, L_SYNC, L_DESTUFF, L_SCAN, L_IDCT, L_COLOR, L_COEF, L_RH0, L_RV1, L_RH2, L_RV3, L_COPY, L_COUNT };
 
 class Context {
@@ -88,8 +99,9 @@ class Context {
   dg_status ensure(DevBuf &b, size_t bytes);
   dg_status ensure_pinned(PinBuf &b, size_t bytes);
   dg_status upload_pools();
-  dg_status launch_all(Batch &b, bool from_fix);
-  dg_status finish(Batch &b);
+  dg_status launch_all(Slot &sl, bool from_fix);
+  dg_status finish(Slot &sl);
+  Slot *find(uint64_t ticket);
 
   int device_;
   bool has_cfg_ = false;
@@ -106,17 +118,14 @@ class Context {
   size_t hpool_uploaded_ = 0, qpool_uploaded_ = 0;
   DevBuf d_hpool_, d_qpool_;
 
-  DevBuf d_scratch_, d_meta_, d_input_;
-  PinBuf h_stage_, h_out_;
-  std::unique_ptr<Batch> cur_;
-  size_t subs_off_ = 0, ckpt_off_ = 0;
+  Slot slots_[2];
+  int next_slot_ = 0;
   uint64_t next_ticket_ = 1;
 
   uint32_t sub_bits_ = kDefaultSubBits;
   bool timing_ = false;
   bool side_stream_ = true;
   int debug_flags_ = 0;
-  std::vector<hipEvent_t> events_;
   // stats
   int64_t stat_batches_ = 0, stat_resync_ = 0, stat_fix_ = 0, stat_mismatch_ = 0, stat_iters_ = 0;
   std::vector<float> last_ms_;

@@ -41,6 +41,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
     }
   }
   d.bpm = bpm;
+  for (uint32_t k = 0; k < bpm; k++) d.comp_bits |= (uint32_t)d.blk_comp[k] << (2 * k);
   d.total_blocks = h.ncomp == 1 ? cbw0 * cbh0 : d.mcux * d.mcuy * bpm;
   d.restart = h.restart;
   d.blocks_per_seg = d.restart * bpm;
