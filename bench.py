@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="images per step")
+    ap.add_argument("--batch", type=int, default=256, help="images per step")
     ap.add_argument("--pool", type=int, default=256, help="unique images per rank held in HBM")
     ap.add_argument("--short-min", type=int, default=256)
     ap.add_argument("--short-max", type=int, default=2048)
@@ -148,15 +148,16 @@ def main() -> int:
     from datago_amd import synth
     from oracle import buckets as B
 
-    torch.cuda.set_device(local)
-    # ---- this rank's slice of the logical sample stream (generator_files.rs:24-42)
-    total_pool = a.pool * world
-    lo = rank * total_pool // world
+    from datago_amd.sharding import get_data_slice_multirank, max_over_ranks, sum_over_ranks
+    # ---- this rank's slice of the logical sample stream (generator_files.rs:24-42):
+    # a.pool images per rank, world * a.pool in total, contiguous slices
+    lo, hi = get_data_slice_multirank(a.pool * world, rank, world)
     workers = a.workers or cpu_share()
     t_gen = time.perf_counter()
     spec_seed = 2  # BASELINE configs[1] seed
-    pool = synth.mixed_corpus(spec_seed * 7919 + lo, a.pool, a.short_min, a.short_max, workers=workers)
+    pool = synth.mixed_corpus(spec_seed, a.pool * world, a.short_min, a.short_max, workers=workers, lo=lo, hi=hi)
     t_gen = time.perf_counter() - t_gen
+    torch.cuda.set_device(local)
     tr = B.ARAwareTransform(a.size, a.ratio, 0.5, 2.0)
     dims = []
     from oracle import oracle as O
@@ -255,16 +256,8 @@ def main() -> int:
     px_total, alg_bytes, coded_bytes, out_px = acc["px"], acc["alg"], acc["coded"], acc["outpx"]
     ctx.set_option("timing", 0)
     # max over ranks; totals over ranks
-    vals = torch.tensor([dt, float(px_total), alg_bytes, float(out_px)], dtype=torch.float64)
-    if world > 1:
-        tmax = vals[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tot = vals[1:].clone()
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        dt_max = float(tmax[0])
-        px_all, alg_all, outpx_all = (float(x) for x in tot)
-    else:
-        dt_max, px_all, alg_all, outpx_all = dt, float(px_total), alg_bytes, float(out_px)
+    (dt_max,) = max_over_ranks([dt], world)
+    px_all, alg_all, outpx_all = sum_over_ranks([float(px_total), alg_bytes, float(out_px)], world)
 
     # ---- end-to-end (host memory in and out: PCIe-inclusive), reported only
     e2e = None

@@ -98,7 +98,7 @@ dg_status Context::init() {
 
 dg_status Context::set_option(const std::string &k, int64_t v) {
   if (k == "sub_bits") {
-    if (v < 64 || v > 65536 || (v & 31)) return DG_ERR_INVALID;
+    if (v != 0 && (v < 64 || v > 65536 || (v & 31))) return DG_ERR_INVALID;
     sub_bits_ = (uint32_t)v;
     return DG_OK;
   }
@@ -123,7 +123,7 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "fix_workgroups") return stat_fix_;
   if (k == "write_mismatch") return stat_mismatch_;
   if (k == "sync_iters_max") return stat_iters_;
-  if (k == "sub_bits") return sub_bits_;
+  if (k == "sub_bits") return last_sub_bits_;
   if (k == "hpool") return (int64_t)hpool_.size();
   if (k == "qpool") return (int64_t)qpool_.size();
   return -1;
@@ -365,6 +365,18 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   if (st) return st;
 
   // ---- 3. layout
+  // Subsequence size: the entropy kernels are latency-bound, so they want as
+  // many lanes as the chip can keep resident, but every subsequence costs a
+  // sync re-decode.  Measured on MI355X (profiles/r01/sweep_v4): 2048 bits is
+  // best up to ~64 MiB of coded data per batch, 4096 above.
+  uint32_t sub_bits = sub_bits_;
+  if (!sub_bits) {
+    uint64_t coded = 0;
+    for (int i = 0; i < n; i++)
+      if (!b.plans[i].status) coded += b.plans[i].hdr.scan_end - b.plans[i].hdr.scan_off;
+    sub_bits = coded >= (64ull << 20) ? 4096 : 2048;
+  }
+  last_sub_bits_ = sub_bits;
   Layout L;        // scratch arena
   Layout IN;       // input arena (host path)
   std::vector<size_t> in_off(n, 0);
@@ -439,8 +451,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     d.nslots = (uint8_t)nslots;
     // entropy data
     d.scan_len = (uint32_t)(h.scan_end - h.scan_off);
-    d.sub_bits = sub_bits_;
-    d.nsub = std::max<uint32_t>(1, (uint32_t)(((uint64_t)d.scan_len * 8 + sub_bits_ - 1) / sub_bits_));
+    d.sub_bits = sub_bits;
+    d.nsub = std::max<uint32_t>(1, (uint32_t)(((uint64_t)d.scan_len * 8 + sub_bits - 1) / sub_bits));
     d.sub_base = sub_base;
     sub_base += d.nsub;
     d.nchunk = std::max<uint32_t>(1, (d.scan_len + kDestuffChunk - 1) / kDestuffChunk);
@@ -553,7 +565,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   b.total_subs = sub_base;
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
-  const size_t ckpt_off = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits_)) * sizeof(Ckpt));
+  const size_t ckpt_off = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits)) * sizeof(Ckpt));
   st = ensure(sl.scratch, L.off + 256);
   if (st) return st;
   if (host_io) {

@@ -122,7 +122,8 @@ class Context {
   int next_slot_ = 0;
   uint64_t next_ticket_ = 1;
 
-  uint32_t sub_bits_ = kDefaultSubBits;
+  uint32_t sub_bits_ = 0;  // 0 = auto per batch (see submit)
+  uint32_t last_sub_bits_ = kDefaultSubBits;
   bool timing_ = false;
   bool side_stream_ = true;
   int debug_flags_ = 0;

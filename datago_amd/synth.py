@@ -99,9 +99,12 @@ def _make_one(args):
 
 
 def mixed_corpus(seed: int, n: int, short_min: int = 256, short_max: int = 2048,
-                 workers: int = 1, restart_marker_rows: int = 0) -> List[bytes]:
+                 workers: int = 1, restart_marker_rows: int = 0, lo: int = 0, hi: int | None = None) -> List[bytes]:
+    """Images [lo, hi) of the logical n-image stream for `seed` (a rank's
+    slice of a sharded corpus is generated without building the rest)."""
     spec = mixed_spec(seed, n, short_min, short_max)
-    jobs = [(seed * 1_000_003 + i, s, restart_marker_rows) for i, s in enumerate(spec)]
+    hi = n if hi is None else hi
+    jobs = [(seed * 1_000_003 + i, spec[i], restart_marker_rows) for i in range(lo, hi)]
     if workers > 1:
         import multiprocessing as mp
         with mp.get_context("fork").Pool(workers) as pool:

@@ -9,7 +9,7 @@
  *   -----------------------------------------------------   ---------------------------------
  *   ImageTransformConfig::get_ar_aware_transform             dg_bucket_table_build
  *       image_processing.rs:77-121 (+ build_image_size_list :188-219)
- *   aspect_ratio_to_str            image_processing.rs:130-133   dg_bucket_key / dg_aspect_ratio_to_str
+ *   aspect_ratio_to_str            image_processing.rs:130-133   dg_aspect_ratio_to_str / dg_bucket_get
  *   ARAwareTransform::get_closest_aspect_ratio  :222-252      dg_closest_bucket
  *   aspect_ratio_to_size.get(key)  :264, panic :334-336       dg_bucket_find_key (-1 = not found)
  *   ImageReader::with_guessed_format (header sniff)
@@ -173,7 +173,14 @@ dg_status dg_synchronize(dg_ctx *ctx);
  * stream).  names[i] points to static strings; returns the number of stages. */
 int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_t cap);
 
-/* Tuning knobs (testing): subsequence size in bytes for the entropy decoder. */
+/* Tuning knobs:
+ *   "sub_bits"    entropy-decoder subsequence size in bits (multiple of 32,
+ *                 64..65536; 0 = auto per batch, the default)
+ *   "timing"      1 = record per-kernel HIP events (dg_last_batch_timings)
+ *   "side_stream" 1 = Lanczos tables on a second stream (default 1)
+ *   "debug_flags" internal switches for kernel bisection
+ * Stats: "batches", "resync_rounds", "fix_workgroups", "write_mismatch",
+ * "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool"; -1 if unknown. */
 dg_status dg_ctx_set_option(dg_ctx *ctx, const char *key, int64_t value);
 int64_t dg_ctx_get_stat(dg_ctx *ctx, const char *key);
 
