@@ -100,8 +100,13 @@ struct ResizePass {
   uint32_t row0;            // H pass: first source row; V pass: source row of temp row 0
   uint32_t C;               // channels
   uint32_t kind;            // 0 none, 1 horizontal, 2 vertical
-  uint32_t pad;
+  uint32_t mode;            // H passes: kHFused = source is the YCbCr planes (upsample + colour
+                            // in the fill), kHDirect = segment too wide for LDS (legacy kernel)
 };
+constexpr uint32_t kHFused = 1, kHDirect = 2;
+constexpr uint32_t kHBandRows = 8;    // rows per workgroup of the band H kernel
+constexpr uint32_t kHBandCols = 128;  // output columns per workgroup
+constexpr uint32_t kHSegPx = 640;     // LDS source segment (pixels) per row
 
 constexpr int kStages = 4;  // R1.H, R1.V, R2.H, R2.V
 
@@ -149,7 +154,8 @@ struct ImageDesc {
   uint32_t out_w, out_h, out_c, out_stride;
   uint64_t final_src;       // copy-kernel source (no pass runs, or gray->RGB expansion)
   uint32_t final_src_stride, copy_needed;
-  uint32_t final_src_c, pad2;
+  uint32_t final_src_c;
+  uint32_t color_fused;     // 1: pass[0] converts colour itself, pix is never written
 };
 
 // One workgroup's work: an image and the first item it handles.

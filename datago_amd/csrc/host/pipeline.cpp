@@ -96,6 +96,20 @@ dg_status Context::init() {
   return DG_OK;
 }
 
+// H pass kernel choice.  The band kernel stages the source pixels of
+// kHBandCols consecutive outputs in LDS: at most 255 * scale + 2 * support
+// (+ window rounding, 8-pixel alignment and ksize slack) pixels, which must
+// fit kHSegPx.  Wider segments (extreme downscales) use the direct kernel;
+// the first pass of a colour JPEG in the band kernel upsamples and converts
+// colour in its fill.
+static uint32_t h_pass_mode(const ResizePass &ps, bool colour_source) {
+  const double scale = (ps.in1 - ps.in0) / (double)ps.out_size;
+  const double fs = scale > 1.0 ? scale : 1.0;
+  const double span = std::ceil((kHBandCols - 1) * scale + 6.0 * fs) + 2.0 + 8.0 + (double)ps.ksize + 8.0;
+  if (span > (double)kHSegPx) return kHDirect;
+  return colour_source ? kHFused : 0u;
+}
+
 dg_status Context::set_option(const std::string &k, int64_t v) {
   if (k == "sub_bits") {
     if (v != 0 && (v < 64 || v > 65536 || (v & 31))) return DG_ERR_INVALID;
@@ -469,8 +483,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     size_t cur_stride;
     if (h.ncomp == 3) {
       d.pix_stride = (uint32_t)align_up((size_t)W * 3, 16);
-      o.pix = L.take((size_t)d.pix_stride * H);
-      cur_stride = d.pix_stride;
+      cur_stride = d.pix_stride;  // the RGB image is only materialised if no pass fuses it
     } else {
       cur_stride = (size_t)d.cbw[0] * 8;
     }
@@ -509,6 +522,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
           ps.row0 = 0;
           ps.C = C;
           ps.dst_stride = (uint32_t)align_up((size_t)k.dw * C, 16);
+          ps.mode = h_pass_mode(ps, r == 0 && h.ncomp == 3);
           o.pass_dst[2 * r] = L.take((size_t)ps.dst_stride * ps.rows);
           o.pass_coef[2 * r] = L.take((size_t)ps.out_size * ps.ksize * 2);
           o.pass_bounds[2 * r] = L.take((size_t)ps.out_size * 8);
@@ -541,6 +555,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         }
       }
     }
+    // colour images whose first pass is not a fused H pass need the RGB image
+    d.color_fused = h.ncomp == 3 && d.pass[0].kind == 1 && (d.pass[0].mode & kHFused);
+    if (h.ncomp == 3 && !d.color_fused) o.pix = L.take((size_t)d.pix_stride * H);
     // final write: the last pass writes straight into the output when the
     // channel count is unchanged; otherwise (or with no pass) k_copy runs.
     if (last_stage >= 0 && d.out_c == C) {
@@ -587,7 +604,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     d.mk = (uint64_t)(uintptr_t)(S + o.mk);
     d.chunk = (uint64_t)(uintptr_t)(S + o.chunk);
     for (int c = 0; c < h.ncomp; c++) d.plane[c] = (uint64_t)(uintptr_t)(S + o.plane[c]);
-    d.pix = h.ncomp == 3 ? (uint64_t)(uintptr_t)(S + o.pix) : 0;
+    d.pix = h.ncomp == 3 && !d.color_fused ? (uint64_t)(uintptr_t)(S + o.pix) : 0;
     uint64_t out = host_io ? (uint64_t)(uintptr_t)(S + o.out) : (uint64_t)(uintptr_t)outs[i];
     d.out = out;
     uint64_t cur = h.ncomp == 3 ? d.pix : d.plane[0];
@@ -605,6 +622,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   // ---- 5. workgroup lists
   for (auto &l : b.lists) l.clear();
+  std::vector<WgItem> hb[2][4];  // band H items per (stage, weight-count class)
   for (int di = 0; di < (int)b.descs.size(); di++) {
     const ImageDesc &d = b.descs[di];
     const uint32_t I = (uint32_t)di;
@@ -615,7 +633,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     uint32_t items = 0;
     for (uint32_t c = 0; c < d.ncomp; c++) items += d.cbh[c] * ((d.cbw[c] + 31) / 32);
     for (uint32_t it = 0; it < items; it++) b.lists[L_IDCT].push_back({I, it});
-    if (d.ncomp == 3) {
+    if (d.ncomp == 3 && !d.color_fused) {
       uint32_t q = (d.width + 7) / 8 * d.height;
       for (uint32_t it = 0; it < q; it += 256) b.lists[L_COLOR].push_back({I, it});
     }
@@ -623,9 +641,13 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       const ResizePass &ps = d.pass[s];
       if (!ps.kind) continue;
       b.lists[L_COEF].push_back({I, (uint32_t)s});
-      if (ps.kind == 1) {  // one workgroup per (row, 512-column tile)
+      if (ps.kind == 1 && (ps.mode & kHDirect)) {  // one workgroup per (row, 512-column tile)
         uint32_t cnt = ps.rows * ((ps.width + 511) / 512);
-        for (uint32_t it = 0; it < cnt; it++) b.lists[L_RH0 + s].push_back({I, it});
+        for (uint32_t it = 0; it < cnt; it++) b.lists[s == 0 ? L_RHX0 : L_RHX2].push_back({I, it});
+      } else if (ps.kind == 1) {  // one workgroup per (band of rows, column tile)
+        uint32_t cnt = ((ps.rows + kHBandRows - 1) / kHBandRows) * ((ps.width + kHBandCols - 1) / kHBandCols);
+        const int cls = ps.ksize <= 8 ? 0 : ps.ksize <= 16 ? 1 : ps.ksize <= 32 ? 2 : 3;
+        for (uint32_t it = 0; it < cnt; it++) hb[s / 2][cls].push_back({I, it});
       } else {
         uint32_t cnt = (ps.width * ps.C + 15) / 16 * ps.rows;
         for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_RH0 + s].push_back({I, it});
@@ -636,6 +658,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_COPY].push_back({I, it});
     }
   }
+  for (int h = 0; h < 2; h++)
+    for (int c = 0; c < 4; c++) {
+      b.hclass[h][c] = (uint32_t)hb[h][c].size();
+      auto &l = b.lists[h ? L_RH2 : L_RH0];
+      l.insert(l.end(), hb[h][c].begin(), hb[h][c].end());
+    }
   // ---- 6. meta buffer: [flags][descs][lists...]
   Layout M;
   b.flags_off = M.take(sizeof(BatchFlags));
@@ -720,11 +748,13 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_color(stream_, dd, lst(L_COLOR), cnt(L_COLOR));
   if (ev(9)) return DG_ERR_DEVICE;
   HIPCHK(hipStreamWaitEvent(stream_, ev_coef_, 0));
-  launch_resize_h(stream_, dd, lst(L_RH0), cnt(L_RH0), 0 | (debug_flags_ << 8));
+  launch_resize_hb(stream_, dd, lst(L_RH0), b.hclass[0], 0);
+  launch_resize_h(stream_, dd, lst(L_RHX0), cnt(L_RHX0), 0 | (debug_flags_ << 8));
   if (ev(10)) return DG_ERR_DEVICE;
   launch_resize_v(stream_, dd, lst(L_RV1), cnt(L_RV1), 1);
   if (ev(11)) return DG_ERR_DEVICE;
-  launch_resize_h(stream_, dd, lst(L_RH2), cnt(L_RH2), 2 | (debug_flags_ << 8));
+  launch_resize_hb(stream_, dd, lst(L_RH2), b.hclass[1], 2);
+  launch_resize_h(stream_, dd, lst(L_RHX2), cnt(L_RHX2), 2 | (debug_flags_ << 8));
   if (ev(12)) return DG_ERR_DEVICE;
   launch_resize_v(stream_, dd, lst(L_RV3), cnt(L_RV3), 3);
   if (ev(13)) return DG_ERR_DEVICE;

@@ -45,6 +45,9 @@ struct Batch {
   // workgroup lists (host copies) and their offsets in the device meta buffer
   std::vector<WgItem> lists[16];
   size_t list_off[16] = {0};
+  // band H lists (L_RH0, L_RH2) are grouped by weight-count class (<=8, <=16,
+  // <=32, more): hclass[stage/2][k] items of class k, in that order
+  uint32_t hclass[2][4] = {{0}};
   size_t desc_off = 0, flags_off = 0;
   size_t meta_bytes = 0;
   size_t total_subs = 0;
@@ -70,7 +73,11 @@ struct Slot {
   size_t subs_off = 0, ckpt_off = 0;
 };
 
-enum ListId { L_HUFF = 0, L_SYNC, L_DESTUFF, L_SCAN, L_IDCT, L_COLOR, L_COEF, L_RH0, L_RV1, L_RH2, L_RV3, L_COPY, L_COUNT };
+enum ListId {
+  L_HUFF = 0, L_SYNC, L_DESTUFF, L_SCAN, L_IDCT, L_COLOR, L_COEF, L_RH0, L_RV1, L_RH2, L_RV3, L_COPY,
+  L_RHX0, L_RHX2,  // H passes whose source segment is too wide for the band kernel
+  L_COUNT
+};
 
 class Context {
  public:

@@ -30,6 +30,9 @@ void launch_color(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uin
 void launch_coeffs(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 // resize passes of one stage: 256 output pixels (H) / 4-byte units (V) per workgroup
 void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage);
+// band H pass: kHBandCols x kHBandRows outputs per workgroup (see kernels.hip);
+// `list` holds ncls[k] items of weight-count class k (<=8, <=16, <=32, more) in order
+void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[4], int stage);
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage);
 // final copy / gray->RGB expansion: 256 output pixels per workgroup
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);

@@ -8,7 +8,10 @@
 //   k_coeffs      Lanczos3 i16 coefficient tables (fast_image_resize semantics)
 //   k_idct        dequant + ISLOW IDCT -> component planes
 //   k_color       fancy upsampling + YCbCr->RGB -> interleaved image
-//   k_resize_h/v  separable convolution passes (R1.H, R1.V, R2.H, R2.V)
+//   k_resize_hb   H passes in row bands (first pass of a colour image fused
+//                 with upsampling + colour conversion); k_resize_h for
+//                 segments wider than LDS
+//   k_resize_v    V passes (R1.V, R2.V)
 //   k_copy        exact-size images / gray->RGB expansion
 // Everything is integer or byte work, so nothing here is MFMA-shaped; the
 // design points are wave64 occupancy for the latency-bound entropy decoder,
@@ -681,8 +684,20 @@ __global__ __launch_bounds__(256) void k_resize_h(const ImageDesc *__restrict__ 
   const uint32_t x1 = x0 + kResizeTile < ps.width ? x0 + kResizeTile : ps.width;
   const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds);  // {start, size} per output
   const uint32_t C = ps.C;
-  const uint32_t sb = (uint32_t)bounds[2 * x0] * C;
-  const uint32_t se = (uint32_t)(bounds[2 * (x1 - 1)] + bounds[2 * (x1 - 1) + 1]) * C;  // source bytes [sb, se)
+  // source bytes [sb, se) of the tile (min/max: trimmed starts are not monotone)
+  __shared__ uint32_t ext[2];
+  if (threadIdx.x == 0) {
+    ext[0] = 0xFFFFFFFFu;
+    ext[1] = 0;
+  }
+  __syncthreads();
+  for (uint32_t x = x0 + threadIdx.x; x < x1; x += 256) {
+    atomicMin(&ext[0], (uint32_t)bounds[2 * x]);
+    atomicMax(&ext[1], (uint32_t)(bounds[2 * x] + bounds[2 * x + 1]));
+  }
+  __syncthreads();
+  const uint32_t sb = ext[0] * C;
+  const uint32_t se = ext[1] * C;
   const DG_GLOBAL uint8_t *srow = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y) * ps.src_stride;
   const bool staged = se - sb + 8 <= kResizeSeg && !(stage_flags & 0x100);
   const uint32_t a0 = sb & ~3u;  // dword-aligned start (src_stride is a multiple of 4)
@@ -707,12 +722,233 @@ __global__ __launch_bounds__(256) void k_resize_h(const ImageDesc *__restrict__ 
   }
 }
 
+// Blocks b and b+8 land on the same XCD (round-robin placement, speed only):
+// map them to consecutive work items so each XCD's L2 sees a contiguous run
+// of rows of one image instead of every eighth row of all of them.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
+  const uint32_t per = n >> 3, rem = n & 7, x = b & 7, l = b >> 3;
+  return x * per + (x < rem ? x : rem) + l;
+}
+
+// ---- band H pass
+//
+// One workgroup = kHBandCols output columns x kHBandRows rows.  Phase 1 stages
+// the source segment of every row of the band in LDS (one dword per pixel,
+// channels in bytes 0..3) with all 256 threads; phase 2 has each thread
+// convolve one output column for kHBandRows/2 rows with the column's Lanczos
+// weights held in registers (one ds_read_b32 per tap); phase 3 stores the
+// band's rows with 16-byte writes.  The fill either copies interleaved bytes
+// (C = 1..4) or — for the first pass of a colour JPEG — upsamples and
+// colour-converts straight from the Y/Cb/Cr planes, so the full-size RGB
+// image never exists in HBM.
+constexpr uint32_t kHSegStride = kHSegPx + 8;
+
+// job j of the fill: 8 source pixels from the planes, p0 % 8 == 0
+__device__ __forceinline__ void hfill_color8(const ImageDesc &im, uint32_t y, uint32_t x0, uint32_t *d) {
+  int32_t Y[8], Cb[8], Cr[8];
+  upsample8(gp<const uint8_t>(im.plane[0]), im.cbw[0] * 8, im.hmax / im.ch[0], im.vmax / im.cv[0], im.cdsw[0],
+            im.cdsh[0], x0, y, Y);
+  upsample8(gp<const uint8_t>(im.plane[1]), im.cbw[1] * 8, im.hmax / im.ch[1], im.vmax / im.cv[1], im.cdsw[1],
+            im.cdsh[1], x0, y, Cb);
+  upsample8(gp<const uint8_t>(im.plane[2]), im.cbw[2] * 8, im.hmax / im.ch[2], im.vmax / im.cv[2], im.cdsw[2],
+            im.cdsh[2], x0, y, Cr);
+  uint32_t v[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint8_t r, g, b;
+    if (im.colorspace == CS_RGB) {
+      r = (uint8_t)Y[k];
+      g = (uint8_t)Cb[k];
+      b = (uint8_t)Cr[k];
+    } else {
+      ycc_to_rgb(Y[k], Cb[k], Cr[k], r, g, b);
+    }
+    v[k] = (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
+  }
+  u32x4 *d4 = (u32x4 *)d;
+  d4[0] = u32x4{v[0], v[1], v[2], v[3]};
+  d4[1] = u32x4{v[4], v[5], v[6], v[7]};
+}
+
+// 4 source pixels at p (p % 4 == 0) of an interleaved C-byte row of `in_size`
+// pixels in rows of `stride` (multiple of 4) bytes
+__device__ __forceinline__ void hfill_bytes4(const DG_GLOBAL uint8_t *row, uint32_t C, uint32_t stride,
+                                             uint32_t in_size, uint32_t p, uint32_t *d) {
+  uint32_t v[4] = {0, 0, 0, 0};
+  if ((p + 4) * C <= stride) {
+    const DG_GLOBAL uint32_t *s4 = (const DG_GLOBAL uint32_t *)(row + (size_t)p * C);
+    if (C == 3) {
+      const uint32_t w0 = s4[0], w1 = s4[1], w2 = s4[2];
+      v[0] = w0 & 0xFFFFFFu;
+      v[1] = (w0 >> 24) | ((w1 & 0xFFFFu) << 8);
+      v[2] = (w1 >> 16) | ((w2 & 0xFFu) << 16);
+      v[3] = w2 >> 8;
+    } else if (C == 1) {
+      const uint32_t w = s4[0];
+      v[0] = w & 0xFF;
+      v[1] = (w >> 8) & 0xFF;
+      v[2] = (w >> 16) & 0xFF;
+      v[3] = w >> 24;
+    } else if (C == 4) {
+      v[0] = s4[0];
+      v[1] = s4[1];
+      v[2] = s4[2];
+      v[3] = s4[3];
+    } else {  // C == 2
+      const uint32_t w0 = s4[0], w1 = s4[1];
+      v[0] = w0 & 0xFFFF;
+      v[1] = w0 >> 16;
+      v[2] = w1 & 0xFFFF;
+      v[3] = w1 >> 16;
+    }
+  } else {
+    for (uint32_t k = 0; k < 4; k++)
+      if (p + k < in_size)
+        for (uint32_t ch = 0; ch < C; ch++) v[k] |= (uint32_t)row[(size_t)(p + k) * C + ch] << (8 * ch);
+  }
+  *(u32x4 *)d = u32x4{v[0], v[1], v[2], v[3]};
+}
+
+template <int KMAX, int C>
+__device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, const int32_t *kw,
+                                           const DG_GLOBAL int16_t *kp, uint32_t ksize, uint32_t n, uint32_t r0,
+                                           uint32_t nrows, int32_t prec, uint8_t *ob, uint32_t col) {
+  constexpr uint32_t R = kHBandRows / 2;  // rows r0, r0 + 2, ...
+  const int32_t bias = 1 << (prec - 1);
+  int32_t a[R][C];
+#pragma unroll
+  for (uint32_t r = 0; r < R; r++)
+#pragma unroll
+    for (int c = 0; c < C; c++) a[r][c] = bias;
+  auto tap = [&](uint32_t i, int32_t w) {
+#pragma unroll
+    for (uint32_t r = 0; r < R; r++) {
+      const uint32_t v = seg[(r0 + 2 * r) * kHSegStride + off + i];
+#pragma unroll
+      for (int c = 0; c < C; c++) a[r][c] += (int32_t)((v >> (8 * c)) & 0xFF) * w;
+    }
+  };
+  if (KMAX > 0) {
+#pragma unroll
+    for (int i = 0; i < (KMAX > 0 ? KMAX : 1); i++)
+      if ((uint32_t)i < ksize) tap((uint32_t)i, kw[i]);
+  } else {
+    for (uint32_t i = 0; i < n; i++) tap(i, kp[i]);
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < R; r++)
+    if (r0 + 2 * r < nrows) {
+      uint8_t *o = ob + (r0 + 2 * r) * (kHBandCols * 4) + col * C;
+#pragma unroll
+      for (int c = 0; c < C; c++) o[c] = clip_shift(a[r][c], prec);
+    }
+}
+
+template <int KMAX>
+__device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps, uint32_t item, uint32_t *seg,
+                                      uint8_t *ob, uint32_t *ext) {
+  const uint32_t tiles = (ps.width + kHBandCols - 1) / kHBandCols;
+  const uint32_t band = item / tiles, tile = item - band * tiles;
+  const uint32_t y0 = band * kHBandRows;
+  const uint32_t nrows = ps.rows - y0 < kHBandRows ? ps.rows - y0 : kHBandRows;
+  const uint32_t x0 = tile * kHBandCols;
+  const uint32_t x1 = x0 + kHBandCols < ps.width ? x0 + kHBandCols : ps.width;
+  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds);
+  const DG_GLOBAL int16_t *coef = gp<const int16_t>(ps.coef);
+  const uint32_t C = ps.C, ksize = ps.ksize;
+  const uint32_t t = threadIdx.x, col = t & (kHBandCols - 1), x = x0 + col;
+  const bool valid = x < x1;
+  // Source segment of the tile.  Trimmed window starts are not strictly
+  // monotone (an exactly-zero edge weight is dropped), so take the min/max.
+  uint32_t st = 0, n = 0;
+  if (valid) {
+    st = (uint32_t)bounds[2 * x];
+    n = (uint32_t)bounds[2 * x + 1];
+  }
+  if (t == 0) {
+    ext[0] = 0xFFFFFFFFu;
+    ext[1] = 0;
+  }
+  __syncthreads();
+  if (valid && t < kHBandCols) {
+    atomicMin(&ext[0], st);
+    atomicMax(&ext[1], st + ksize);
+  }
+  __syncthreads();
+  const uint32_t p0 = ext[0] & ~7u;
+  uint32_t p1 = ext[1];
+  if (p1 - p0 > kHSegPx) p1 = p0 + kHSegPx;  // host sizing guarantees this never triggers
+  const uint32_t pe = p1 < ps.in_size ? p1 : ps.in_size;
+  // phase 1: fill
+  if (ps.mode & kHFused) {
+    const uint32_t noct = (pe - p0 + 7) >> 3;
+    for (uint32_t j = t; j < noct * nrows; j += blockDim.x) {
+      const uint32_t r = j / noct, q = j - r * noct;
+      hfill_color8(im, ps.row0 + y0 + r, p0 + 8 * q, seg + r * kHSegStride + 8 * q);
+    }
+  } else {
+    const uint32_t nu = (pe - p0 + 3) >> 2;
+    const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0) * ps.src_stride;
+    for (uint32_t j = t; j < nu * nrows; j += blockDim.x) {
+      const uint32_t r = j / nu, u = j - r * nu;
+      hfill_bytes4(src + (size_t)r * ps.src_stride, C, ps.src_stride, ps.in_size, p0 + 4 * u,
+                   seg + r * kHSegStride + 4 * u);
+    }
+  }
+  int32_t kw[KMAX > 0 ? KMAX : 1];
+  const DG_GLOBAL int16_t *kp = coef + (size_t)(valid ? x : x0) * ksize;
+  if (KMAX > 0) {
+#pragma unroll
+    for (int i = 0; i < (KMAX > 0 ? KMAX : 1); i++) kw[i] = (valid && (uint32_t)i < n) ? (int32_t)kp[i] : 0;
+  }
+  __syncthreads();
+  // phase 2: convolve (thread: column col, rows r0, r0 + 2, ...)
+  if (valid) {
+    const uint32_t off = st - p0, r0 = t / kHBandCols;
+    const int32_t prec = ps.precision;
+    if (C == 3)
+      hconv_rows<KMAX, 3>(seg, off, kw, kp, ksize, n, r0, nrows, prec, ob, col);
+    else if (C == 1)
+      hconv_rows<KMAX, 1>(seg, off, kw, kp, ksize, n, r0, nrows, prec, ob, col);
+    else if (C == 4)
+      hconv_rows<KMAX, 4>(seg, off, kw, kp, ksize, n, r0, nrows, prec, ob, col);
+    else
+      hconv_rows<KMAX, 2>(seg, off, kw, kp, ksize, n, r0, nrows, prec, ob, col);
+  }
+  __syncthreads();
+  // phase 3: store the band's rows, 16 bytes per thread per step
+  const uint32_t rb = (x1 - x0) * C, cpr = (rb + 15) >> 4;
+  DG_GLOBAL uint8_t *dst = gp<uint8_t>(ps.dst) + (size_t)y0 * ps.dst_stride + (size_t)x0 * C;
+  for (uint32_t j = t; j < cpr * nrows; j += blockDim.x) {
+    const uint32_t r = j / cpr, b = (j - r * cpr) * 16;
+    DG_GLOBAL uint8_t *d = dst + (size_t)r * ps.dst_stride + b;
+    const uint8_t *o = ob + r * (kHBandCols * 4) + b;
+    if (b + 16 <= rb && (((uintptr_t)d) & 15) == 0) {
+      *(DG_GLOBAL u32x4 *)d = *(const u32x4 *)o;
+    } else {
+      const uint32_t e = b + 16 < rb ? 16 : rb - b;
+      for (uint32_t i = 0; i < e; i++) d[i] = o[i];
+    }
+  }
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_resize_hb(const ImageDesc *__restrict__ imgs,
+                                                   const WgItem *__restrict__ list, int stage) {
+  __shared__ __attribute__((aligned(16))) uint32_t seg[kHBandRows * kHSegStride];
+  __shared__ __attribute__((aligned(16))) uint8_t ob[kHBandRows * kHBandCols * 4];
+  __shared__ uint32_t ext[2];
+  const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
+  const ImageDesc &im = imgs[it.image];
+  hband<KMAX>(im, im.pass[stage], it.item0, seg, ob, ext);
+}
+
 // Vertical pass: each thread produces 16 consecutive bytes of one output row
 // (channel-agnostic), one 16-byte load per tap: a wave streams 1 KiB of a
 // source row per tap.
 __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ imgs,
                                                   const WgItem *__restrict__ list, int stage) {
-  const WgItem it = list[blockIdx.x];
+  const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
   const ResizePass &ps = imgs[it.image].pass[stage];
   const uint32_t rowbytes = ps.width * ps.C;
   const uint32_t units = (rowbytes + 15) / 16;
@@ -827,6 +1063,15 @@ void launch_coeffs(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t
 }
 void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
   DG_LAUNCH(k_resize_h, nwg, st, imgs, list, stage);
+}
+void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[4], int stage) {
+  DG_LAUNCH(k_resize_hb<8>, ncls[0], st, imgs, list, stage);
+  list += ncls[0];
+  DG_LAUNCH(k_resize_hb<16>, ncls[1], st, imgs, list, stage);
+  list += ncls[1];
+  DG_LAUNCH(k_resize_hb<32>, ncls[2], st, imgs, list, stage);
+  list += ncls[2];
+  DG_LAUNCH(k_resize_hb<0>, ncls[3], st, imgs, list, stage);
 }
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
   DG_LAUNCH(k_resize_v, nwg, st, imgs, list, stage);

@@ -98,6 +98,19 @@ def _make_one(args):
     return make_jpeg(seed, w, h, q, ss, gray, rst)
 
 
+def _pool_map(jobs, workers):
+    # close + join (not the context manager's terminate): workers that get
+    # SIGTERM under a profiler's signal handler can hang the parent's join
+    import multiprocessing as mp
+    pool = mp.get_context("fork").Pool(workers)
+    try:
+        out = pool.map(_make_one, jobs, chunksize=4)
+    finally:
+        pool.close()
+        pool.join()
+    return out
+
+
 def mixed_corpus(seed: int, n: int, short_min: int = 256, short_max: int = 2048,
                  workers: int = 1, restart_marker_rows: int = 0, lo: int = 0, hi: int | None = None) -> List[bytes]:
     """Images [lo, hi) of the logical n-image stream for `seed` (a rank's
@@ -106,9 +119,7 @@ def mixed_corpus(seed: int, n: int, short_min: int = 256, short_max: int = 2048,
     hi = n if hi is None else hi
     jobs = [(seed * 1_000_003 + i, spec[i], restart_marker_rows) for i in range(lo, hi)]
     if workers > 1:
-        import multiprocessing as mp
-        with mp.get_context("fork").Pool(workers) as pool:
-            return pool.map(_make_one, jobs, chunksize=4)
+        return _pool_map(jobs, workers)
     return [_make_one(j) for j in jobs]
 
 
@@ -116,7 +127,5 @@ def uniform_corpus(seed: int, n: int, w: int = 640, h: int = 480, quality: int =
                    subsampling: str = "4:2:0", workers: int = 1) -> List[bytes]:
     jobs = [(seed * 1_000_003 + i, (w, h, quality, subsampling, False), 0) for i in range(n)]
     if workers > 1:
-        import multiprocessing as mp
-        with mp.get_context("fork").Pool(workers) as pool:
-            return pool.map(_make_one, jobs, chunksize=4)
+        return _pool_map(jobs, workers)
     return [_make_one(j) for j in jobs]

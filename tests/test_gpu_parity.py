@@ -222,3 +222,32 @@ def test_large_full_size_properties(ctx1024):
         pil = np.asarray(Image.open(io.BytesIO(data)))
         ref = O.crop_and_resize(pil, meta.width, meta.height, O.MODE_FIR)
         assert np.array_equal(arr, ref)
+
+
+# Horizontal-pass kernel classes: register-resident weights for
+# ksize <= 8 / 16 / 32, weights from global beyond that, and the direct kernel
+# when the source segment of a 256-column tile exceeds LDS; colour images use
+# the fused upsample + colour fill, gray the byte fill.
+H_CLASS_CASES = [
+    (300, 200, "4:2:0", False),   # upscale: ksize 7
+    (700, 520, "4:2:2", False),   # mild downscale: <= 16
+    (2000, 1500, "4:4:4", False), # ~3.4x: <= 32
+    (4000, 3000, "4:2:0", False), # ~6.8x: generic weights
+    (6400, 4000, "4:2:0", False), # ~10x: direct kernel
+    (1999, 1001, "4:2:0", True),  # gray, odd sizes
+    (7000, 900, "4:2:2", False),  # AR beyond the bucket range, very wide
+]
+
+
+@pytest.mark.parametrize("case", H_CLASS_CASES, ids=lambda c: f"{c[0]}x{c[1]}_{c[2]}_{'L' if c[3] else 'RGB'}")
+def test_h_pass_classes_bit_exact(ctx512, case):
+    w, h, ss, gray = case
+    data = synth.make_jpeg(40 + w % 97, w, h, 88, ss, gray=gray)
+    st, arr, meta = ctx512.decode_one(data)
+    assert st == 0
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    tw, th = t.target_size(w, h)
+    ref = _oracle_resized(data, tw, th)
+    assert arr.shape == ref.shape
+    d = np.abs(arr.astype(int) - ref.astype(int))
+    assert d.max() == 0, (int(d.max()), int((d > 0).sum()), np.argwhere(d > 0)[:4].tolist())

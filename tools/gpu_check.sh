@@ -7,8 +7,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
 mkdir -p $OUT
 STEPS=${STEPS:-10}
-BATCH=${BATCH:-64}
-POOL=${POOL:-128}
+BATCH=${BATCH:-256}
+POOL=${POOL:-256}
 step() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
   echo "=== $name: $*" | tee -a $OUT/steps.log
