@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--ratio", type=int, default=32)
     ap.add_argument("--sub-bits", type=int, default=0)
     ap.add_argument("--workers", type=int, default=0, help="corpus generation processes")
+    ap.add_argument("--lead-bits", type=int, default=-1, help="entropy lead-in bits (-1 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=3, help="host-memory (PCIe-inclusive) steps")
@@ -179,6 +180,8 @@ def main() -> int:
                     min_aspect_ratio=0.5, max_aspect_ratio=2.0)
     if a.sub_bits:
         ctx.set_option("sub_bits", a.sub_bits)
+    if a.lead_bits >= 0:
+        ctx.set_option("lead_bits", a.lead_bits)
     # ---- pool -> HBM (one arena, 16-byte aligned entries)
     offs, o = [], 0
     for d in pool:
@@ -315,13 +318,15 @@ def main() -> int:
                                   "achieved_GBs": round(per_step_alg / (gpu_ms / 1e3) / 1e9, 2),
                                   "frac": round(per_step_alg / (gpu_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)},
             "stages_ms_per_step": {k: round(v / steps, 4) for k, v in stage_tot.items()},
+            "stages_alg_GBs": {k: round(stage_alg[k] / (stage_tot[k] / 1e3) / 1e9, 1)
+                               for k in stage_tot if stage_alg.get(k) and stage_tot[k] > 0},
             "output_mpix_s": round(outpx_all / dt_max / 1e6, 2),
             "images_per_s": round(B_ * a.steps * world / dt_max, 1),
             "e2e_host_mpix_s": round(e2e, 2) if e2e else None,
             "corpus_gen_s": round(t_gen, 1),
             "stats": {"resync_rounds": ctx.stat("resync_rounds"), "fix_workgroups": ctx.stat("fix_workgroups"),
                       "write_mismatch": ctx.stat("write_mismatch"), "sync_iters_max": ctx.stat("sync_iters_max"),
-                      "sub_bits": ctx.stat("sub_bits")},
+                      "sub_bits": ctx.stat("sub_bits"), "lead_bits": a.lead_bits},
         }
         if world == 1 and not a.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(pool, targets, a.cpu_seconds)

@@ -29,12 +29,18 @@ DG_HD uint32_t bswap32(uint32_t x) {
 
 // 64-bit window over a big-endian bit stream stored as bytes (the stream base
 // is 4-byte aligned and zero-padded by >= 16 bytes past its end).
+//
+// Refills are software-pipelined: the window keeps the next word raw (not
+// yet byte-swapped) and a shift loads the one after it without using it, so
+// the load's latency is covered by at least one symbol's worth of work
+// instead of stalling the whole wave in the lanes' divergent refills.  One
+// symbol consumes at most 31 bits, so with pos - base < 32 before a symbol at
+// most one 32-bit shift follows it.
 struct BitWin {
-  const DG_GLOBAL uint32_t *w;  // stream as little-endian words (byte-swapped on load)
+  const DG_GLOBAL uint32_t *w;  // stream as little-endian words (byte-swapped on use)
   uint64_t win;       // bits [base, base + 64)
   uint32_t base;      // bit position of win's MSB (multiple of 32)
-  uint32_t next;      // prefetched word at base + 64
-  uint32_t nidx;      // index of `next`
+  uint32_t nraw;      // raw word base/32 + 2
 };
 
 DG_HD void bw_init(BitWin &b, const DG_GLOBAL uint8_t *stream, uint32_t pos) {
@@ -42,25 +48,23 @@ DG_HD void bw_init(BitWin &b, const DG_GLOBAL uint8_t *stream, uint32_t pos) {
   uint32_t i = pos >> 5;
   b.base = i << 5;
   b.win = ((uint64_t)bswap32(b.w[i]) << 32) | bswap32(b.w[i + 1]);
-  b.nidx = i + 2;
-  b.next = bswap32(b.w[b.nidx]);
+  b.nraw = b.w[i + 2];
 }
 
 // 32 bits starting at pos (requires base <= pos < base + 32).
 DG_HD uint32_t bw_peek(const BitWin &b, uint32_t pos) { return (uint32_t)((b.win << (pos - b.base)) >> 32); }
 
-DG_HD void bw_advance(BitWin &b, uint32_t pos) {
-  while (pos - b.base >= 32) {
-    b.win = (b.win << 32) | b.next;
+// after a symbol: base <= pos < base + 64 -> base <= pos < base + 32
+DG_HD void bw_shift(BitWin &b, uint32_t pos) {
+  if (pos - b.base >= 32) {
+    b.win = (b.win << 32) | bswap32(b.nraw);
     b.base += 32;
-    b.nidx++;
-    b.next = bswap32(b.w[b.nidx]);
+    b.nraw = b.w[(b.base >> 5) + 2];
   }
 }
 
 DG_HD void bw_seek(BitWin &b, uint32_t pos) {
-  if (pos - b.base >= 64u) bw_init(b, (const DG_GLOBAL uint8_t *)b.w, pos);
-  else bw_advance(b, pos);
+  if (pos - b.base >= 32u) bw_init(b, (const DG_GLOBAL uint8_t *)b.w, pos);
 }
 
 // Decode one Huffman code from the top bits of `bits`; returns (len << 8) | sym.
@@ -166,6 +170,61 @@ DG_HD uint32_t first_marker(const DG_GLOBAL uint32_t *mk, uint32_t nmk, uint32_t
   return lo < nmk ? mk[lo] : kInf;
 }
 
+// Entry-state guess for subsequence s: decode (state only) from `lead` bits
+// before its start — from a guessed MCU start there, or exactly from the
+// scan start / a restart marker when one is closer — up to the first symbol
+// boundary at or after the start.  JPEG decodes self-synchronise within a few
+// hundred to a few thousand bits (tools/sync_stats.cpp; slowest for 4:2:0,
+// whose 6-block MCU phase must also lock), so with a long enough lead the
+// guess is the true state and k_huff_sync's verification loop has nothing to
+// re-decode.
+template <class TAB>
+DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uint8_t *stream,
+                       const DG_GLOBAL uint32_t *mk, uint32_t s, uint32_t lead) {
+  const uint32_t a0 = s * im.sub_bits;
+  if (s == 0 || lead == 0 || a0 >= im.ds_bits) return pack_state(0, 0, 0);
+  uint32_t pos = a0 > lead ? a0 - lead : 0u;
+  uint32_t r = 0, z = 0, midx;
+  uint32_t mpos = im.nmk ? first_marker(mk, im.nmk, pos, midx) : kInf;
+  const uint32_t bpm = im.bpm, slotmap = im.slotmap, cbits = im.comp_bits;
+  uint32_t comp = cbits & 3u;
+  BitWin b;
+  bw_init(b, stream, pos);
+  for (;;) {
+    if (pos >= mpos) {  // restart marker before the start: exact state from here
+      pos = mpos;
+      r = 0;
+      z = 0;
+      comp = cbits & 3u;
+      midx++;
+      mpos = midx < im.nmk ? mk[midx] : kInf;
+      bw_seek(b, pos);
+    }
+    if (pos >= a0) break;
+    const uint32_t bits = bw_peek(b, pos);
+    const bool isdc = (z == 0);
+    const uint32_t slot = (slotmap >> (((comp << 1) | (isdc ? 0u : 1u)) << 2)) & 15u;
+    const uint32_t e = huff_lookup(tabs[slot], bits);
+    const uint32_t len = e >> 8, sym = e & 0xFFu;
+    const uint32_t size = sym & 15u;
+    pos += len + size;
+    bw_shift(b, pos);
+    if (isdc) {
+      z = 1;
+    } else {
+      const uint32_t run = sym >> 4;
+      z = (size == 0 && run != 15u) ? 64u : z + run + 1u;
+    }
+    if (z >= 64) {
+      z = 0;
+      r = (r + 1 == bpm) ? 0 : r + 1;
+      comp = (cbits >> (2 * r)) & 3u;
+    }
+  }
+  const uint32_t rel = pos - a0;
+  return pack_state(rel > 255 ? 255 : rel, r, z);
+}
+
 // Decode the symbols of subsequence s of image im from entry state `in`.
 //   stream: destuffed bytes (4-byte aligned, zero padded); mk: marker bit positions
 //   tabs: Huffman tables indexed by slot (im.dc_slot / im.ac_slot)
@@ -266,7 +325,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
     int32_t v = 0;
     if (size) v = huff_extend((int32_t)((bits << len) >> (32 - size)), (int32_t)size);
     pos += len + size;
-    bw_advance(b, pos);
+    bw_shift(b, pos);
     if (isdc) {
       acc.n++;
       add3(acc.dc, comp, v);

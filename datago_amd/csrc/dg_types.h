@@ -124,7 +124,8 @@ struct ImageDesc {
   uint32_t ds_bits;         // destuffed length in bits (written by k_destuff_scan)
   uint32_t nmk;             // RST markers (written by k_destuff_scan)
   uint32_t slotmap;         // Huffman slot of (component c, dc=0/ac=1) at nibble 2c+ac
-  uint32_t mk_cap, pad_mk;  // capacity of the marker list
+  uint32_t mk_cap;          // capacity of the marker list
+  uint32_t lead_bits;       // k_huff_sync lead-in before each subsequence (lead_in)
   uint32_t restart;         // restart interval (MCUs), 0 = none
   uint32_t blocks_per_seg;  // restart * bpm, 0 = unlimited
   uint32_t total_blocks;

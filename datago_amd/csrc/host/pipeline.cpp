@@ -116,6 +116,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     sub_bits_ = (uint32_t)v;
     return DG_OK;
   }
+  if (k == "lead_bits") {
+    if (v < -1 || v > (1 << 20)) return DG_ERR_INVALID;
+    lead_bits_ = v;
+    return DG_OK;
+  }
   if (k == "timing") {
     timing_ = v != 0;
     return DG_OK;
@@ -466,6 +471,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     // entropy data
     d.scan_len = (uint32_t)(h.scan_end - h.scan_off);
     d.sub_bits = sub_bits;
+    // lead-in before each subsequence (lead_in in dg_entropy.h): covers the
+    // self-synchronisation distance, which is longest for 6-block MCUs
+    // (4:2:0; p99.9 ~7 kbit on the bench corpus, tools/sync_stats.cpp)
+    d.lead_bits = lead_bits_ >= 0 ? (uint32_t)lead_bits_ : (bpm >= 4 ? 6144u : 2048u);
     d.nsub = std::max<uint32_t>(1, (uint32_t)(((uint64_t)d.scan_len * 8 + sub_bits - 1) / sub_bits));
     d.sub_base = sub_base;
     sub_base += d.nsub;
@@ -631,7 +640,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     for (uint32_t c = 0; c < d.nchunk; c++) b.lists[L_DESTUFF].push_back({I, c});
     b.lists[L_SCAN].push_back({I, 0});
     uint32_t items = 0;
-    for (uint32_t c = 0; c < d.ncomp; c++) items += d.cbh[c] * ((d.cbw[c] + 31) / 32);
+    for (uint32_t c = 0; c < d.ncomp; c++) items += d.cbh[c] * ((d.cbw[c] + 63) / 64);  // kIdctBlocks
     for (uint32_t it = 0; it < items; it++) b.lists[L_IDCT].push_back({I, it});
     if (d.ncomp == 3 && !d.color_fused) {
       uint32_t q = (d.width + 7) / 8 * d.height;

@@ -130,6 +130,7 @@ class Context {
   uint64_t next_ticket_ = 1;
 
   uint32_t sub_bits_ = 0;  // 0 = auto per batch (see submit)
+  int64_t lead_bits_ = -1;  // -1 = auto per image (see submit)
   uint32_t last_sub_bits_ = kDefaultSubBits;
   bool timing_ = false;
   bool side_stream_ = true;

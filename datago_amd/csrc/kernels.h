@@ -21,7 +21,7 @@ void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
 void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs);
 void launch_huff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                        const HuffTable *pool, const SubState *subs, BatchFlags *flags);
-// dequant + IDCT: 32 blocks of one block row per workgroup
+// dequant + IDCT: 64 blocks of one block row per workgroup
 void launch_idct(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                  const QuantTable *qpool);
 // upsample + colour convert: 256 x 4-pixel quads per workgroup

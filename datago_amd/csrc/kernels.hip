@@ -202,7 +202,8 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   const DG_GLOBAL uint8_t *scan = gp<const uint8_t>(im.ds);
   const DG_GLOBAL uint32_t *mkp = gp<const uint32_t>(im.mk);
   RangeAcc acc = {0, 0, 0, {0, 0, 0}};
-  uint32_t in = pack_state(0, 0, 0);  // exact for s == 0, a guess otherwise
+  // entry state: exact for s == 0, otherwise the lead-in decode's guess
+  uint32_t in = active ? lead_in(im, tabs, scan, mkp, s, im.lead_bits) : pack_state(0, 0, 0);
   if (active) decode_range<false>(im, tabs, scan, mkp, s, in, acc, nullptr, ck);
   ex[t] = active ? acc.out : 0u;
   ins[t] = in;
@@ -366,60 +367,84 @@ __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict_
 
 // ------------------------------------------------------------ IDCT
 
+// One workgroup = kIdctBlocks consecutive blocks of one block row of one
+// component; 8 lanes per block, each lane owning two blocks (slot, slot + 32)
+// so two independent 16-byte coefficient loads are in flight per lane and
+// the two LDS transposes share their barriers.  Lane `lane` dequantises
+// column `lane` in pass 1 (its 8 quant values come from cached loads that
+// every block of the wave shares), then runs row `lane` in pass 2.
+constexpr uint32_t kIdctBlocks = 64;
+
 __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
                                               const QuantTable *__restrict__ qpool) {
   constexpr int LD = 65;  // padded block stride (dwords): breaks the 64-dword bank period
-  __shared__ int32_t blkv[32 * LD];
+  __shared__ int32_t blkv[kIdctBlocks * LD];
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
-  // item -> (component, block row, chunk of 32 blocks)
+  // item -> (component, block row, chunk of kIdctBlocks blocks)
   uint32_t item = it.item0, c = 0;
   for (; c < im.ncomp; c++) {
-    uint32_t ck = (im.cbw[c] + 31) / 32;
+    uint32_t ck = (im.cbw[c] + kIdctBlocks - 1) / kIdctBlocks;
     uint32_t n = im.cbh[c] * ck;
     if (item < n) break;
     item -= n;
   }
-  const uint32_t ck = (im.cbw[c] + 31) / 32;
+  const uint32_t ck = (im.cbw[c] + kIdctBlocks - 1) / kIdctBlocks;
   const uint32_t by = item / ck, chunk = item - by * ck;
   const int t = threadIdx.x, slot = t >> 3, lane = t & 7;
-  const uint32_t bx = chunk * 32 + slot;
-  const bool valid = bx < im.cbw[c];
-  const uint16_t *q = qpool[im.qpool[c]].q;
-  int32_t *bv = blkv + slot * LD;
-  if (valid) {
-    uint32_t b;
-    if (im.ncomp == 1) {
-      b = by * im.cbw[0] + bx;
-    } else {
-      uint32_t my = by / im.cv[c], vy = by - my * im.cv[c];
-      uint32_t mx = bx / im.ch[c], hx = bx - mx * im.ch[c];
-      b = (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * im.ch[c] + hx;
-    }
-    const DG_GLOBAL int16_t *src = gp<const int16_t>(im.coef) + (size_t)b * 64 + lane * 8;
-    u32x4 raw = *(const DG_GLOBAL u32x4 *)src;
-    int16_t v[8];
-    __builtin_memcpy(v, &raw, 16);
+  const uint32_t cbw = im.cbw[c];
+  const uint32_t bx0 = chunk * kIdctBlocks + slot, bx1 = bx0 + 32;
+  const bool v0 = bx0 < cbw, v1 = bx1 < cbw;
+  const DG_GLOBAL int16_t *coef = gp<const int16_t>(im.coef);
+  auto block_index = [&](uint32_t bx) -> uint32_t {
+    if (im.ncomp == 1) return by * im.cbw[0] + bx;
+    uint32_t my = by / im.cv[c], vy = by - my * im.cv[c];
+    uint32_t mx = bx / im.ch[c], hx = bx - mx * im.ch[c];
+    return (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * im.ch[c] + hx;
+  };
+  u32x4 r0 = {0, 0, 0, 0}, r1 = {0, 0, 0, 0};
+  if (v0) r0 = *(const DG_GLOBAL u32x4 *)(coef + (size_t)block_index(bx0) * 64 + lane * 8);
+  if (v1) r1 = *(const DG_GLOBAL u32x4 *)(coef + (size_t)block_index(bx1) * 64 + lane * 8);
+  const DG_GLOBAL uint16_t *q = gp<const uint16_t>((uint64_t)(uintptr_t)qpool[im.qpool[c]].q);
+  int32_t qc[8];  // column `lane` of the quant table
+#pragma unroll
+  for (int r = 0; r < 8; r++) qc[r] = q[r * 8 + lane];
+  int32_t *bv0 = blkv + slot * LD, *bv1 = blkv + (slot + 32) * LD;
+  {
+    int16_t a[8], b[8];
+    __builtin_memcpy(a, &r0, 16);
+    __builtin_memcpy(b, &r1, 16);
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      int n = kZigzagToNatural[lane * 8 + i];
-      bv[n] = (int32_t)v[i] * (int32_t)q[n];
+      const int n = kZigzagToNatural[lane * 8 + i];
+      bv0[n] = a[i];
+      bv1[n] = b[i];
     }
   }
   __syncthreads();
-  int32_t o[8];
-  if (valid) {  // pass 1: column `lane`
-    idct_1d(bv[0 * 8 + lane], bv[1 * 8 + lane], bv[2 * 8 + lane], bv[3 * 8 + lane], bv[4 * 8 + lane],
-            bv[5 * 8 + lane], bv[6 * 8 + lane], bv[7 * 8 + lane], o);
-  }
+  int32_t o0[8], o1[8];
+  // pass 1: column `lane`, dequantised on the way in
+  idct_1d(bv0[0 * 8 + lane] * qc[0], bv0[1 * 8 + lane] * qc[1], bv0[2 * 8 + lane] * qc[2],
+          bv0[3 * 8 + lane] * qc[3], bv0[4 * 8 + lane] * qc[4], bv0[5 * 8 + lane] * qc[5],
+          bv0[6 * 8 + lane] * qc[6], bv0[7 * 8 + lane] * qc[7], o0);
+  idct_1d(bv1[0 * 8 + lane] * qc[0], bv1[1 * 8 + lane] * qc[1], bv1[2 * 8 + lane] * qc[2],
+          bv1[3 * 8 + lane] * qc[3], bv1[4 * 8 + lane] * qc[4], bv1[5 * 8 + lane] * qc[5],
+          bv1[6 * 8 + lane] * qc[6], bv1[7 * 8 + lane] * qc[7], o1);
   __syncthreads();
-  if (valid) {
 #pragma unroll
-    for (int r = 0; r < 8; r++) bv[r * 8 + lane] = descale(o[r], kConstBits - kPass1Bits);
+  for (int r = 0; r < 8; r++) {
+    bv0[r * 8 + lane] = descale(o0[r], kConstBits - kPass1Bits);
+    bv1[r * 8 + lane] = descale(o1[r], kConstBits - kPass1Bits);
   }
   __syncthreads();
-  if (valid) {  // pass 2: row `lane`
-    const int32_t *w = bv + lane * 8;
+  // pass 2: row `lane`
+  const uint32_t pst = cbw * 8;
+  DG_GLOBAL uint8_t *plane = gp<uint8_t>(im.plane[c]) + (size_t)(by * 8 + lane) * pst;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int32_t *w = (h ? bv1 : bv0) + lane * 8;
+    const bool v = h ? v1 : v0;
+    int32_t o[8];
     idct_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
@@ -427,9 +452,7 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
       lo |= (uint32_t)idct_out(o[i]) << (8 * i);
       hi |= (uint32_t)idct_out(o[i + 4]) << (8 * i);
     }
-    DG_GLOBAL uint8_t *dst = gp<uint8_t>(im.plane[c]) + (size_t)(by * 8 + lane) * (im.cbw[c] * 8) + bx * 8;
-    u32x2 v2 = {lo, hi};
-    *(DG_GLOBAL u32x2 *)dst = v2;
+    if (v) *(DG_GLOBAL u32x2 *)(plane + (size_t)(h ? bx1 : bx0) * 8) = u32x2{lo, hi};
   }
 }
 

@@ -14,6 +14,9 @@
 
 using namespace dg;
 
+static uint32_t g_lead = 0;
+extern "C" void emu_set_lead(uint32_t lead) { g_lead = lead; }
+
 extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bits, int16_t *out,
                                 size_t cap_blocks, size_t *nblocks, int64_t *stats) {
   JpegHeader h;
@@ -71,6 +74,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
   d.nmk = (uint32_t)mk.size();
   ds.resize(((ds.size() + 3) & ~(size_t)3) + 32, 0);
   d.sub_bits = sub_bits;
+  d.lead_bits = g_lead;
   d.nsub = d.scan_len ? (uint32_t)(((uint64_t)d.scan_len * 8 + sub_bits - 1) / sub_bits) : 1;
   const uint8_t *scan = ds.data();
   const uint32_t *mkp = mk.data();
@@ -92,7 +96,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
       active[t] = si >= 0 && si < (int64_t)d.nsub;
       head[t] = (t == 0) || (s0 == 0 && t == 1);
       if (!active[t]) continue;
-      ins[t] = pack_state(0, 0, 0);
+      ins[t] = lead_in(d, tabs.data(), scan, mkp, (uint32_t)si, d.lead_bits);
       decode_range<false>(d, tabs.data(), scan, mkp, (uint32_t)si, ins[t], acc[t], nullptr, t ? ckp((uint32_t)si) : nullptr);
       ex[t] = acc[t].out;
     }

@@ -26,11 +26,13 @@ def emu():
         subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
                         "-I" + os.path.join(ROOT, "datago_amd", "csrc"), "-o", SO] + srcs, check=True)
     E = ctypes.CDLL(SO)
+    E.emu_set_lead.argtypes = [ctypes.c_uint32]
     E.emu_decode_coefs.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32,
                                    ctypes.POINTER(ctypes.c_int16), ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int64)]
 
-    def run(data, sub_bits):
+    def run(data, sub_bits, lead=0):
+        E.emu_set_lead(lead)
         cap = 1 << 18
         out = np.zeros((cap, 64), np.int16)
         nb = ctypes.c_size_t()
@@ -42,8 +44,8 @@ def emu():
 
 
 @pytest.mark.parametrize("seed", range(24))
-@pytest.mark.parametrize("sub_bits", [128, 1024, 4096])
-def test_emulated_parallel_decode_matches_oracle(emu, seed, sub_bits):
+@pytest.mark.parametrize("sub_bits,lead", [(128, 0), (1024, 0), (4096, 0), (512, 96), (1024, 2048), (4096, 6144)])
+def test_emulated_parallel_decode_matches_oracle(emu, seed, sub_bits, lead):
     rng = np.random.default_rng(seed)
     w, h = int(rng.integers(1, 700)), int(rng.integers(1, 700))
     ss = ["4:2:0", "4:2:2", "4:4:4"][seed % 3]
@@ -51,7 +53,7 @@ def test_emulated_parallel_decode_matches_oracle(emu, seed, sub_bits):
     data = synth.encode_jpeg(synth.synth_pixels(rng, w, h, seed % 7 == 0), int(rng.integers(30, 101)), ss,
                              restart_marker_rows=rst)
     st, ref = O.jpeg_coefs(data)
-    r, co, stats = emu(data, sub_bits)
+    r, co, stats = emu(data, sub_bits, lead)
     assert r == 0 and st == 0
     assert co.shape == ref.shape
     assert np.array_equal(co, ref)
