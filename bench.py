@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--sub-bits", type=int, default=0)
     ap.add_argument("--workers", type=int, default=0, help="corpus generation processes")
     ap.add_argument("--lead-bits", type=int, default=-1, help="entropy lead-in bits (-1 = library default)")
+    ap.add_argument("--wg-timing", action="store_true", help="debug: per-workgroup timing of the entropy kernels")
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=3, help="host-memory (PCIe-inclusive) steps")
@@ -182,6 +183,8 @@ def main() -> int:
         ctx.set_option("sub_bits", a.sub_bits)
     if a.lead_bits >= 0:
         ctx.set_option("lead_bits", a.lead_bits)
+    if a.wg_timing:
+        ctx.set_option("wg_timing", 1)
     # ---- pool -> HBM (one arena, 16-byte aligned entries)
     offs, o = [], 0
     for d in pool:
@@ -327,6 +330,8 @@ def main() -> int:
             "stats": {"resync_rounds": ctx.stat("resync_rounds"), "fix_workgroups": ctx.stat("fix_workgroups"),
                       "write_mismatch": ctx.stat("write_mismatch"), "sync_iters_max": ctx.stat("sync_iters_max"),
                       "sub_bits": ctx.stat("sub_bits"), "lead_bits": a.lead_bits},
+            "wg_timing_us": ({f"{k}_{q}": ctx.stat(f"wg_{k}_{q}") / 1000 for k in ("sync", "write")
+                              for q in ("span", "mean", "p90", "max")} if a.wg_timing else None),
         }
         if world == 1 and not a.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(pool, targets, a.cpu_seconds)

@@ -262,63 +262,80 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
     w->cur = -1;
     if (z > 0) wc_begin(*w, w->nin > 0 ? wc_index(*w, w->nin - 1) : -1, z);
   }
+  // Per symbol only one compare against the next "event" (restart marker,
+  // checkpoint, end of range); the Huffman tables of the current block are
+  // resolved when the block changes, not per symbol.
+  auto next_event = [&]() -> uint32_t {
+    uint32_t e = a1 < mpos ? a1 : mpos;
+    return (k < nck && cpos < e) ? cpos : e;
+  };
+  auto block_tables = [&](const TAB *&tdc, const TAB *&tac) {
+    tdc = &tabs[(slotmap >> ((comp << 1) << 2)) & 15u];
+    tac = &tabs[(slotmap >> (((comp << 1) | 1u) << 2)) & 15u];
+  };
+  const TAB *tdc, *tac;
+  block_tables(tdc, tac);
+  uint32_t ev = next_event();
   for (;;) {
-    if (pos >= mpos) {  // restart marker: hard resync
-      bool owned = mpos < a1;
-      if (WRITE && z > 0) wc_flush(*w, z);
-      pos = mpos;
-      r = 0;
-      z = 0;
-      comp = cbits & 3u;
-      if (owned) {
-        acc.m++;
-        acc.n = 0;
-        acc.dc[0] = acc.dc[1] = acc.dc[2] = 0;
-        if (WRITE) {
-          w->seg++;
-          w->nin = 0;
-          w->pred[0] = w->pred[1] = w->pred[2] = 0;
+    if (pos >= ev) {
+      if (pos >= mpos) {  // restart marker: hard resync
+        bool owned = mpos < a1;
+        if (WRITE && z > 0) wc_flush(*w, z);
+        pos = mpos;
+        r = 0;
+        z = 0;
+        comp = cbits & 3u;
+        block_tables(tdc, tac);
+        if (owned) {
+          acc.m++;
+          acc.n = 0;
+          acc.dc[0] = acc.dc[1] = acc.dc[2] = 0;
+          if (WRITE) {
+            w->seg++;
+            w->nin = 0;
+            w->pred[0] = w->pred[1] = w->pred[2] = 0;
+          }
         }
+        midx++;
+        mpos = midx < im.nmk ? mk[midx] : kInf;
+        bw_seek(b, pos);
       }
-      midx++;
-      mpos = midx < im.nmk ? mk[midx] : kInf;
-      bw_seek(b, pos);
-    }
-    if (k < nck && cpos < a1 && pos >= cpos) {  // first boundary at/after checkpoint k
-      uint32_t rel = pos - cpos;
-      uint32_t st = pack_state(rel > 255 ? 255 : rel, r, z);
-      DG_GLOBAL Ckpt &c = ck[k];
-      if (merge && c.st == st) {  // rejoined the previous decode: acc (+) tail_k
-        if (c.m) {
-          acc.m += c.m;
-          acc.n = c.n;
-          acc.dc[0] = c.dc[0];
-          acc.dc[1] = c.dc[1];
-          acc.dc[2] = c.dc[2];
-        } else {
-          acc.n += c.n;
-          acc.dc[0] += c.dc[0];
-          acc.dc[1] += c.dc[1];
-          acc.dc[2] += c.dc[2];
+      if (k < nck && cpos < a1 && pos >= cpos) {  // first boundary at/after checkpoint k
+        uint32_t rel = pos - cpos;
+        uint32_t st = pack_state(rel > 255 ? 255 : rel, r, z);
+        DG_GLOBAL Ckpt &c = ck[k];
+        if (merge && c.st == st) {  // rejoined the previous decode: acc (+) tail_k
+          if (c.m) {
+            acc.m += c.m;
+            acc.n = c.n;
+            acc.dc[0] = c.dc[0];
+            acc.dc[1] = c.dc[1];
+            acc.dc[2] = c.dc[2];
+          } else {
+            acc.n += c.n;
+            acc.dc[0] += c.dc[0];
+            acc.dc[1] += c.dc[1];
+            acc.dc[2] += c.dc[2];
+          }
+          acc.out = old_out;
+          merged = true;
+          break;
         }
-        acc.out = old_out;
-        merged = true;
-        break;
+        c.st = st;  // record the prefix for now; turned into a tail at the end
+        c.m = acc.m;
+        c.n = acc.n;
+        c.dc[0] = acc.dc[0];
+        c.dc[1] = acc.dc[1];
+        c.dc[2] = acc.dc[2];
+        k++;
+        cpos += kCkptBits;
       }
-      c.st = st;  // record the prefix for now; turned into a tail at the end
-      c.m = acc.m;
-      c.n = acc.n;
-      c.dc[0] = acc.dc[0];
-      c.dc[1] = acc.dc[1];
-      c.dc[2] = acc.dc[2];
-      k++;
-      cpos += kCkptBits;
+      if (pos >= a1) break;
+      ev = next_event();
     }
-    if (pos >= a1) break;
     const uint32_t bits = bw_peek(b, pos);
     const bool isdc = (z == 0);
-    const uint32_t slot = (slotmap >> (((comp << 1) | (isdc ? 0u : 1u)) << 2)) & 15u;
-    const uint32_t e = huff_lookup(tabs[slot], bits);
+    const uint32_t e = huff_lookup(*(isdc ? tdc : tac), bits);
     const uint32_t len = e >> 8, sym = e & 0xFFu;
     const uint32_t size = sym & 15u;
     const uint32_t run = isdc ? 0u : (sym >> 4);
@@ -349,6 +366,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       z = 0;
       r = (r + 1 == bpm) ? 0 : r + 1;
       comp = (cbits >> (2 * r)) & 3u;
+      block_tables(tdc, tac);
     }
   }
   if (WRITE && z > 0) wc_flush(*w, z);

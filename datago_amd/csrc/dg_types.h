@@ -171,6 +171,9 @@ struct BatchFlags {
   uint32_t fix_count;       // workgroups k_huff_fix had to re-run
   uint32_t write_mismatch;  // k_huff_write exit != next subsequence's input
   uint32_t sync_iters_max;  // longest intra-workgroup sync loop
+  uint64_t wgtime;          // debug: device array of {start, end} s_memrealtime per workgroup, 0 = off
+  uint32_t wgtime_write;    // first record of k_huff_write's workgroups
+  uint32_t pad;
 };
 
 }  // namespace dg

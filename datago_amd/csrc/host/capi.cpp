@@ -211,7 +211,7 @@ dg_status dg_memcpy_d2h(dg_ctx *ctx, void *dst, const void *src, size_t bytes) {
 dg_status dg_synchronize(dg_ctx *ctx) {
   if (!ctx) return DG_ERR_INVALID;
   hipSetDevice(ctx->c.device());
-  return hipStreamSynchronize(ctx->c.stream()) == hipSuccess ? DG_OK : DG_ERR_DEVICE;
+  return ctx->c.sync_all();
 }
 
 int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_t cap) {

@@ -44,12 +44,17 @@ Context::Context(int device, const dg_image_config *cfg) : device_(device) {
 
 Context::~Context() {
   hipSetDevice(device_);
-  if (stream_) hipStreamSynchronize(stream_);
+  sync_all();
   for (DevBuf *b : {&d_hpool_, &d_qpool_})
     if (b->p) hipFree(b->p);
   for (Slot &sl : slots_) {
     for (auto e : sl.ev) hipEventDestroy(e);
     if (sl.done) hipEventDestroy(sl.done);
+    for (hipEvent_t e : {sl.ev_meta, sl.ev_coef})
+      if (e) hipEventDestroy(e);
+    for (hipStream_t q : {sl.st, sl.side})
+      if (q) hipStreamDestroy(q);
+    if (sl.wgt.p) hipFree(sl.wgt.p);
     for (DevBuf *b : {&sl.scratch, &sl.meta, &sl.input})
       if (b->p) hipFree(b->p);
     for (PinBuf *b : {&sl.stage, &sl.out})
@@ -92,6 +97,24 @@ dg_status Context::init() {
     sl.ev.resize(17);
     for (auto &e : sl.ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    HIPCHK(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&sl.side, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_meta, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_coef, hipEventDisableTiming));
+  }
+  return DG_OK;
+}
+
+dg_status Context::sync_all() {
+  bool ok = true;
+  for (hipStream_t q : {stream_, side_})
+    if (q) ok &= hipStreamSynchronize(q) == hipSuccess;
+  for (Slot &sl : slots_)
+    for (hipStream_t q : {sl.st, sl.side})
+      if (q) ok &= hipStreamSynchronize(q) == hipSuccess;
+  if (!ok) {
+    set_error("HIP stream synchronisation failed");
+    return DG_ERR_DEVICE;
   }
   return DG_OK;
 }
@@ -121,6 +144,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     lead_bits_ = v;
     return DG_OK;
   }
+  if (k == "wg_timing") {
+    wg_timing_ = v != 0;
+    return DG_OK;
+  }
   if (k == "timing") {
     timing_ = v != 0;
     return DG_OK;
@@ -142,6 +169,12 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "fix_workgroups") return stat_fix_;
   if (k == "write_mismatch") return stat_mismatch_;
   if (k == "sync_iters_max") return stat_iters_;
+  {  // wg_timing summaries, in nanoseconds: wg_{sync,write}_{span,mean,p90,max}
+    static const char *kn[2] = {"sync", "write"}, *sn[4] = {"span", "mean", "p90", "max"};
+    for (int a = 0; a < 2; a++)
+      for (int q = 0; q < 4; q++)
+        if (k == std::string("wg_") + kn[a] + "_" + sn[q]) return (int64_t)(wgstat_[a][q] * 1000.0);
+  }
   if (k == "sub_bits") return last_sub_bits_;
   if (k == "hpool") return (int64_t)hpool_.size();
   if (k == "qpool") return (int64_t)qpool_.size();
@@ -162,10 +195,16 @@ int Context::timings(const char **names, float *ms, int cap) {
   return n;
 }
 
-dg_status Context::ensure(DevBuf &b, size_t bytes) {
+// Grow a device buffer.  `user`: the only stream that can still be using it
+// (a slot's own buffers); nullptr = shared by every stream (the table pools).
+dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
   if (b.cap >= bytes) return DG_OK;
   if (b.p) {
-    HIPCHK(hipStreamSynchronize(stream_));
+    if (user) {
+      HIPCHK(hipStreamSynchronize(user));
+    } else if (dg_status st = sync_all()) {
+      return st;
+    }
     HIPCHK(hipFree(b.p));
     b.p = nullptr;
     b.cap = 0;
@@ -181,10 +220,14 @@ dg_status Context::ensure(DevBuf &b, size_t bytes) {
   return DG_OK;
 }
 
-dg_status Context::ensure_pinned(PinBuf &b, size_t bytes) {
+dg_status Context::ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user) {
   if (b.cap >= bytes) return DG_OK;
   if (b.p) {
-    HIPCHK(hipStreamSynchronize(stream_));
+    if (user) {
+      HIPCHK(hipStreamSynchronize(user));
+    } else if (dg_status st = sync_all()) {
+      return st;
+    }
     HIPCHK(hipHostFree(b.p));
     b.p = nullptr;
     b.cap = 0;
@@ -592,10 +635,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.total_subs = sub_base;
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
   const size_t ckpt_off = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits)) * sizeof(Ckpt));
-  st = ensure(sl.scratch, L.off + 256);
+  st = ensure(sl.scratch, L.off + 256, sl.st);
   if (st) return st;
   if (host_io) {
-    st = ensure(sl.input, IN.off + 64);
+    st = ensure(sl.input, IN.off + 64, sl.st);
     if (st) return st;
   }
   // ---- 4. patch device addresses
@@ -679,13 +722,21 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.desc_off = M.take(b.descs.size() * sizeof(ImageDesc));
   for (int l = 0; l < L_COUNT; l++) b.list_off[l] = M.take(b.lists[l].size() * sizeof(WgItem));
   b.meta_bytes = M.off;
-  st = ensure(sl.meta, b.meta_bytes + 256);
+  st = ensure(sl.meta, b.meta_bytes + 256, sl.st);
   if (st) return st;
   size_t stage_bytes = b.meta_bytes + (host_io ? IN.off : 0);
-  st = ensure_pinned(sl.stage, stage_bytes + 256);
+  st = ensure_pinned(sl.stage, stage_bytes + 256, sl.st);
   if (st) return st;
   char *P = (char *)sl.stage.p;
   memset(P + b.flags_off, 0, sizeof(BatchFlags));
+  if (wg_timing_) {
+    const size_t nrec = b.lists[L_SYNC].size() + b.lists[L_HUFF].size();
+    st = ensure(sl.wgt, nrec * 16 + 64, sl.st);
+    if (st) return st;
+    BatchFlags *bf = (BatchFlags *)(P + b.flags_off);
+    bf->wgtime = (uint64_t)(uintptr_t)sl.wgt.p;
+    bf->wgtime_write = (uint32_t)b.lists[L_SYNC].size();
+  }
   memcpy(P + b.desc_off, b.descs.data(), b.descs.size() * sizeof(ImageDesc));
   for (int l = 0; l < L_COUNT; l++)
     if (!b.lists[l].empty()) memcpy(P + b.list_off[l], b.lists[l].data(), b.lists[l].size() * sizeof(WgItem));
@@ -693,9 +744,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     for (int i = 0; i < n; i++)
       if (b.desc_of[i] >= 0) memcpy(P + b.meta_bytes + in_off[i], h_srcs[i], lens[i]);
   }
-  if (timing_) HIPCHK(hipEventRecord(sl.ev[0], stream_));
-  HIPCHK(hipMemcpyAsync(sl.meta.p, P, b.meta_bytes, hipMemcpyHostToDevice, stream_));
-  if (host_io && IN.off) HIPCHK(hipMemcpyAsync(sl.input.p, P + b.meta_bytes, IN.off, hipMemcpyHostToDevice, stream_));
+  if (timing_) HIPCHK(hipEventRecord(sl.ev[0], sl.st));
+  HIPCHK(hipMemcpyAsync(sl.meta.p, P, b.meta_bytes, hipMemcpyHostToDevice, sl.st));
+  if (host_io && IN.off) HIPCHK(hipMemcpyAsync(sl.input.p, P + b.meta_bytes, IN.off, hipMemcpyHostToDevice, sl.st));
   b.stage_ms.clear();
   sl.subs_off = subs_off;  // SubStates and checkpoints live in the scratch arena
   sl.ckpt_off = ckpt_off;
@@ -724,50 +775,50 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   auto lst = [&](int l) { return (const WgItem *)(M + b.list_off[l]); };
   auto cnt = [&](int l) { return (uint32_t)b.lists[l].size(); };
   auto ev = [&](int i) -> dg_status {
-    if (timing_) HIPCHK(hipEventRecord(sl.ev[i], stream_));
+    if (timing_) HIPCHK(hipEventRecord(sl.ev[i], sl.st));
     return DG_OK;
   };
-  if (from_fix) HIPCHK(hipMemsetAsync(fl, 0, sizeof(BatchFlags), stream_));
+  if (from_fix) HIPCHK(hipMemsetAsync(fl, 0, sizeof(BatchFlags), sl.st));
   if (ev(1)) return DG_ERR_DEVICE;
   if (!from_fix) {
     // Lanczos coefficient tables depend only on the plan: compute them on a
     // side stream, overlapped with the entropy decode.
-    hipStream_t cs = side_stream_ ? side_ : stream_;
-    HIPCHK(hipEventRecord(ev_meta_, stream_));
-    HIPCHK(hipStreamWaitEvent(cs, ev_meta_, 0));
+    hipStream_t cs = side_stream_ ? sl.side : sl.st;
+    HIPCHK(hipEventRecord(sl.ev_meta, sl.st));
+    HIPCHK(hipStreamWaitEvent(cs, sl.ev_meta, 0));
     launch_coeffs(cs, dm, lst(L_COEF), cnt(L_COEF));
-    HIPCHK(hipEventRecord(ev_coef_, cs));
-    launch_destuff_count(stream_, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
-    launch_destuff_scan(stream_, dm, lst(L_SCAN), cnt(L_SCAN));
-    launch_destuff_write(stream_, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
+    HIPCHK(hipEventRecord(sl.ev_coef, cs));
+    launch_destuff_count(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
+    launch_destuff_scan(sl.st, dm, lst(L_SCAN), cnt(L_SCAN));
+    launch_destuff_write(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
   }
   if (ev(2)) return DG_ERR_DEVICE;
   Ckpt *ck = (Ckpt *)((char *)sl.scratch.p + sl.ckpt_off);
-  if (!from_fix) launch_huff_sync(stream_, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
+  if (!from_fix) launch_huff_sync(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
   if (ev(3)) return DG_ERR_DEVICE;
-  launch_huff_fix(stream_, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
+  launch_huff_fix(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
   if (ev(4)) return DG_ERR_DEVICE;
-  launch_huff_scan(stream_, dm, lst(L_SCAN), cnt(L_SCAN), subs);
+  launch_huff_scan(sl.st, dm, lst(L_SCAN), cnt(L_SCAN), subs);
   if (ev(5)) return DG_ERR_DEVICE;
-  launch_huff_write(stream_, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+  launch_huff_write(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
   if (ev(6)) return DG_ERR_DEVICE;
   if (ev(7)) return DG_ERR_DEVICE;
-  launch_idct(stream_, dd, lst(L_IDCT), cnt(L_IDCT), qp);
+  launch_idct(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);
   if (ev(8)) return DG_ERR_DEVICE;
-  launch_color(stream_, dd, lst(L_COLOR), cnt(L_COLOR));
+  launch_color(sl.st, dd, lst(L_COLOR), cnt(L_COLOR));
   if (ev(9)) return DG_ERR_DEVICE;
-  HIPCHK(hipStreamWaitEvent(stream_, ev_coef_, 0));
-  launch_resize_hb(stream_, dd, lst(L_RH0), b.hclass[0], 0);
-  launch_resize_h(stream_, dd, lst(L_RHX0), cnt(L_RHX0), 0 | (debug_flags_ << 8));
+  HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_coef, 0));
+  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0);
+  launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | (debug_flags_ << 8));
   if (ev(10)) return DG_ERR_DEVICE;
-  launch_resize_v(stream_, dd, lst(L_RV1), cnt(L_RV1), 1);
+  launch_resize_v(sl.st, dd, lst(L_RV1), cnt(L_RV1), 1);
   if (ev(11)) return DG_ERR_DEVICE;
-  launch_resize_hb(stream_, dd, lst(L_RH2), b.hclass[1], 2);
-  launch_resize_h(stream_, dd, lst(L_RHX2), cnt(L_RHX2), 2 | (debug_flags_ << 8));
+  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2);
+  launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | (debug_flags_ << 8));
   if (ev(12)) return DG_ERR_DEVICE;
-  launch_resize_v(stream_, dd, lst(L_RV3), cnt(L_RV3), 3);
+  launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3);
   if (ev(13)) return DG_ERR_DEVICE;
-  launch_copy(stream_, dd, lst(L_COPY), cnt(L_COPY));
+  launch_copy(sl.st, dd, lst(L_COPY), cnt(L_COPY));
   if (ev(14)) return DG_ERR_DEVICE;
   HIPCHK(hipGetLastError());
   // read back flags + per-image status (descs) for finish(), then outputs (host path)
@@ -776,20 +827,20 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (b.host_io)
     for (int i = 0; i < b.n; i++)
       if (b.desc_of[i] >= 0) total += align_up(b.plans[i].out_bytes, 16);
-  dg_status st = ensure_pinned(sl.out, total + 256);
+  dg_status st = ensure_pinned(sl.out, total + 256, sl.st);
   if (st) return st;
-  HIPCHK(hipMemcpyAsync(sl.out.p, M, back, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipMemcpyAsync(sl.out.p, M, back, hipMemcpyDeviceToHost, sl.st));
   if (b.host_io) {
     size_t off = align_up(back, 256);
     for (int i = 0; i < b.n; i++) {
       if (b.desc_of[i] < 0) continue;
       HIPCHK(hipMemcpyAsync((char *)sl.out.p + off, (char *)sl.scratch.p + b.out_dev_off[i], b.plans[i].out_bytes,
-                            hipMemcpyDeviceToHost, stream_));
+                            hipMemcpyDeviceToHost, sl.st));
       off += align_up(b.plans[i].out_bytes, 16);
     }
   }
   if (ev(15)) return DG_ERR_DEVICE;
-  HIPCHK(hipEventRecord(sl.done, stream_));
+  HIPCHK(hipEventRecord(sl.done, sl.st));
   return DG_OK;
 }
 
@@ -808,6 +859,30 @@ dg_status Context::finish(Slot &sl) {
     stat_resync_++;
     dg_status st = launch_all(sl, true);
     if (st) return st;
+  }
+  if (b.flags.wgtime) {
+    const size_t ns = b.lists[L_SYNC].size(), nw = b.lists[L_HUFF].size();
+    std::vector<uint64_t> rec(2 * (ns + nw));
+    HIPCHK(hipMemcpy(rec.data(), sl.wgt.p, rec.size() * 8, hipMemcpyDeviceToHost));
+    for (int a = 0; a < 2; a++) {
+      const size_t r0 = a ? ns : 0, n = a ? nw : ns;
+      if (!n) continue;
+      uint64_t lo = ~0ull, hi = 0;
+      std::vector<double> d(n);
+      double sum = 0;
+      for (size_t i = 0; i < n; i++) {
+        const uint64_t t0 = rec[2 * (r0 + i)], t1 = rec[2 * (r0 + i) + 1];
+        lo = std::min(lo, t0);
+        hi = std::max(hi, t1);
+        d[i] = (double)(t1 - t0) * 0.01;  // 100 MHz ticks -> us
+        sum += d[i];
+      }
+      std::sort(d.begin(), d.end());
+      wgstat_[a][0] = (double)(hi - lo) * 0.01;
+      wgstat_[a][1] = sum / (double)n;
+      wgstat_[a][2] = d[(size_t)(0.9 * (double)(n - 1))];
+      wgstat_[a][3] = d.back();
+    }
   }
   if (timing_) {
     last_ms_.assign(kNumStages, 0.f);

@@ -66,9 +66,15 @@ struct Batch {
 // and upload batch k+1 while the GPU still runs batch k.
 struct Slot {
   DevBuf scratch, meta, input;
+  DevBuf wgt;  // debug: per-workgroup timestamps of the entropy kernels (option "wg_timing")
   PinBuf stage, out;
   std::vector<hipEvent_t> ev;  // per-stage timing events
   hipEvent_t done = nullptr;   // recorded after the batch's last copy
+  // Each slot has its own streams, so batch k+1's entropy kernels can run
+  // beside batch k's pixel kernels (the entropy kernels leave most CUs idle
+  // in their tails).
+  hipStream_t st = nullptr, side = nullptr;
+  hipEvent_t ev_meta = nullptr, ev_coef = nullptr;
   std::unique_ptr<Batch> batch;
   size_t subs_off = 0, ckpt_off = 0;
 };
@@ -95,6 +101,7 @@ class Context {
   const BucketTable *buckets() const { return buckets_.get(); }
   int device() const { return device_; }
   hipStream_t stream() const { return stream_; }
+  dg_status sync_all();  // every stream of the context
   dg_status set_option(const std::string &k, int64_t v);
   int64_t get_stat(const std::string &k);
   int timings(const char **names, float *ms, int cap);
@@ -103,8 +110,8 @@ class Context {
   dg_status plan_image(const uint8_t *h, size_t len, int32_t forced, ImagePlan &p);
   int pool_huff(const HuffSpec &s);
   int pool_quant(const uint16_t *q);
-  dg_status ensure(DevBuf &b, size_t bytes);
-  dg_status ensure_pinned(PinBuf &b, size_t bytes);
+  dg_status ensure(DevBuf &b, size_t bytes, hipStream_t user = nullptr);
+  dg_status ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user = nullptr);
   dg_status upload_pools();
   dg_status launch_all(Slot &sl, bool from_fix);
   dg_status finish(Slot &sl);
@@ -135,6 +142,9 @@ class Context {
   bool timing_ = false;
   bool side_stream_ = true;
   int debug_flags_ = 0;
+  bool wg_timing_ = false;
+  // "wg_timing" summaries of the last batch (microseconds): per kernel {span, mean, p90, max}
+  double wgstat_[2][4] = {{0}};
   // stats
   int64_t stat_batches_ = 0, stat_resync_ = 0, stat_fix_ = 0, stat_mismatch_ = 0, stat_iters_ = 0;
   std::vector<float> last_ms_;

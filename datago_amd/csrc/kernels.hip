@@ -39,32 +39,85 @@ __device__ __forceinline__ void load_tables(HuffTable *tabs, const HuffTable *po
 
 // ------------------------------------------------------------ destuffing
 // Raw scan -> destuffed stream + RST marker positions, in three passes over
-// 4 KiB raw chunks (count / per-image scan / write).  The coded data is a few
-// percent of the pixel traffic, so plain byte loads are fine here.
+// 4 KiB raw chunks (count / per-image scan / write).  Each thread owns 16 raw
+// bytes, read with six aligned dword loads that also cover its neighbours;
+// chunks of 16 with no 0xFF byte (all but a few percent of them) are kept
+// whole without per-byte work.  The write pass stages the chunk's kept bytes
+// in LDS and stores them with aligned dwords.
 
-template <class P>
-__device__ __forceinline__ void destuff_thread(P raw, uint32_t n, uint32_t i0, uint32_t &kept,
-                                               uint32_t &mks, uint32_t keepmask[1], uint32_t &mkmask) {
-  kept = 0;
-  mks = 0;
-  keepmask[0] = 0;
-  mkmask = 0;
+struct Destuff16 {
+  uint32_t kept, mks;  // kept bytes, RST markers among the 16
+  uint32_t km, mm;     // per-byte keep / marker masks
+  uint32_t r[4];       // the 16 raw bytes, little-endian
+};
+
+__device__ __forceinline__ bool has_ff(uint32_t x) {
+  const uint32_t v = ~x;
+  return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u;
+}
+
+__device__ __forceinline__ Destuff16 destuff16(const DG_GLOBAL uint8_t *raw, uint32_t n, uint32_t i0) {
+  Destuff16 d;
+  d.kept = d.mks = d.km = d.mm = 0;
+  d.r[0] = d.r[1] = d.r[2] = d.r[3] = 0;
+  if (i0 >= n) return d;
+  if (i0 >= 4 && i0 + 24 <= n) {
+    // bytes [i0 - 1, i0 + 17) from the aligned 24-byte window at A (inside the scan)
+    const uintptr_t base = (uintptr_t)(raw + i0 - 1);
+    const DG_GLOBAL uint32_t *w4 = (const DG_GLOBAL uint32_t *)(base & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(base & 3);
+    uint32_t w[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) w[k] = w4[k];
+    // window dwords starting at byte sh (prev = byte 0 of W0) and sh + 1 (the 16 raw bytes)
+    uint32_t W[5];
+#pragma unroll
+    for (int m = 0; m < 5; m++) W[m] = __builtin_amdgcn_alignbyte(w[m + 1], w[m], sh);
+    uint32_t R[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) R[m] = (W[m] >> 8) | (W[m + 1] << 24);
+    const uint32_t prev = W[0] & 0xFFu;
+    const uint32_t next = W[4] >> 8 & 0xFFu;  // byte i0 + 16
+#pragma unroll
+    for (int m = 0; m < 4; m++) d.r[m] = R[m];
+    if (prev != 0xFFu && !has_ff(R[0]) && !has_ff(R[1]) && !has_ff(R[2]) && !has_ff(R[3])) {
+      d.kept = 16;
+      d.km = 0xFFFFu;
+      return d;
+    }
+    uint32_t p = prev;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++) {
+      const uint32_t cur = (R[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      const uint32_t nx = j < 15 ? (R[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xFFu : next;
+      uint32_t mk;
+      const uint32_t k = destuff_keep(p, cur, nx, false, &mk);
+      d.km |= k << j;
+      d.mm |= mk << j;
+      d.kept += k;
+      d.mks += mk;
+      p = cur;
+    }
+    return d;
+  }
+  // scan head / tail: byte loads
   uint32_t prev = i0 ? raw[i0 - 1] : 0u;
-  uint32_t cur = i0 < n ? raw[i0] : 0u;
-#pragma unroll 4
+  uint32_t cur = raw[i0];
   for (uint32_t j = 0; j < 16; j++) {
-    uint32_t i = i0 + j;
+    const uint32_t i = i0 + j;
     if (i >= n) break;
-    uint32_t next = i + 1 < n ? raw[i + 1] : 0xD9u;
-    uint32_t m;
-    uint32_t k = destuff_keep(prev, cur, next, i == 0, &m);
-    keepmask[0] |= k << j;
-    mkmask |= m << j;
-    kept += k;
-    mks += m;
+    const uint32_t next = i + 1 < n ? raw[i + 1] : 0xD9u;
+    d.r[j >> 2] |= cur << (8 * (j & 3));
+    uint32_t mk;
+    const uint32_t k = destuff_keep(prev, cur, next, i == 0, &mk);
+    d.km |= k << j;
+    d.mm |= mk << j;
+    d.kept += k;
+    d.mks += mk;
     prev = cur;
     cur = next;
   }
+  return d;
 }
 
 __global__ __launch_bounds__(256) void k_destuff_count(const ImageDesc *__restrict__ imgs,
@@ -73,10 +126,9 @@ __global__ __launch_bounds__(256) void k_destuff_count(const ImageDesc *__restri
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
   const int t = threadIdx.x;
-  uint32_t kept, mks, km[1], mm;
-  destuff_thread(gp<const uint8_t>(im.scan), im.scan_len, it.item0 * kDestuffChunk + t * 16, kept, mks, km, mm);
-  rk[t] = kept;
-  rm[t] = mks;
+  const Destuff16 d = destuff16(gp<const uint8_t>(im.scan), im.scan_len, it.item0 * kDestuffChunk + t * 16);
+  rk[t] = d.kept;
+  rm[t] = d.mks;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
     if (t < off) {
@@ -131,15 +183,13 @@ __global__ __launch_bounds__(256) void k_destuff_scan(ImageDesc *__restrict__ im
 __global__ __launch_bounds__(256) void k_destuff_write(const ImageDesc *__restrict__ imgs,
                                                        const WgItem *__restrict__ list) {
   __shared__ uint32_t sk[256], sm[256];
+  __shared__ uint8_t buf[kDestuffChunk];
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
   const int t = threadIdx.x;
-  const DG_GLOBAL uint8_t *raw = gp<const uint8_t>(im.scan);
-  const uint32_t i0 = it.item0 * kDestuffChunk + t * 16;
-  uint32_t kept, mks, km[1], mm;
-  destuff_thread(raw, im.scan_len, i0, kept, mks, km, mm);
-  sk[t] = kept;
-  sm[t] = mks;
+  const Destuff16 d = destuff16(gp<const uint8_t>(im.scan), im.scan_len, it.item0 * kDestuffChunk + t * 16);
+  sk[t] = d.kept;
+  sm[t] = d.mks;
   __syncthreads();
   for (int off = 1; off < 256; off <<= 1) {
     uint32_t a = t >= off ? sk[t - off] : 0u, b = t >= off ? sm[t - off] : 0u;
@@ -149,20 +199,51 @@ __global__ __launch_bounds__(256) void k_destuff_write(const ImageDesc *__restri
     __syncthreads();
   }
   const DG_GLOBAL uint32_t *ch = gp<const uint32_t>(im.chunk) + it.item0 * 4;
-  uint32_t o = ch[2] + sk[t] - kept;
-  uint32_t mo = ch[3] + sm[t] - mks;
-  DG_GLOBAL uint8_t *ds = gp<uint8_t>(im.ds);
-  DG_GLOBAL uint32_t *mk = gp<uint32_t>(im.mk);
-  for (uint32_t j = 0; j < 16; j++) {
-    if ((mm >> j) & 1u) {
-      if (mo < im.mk_cap) mk[mo] = o * 8;
-      mo++;
+  const uint32_t O = ch[2];           // chunk's first output byte
+  uint32_t o = sk[t] - d.kept;        // this thread's first byte within the chunk
+  const uint32_t total = sk[255];
+  if (d.km == 0xFFFFu) {
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++) buf[o + j] = (uint8_t)(d.r[j >> 2] >> (8 * (j & 3)));
+  } else {
+    uint32_t mo = ch[3] + sm[t] - d.mks;
+    DG_GLOBAL uint32_t *mk = gp<uint32_t>(im.mk);
+    for (uint32_t j = 0; j < 16; j++) {
+      if ((d.mm >> j) & 1u) {
+        if (mo < im.mk_cap) mk[mo] = (O + o) * 8;
+        mo++;
+      }
+      if ((d.km >> j) & 1u) buf[o++] = (uint8_t)(d.r[j >> 2] >> (8 * (j & 3)));
     }
-    if ((km[0] >> j) & 1u) ds[o++] = raw[i0 + j];
   }
+  __syncthreads();
+  // buf[0, total) -> ds[O, O + total): head bytes, aligned dwords, tail bytes
+  DG_GLOBAL uint8_t *ds = gp<uint8_t>(im.ds) + O;
+  const uint32_t mis = (uint32_t)((4u - ((uintptr_t)ds & 3u)) & 3u);  // bytes to the next dword boundary
+  const uint32_t head = mis < total ? mis : total;
+  const uint32_t nd = (total - head) >> 2;
+  if ((uint32_t)t < head) ds[t] = buf[t];
+  DG_GLOBAL uint32_t *d4 = (DG_GLOBAL uint32_t *)(ds + head);
+  for (uint32_t q = t; q < nd; q += 256) {
+    const uint32_t b0 = head + 4 * q;
+    d4[q] = (uint32_t)buf[b0] | ((uint32_t)buf[b0 + 1] << 8) | ((uint32_t)buf[b0 + 2] << 16) |
+            ((uint32_t)buf[b0 + 3] << 24);
+  }
+  const uint32_t tail0 = head + 4 * nd;
+  if ((uint32_t)t < total - tail0) ds[tail0 + t] = buf[tail0 + t];
 }
 
 // ------------------------------------------------------------ entropy decode
+
+// debug: {start, end} of workgroup `rec` in s_memrealtime ticks (100 MHz)
+__device__ __forceinline__ uint64_t wg_clock() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void wg_time_store(const BatchFlags *flags, uint32_t rec, uint64_t t0) {
+  if (flags->wgtime && threadIdx.x == 0) {
+    DG_GLOBAL uint64_t *p = gp<uint64_t>(flags->wgtime) + 2 * (size_t)rec;
+    p[0] = t0;
+    p[1] = wg_clock();
+  }
+}
 
 // Workgroup layout for sync/fix: 255 useful subsequences per workgroup.
 // Thread 0 is a lead-in: it decodes the previous workgroup's last subsequence
@@ -187,6 +268,7 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
                                                    BatchFlags *flags) {
   __shared__ HuffTable tabs[kMaxSlots];
   __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
+  const uint64_t t_start = wg_clock();
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
   load_tables(tabs, pool, im);
@@ -223,6 +305,7 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   }
   if (active && t > 0) store_sub(subs[im.sub_base + s], ins[t], ex[t], acc);
   if (t == 0) atomicMax(&flags->sync_iters_max, iters);
+  wg_time_store(flags, blockIdx.x, t_start);
 }
 
 __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ imgs,
@@ -340,29 +423,35 @@ __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict_
                                                     const SubState *__restrict__ subs, BatchFlags *flags) {
   __shared__ HuffTable tabs[kMaxSlots];
   __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][64];
+  const uint64_t t_start = wg_clock();
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
   load_tables(tabs, pool, im);
   __syncthreads();
   const int t = threadIdx.x;
   const uint32_t s = it.item0 + t;
-  if (s >= im.nsub) return;
-  const SubState ss = subs[im.sub_base + s];
-  WriteCtx w;
-  w.blk = blk[t];
-  w.coef = gp<int16_t>(im.coef);
-  w.seg = ss.seg;
-  w.nin = ss.nin;
-  w.pred[0] = ss.dcin[0];
-  w.pred[1] = ss.dcin[1];
-  w.pred[2] = ss.dcin[2];
-  w.blocks_per_seg = im.blocks_per_seg;
-  w.total_blocks = im.total_blocks;
-  w.cur = -1;
-  w.zs = 0;
-  RangeAcc acc;
-  decode_range<true>(im, tabs, gp<const uint8_t>(im.ds), gp<const uint32_t>(im.mk), s, ss.in, acc, &w);
-  if (acc.out != ss.out) atomicAdd(&flags->write_mismatch, 1u);
+  if (s < im.nsub) {
+    const SubState ss = subs[im.sub_base + s];
+    WriteCtx w;
+    w.blk = blk[t];
+    w.coef = gp<int16_t>(im.coef);
+    w.seg = ss.seg;
+    w.nin = ss.nin;
+    w.pred[0] = ss.dcin[0];
+    w.pred[1] = ss.dcin[1];
+    w.pred[2] = ss.dcin[2];
+    w.blocks_per_seg = im.blocks_per_seg;
+    w.total_blocks = im.total_blocks;
+    w.cur = -1;
+    w.zs = 0;
+    RangeAcc acc;
+    decode_range<true>(im, tabs, gp<const uint8_t>(im.ds), gp<const uint32_t>(im.mk), s, ss.in, acc, &w);
+    if (acc.out != ss.out) atomicAdd(&flags->write_mismatch, 1u);
+  }
+  if (flags->wgtime) {
+    __syncthreads();
+    wg_time_store(flags, flags->wgtime_write + blockIdx.x, t_start);
+  }
 }
 
 // ------------------------------------------------------------ IDCT

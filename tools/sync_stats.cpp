@@ -95,13 +95,24 @@ int main(int argc, char **argv) {
     d.bpm = bpm;
     const uint32_t total = (uint32_t)d.ds.size() * 8;
     std::vector<uint16_t> truth(total + 64, 0);  // (r << 7 | z) + 1 at true boundaries
+    uint64_t nsym = 0;
+    uint32_t worst = 0;  // most symbols in any S-bit window starting at a multiple of S
     {
-      uint32_t pos = 0, r = 0, z = 0;
+      uint32_t pos = 0, r = 0, z = 0, wstart = 0, wcount = 0;
       while (pos < total) {
         truth[pos] = (uint16_t)(((r << 7) | z) + 1);
         d.step(pos, r, z);
+        nsym++;
+        wcount++;
+        if (pos - wstart >= S) {
+          worst = std::max(worst, wcount);
+          wstart += S;
+          wcount = 0;
+        }
       }
     }
+    printf("  symbols=%llu bits=%u bits/sym=%.2f worst_syms_per_S=%u mean_syms_per_S=%.0f\n", (unsigned long long)nsym,
+           total, (double)total / (double)nsym, worst, (double)nsym * S / total);
     std::vector<uint32_t> dist;
     for (uint32_t a0 = S; a0 + 64 < total; a0 += S) {
       uint32_t pos = a0, r = 0, z = 0, n = 0;
