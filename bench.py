@@ -124,21 +124,33 @@ def stage_bytes(L, data: bytes, dim, target) -> dict:
          "color": (64 * nblk + 3 * w * h) if nc == 3 else 0.0, "coeffs": 0.0,
          "resize_h1": 0.0, "resize_v1": 0.0, "resize_h2": 0.0, "resize_v2": 0.0, "copy": 0.0}
     if (w, h) != (tw, th):
+        # mirrors the pass plan in pipeline.cpp: integral crop offsets fold into call 1
         nw, nh = B.scaled_size(w, h, tw, th)
-        cw = w
+        l, t, bw, bh = B.fit_crop_box(nw, nh, tw, th)
+        fold_x = abs(l - round(l)) <= 1e-6 and abs(bw - tw) <= 1e-6
+        fold_y = abs(t - round(t)) <= 1e-6 and abs(bh - th) <= 1e-6
+        cw, ch = w, h
         if nw != w:
+            wx = tw if fold_x else nw
             if nc == 3:  # fused: upsample + colour from the planes inside the first H pass
-                b["resize_h1"] = b["color"] - 3 * w * h + nc * nw * h
+                b["resize_h1"] = b["color"] - 3 * w * h + nc * wx * h
                 b["color"] = 0.0
             else:
-                b["resize_h1"] = nc * (w * h + nw * h)
-            cw = nw
+                b["resize_h1"] = nc * (w * h + wx * h)
+            cw = wx
+        elif fold_x:
+            cw = tw
         if nh != h:
-            b["resize_v1"] = nc * (cw * h + cw * nh)
-        if tw != nw:
-            b["resize_h2"] = nc * (nw * nh + tw * nh)
-        if th != nh:
-            b["resize_v2"] = nc * (tw * nh + tw * th)
+            hy = th if fold_y else nh
+            b["resize_v1"] = nc * (cw * h + cw * hy)
+            ch = hy
+        elif fold_y:
+            ch = th
+        if not fold_x:
+            b["resize_h2"] = nc * (cw * ch + tw * ch)
+            cw = tw
+        if not fold_y:
+            b["resize_v2"] = nc * (cw * ch + cw * th)
     else:
         b["copy"] = 2 * nc * w * h
     return b

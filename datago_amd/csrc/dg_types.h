@@ -97,6 +97,8 @@ struct ResizePass {
   int32_t precision;        // written by k_coeffs
   uint32_t src_stride, dst_stride;  // bytes per row
   uint32_t width, rows;     // output extent of this pass (pixels, rows)
+  uint32_t out0;            // first output (of out_size) computed: integral crops fold into the pass
+  uint32_t pad0;
   uint32_t row0;            // H pass: first source row; V pass: source row of temp row 0
   uint32_t C;               // channels
   uint32_t kind;            // 0 none, 1 horizontal, 2 vertical

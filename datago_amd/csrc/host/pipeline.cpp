@@ -448,7 +448,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.descs.reserve(n);
   // first pass: sizes only (pointers are patched after allocation)
   struct Offs {
-    size_t coef, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], tmp, out, ds, mk, chunk;
+    size_t coef, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], pass_srcoff[kStages];
+    size_t final_off, tmp, out, ds, mk, chunk;
   };
   std::vector<Offs> offs;
   for (int i = 0; i < n; i++) {
@@ -544,67 +545,80 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     d.out_h = p.out_h;
     d.out_c = p.out_c;
     d.out_stride = p.out_w * p.out_c;
-    uint32_t cw = W, chh = H;
-    int nst = 0;
+    // Passes (fast_image_resize semantics, B1): call 1 resizes W x H to the
+    // scaled nw x nh, call 2 crops the bucket out of it with a possibly
+    // fractional (x.5) offset.  An integral crop offset on an axis is only a
+    // window of call 1's outputs on that axis, so call 1's pass computes just
+    // that window (out0 / width) and call 2 needs no pass there; a fractional
+    // offset keeps call 2's sub-pixel pass.  Without a call-1 pass on an axis
+    // the window is a plain offset into the current image.
+    uint32_t cw = W, chh = H;     // extent of the current image's valid window
+    uint32_t xoff = 0, yoff = 0;  // window origin (pixels, rows) inside the current buffer
     int last_stage = -1;
+    auto add_pass = [&](int stage, uint32_t kind, double in0, double in1, uint32_t in_size, uint32_t out_size,
+                        uint32_t out0, uint32_t width, uint32_t rows, uint32_t row0) -> ResizePass & {
+      ResizePass &ps = d.pass[stage];
+      ps.kind = kind;
+      ps.in0 = in0;
+      ps.in1 = in1;
+      ps.in_size = in_size;
+      ps.out_size = out_size;
+      ps.out0 = out0;
+      ps.ksize = fir_ksize(in0, in1, out_size);
+      ps.src_stride = (uint32_t)cur_stride;
+      ps.width = width;
+      ps.rows = rows;
+      ps.row0 = row0;
+      ps.C = C;
+      ps.dst_stride = (uint32_t)align_up((size_t)width * C, 16);
+      o.pass_srcoff[stage] = (size_t)xoff * C;  // column window of the source (V passes)
+      o.pass_dst[stage] = L.take((size_t)ps.dst_stride * ps.rows);
+      o.pass_coef[stage] = L.take((size_t)out_size * ps.ksize * 2);
+      o.pass_bounds[stage] = L.take((size_t)out_size * 8);
+      cur_stride = ps.dst_stride;
+      last_stage = stage;
+      return ps;
+    };
     if (has_cfg_ && !(W == p.out_w && H == p.out_h)) {
       uint32_t nw, nh;
       scaled_size(W, H, p.out_w, p.out_h, nw, nh);
       double l, t, bw, bh;
       fit_crop_box(nw, nh, p.out_w, p.out_h, l, t, bw, bh);
-      struct Call {
-        uint32_t dw, dh;
-        double x0, y0, x1, y1;
-      } calls[2] = {{nw, nh, 0.0, 0.0, (double)W, (double)H}, {p.out_w, p.out_h, l, t, l + bw, t + bh}};
-      for (int r = 0; r < 2; r++) {
-        const Call &k = calls[r];
-        bool need_h = k.dw != cw || k.x0 != 0.0 || k.x1 != (double)k.dw;
-        bool need_v = k.dh != chh || k.y0 != 0.0 || k.y1 != (double)k.dh;
-        if (need_h) {
-          ResizePass &ps = d.pass[2 * r];
-          ps.kind = 1;
-          ps.in0 = k.x0;
-          ps.in1 = k.x1;
-          ps.in_size = cw;
-          ps.out_size = k.dw;
-          ps.ksize = fir_ksize(k.x0, k.x1, k.dw);
-          ps.src_stride = (uint32_t)cur_stride;
-          ps.width = k.dw;
-          ps.rows = chh;
-          ps.row0 = 0;
-          ps.C = C;
-          ps.dst_stride = (uint32_t)align_up((size_t)k.dw * C, 16);
-          ps.mode = h_pass_mode(ps, r == 0 && h.ncomp == 3);
-          o.pass_dst[2 * r] = L.take((size_t)ps.dst_stride * ps.rows);
-          o.pass_coef[2 * r] = L.take((size_t)ps.out_size * ps.ksize * 2);
-          o.pass_bounds[2 * r] = L.take((size_t)ps.out_size * 8);
-          cw = k.dw;
-          cur_stride = ps.dst_stride;
-          last_stage = 2 * r;
-          nst++;
-        }
-        if (need_v) {
-          ResizePass &ps = d.pass[2 * r + 1];
-          ps.kind = 2;
-          ps.in0 = k.y0;
-          ps.in1 = k.y1;
-          ps.in_size = chh;
-          ps.out_size = k.dh;
-          ps.ksize = fir_ksize(k.y0, k.y1, k.dh);
-          ps.src_stride = (uint32_t)cur_stride;
-          ps.width = cw;
-          ps.rows = k.dh;
-          ps.row0 = 0;
-          ps.C = C;
-          ps.dst_stride = (uint32_t)align_up((size_t)cw * C, 16);
-          o.pass_dst[2 * r + 1] = L.take((size_t)ps.dst_stride * ps.rows);
-          o.pass_coef[2 * r + 1] = L.take((size_t)ps.out_size * ps.ksize * 2);
-          o.pass_bounds[2 * r + 1] = L.take((size_t)ps.out_size * 8);
-          chh = k.dh;
-          cur_stride = ps.dst_stride;
-          last_stage = 2 * r + 1;
-          nst++;
-        }
+      // A window is exact for a scale-1 crop at an integral offset.  The crop box
+      // comes out of f64 arithmetic (640x480 -> top 6.000000000000028, height
+      // 431.99999999999994): deviations this small leave the i16 Lanczos
+      // weights exactly one-hot (they are < 2^-15 off), so the sub-pixel pass
+      // would copy pixel rint(offset) + i and the window is still bit-exact.
+      auto near_int = [](double v, double tgt) { return std::fabs(v - tgt) <= 1e-6; };
+      const bool fold_x = near_int(l, std::rint(l)) && near_int(bw, (double)p.out_w);
+      const bool fold_y = near_int(t, std::rint(t)) && near_int(bh, (double)p.out_h);
+      const uint32_t lx = fold_x ? (uint32_t)std::rint(l) : 0u, ty = fold_y ? (uint32_t)std::rint(t) : 0u;
+      if (nw != W) {  // call 1, horizontal
+        ResizePass &ps = add_pass(0, 1, 0.0, (double)W, W, nw, fold_x ? lx : 0u, fold_x ? p.out_w : nw, chh, 0);
+        ps.mode = h_pass_mode(ps, h.ncomp == 3);
+        cw = ps.width;
+      } else if (fold_x) {
+        xoff = lx;
+        cw = p.out_w;
+      }
+      if (nh != H) {  // call 1, vertical (reads the column window, absorbs xoff)
+        ResizePass &ps = add_pass(1, 2, 0.0, (double)H, H, nh, fold_y ? ty : 0u, cw, fold_y ? p.out_h : nh, 0);
+        chh = ps.rows;
+        xoff = 0;
+      } else if (fold_y) {
+        yoff = ty;
+        chh = p.out_h;
+      }
+      if (!fold_x) {  // call 2, horizontal sub-pixel crop (reads the row window, absorbs yoff)
+        ResizePass &ps = add_pass(2, 1, l, l + bw, cw, p.out_w, 0, p.out_w, chh, yoff);
+        ps.mode = h_pass_mode(ps, false);
+        cw = p.out_w;
+        yoff = 0;
+      }
+      if (!fold_y) {  // call 2, vertical sub-pixel crop (reads the column window, absorbs xoff)
+        add_pass(3, 2, t, t + bh, chh, p.out_h, 0, cw, p.out_h, 0);
+        chh = p.out_h;
+        xoff = 0;
       }
     }
     // colour images whose first pass is not a fused H pass need the RGB image
@@ -620,8 +634,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       d.copy_needed = 1;
       d.final_src_c = C;
       d.final_src_stride = (uint32_t)cur_stride;
+      o.final_off = (size_t)yoff * cur_stride + (size_t)xoff * C;  // an uncomputed integral crop
     }
-    (void)nst;
     if (host_io) {
       o.out = L.take(p.out_bytes, 16);
       b.out_dev_off[i] = o.out;
@@ -663,13 +677,13 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     for (int s = 0; s < kStages; s++) {
       ResizePass &ps = d.pass[s];
       if (!ps.kind) continue;
-      ps.src = cur;
+      ps.src = cur + o.pass_srcoff[s];
       ps.dst = o.pass_dst[s] == (size_t)-1 ? out : (uint64_t)(uintptr_t)(S + o.pass_dst[s]);
       ps.coef = (uint64_t)(uintptr_t)(S + o.pass_coef[s]);
       ps.bounds = (uint64_t)(uintptr_t)(S + o.pass_bounds[s]);
       cur = ps.dst;
     }
-    d.final_src = cur;
+    d.final_src = cur + (d.copy_needed ? o.final_off : 0);
     (void)subs_off;
   }
   // ---- 5. workgroup lists

@@ -794,7 +794,7 @@ __global__ __launch_bounds__(256) void k_resize_h(const ImageDesc *__restrict__ 
   if (y >= ps.rows) return;
   const uint32_t x0 = tile * kResizeTile;
   const uint32_t x1 = x0 + kResizeTile < ps.width ? x0 + kResizeTile : ps.width;
-  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds);  // {start, size} per output
+  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds) + 2 * ps.out0;  // {start, size} per output
   const uint32_t C = ps.C;
   // source bytes [sb, se) of the tile (min/max: trimmed starts are not monotone)
   __shared__ uint32_t ext[2];
@@ -821,7 +821,7 @@ __global__ __launch_bounds__(256) void k_resize_h(const ImageDesc *__restrict__ 
   }
   __syncthreads();
   DG_GLOBAL uint8_t *drow = gp<uint8_t>(ps.dst) + (size_t)y * ps.dst_stride;
-  const DG_GLOBAL int16_t *coef = gp<const int16_t>(ps.coef);
+  const DG_GLOBAL int16_t *coef = gp<const int16_t>(ps.coef) + (size_t)ps.out0 * ps.ksize;
   const int32_t prec = ps.precision;
   if (staged) {
     for (uint32_t x = x0 + threadIdx.x; x < x1; x += 256)
@@ -965,9 +965,10 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
   const uint32_t nrows = ps.rows - y0 < kHBandRows ? ps.rows - y0 : kHBandRows;
   const uint32_t x0 = tile * kHBandCols;
   const uint32_t x1 = x0 + kHBandCols < ps.width ? x0 + kHBandCols : ps.width;
-  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds);
-  const DG_GLOBAL int16_t *coef = gp<const int16_t>(ps.coef);
+  // coefficient tables cover all out_size outputs; this pass computes [out0, out0 + width)
+  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds) + 2 * ps.out0;
   const uint32_t C = ps.C, ksize = ps.ksize;
+  const DG_GLOBAL int16_t *coef = gp<const int16_t>(ps.coef) + (size_t)ps.out0 * ksize;
   const uint32_t t = threadIdx.x, col = t & (kHBandCols - 1), x = x0 + col;
   const bool valid = x < x1;
   // Source segment of the tile.  Trimmed window starts are not strictly
@@ -992,19 +993,19 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
   if (p1 - p0 > kHSegPx) p1 = p0 + kHSegPx;  // host sizing guarantees this never triggers
   const uint32_t pe = p1 < ps.in_size ? p1 : ps.in_size;
   // phase 1: fill
-  if (ps.mode & kHFused) {
-    const uint32_t noct = (pe - p0 + 7) >> 3;
-    for (uint32_t j = t; j < noct * nrows; j += blockDim.x) {
-      const uint32_t r = j / noct, q = j - r * noct;
-      hfill_color8(im, ps.row0 + y0 + r, p0 + 8 * q, seg + r * kHSegStride + 8 * q);
-    }
-  } else {
-    const uint32_t nu = (pe - p0 + 3) >> 2;
-    const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0) * ps.src_stride;
-    for (uint32_t j = t; j < nu * nrows; j += blockDim.x) {
-      const uint32_t r = j / nu, u = j - r * nu;
-      hfill_bytes4(src + (size_t)r * ps.src_stride, C, ps.src_stride, ps.in_size, p0 + 4 * u,
-                   seg + r * kHSegStride + 4 * u);
+  // fill: 32 threads per row (kHBandRows * 32 == 256), no divisions
+  static_assert(kHBandRows * 32 == 256, "fill mapping");
+  const uint32_t fr = t >> 5, fl = t & 31;
+  if (fr < nrows) {
+    if (ps.mode & kHFused) {
+      const uint32_t noct = (pe - p0 + 7) >> 3;
+      for (uint32_t q = fl; q < noct; q += 32)
+        hfill_color8(im, ps.row0 + y0 + fr, p0 + 8 * q, seg + fr * kHSegStride + 8 * q);
+    } else {
+      const uint32_t nu = (pe - p0 + 3) >> 2;
+      const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0 + fr) * ps.src_stride;
+      for (uint32_t u = fl; u < nu; u += 32)
+        hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * u, seg + fr * kHSegStride + 4 * u);
     }
   }
   int32_t kw[KMAX > 0 ? KMAX : 1];
@@ -1029,10 +1030,10 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
   }
   __syncthreads();
   // phase 3: store the band's rows, 16 bytes per thread per step
-  const uint32_t rb = (x1 - x0) * C, cpr = (rb + 15) >> 4;
+  const uint32_t rb = (x1 - x0) * C;  // <= kHBandCols * 4 = 512 bytes: 32 chunks of 16
   DG_GLOBAL uint8_t *dst = gp<uint8_t>(ps.dst) + (size_t)y0 * ps.dst_stride + (size_t)x0 * C;
-  for (uint32_t j = t; j < cpr * nrows; j += blockDim.x) {
-    const uint32_t r = j / cpr, b = (j - r * cpr) * 16;
+  if (fr < nrows && fl * 16 < rb) {
+    const uint32_t r = fr, b = fl * 16;
     DG_GLOBAL uint8_t *d = dst + (size_t)r * ps.dst_stride + b;
     const uint8_t *o = ob + r * (kHBandCols * 4) + b;
     if (b + 16 <= rb && (((uintptr_t)d) & 15) == 0) {
@@ -1069,9 +1070,10 @@ __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ 
   const uint32_t y = idx / units, u = idx - y * units;
   const uint32_t b0 = u * 16;
   const uint32_t nb = rowbytes - b0 < 16 ? rowbytes - b0 : 16;
+  const uint32_t yc = y + ps.out0;  // coefficient row: the pass may compute a window of out_size
   const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds);
-  const int32_t start = bounds[2 * y], n = bounds[2 * y + 1];
-  const DG_GLOBAL int16_t *k = gp<const int16_t>(ps.coef) + (size_t)y * ps.ksize;
+  const int32_t start = bounds[2 * yc], n = bounds[2 * yc + 1];
+  const DG_GLOBAL int16_t *k = gp<const int16_t>(ps.coef) + (size_t)yc * ps.ksize;
   const int32_t prec = ps.precision, bias = 1 << (prec - 1);
   int32_t a[16];
 #pragma unroll

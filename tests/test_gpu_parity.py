@@ -251,3 +251,33 @@ def test_h_pass_classes_bit_exact(ctx512, case):
     assert arr.shape == ref.shape
     d = np.abs(arr.astype(int) - ref.astype(int))
     assert d.max() == 0, (int(d.max()), int((d > 0).sum()), np.argwhere(d > 0)[:4].tolist())
+
+
+# Crop folding: an integral crop offset is a window of call 1's
+# outputs, a fractional one keeps call 2's sub-pixel pass; without a call-1
+# pass on an axis the window is a plain offset (these sizes have scale 1 on
+# one or both axes at the 512/16 buckets: 592x432 / 432x592 / 512x512).
+CROP_CASES = [
+    (700, 432, False),   # scale 1, integral x crop: no pass at all, offset copy
+    (701, 432, False),   # scale 1, x.5 crop: H2 alone
+    (432, 700, True),    # gray, integral y crop
+    (432, 701, False),   # y.5 crop: V2 alone
+    (1184, 865, False),  # downscale, y crop window folded into V1
+    (1185, 864, True),   # gray, downscale
+    (640, 480, False),   # 592x444 -> crop top 6 (integral, folded into V1)
+]
+
+
+@pytest.mark.parametrize("case", CROP_CASES, ids=lambda c: f"{c[0]}x{c[1]}_{'L' if c[2] else 'RGB'}")
+def test_crop_folding_bit_exact(ctx512, case):
+    w, h, gray = case
+    data = synth.make_jpeg(60 + w % 89 + h % 7, w, h, 90, "4:2:0", gray=gray)
+    st, arr, meta = ctx512.decode_one(data)
+    assert st == 0
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    tw, th = t.target_size(w, h)
+    assert (meta.width, meta.height) == (tw, th)
+    ref = _oracle_resized(data, tw, th)
+    assert arr.shape == ref.shape
+    d = np.abs(arr.astype(int) - ref.astype(int))
+    assert d.max() == 0, (int(d.max()), int((d > 0).sum()))
