@@ -48,6 +48,12 @@ def parse():
     ap.add_argument("--sub-bits", type=int, default=0)
     ap.add_argument("--workers", type=int, default=0, help="corpus generation processes")
     ap.add_argument("--lead-bits", type=int, default=-1, help="entropy lead-in bits (-1 = library default)")
+    ap.add_argument("--serial-steps", type=int, default=3,
+                    help="untimed batches run one at a time after the timed region: per-kernel times without "
+                         "the overlap of consecutive batches (roofline_isolated)")
+    ap.add_argument("--pmc-json", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01",
+                                                       "pmc_traffic.json"),
+                    help="per-stage HBM bytes from a PMC run of this configuration (tools/pmc_traffic.py)")
     ap.add_argument("--wg-timing", action="store_true", help="debug: per-workgroup timing of the entropy kernels")
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -104,6 +110,11 @@ def cpu_baseline(pool, targets, seconds: float):
 
 
 # ------------------------------------------------------------- roofline
+
+def pmc_config_key(a) -> str:
+    """Identifies the workload a PMC traffic file was measured on."""
+    return f"batch={a.batch} pool={a.pool} size={a.size}/{a.ratio} short={a.short_min}-{a.short_max}"
+
 
 def stage_bytes(L, data: bytes, dim, target) -> dict:
     """Algorithmic bytes each kernel stage must move for one image (DESIGN.md
@@ -286,6 +297,20 @@ def main() -> int:
     (dt_max,) = max_over_ranks([dt], world)
     px_all, alg_all, outpx_all = sum_over_ranks([float(px_total), alg_bytes, float(out_px)], world)
 
+    # ---- isolated per-kernel times: batches one at a time (untimed, reported only)
+    ser_tot, ser_alg, ser_n = {}, {}, 0
+    if a.serial_steps > 0:
+        ctx.set_option("timing", 1)
+        for k in range(a.serial_steps):
+            idx = complete(submit(k))
+            ser_n += 1
+            for i in idx:
+                for kk, vv in img_stage_bytes[i].items():
+                    ser_alg[kk] = ser_alg.get(kk, 0.0) + vv
+            for name, ms in ctx.timings().items():
+                ser_tot[name] = ser_tot.get(name, 0.0) + ms
+        ctx.set_option("timing", 0)
+
     # ---- end-to-end (host memory in and out: PCIe-inclusive), reported only
     e2e = None
     if a.e2e_steps > 0 and rank == 0:
@@ -308,6 +333,25 @@ def main() -> int:
         dom_alg = stage_alg[dom] / steps if dom in stage_alg else 0.0
         achieved = dom_alg / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
         gpu_ms = sum(kern.values()) / steps
+        traffic, traffic_src = None, None
+        try:
+            with open(a.pmc_json) as f:
+                pmc = json.load(f)
+            if pmc.get("config") == pmc_config_key(a) and dom in pmc.get("bytes_per_batch", {}):
+                traffic = pmc["bytes_per_batch"][dom] * (B_ / pmc.get("images_per_batch", B_))
+                traffic_src = f"{os.path.relpath(a.pmc_json)} ({pmc.get('correction', '')})"
+        except (OSError, ValueError):
+            pass
+        iso = None
+        if ser_n:
+            skern = {k: v / ser_n for k, v in ser_tot.items() if k not in ("upload", "download")}
+            sdom = max(skern, key=skern.get)
+            sach = (ser_alg.get(sdom, 0.0) / ser_n) / (skern[sdom] / 1e3) / 1e9 if skern[sdom] > 0 else 0.0
+            iso = {"kernel": sdom, "kernel_ms_per_launch": round(skern[sdom], 4), "achieved": round(sach, 2),
+                   "unit": "GB/s", "frac": round(sach / HBM_PEAK_GBS, 5), "batches": ser_n,
+                   "stages_ms": {k: round(v, 4) for k, v in skern.items()},
+                   "stages_alg_GBs": {k: round(ser_alg[k] / ser_n / (v / 1e3) / 1e9, 1)
+                                      for k, v in skern.items() if ser_alg.get(k) and v > 0}}
         result = {
             "metric": "Mpixel/s device-resident JPEG decode+bucket-resize at 1/2/4/8 MI355X",
             "value": round(px_all / dt_max / 1e6, 2),
@@ -327,8 +371,12 @@ def main() -> int:
                        "short_side": [a.short_min, a.short_max], "buckets": f"{a.size}/{a.ratio}/0.5/2.0",
                        "parallelism": f"dp{world} (sample shards, no collectives)"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel_ms_per_launch": round(dom_ms, 4)},
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
+                         "alg_bytes_per_launch": round(dom_alg), "kernel_ms_per_launch": round(dom_ms, 4),
+                         "note": "per step (one batch); kernel times from HIP events on the slot stream over the "
+                                 "timed region, where consecutive batches overlap"},
+            "roofline_isolated": iso,
             "roofline_pipeline": {"alg_bytes_per_step": round(per_step_alg), "gpu_ms_per_step": round(gpu_ms, 4),
                                   "achieved_GBs": round(per_step_alg / (gpu_ms / 1e3) / 1e9, 2),
                                   "frac": round(per_step_alg / (gpu_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)},

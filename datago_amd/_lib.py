@@ -266,7 +266,19 @@ class Context:
         return res
 
     def decode_one(self, data: bytes, forced_bucket: int = -1):
-        return self.decode_batch([data], [forced_bucket])[0]
+        """dg_decode_one: one image; concurrent callers (threads) are coalesced
+        into shared GPU batches by the library."""
+        st, nb = self.output_size(data, forced_bucket)
+        if st != DG_OK:
+            return st, None, PayloadMeta()
+        out = np.empty(max(nb, 1), np.uint8)
+        m = PayloadMeta()
+        st = load().dg_decode_one(self._h, data, len(data), forced_bucket, out.ctypes.data, max(nb, 1),
+                                  ctypes.byref(m))
+        if st != DG_OK:
+            return st, None, m
+        c = int(m.nbytes // (m.width * m.height)) if m.width and m.height else 0
+        return DG_OK, out[: m.nbytes].reshape(m.height, m.width, c), m
 
     # -- device-resident path (bench): coded bytes already in HBM
     def alloc(self, nbytes: int) -> int:

@@ -36,19 +36,38 @@ DG_HD uint32_t bswap32(uint32_t x) {
 // instead of stalling the whole wave in the lanes' divergent refills.  One
 // symbol consumes at most 31 bits, so with pos - base < 32 before a symbol at
 // most one 32-bit shift follows it.
+// Destuffed streams are stored word-interleaved across groups of 64
+// subsequences: logical 32-bit word w of subsequence s = w >> lsw (2^lsw
+// words per subsequence) sits in row (s / 64) * 2^lsw + (w mod 2^lsw),
+// column s mod 64 of a 64-word-wide array.  The 64 lanes of a wave decode
+// 64 consecutive subsequences at about the same relative position, so their
+// loads hit the same 256-byte rows: coalesced and L2-resident, instead of 64
+// lines scattered 2^lsw words apart that the L2 cannot hold for the whole
+// batch (PMC: 17x fetch amplification with the plain layout).
+DG_HD uint32_t ds_word_index(uint32_t w, uint32_t lsw) {
+  const uint32_t s = w >> lsw, j = w & ((1u << lsw) - 1u);
+  return ((((s >> 6) << lsw) + j) << 6) + (s & 63u);
+}
+// physical words needed for a stream of nsub subsequences (+ one column of margin)
+DG_HD uint64_t ds_words_alloc(uint32_t nsub, uint32_t lsw) { return ((uint64_t)(nsub / 64 + 1) << lsw) * 64; }
+
 struct BitWin {
-  const DG_GLOBAL uint32_t *w;  // stream as little-endian words (byte-swapped on use)
+  const DG_GLOBAL uint32_t *w;  // interleaved stream as little-endian words (byte-swapped on use)
   uint64_t win;       // bits [base, base + 64)
   uint32_t base;      // bit position of win's MSB (multiple of 32)
   uint32_t nraw;      // raw word base/32 + 2
+  uint32_t lsw;       // log2(words per subsequence)
 };
 
-DG_HD void bw_init(BitWin &b, const DG_GLOBAL uint8_t *stream, uint32_t pos) {
+DG_HD uint32_t bw_word(const BitWin &b, uint32_t i) { return b.w[ds_word_index(i, b.lsw)]; }
+
+DG_HD void bw_init(BitWin &b, const DG_GLOBAL uint8_t *stream, uint32_t lsw, uint32_t pos) {
   b.w = (const DG_GLOBAL uint32_t *)stream;
+  b.lsw = lsw;
   uint32_t i = pos >> 5;
   b.base = i << 5;
-  b.win = ((uint64_t)bswap32(b.w[i]) << 32) | bswap32(b.w[i + 1]);
-  b.nraw = b.w[i + 2];
+  b.win = ((uint64_t)bswap32(bw_word(b, i)) << 32) | bswap32(bw_word(b, i + 1));
+  b.nraw = bw_word(b, i + 2);
 }
 
 // 32 bits starting at pos (requires base <= pos < base + 32).
@@ -59,12 +78,12 @@ DG_HD void bw_shift(BitWin &b, uint32_t pos) {
   if (pos - b.base >= 32) {
     b.win = (b.win << 32) | bswap32(b.nraw);
     b.base += 32;
-    b.nraw = b.w[(b.base >> 5) + 2];
+    b.nraw = bw_word(b, (b.base >> 5) + 2);
   }
 }
 
 DG_HD void bw_seek(BitWin &b, uint32_t pos) {
-  if (pos - b.base >= 32u) bw_init(b, (const DG_GLOBAL uint8_t *)b.w, pos);
+  if (pos - b.base >= 32u) bw_init(b, (const DG_GLOBAL uint8_t *)b.w, b.lsw, pos);
 }
 
 // Decode one Huffman code from the top bits of `bits`; returns (len << 8) | sym.
@@ -189,7 +208,7 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
   const uint32_t bpm = im.bpm, slotmap = im.slotmap, cbits = im.comp_bits;
   uint32_t comp = cbits & 3u;
   BitWin b;
-  bw_init(b, stream, pos);
+  bw_init(b, stream, im.ds_lsw, pos);
   for (;;) {
     if (pos >= mpos) {  // restart marker before the start: exact state from here
       pos = mpos;
@@ -252,7 +271,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
   const uint32_t bpm = im.bpm;
   const uint32_t slotmap = im.slotmap;  // 4 bits per (component, dc/ac)
   BitWin b;
-  bw_init(b, stream, pos < a1 ? pos : a0);
+  bw_init(b, stream, im.ds_lsw, pos < a1 ? pos : a0);
   const uint32_t cbits = im.comp_bits;
   uint32_t comp = (cbits >> (2 * r)) & 3u;
   const uint32_t nck = ck ? num_ckpt(S) : 0;

@@ -119,7 +119,7 @@ struct ImageDesc {
   uint32_t nsub;            // subsequences (sized from the raw length)
   uint32_t sub_base;        // first SubState index
   uint32_t sub_bits;        // bits per subsequence
-  uint64_t ds;              // destuffed stream (4-byte aligned, >= 32 zero bytes of padding)
+  uint64_t ds;              // destuffed stream, word-interleaved (ds_word_index), >= 64 zero bytes past its end
   uint64_t mk;              // RST marker positions in ds (bits), ascending
   uint64_t chunk;           // destuff per-chunk records: uint32 {cnt, mkc, off, mkoff}
   uint32_t nchunk;          // raw chunks of kDestuffChunk bytes
@@ -128,6 +128,8 @@ struct ImageDesc {
   uint32_t slotmap;         // Huffman slot of (component c, dc=0/ac=1) at nibble 2c+ac
   uint32_t mk_cap;          // capacity of the marker list
   uint32_t lead_bits;       // k_huff_sync lead-in before each subsequence (lead_in)
+  uint32_t ds_lsw;          // log2(32-bit words per subsequence) of the interleaved stream
+  uint32_t pad_ds;
   uint32_t restart;         // restart interval (MCUs), 0 = none
   uint32_t blocks_per_seg;  // restart * bpm, 0 = unlimited
   uint32_t total_blocks;

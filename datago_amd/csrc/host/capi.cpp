@@ -174,17 +174,7 @@ dg_status dg_poll(dg_ctx *ctx, uint64_t ticket) { return ctx ? ctx->c.poll(ticke
 dg_status dg_decode_one(dg_ctx *ctx, const uint8_t *src, size_t len, int32_t forced, uint8_t *out, uint64_t cap,
                         dg_payload_meta *meta) {
   if (!ctx || !meta) return DG_ERR_INVALID;
-  uint64_t t = 0;
-  const uint8_t *srcs[1] = {src};
-  size_t lens[1] = {len};
-  int32_t f[1] = {forced};
-  uint8_t *outs[1] = {out};
-  uint64_t caps[1] = {cap};
-  dg_status st = ctx->c.submit(1, srcs, nullptr, lens, f, outs, caps, meta, true, &t);
-  if (st) return st;
-  st = ctx->c.wait(t);
-  if (st) return st;
-  return (dg_status)meta->status;
+  return ctx->c.decode_one(src, len, forced, out, cap, meta);
 }
 
 dg_status dg_device_alloc(dg_ctx *ctx, size_t bytes, void **dptr) {

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 
 #include "../dg_entropy.h"
@@ -50,8 +51,9 @@ Context::~Context() {
   for (Slot &sl : slots_) {
     for (auto e : sl.ev) hipEventDestroy(e);
     if (sl.done) hipEventDestroy(sl.done);
-    for (hipEvent_t e : {sl.ev_meta, sl.ev_coef})
+    for (hipEvent_t e : {sl.ev_meta, sl.ev_coef, sl.ev_zero})
       if (e) hipEventDestroy(e);
+    if (sl.coef.p) hipFree(sl.coef.p);
     for (hipStream_t q : {sl.st, sl.side})
       if (q) hipStreamDestroy(q);
     if (sl.wgt.p) hipFree(sl.wgt.p);
@@ -101,6 +103,7 @@ dg_status Context::init() {
     HIPCHK(hipStreamCreateWithFlags(&sl.side, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_meta, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_coef, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_zero, hipEventDisableTiming));
   }
   return DG_OK;
 }
@@ -135,13 +138,25 @@ static uint32_t h_pass_mode(const ResizePass &ps, bool colour_source) {
 
 dg_status Context::set_option(const std::string &k, int64_t v) {
   if (k == "sub_bits") {
-    if (v != 0 && (v < 64 || v > 65536 || (v & 31))) return DG_ERR_INVALID;
+    if (v != 0 && (v < 64 || v > 65536 || (v & (v - 1)))) return DG_ERR_INVALID;  // power of two
     sub_bits_ = (uint32_t)v;
     return DG_OK;
   }
   if (k == "lead_bits") {
     if (v < -1 || v > (1 << 20)) return DG_ERR_INVALID;
     lead_bits_ = v;
+    return DG_OK;
+  }
+  if (k == "coalesce_max") {
+    if (v < 1 || v > 4096) return DG_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(cmu_);
+    coalesce_max_ = (int)v;
+    return DG_OK;
+  }
+  if (k == "coalesce_us") {
+    if (v < 0 || v > 1000000) return DG_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(cmu_);
+    coalesce_us_ = (int)v;
     return DG_OK;
   }
   if (k == "wg_timing") {
@@ -165,6 +180,8 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
 
 int64_t Context::get_stat(const std::string &k) {
   if (k == "batches") return stat_batches_;
+  if (k == "coalesced_batches") return stat_coalesced_batches_;
+  if (k == "coalesced_images") return stat_coalesced_images_;
   if (k == "resync_rounds") return stat_resync_;
   if (k == "fix_workgroups") return stat_fix_;
   if (k == "write_mismatch") return stat_mismatch_;
@@ -440,6 +457,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   last_sub_bits_ = sub_bits;
   Layout L;        // scratch arena
+  Layout CO;       // coefficient arena (zero-filled per batch)
   Layout IN;       // input arena (host path)
   std::vector<size_t> in_off(n, 0);
   size_t out_total = 0;
@@ -525,12 +543,14 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     d.nchunk = std::max<uint32_t>(1, (d.scan_len + kDestuffChunk - 1) / kDestuffChunk);
     uint32_t mcus = h.ncomp == 1 ? d.total_blocks : d.mcux * d.mcuy;
     d.mk_cap = (d.restart ? mcus / d.restart + 2 : 0) + 64;
-    o.ds = L.take((size_t)d.scan_len + 64, 16);
+    d.ds_lsw = 0;
+    while ((32u << d.ds_lsw) < sub_bits) d.ds_lsw++;
+    o.ds = L.take((size_t)ds_words_alloc(d.nsub, d.ds_lsw) * 4, 256);
     o.mk = L.take((size_t)d.mk_cap * 4, 16);
     o.chunk = L.take((size_t)d.nchunk * 16, 16);
     if (host_io) in_off[i] = IN.take(lens[i] + 16, 16);
     // buffers
-    o.coef = L.take((size_t)d.total_blocks * 128);
+    o.coef = CO.take((size_t)d.total_blocks * 128);
     for (int c = 0; c < h.ncomp; c++) o.plane[c] = L.take((size_t)d.cbw[c] * 8 * d.cbh[c] * 8);
     const uint32_t C = d.dec_c;
     size_t cur_stride;
@@ -651,6 +671,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   const size_t ckpt_off = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits)) * sizeof(Ckpt));
   st = ensure(sl.scratch, L.off + 256, sl.st);
   if (st) return st;
+  st = ensure(sl.coef, CO.off + 256, sl.st);
+  if (st) return st;
+  sl.coef_bytes = CO.off;
   if (host_io) {
     st = ensure(sl.input, IN.off + 64, sl.st);
     if (st) return st;
@@ -665,7 +688,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     const JpegHeader &h = b.plans[i].hdr;
     const uint8_t *src = host_io ? (const uint8_t *)sl.input.p + in_off[i] : d_srcs[i];
     d.scan = (uint64_t)(uintptr_t)(src + h.scan_off);
-    d.coef = (uint64_t)(uintptr_t)(S + o.coef);
+    d.coef = (uint64_t)(uintptr_t)((char *)sl.coef.p + o.coef);
     d.ds = (uint64_t)(uintptr_t)(S + o.ds);
     d.mk = (uint64_t)(uintptr_t)(S + o.mk);
     d.chunk = (uint64_t)(uintptr_t)(S + o.chunk);
@@ -800,6 +823,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     hipStream_t cs = side_stream_ ? sl.side : sl.st;
     HIPCHK(hipEventRecord(sl.ev_meta, sl.st));
     HIPCHK(hipStreamWaitEvent(cs, sl.ev_meta, 0));
+
     launch_coeffs(cs, dm, lst(L_COEF), cnt(L_COEF));
     HIPCHK(hipEventRecord(sl.ev_coef, cs));
     launch_destuff_count(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
@@ -927,12 +951,98 @@ Slot *Context::find(uint64_t ticket) {
 }
 
 dg_status Context::wait(uint64_t ticket) {
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    HIPCHK(hipSetDevice(device_));
+    Slot *sl = find(ticket);
+    if (!sl) return ticket < next_ticket_ ? DG_OK : DG_ERR_INVALID;  // already recycled => completed
+    if (sl->batch->done) return DG_OK;
+    ev = sl->done;
+  }
+  // block on the GPU without holding the context lock, so other threads can
+  // plan and submit meanwhile (if the slot is recycled first, the wait below
+  // only takes longer; the ticket then reads as completed)
+  HIPCHK(hipEventSynchronize(ev));
   std::lock_guard<std::mutex> lk(mu_);
-  HIPCHK(hipSetDevice(device_));
   Slot *sl = find(ticket);
-  if (!sl) return ticket < next_ticket_ ? DG_OK : DG_ERR_INVALID;  // already recycled => completed
+  if (!sl) return ticket < next_ticket_ ? DG_OK : DG_ERR_INVALID;
   if (sl->batch->done) return DG_OK;
   return finish(*sl);
+}
+
+dg_status Context::flush_batch(std::vector<OneReq *> &batch) {
+  const int n = (int)batch.size();
+  std::vector<const uint8_t *> srcs(n);
+  std::vector<size_t> lens(n);
+  std::vector<int32_t> forced(n);
+  std::vector<uint8_t *> outs(n);
+  std::vector<uint64_t> caps(n);
+  std::vector<dg_payload_meta> metas(n);
+  for (int i = 0; i < n; i++) {
+    srcs[i] = batch[i]->src;
+    lens[i] = batch[i]->len;
+    forced[i] = batch[i]->forced;
+    outs[i] = batch[i]->out;
+    caps[i] = batch[i]->cap;
+  }
+  uint64_t t = 0;
+  dg_status st = submit(n, srcs.data(), nullptr, lens.data(), forced.data(), outs.data(), caps.data(), metas.data(),
+                        true, &t);
+  if (!st) st = wait(t);
+  for (int i = 0; i < n; i++) {
+    *batch[i]->meta = metas[i];
+    batch[i]->st = st ? st : (dg_status)metas[i].status;
+  }
+  return st;
+}
+
+dg_status Context::decode_one(const uint8_t *src, size_t len, int32_t forced, uint8_t *out, uint64_t cap,
+                              dg_payload_meta *meta) {
+  OneReq r{src, len, forced, out, cap, meta, false, DG_OK};
+  if (coalesce_max_ <= 1) {
+    std::vector<OneReq *> one{&r};
+    flush_batch(one);
+    return r.st;
+  }
+  std::unique_lock<std::mutex> lk(cmu_);
+  callers_++;
+  pending_.push_back(&r);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(coalesce_us_);
+  for (;;) {
+    if (r.done) break;
+    // flush when the batch is full, when every caller in here is already
+    // waiting (nobody else can add), or at the deadline; two batches in
+    // flight at most (the context's two slots)
+    const bool ready = !pending_.empty() &&
+                       ((int)pending_.size() >= coalesce_max_ || (int)pending_.size() >= callers_ - inflight_reqs_ ||
+                        std::chrono::steady_clock::now() >= deadline);
+    if (ready && inflight_ < 2 && std::find(pending_.begin(), pending_.end(), &r) != pending_.end()) {
+      std::vector<OneReq *> batch;
+      const size_t take = std::min(pending_.size(), (size_t)coalesce_max_);
+      batch.assign(pending_.begin(), pending_.begin() + take);
+      pending_.erase(pending_.begin(), pending_.begin() + take);
+      inflight_++;
+      inflight_reqs_ += (int)batch.size();
+      stat_coalesced_batches_++;
+      stat_coalesced_images_ += (int64_t)batch.size();
+      lk.unlock();
+      flush_batch(batch);
+      lk.lock();
+      for (OneReq *q : batch) q->done = true;
+      inflight_--;
+      inflight_reqs_ -= (int)batch.size();
+      ccv_.notify_all();
+      continue;
+    }
+    if (ready)
+      ccv_.wait(lk);
+    else
+      ccv_.wait_until(lk, deadline);
+  }
+  callers_--;
+  ccv_.notify_all();
+  return r.st;
 }
 
 dg_status Context::poll(uint64_t ticket) {

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -67,6 +68,8 @@ struct Batch {
 struct Slot {
   DevBuf scratch, meta, input;
   DevBuf wgt;  // debug: per-workgroup timestamps of the entropy kernels (option "wg_timing")
+  DevBuf coef;  // coefficient arena of the batch (k_huff_write -> k_idct)
+  size_t coef_bytes = 0;
   PinBuf stage, out;
   std::vector<hipEvent_t> ev;  // per-stage timing events
   hipEvent_t done = nullptr;   // recorded after the batch's last copy
@@ -74,7 +77,7 @@ struct Slot {
   // beside batch k's pixel kernels (the entropy kernels leave most CUs idle
   // in their tails).
   hipStream_t st = nullptr, side = nullptr;
-  hipEvent_t ev_meta = nullptr, ev_coef = nullptr;
+  hipEvent_t ev_meta = nullptr, ev_coef = nullptr, ev_zero = nullptr;
   std::unique_ptr<Batch> batch;
   size_t subs_off = 0, ckpt_off = 0;
 };
@@ -96,6 +99,10 @@ class Context {
                    bool host_io, uint64_t *ticket);
   dg_status wait(uint64_t ticket);
   dg_status poll(uint64_t ticket);
+  // One image, coalesced with concurrent callers into shared GPU batches
+  // (SURVEY §8(b).6): returns the image's status.
+  dg_status decode_one(const uint8_t *src, size_t len, int32_t forced, uint8_t *out, uint64_t cap,
+                       dg_payload_meta *meta);
   dg_status output_size(const uint8_t *bytes, size_t len, int32_t forced, uint64_t *nbytes);
 
   const BucketTable *buckets() const { return buckets_.get(); }
@@ -124,6 +131,25 @@ class Context {
   hipStream_t stream_ = nullptr, side_ = nullptr;
   hipEvent_t ev_meta_ = nullptr, ev_coef_ = nullptr;
   std::mutex mu_;
+
+  // decode_one coalescing (options "coalesce_max", "coalesce_us")
+  struct OneReq {
+    const uint8_t *src;
+    size_t len;
+    int32_t forced;
+    uint8_t *out;
+    uint64_t cap;
+    dg_payload_meta *meta;
+    bool done;
+    dg_status st;
+  };
+  std::mutex cmu_;
+  std::condition_variable ccv_;
+  std::vector<OneReq *> pending_;
+  int callers_ = 0, inflight_ = 0, inflight_reqs_ = 0;
+  int coalesce_max_ = 64, coalesce_us_ = 500;
+  int64_t stat_coalesced_batches_ = 0, stat_coalesced_images_ = 0;
+  dg_status flush_batch(std::vector<OneReq *> &batch);
 
   std::vector<HuffTable> hpool_;
   std::unordered_map<std::string, int> hpool_idx_;

@@ -176,8 +176,12 @@ __global__ __launch_bounds__(256) void k_destuff_scan(ImageDesc *__restrict__ im
     im.ds_bits = ck * 8;
     im.nmk = cm < im.mk_cap ? cm : im.mk_cap;
   }
+  // zero padding (64 bytes) for the bit-window reader, in the interleaved layout
   DG_GLOBAL uint8_t *ds = gp<uint8_t>(im.ds);
-  if (t < 48) ds[ck + t] = 0;  // zero padding for the bit-window reader
+  if (t < 64) {
+    const uint32_t q = ck + t;
+    ds[(size_t)ds_word_index(q >> 2, im.ds_lsw) * 4 + (q & 3)] = 0;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_destuff_write(const ImageDesc *__restrict__ imgs,
@@ -217,20 +221,29 @@ __global__ __launch_bounds__(256) void k_destuff_write(const ImageDesc *__restri
     }
   }
   __syncthreads();
-  // buf[0, total) -> ds[O, O + total): head bytes, aligned dwords, tail bytes
-  DG_GLOBAL uint8_t *ds = gp<uint8_t>(im.ds) + O;
-  const uint32_t mis = (uint32_t)((4u - ((uintptr_t)ds & 3u)) & 3u);  // bytes to the next dword boundary
+  // buf[0, total) -> logical bytes [O, O + total) of the interleaved stream:
+  // partial words at both ends byte by byte, whole words as dword stores
+  DG_GLOBAL uint8_t *ds = gp<uint8_t>(im.ds);
+  DG_GLOBAL uint32_t *ds4 = (DG_GLOBAL uint32_t *)ds;
+  const uint32_t lsw = im.ds_lsw;
+  const uint32_t mis = (4u - (O & 3u)) & 3u;  // bytes to the next word boundary
   const uint32_t head = mis < total ? mis : total;
   const uint32_t nd = (total - head) >> 2;
-  if ((uint32_t)t < head) ds[t] = buf[t];
-  DG_GLOBAL uint32_t *d4 = (DG_GLOBAL uint32_t *)(ds + head);
+  if ((uint32_t)t < head) {
+    const uint32_t q = O + t;
+    ds[(size_t)ds_word_index(q >> 2, lsw) * 4 + (q & 3)] = buf[t];
+  }
+  const uint32_t w0 = (O + head) >> 2;  // first whole logical word
   for (uint32_t q = t; q < nd; q += 256) {
     const uint32_t b0 = head + 4 * q;
-    d4[q] = (uint32_t)buf[b0] | ((uint32_t)buf[b0 + 1] << 8) | ((uint32_t)buf[b0 + 2] << 16) |
-            ((uint32_t)buf[b0 + 3] << 24);
+    ds4[ds_word_index(w0 + q, lsw)] = (uint32_t)buf[b0] | ((uint32_t)buf[b0 + 1] << 8) |
+                                      ((uint32_t)buf[b0 + 2] << 16) | ((uint32_t)buf[b0 + 3] << 24);
   }
   const uint32_t tail0 = head + 4 * nd;
-  if ((uint32_t)t < total - tail0) ds[tail0 + t] = buf[tail0 + t];
+  if ((uint32_t)t < total - tail0) {
+    const uint32_t q = O + tail0 + t;
+    ds[(size_t)ds_word_index(q >> 2, lsw) * 4 + (q & 3)] = buf[tail0 + t];
+  }
 }
 
 // ------------------------------------------------------------ entropy decode

@@ -148,7 +148,11 @@ dg_status dg_submit(dg_ctx *ctx, int32_t n, const uint8_t *const *srcs, const si
 dg_status dg_wait(dg_ctx *ctx, uint64_t ticket);
 dg_status dg_poll(dg_ctx *ctx, uint64_t ticket);
 
-/* Synchronous single-image convenience (image_payload_from_path equivalent). */
+/* Synchronous single image (image_payload_from_path equivalent).  Calls from
+ * concurrent threads are coalesced into shared GPU batches (one 0.3 MP image
+ * cannot fill the GPU): a call waits until the batch is full ("coalesce_max"),
+ * every concurrent caller is waiting, or "coalesce_us" has passed.  Returns
+ * the image's status. */
 dg_status dg_decode_one(dg_ctx *ctx, const uint8_t *src, size_t len, int32_t forced_bucket,
                         uint8_t *out, uint64_t out_cap, dg_payload_meta *meta);
 
@@ -176,10 +180,14 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
 /* Tuning knobs:
  *   "sub_bits"    entropy-decoder subsequence size in bits (multiple of 32,
  *                 64..65536; 0 = auto per batch, the default)
+ *   "lead_bits"   entropy lead-in before each subsequence (-1 = auto per image)
+ *   "coalesce_max" dg_decode_one: most images merged into one GPU batch (1 = off; default 64)
+ *   "coalesce_us" dg_decode_one: longest wait for other callers (default 500)
+ *   "wg_timing"   debug: per-workgroup timestamps of the entropy kernels
  *   "timing"      1 = record per-kernel HIP events (dg_last_batch_timings)
  *   "side_stream" 1 = Lanczos tables on a second stream (default 1)
  *   "debug_flags" internal switches for kernel bisection
- * Stats: "batches", "resync_rounds", "fix_workgroups", "write_mismatch",
+ * Stats: "batches", "coalesced_batches", "coalesced_images", "resync_rounds", "fix_workgroups", "write_mismatch",
  * "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool"; -1 if unknown. */
 dg_status dg_ctx_set_option(dg_ctx *ctx, const char *key, int64_t value);
 int64_t dg_ctx_get_stat(dg_ctx *ctx, const char *key);

@@ -72,11 +72,21 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
   }
   d.ds_bits = (uint32_t)ds.size() * 8;
   d.nmk = (uint32_t)mk.size();
-  ds.resize(((ds.size() + 3) & ~(size_t)3) + 32, 0);
+  ds.resize(((ds.size() + 3) & ~(size_t)3) + 64, 0);
   d.sub_bits = sub_bits;
   d.lead_bits = g_lead;
   d.nsub = d.scan_len ? (uint32_t)(((uint64_t)d.scan_len * 8 + sub_bits - 1) / sub_bits) : 1;
-  const uint8_t *scan = ds.data();
+  // the kernels' word-interleaved layout (ds_word_index)
+  d.ds_lsw = 0;
+  while ((32u << d.ds_lsw) < sub_bits) d.ds_lsw++;
+  std::vector<uint32_t> phys((size_t)ds_words_alloc(d.nsub, d.ds_lsw), 0u);
+  for (size_t wi = 0; wi * 4 < ds.size(); wi++) {
+    uint32_t v;
+    memcpy(&v, &ds[wi * 4], 4);
+    const uint32_t pi = ds_word_index((uint32_t)wi, d.ds_lsw);
+    if (pi < phys.size()) phys[pi] = v;
+  }
+  const uint8_t *scan = (const uint8_t *)phys.data();
   const uint32_t *mkp = mk.data();
   std::vector<SubState> subs(d.nsub);
   const uint32_t NCK = num_ckpt(d.sub_bits);

@@ -281,3 +281,32 @@ def test_crop_folding_bit_exact(ctx512, case):
     assert arr.shape == ref.shape
     d = np.abs(arr.astype(int) - ref.astype(int))
     assert d.max() == 0, (int(d.max()), int((d > 0).sum()))
+
+
+def test_decode_one_coalesces_concurrent_callers(ctx512):
+    # concurrent single-image calls (one per tokio task in the
+    # reference) are merged into shared GPU batches, results unchanged
+    import threading
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+    ctx.set_option("coalesce_us", 20000)
+    datas = _rand_jpegs(7, 32, maxdim=500)
+    res = [None] * len(datas)
+
+    def work(k):
+        for i in range(k, len(datas), 8):
+            res[i] = ctx.decode_one(datas[i])
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    for data, (st, arr, meta) in zip(datas, res):
+        assert st == 0
+        w, h = O.jpeg_info(data)[1:3]
+        assert np.array_equal(arr, _oracle_resized(data, *t.target_size(w, h)))
+    assert ctx.stat("coalesced_images") == len(datas)
+    assert ctx.stat("coalesced_batches") < len(datas)  # merged

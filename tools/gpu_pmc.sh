@@ -21,3 +21,7 @@ run sq SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY S
 run sq2 SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR &&
 run fetch FETCH_SIZE &&
 run write WRITE_SIZE
+rc=$?
+[ $rc -eq 0 ] || exit $rc
+python tools/pmc_traffic.py $OUT "batch=${BATCH:-256} pool=${POOL:-256} size=1024/32 short=256-2048" ${BATCH:-256} \
+    > $OUT/pmc_traffic.json && python tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt

@@ -1,0 +1,83 @@
+"""Per-stage HBM traffic of bench.py from rocprofv3 PMC passes
+(tools/gpu_pmc.sh: separate FETCH_SIZE and WRITE_SIZE passes).
+
+Kernels are mapped to bench stages by dispatch order within each batch
+(k_huff_sync starts a batch; k_resize_hb launches before a batch's first
+k_resize_v are call 1's H pass, later ones call 2's; the first k_resize_v is
+call 1's V pass, the second call 2's).  FETCH_SIZE is in KiB and, on gfx950,
+reports half the bytes of wide (16 B/lane) coalesced reads
+(MI355X_MICROARCH.md, HBM section): it is doubled here and labelled so;
+WRITE_SIZE is taken as is.  Output: JSON with bytes per batch per stage.
+
+  python tools/pmc_traffic.py gpurun_out/pmc > profiles/r01/pmc_traffic.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def stage_sequence(rows):
+    """[(dispatch_id, stage)] for the dg:: kernels, in dispatch order."""
+    out = []
+    phase = None
+    nv = 0
+    for r in sorted(rows, key=lambda r: int(r["Dispatch_Id"])):
+        k = r["Kernel_Name"]
+        if "dg::" not in k:
+            continue
+        name = k.split("(")[0].replace("void ", "").replace("dg::", "")
+        if name.startswith("k_huff_sync"):
+            nv = 0
+            phase = "h1"
+        if name.startswith("k_destuff"):
+            st = "destuff"
+        elif name.startswith("k_huff_"):
+            st = name[2:].replace("huff_", "huff_")
+        elif name.startswith("k_resize_v"):
+            nv += 1
+            st = "resize_v1" if nv == 1 else "resize_v2"
+            phase = "h2"
+        elif name.startswith("k_resize_h"):
+            st = "resize_h1" if phase in (None, "h1") else "resize_h2"
+        else:
+            st = name[2:]  # idct, color, coeffs, copy
+        out.append((int(r["Dispatch_Id"]), st))
+    return out
+
+
+def main(root, config=None, images_per_batch=None):
+    res = {}
+    for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        files = glob.glob(os.path.join(root, sub, "**", "*counter_collection.csv"), recursive=True)
+        rows = [r for f in files for r in csv.DictReader(open(f)) if r["Counter_Name"] == counter]
+        seq = dict(stage_sequence(rows))
+        per = defaultdict(float)
+        nbatch = sum(1 for r in rows if "k_huff_sync" in r["Kernel_Name"])
+        for r in rows:
+            d = int(r["Dispatch_Id"])
+            if d in seq:
+                per[seq[d]] += float(r["Counter_Value"]) * 1024.0
+        res[counter] = ({k: v / max(nbatch, 1) for k, v in per.items()}, nbatch)
+    fetch, nb = res["FETCH_SIZE"]
+    write, _ = res["WRITE_SIZE"]
+    stages = sorted(set(fetch) | set(write))
+    out = {
+        "config": config,
+        "images_per_batch": int(images_per_batch) if images_per_batch else None,
+        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (tools/gpu_pmc.sh)",
+        "batches": nb,
+        "correction": "FETCH_SIZE x2 (gfx950 reports half of wide reads; uncalibrated for narrower accesses)",
+        "bytes_per_batch": {s: round(2.0 * fetch.get(s, 0.0) + write.get(s, 0.0)) for s in stages},
+        "fetch_bytes_per_batch_x2": {s: round(2.0 * fetch.get(s, 0.0)) for s in stages},
+        "write_bytes_per_batch": {s: round(write.get(s, 0.0)) for s in stages},
+    }
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    # usage: pmc_traffic.py ROOT CONFIG_KEY IMAGES_PER_BATCH  (CONFIG_KEY as bench.pmc_config_key)
+    main(*(sys.argv[1:4] if len(sys.argv) > 1 else ["gpurun_out/pmc"]))
