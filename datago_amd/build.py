@@ -22,6 +22,8 @@ ARCH = os.environ.get("DG_OFFLOAD_ARCH", "gfx950")
 SOURCES = [
     # (source, is_device_code)
     ("kernels.hip", True),
+    ("dg_png.hip", True),
+    ("host/png_header.cpp", False),
     ("host/pipeline.cpp", False),
     ("host/capi.cpp", False),
     ("host/jpeg_header.cpp", False),

@@ -112,6 +112,44 @@ constexpr uint32_t kHSegPx = 640;     // LDS source segment (pixels) per row
 
 constexpr int kStages = 4;  // R1.H, R1.V, R2.H, R2.V
 
+// ---- PNG (ImageDesc::fmt == kFmtPng)
+constexpr uint32_t kFmtJpeg = 0, kFmtPng = 1;
+// IDAT payloads are gathered into one contiguous zlib stream (k_png_gather),
+// inflated into filtered scanlines (k_png_inflate, one wave per image),
+// unfiltered (k_png_unfilter, one wave per image, 64-row diagonal wavefront)
+// and, for palette / sub-byte / tRNS images, expanded to 8-bit L/LA/RGB/RGBA
+// (k_png_expand).
+struct PngDesc {
+  uint64_t zs;        // contiguous zlib stream
+  uint64_t raw;       // inflated scanlines: height x (1 + rowbytes)
+  uint64_t unf;       // unfiltered scanlines (stride ustride); == pix when expand == 0
+  uint64_t pal;       // 256 x RGBA palette (device), 0 if none
+  uint32_t zlen;      // zlib bytes
+  uint32_t rowbytes;  // bytes per scanline (without the filter byte)
+  uint32_t ustride;   // stride of unf
+  uint32_t bpp;       // filter unit (bytes)
+  uint32_t ctype, depth, expand, has_trns;
+  uint32_t trns[3];   // gray / RGB transparency key
+  uint32_t pad;
+};
+// A gather job: copy `len` bytes (one IDAT payload) from src to dst.
+struct GatherJob {
+  uint64_t src, dst;
+  uint32_t len, pad;
+};
+constexpr uint32_t kGatherPiece = 16384;  // bytes per gather workgroup
+
+// fast_image_resize mul_div_alpha (U8x2 / U8x4): an in-place program over one
+// buffer.  prog holds up to three 2-bit ops, lowest first: 1 = multiply
+// colour by alpha, 2 = divide by alpha.
+struct AlphaOp {
+  uint64_t buf;
+  uint32_t stride, width, rows, prog;
+  uint32_t on_decoded;  // buf is the decoded image (not re-created by a resync round)
+  uint32_t pad;
+};
+constexpr uint32_t kAlphaPoints = 3;  // before call 1, between the calls, after call 2
+
 struct ImageDesc {
   // ---- entropy stream
   uint64_t scan;            // device address of the first raw entropy-coded byte
@@ -161,6 +199,13 @@ struct ImageDesc {
   uint32_t final_src_stride, copy_needed;
   uint32_t final_src_c;
   uint32_t color_fused;     // 1: pass[0] converts colour itself, pix is never written
+  // ---- format, PNG, alpha handling, final conversion
+  uint32_t fmt;             // kFmtJpeg / kFmtPng
+  uint32_t copy_mode;       // k_copy: 0 same channels, 1 L->RGB, 2 RGBA->RGB blend over gray,
+                            // 3 LA->RGB of a resized LA image (GrayImage over the LA bytes, B3),
+                            // 4 LA->RGB of an unresized LumaA8 (alpha dropped)
+  PngDesc png;
+  AlphaOp aop[kAlphaPoints];
 };
 
 // One workgroup's work: an image and the first item it handles.

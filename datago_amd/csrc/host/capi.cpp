@@ -8,6 +8,7 @@
 #include "buckets.h"
 #include "jpeg_header.h"
 #include "pipeline.h"
+#include "png_header.h"
 
 namespace dg {
 extern thread_local std::string g_last_error;
@@ -93,13 +94,20 @@ dg_status dg_probe(const uint8_t *bytes, size_t len, dg_probe_info *out) {
   memset(out, 0, sizeof(*out));
   if (!bytes || !len) return DG_ERR_CORRUPT;
   if (dg::is_png(bytes, len)) {
+    dg::PngHeader h;
+    dg::parse_png_header(bytes, len, h);
     out->format = DG_FMT_PNG;
-    if (len >= 24) {
-      out->width = (uint32_t)bytes[16] << 24 | (uint32_t)bytes[17] << 16 | (uint32_t)bytes[18] << 8 | bytes[19];
-      out->height = (uint32_t)bytes[20] << 24 | (uint32_t)bytes[21] << 16 | (uint32_t)bytes[22] << 8 | bytes[23];
-      if (len >= 26) out->bit_depth = bytes[24];
+    out->width = h.width;
+    out->height = h.height;
+    out->components = h.out_c;   // channels after EXPAND (L8 1, La8 2, Rgb8 3, Rgba8 4)
+    out->bit_depth = h.depth;
+    out->precision = h.depth;
+    out->progressive = h.interlace;  // Adam7
+    out->gpu_supported = h.status == dg::PH_OK;
+    if (h.status == dg::PH_CORRUPT) {
+      dg::set_error(h.why);
+      return DG_ERR_CORRUPT;
     }
-    out->gpu_supported = 0;
     return DG_OK;
   }
   if (!dg::is_jpeg(bytes, len)) {

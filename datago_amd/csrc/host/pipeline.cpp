@@ -34,6 +34,12 @@ void set_error(const std::string &s) { g_last_error = s; }
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+static const char *kStageNames[] = {"upload",     "png_inflate", "png_unfilter", "destuff",   "huff_sync",
+                                    "huff_fix",   "huff_scan",   "huff_write",   "coeffs",    "idct",
+                                    "color",      "resize_h1",   "resize_v1",    "resize_h2", "resize_v2",
+                                    "copy",       "download"};
+static const int kNumStages = 17;
+
 Context::Context(int device, const dg_image_config *cfg) : device_(device) {
   if (cfg && cfg->crop_and_resize) {
     has_cfg_ = true;
@@ -96,7 +102,7 @@ dg_status Context::init() {
   HIPCHK(hipEventCreateWithFlags(&ev_meta_, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&ev_coef_, hipEventDisableTiming));
   for (Slot &sl : slots_) {
-    sl.ev.resize(17);
+    sl.ev.resize(kNumStages + 1);
     for (auto &e : sl.ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
@@ -198,10 +204,6 @@ int64_t Context::get_stat(const std::string &k) {
   return -1;
 }
 
-static const char *kStageNames[] = {"upload",    "destuff",   "huff_sync", "huff_fix",  "huff_scan",
-                                    "huff_write", "coeffs",   "idct",      "color",     "resize_h1",
-                                    "resize_v1", "resize_h2", "resize_v2", "copy",      "download"};
-static const int kNumStages = 15;
 
 int Context::timings(const char **names, float *ms, int cap) {
   int n = (int)last_ms_.size();
@@ -321,17 +323,37 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
     p.status = DG_ERR_CORRUPT;
     return DG_OK;
   }
-  if (!is_jpeg(h, len)) {
-    p.status = is_png(h, len) ? DG_ERR_UNSUPPORTED : DG_ERR_CORRUPT;
-    return DG_OK;
+  uint32_t W, H, C;
+  if (is_png(h, len)) {
+    p.fmt = kFmtPng;
+    parse_png_header(h, len, p.png);
+    if (p.png.status != PH_OK) {
+      p.status = p.png.status == PH_UNSUPPORTED ? DG_ERR_UNSUPPORTED : DG_ERR_CORRUPT;
+      return DG_OK;
+    }
+    // the decoder's working set (raw + unfiltered + expanded) must stay 32-bit addressable
+    const uint64_t raw = (uint64_t)p.png.height * (p.png.rowbytes + 1ull);
+    if (raw >= (1ull << 31) || (uint64_t)p.png.width * p.png.height * 4ull >= (1ull << 31)) {
+      p.status = DG_ERR_UNSUPPORTED;
+      return DG_OK;
+    }
+    W = p.png.width;
+    H = p.png.height;
+    C = (uint32_t)p.png.out_c;
+  } else {
+    if (!is_jpeg(h, len)) {
+      p.status = DG_ERR_CORRUPT;
+      return DG_OK;
+    }
+    parse_jpeg_header(h, len, p.hdr);
+    if (p.hdr.status != JH_OK) {
+      p.status = p.hdr.status == JH_UNSUPPORTED ? DG_ERR_UNSUPPORTED : DG_ERR_CORRUPT;
+      return DG_OK;
+    }
+    W = p.hdr.width;
+    H = p.hdr.height;
+    C = p.hdr.ncomp == 1 ? 1 : 3;
   }
-  parse_jpeg_header(h, len, p.hdr);
-  if (p.hdr.status != JH_OK) {
-    p.status = p.hdr.status == JH_UNSUPPORTED ? DG_ERR_UNSUPPORTED : DG_ERR_CORRUPT;
-    return DG_OK;
-  }
-  const uint32_t W = p.hdr.width, H = p.hdr.height;
-  const uint32_t C = p.hdr.ncomp == 1 ? 1 : 3;
   p.channels = (int32_t)C;  // pre-transform (image_processing.rs:349-351)
   p.bit_depth = 8;
   uint32_t ow = W, oh = H;
@@ -349,7 +371,7 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
   }
   p.out_w = ow;
   p.out_h = oh;
-  p.out_c = (cfg_.image_to_rgb8 && C == 1) ? 3 : C;
+  p.out_c = cfg_.image_to_rgb8 ? 3 : C;  // convert_to_rgb8 (:163-186)
   if (cfg_.image_to_rgb8) p.channels = 3;  // image_processing.rs:367-372
   p.out_bytes = (uint64_t)ow * oh * p.out_c;
   if (cfg_.pre_encode_images) p.status = DG_ERR_UNSUPPORTED;
@@ -360,7 +382,7 @@ dg_status Context::output_size(const uint8_t *bytes, size_t len, int32_t forced,
   ImagePlan p;
   plan_image(bytes, len, forced, p);
   *nbytes = p.out_bytes;
-  if (p.status) set_error(p.hdr.why ? p.hdr.why : "unsupported");
+  if (p.status) set_error(p.fmt == kFmtPng ? p.png.why : (p.hdr.why ? p.hdr.why : "unsupported"));
   return (dg_status)p.status;
 }
 
@@ -406,9 +428,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     memset(&m, 0, sizeof(m));
     m.status = p.status;
     m.bucket = p.bucket;
-    if (p.hdr.status == JH_OK) {
+    if (p.fmt == kFmtJpeg && p.hdr.status == JH_OK) {
       m.original_width = p.hdr.width;
       m.original_height = p.hdr.height;
+    } else if (p.fmt == kFmtPng && p.png.status == PH_OK) {
+      m.original_width = p.png.width;
+      m.original_height = p.png.height;
     }
     m.width = p.out_w;
     m.height = p.out_h;
@@ -428,7 +453,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   // ---- 2. table pools
   for (int i = 0; i < n; i++) {
     ImagePlan &p = b.plans[i];
-    if (p.status) continue;
+    if (p.status || p.fmt != kFmtJpeg) continue;
     bool ok = true;
     for (int c = 0; c < p.hdr.ncomp; c++) {
       if (pool_huff(p.hdr.dc[p.hdr.comp[c].td]) < 0 || pool_huff(p.hdr.ac[p.hdr.comp[c].ta]) < 0 ||
@@ -452,7 +477,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   if (!sub_bits) {
     uint64_t coded = 0;
     for (int i = 0; i < n; i++)
-      if (!b.plans[i].status) coded += b.plans[i].hdr.scan_end - b.plans[i].hdr.scan_off;
+      if (!b.plans[i].status && b.plans[i].fmt == kFmtJpeg) coded += b.plans[i].hdr.scan_end - b.plans[i].hdr.scan_off;
     sub_bits = coded >= (64ull << 20) ? 4096 : 2048;
   }
   last_sub_bits_ = sub_bits;
@@ -468,17 +493,61 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   struct Offs {
     size_t coef, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], pass_srcoff[kStages];
     size_t final_off, tmp, out, ds, mk, chunk;
+    size_t zs, raw, unf, pal;
+    // alpha programs: buffer = dst of pass `stage` (-1: the decoded image), byte offset
+    int aop_stage[kAlphaPoints];
+    size_t aop_off[kAlphaPoints];
   };
   std::vector<Offs> offs;
   for (int i = 0; i < n; i++) {
     ImagePlan &p = b.plans[i];
     if (p.status) continue;
-    const JpegHeader &h = p.hdr;
     ImageDesc d;
     memset(&d, 0, sizeof(d));
     Offs o;
     memset(&o, 0, sizeof(o));
-    const uint32_t W = h.width, H = h.height;
+    uint32_t W, H, C;
+    size_t cur_stride;
+    bool colour = false;  // the source is the YCbCr planes of a colour JPEG
+    if (p.fmt == kFmtPng) {
+      const PngHeader &g = p.png;
+      W = g.width;
+      H = g.height;
+      C = (uint32_t)g.out_c;
+      d.fmt = kFmtPng;
+      d.width = W;
+      d.height = H;
+      d.dec_c = (uint8_t)C;
+      PngDesc &pd = d.png;
+      pd.zlen = (uint32_t)g.zlen;
+      pd.rowbytes = g.rowbytes;
+      pd.ustride = (uint32_t)align_up(g.rowbytes, 16);
+      pd.bpp = (uint32_t)g.bpp;
+      pd.ctype = (uint32_t)g.ctype;
+      pd.depth = (uint32_t)g.depth;
+      pd.has_trns = (uint32_t)g.has_trns;
+      for (int k = 0; k < 3; k++) pd.trns[k] = g.trns[k];
+      pd.expand = g.ctype == 3 || g.depth < 8 || g.has_trns;
+      o.zs = L.take((size_t)g.zlen + 64, 256);
+      o.raw = L.take((size_t)H * (g.rowbytes + 1) + 16, 256);
+      o.unf = L.take((size_t)H * pd.ustride, 256);
+      if (pd.expand) {
+        d.pix_stride = (uint32_t)align_up((size_t)W * C, 16);
+        o.pix = L.take((size_t)d.pix_stride * H);
+      } else {
+        d.pix_stride = pd.ustride;
+      }
+      if (g.ctype == 3) {
+        o.pal = b.blob.size();
+        b.blob.insert(b.blob.end(), &g.pal[0][0], &g.pal[0][0] + 1024);
+      }
+      if (host_io) in_off[i] = IN.take(lens[i] + 16, 16);
+      cur_stride = d.pix_stride;
+      b.any_png = true;
+    } else {
+    const JpegHeader &h = p.hdr;
+    W = h.width;
+    H = h.height;
     d.width = W;
     d.height = H;
     d.ncomp = (uint8_t)h.ncomp;
@@ -552,14 +621,15 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     // buffers
     o.coef = CO.take((size_t)d.total_blocks * 128);
     for (int c = 0; c < h.ncomp; c++) o.plane[c] = L.take((size_t)d.cbw[c] * 8 * d.cbh[c] * 8);
-    const uint32_t C = d.dec_c;
-    size_t cur_stride;
+    C = d.dec_c;
+    colour = h.ncomp == 3;
     if (h.ncomp == 3) {
       d.pix_stride = (uint32_t)align_up((size_t)W * 3, 16);
       cur_stride = d.pix_stride;  // the RGB image is only materialised if no pass fuses it
     } else {
       cur_stride = (size_t)d.cbw[0] * 8;
     }
+    }  // JPEG
     // resize plan (image_processing.rs:264-325)
     d.out_w = p.out_w;
     d.out_h = p.out_h;
@@ -615,7 +685,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       const uint32_t lx = fold_x ? (uint32_t)std::rint(l) : 0u, ty = fold_y ? (uint32_t)std::rint(t) : 0u;
       if (nw != W) {  // call 1, horizontal
         ResizePass &ps = add_pass(0, 1, 0.0, (double)W, W, nw, fold_x ? lx : 0u, fold_x ? p.out_w : nw, chh, 0);
-        ps.mode = h_pass_mode(ps, h.ncomp == 3);
+        ps.mode = h_pass_mode(ps, colour);
         cw = ps.width;
       } else if (fold_x) {
         xoff = lx;
@@ -640,10 +710,43 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         chh = p.out_h;
         xoff = 0;
       }
+      // U8x2 / U8x4: fast_image_resize multiplies colour by alpha before each
+      // convolution call and divides after (mul_div_alpha); a call
+      // whose crop box has the destination's size at integral offsets is a
+      // copy and touches no alpha.  Programs run in place at three points.
+      if (C == 2 || C == 4) {
+        const bool call1 = !(nw == W && nh == H);
+        const bool call2 = !(bw == (double)p.out_w && bh == (double)p.out_h && l == std::floor(l) &&
+                             t == std::floor(t));
+        const bool call2_passes = d.pass[2].kind || d.pass[3].kind;
+        const int s1 = d.pass[1].kind ? 1 : 0;  // last call-1 pass (when call1)
+        auto set = [&](int k, int stage, uint32_t w, uint32_t rows, uint32_t prog) {
+          if (!prog) return;
+          o.aop_stage[k] = stage;
+          d.aop[k].width = w;
+          d.aop[k].rows = rows;
+          d.aop[k].prog = prog;
+          b.any_alpha = true;
+        };
+        set(0, -1, W, H, call1 ? 1u : 0u);
+        uint32_t prog1 = 0, sh = 0;
+        auto push = [&](uint32_t op) {
+          prog1 |= op << sh;
+          sh += 2;
+        };
+        if (call1) push(2);
+        if (call2) push(1);
+        if (call2 && !call2_passes) push(2);
+        if (call1)
+          set(1, s1, d.pass[s1].width, d.pass[s1].rows, prog1);
+        else
+          set(1, -1, W, H, prog1);
+        if (call2 && call2_passes) set(2, d.pass[3].kind ? 3 : 2, p.out_w, p.out_h, 2u);
+      }
     }
     // colour images whose first pass is not a fused H pass need the RGB image
-    d.color_fused = h.ncomp == 3 && d.pass[0].kind == 1 && (d.pass[0].mode & kHFused);
-    if (h.ncomp == 3 && !d.color_fused) o.pix = L.take((size_t)d.pix_stride * H);
+    d.color_fused = colour && d.pass[0].kind == 1 && (d.pass[0].mode & kHFused);
+    if (colour && !d.color_fused) o.pix = L.take((size_t)d.pix_stride * H);
     // final write: the last pass writes straight into the output when the
     // channel count is unchanged; otherwise (or with no pass) k_copy runs.
     if (last_stage >= 0 && d.out_c == C) {
@@ -655,6 +758,14 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       d.final_src_c = C;
       d.final_src_stride = (uint32_t)cur_stride;
       o.final_off = (size_t)yoff * cur_stride + (size_t)xoff * C;  // an uncomputed integral crop
+      if (d.out_c == C)
+        d.copy_mode = 0;
+      else if (C == 1)
+        d.copy_mode = 1;  // L8 -> RGB8
+      else if (C == 4)
+        d.copy_mode = 2;  // RGBA8 -> RGB8 over gray
+      else  // LA8 -> RGB8: resized images went through image_to_dyn_image's GrayImage (B3)
+        d.copy_mode = (has_cfg_ && !(W == p.out_w && H == p.out_h)) ? 3 : 4;
     }
     if (host_io) {
       o.out = L.take(p.out_bytes, 16);
@@ -687,6 +798,27 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     const Offs &o = offs[k++];
     const JpegHeader &h = b.plans[i].hdr;
     const uint8_t *src = host_io ? (const uint8_t *)sl.input.p + in_off[i] : d_srcs[i];
+    uint64_t out = host_io ? (uint64_t)(uintptr_t)(S + o.out) : (uint64_t)(uintptr_t)outs[i];
+    d.out = out;
+    if (d.fmt == kFmtPng) {
+      const PngHeader &g = b.plans[i].png;
+      PngDesc &pd = d.png;
+      pd.zs = (uint64_t)(uintptr_t)(S + o.zs);
+      pd.raw = (uint64_t)(uintptr_t)(S + o.raw);
+      pd.unf = (uint64_t)(uintptr_t)(S + o.unf);
+      d.pix = pd.expand ? (uint64_t)(uintptr_t)(S + o.pix) : pd.unf;
+      pd.pal = g.ctype == 3 ? o.pal + 1 : 0;  // blob offset + 1, made absolute with the meta buffer
+      uint64_t zo = 0;
+      for (size_t c = 0; c < g.idat_off.size(); c++) {
+        GatherJob j;
+        j.src = (uint64_t)(uintptr_t)(src + g.idat_off[c]);
+        j.dst = pd.zs + zo;
+        j.len = g.idat_len[c];
+        j.pad = 0;
+        zo += g.idat_len[c];
+        b.gjobs.push_back(j);
+      }
+    } else {
     d.scan = (uint64_t)(uintptr_t)(src + h.scan_off);
     d.coef = (uint64_t)(uintptr_t)((char *)sl.coef.p + o.coef);
     d.ds = (uint64_t)(uintptr_t)(S + o.ds);
@@ -694,9 +826,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     d.chunk = (uint64_t)(uintptr_t)(S + o.chunk);
     for (int c = 0; c < h.ncomp; c++) d.plane[c] = (uint64_t)(uintptr_t)(S + o.plane[c]);
     d.pix = h.ncomp == 3 && !d.color_fused ? (uint64_t)(uintptr_t)(S + o.pix) : 0;
-    uint64_t out = host_io ? (uint64_t)(uintptr_t)(S + o.out) : (uint64_t)(uintptr_t)outs[i];
-    d.out = out;
-    uint64_t cur = h.ncomp == 3 ? d.pix : d.plane[0];
+    }  // JPEG
+    uint64_t cur = (d.fmt == kFmtPng || h.ncomp == 3) ? d.pix : d.plane[0];
+    const uint64_t decoded = cur;
+    const uint32_t decoded_stride = d.fmt == kFmtPng ? d.pix_stride : (h.ncomp == 3 ? d.pix_stride : d.cbw[0] * 8);
     for (int s = 0; s < kStages; s++) {
       ResizePass &ps = d.pass[s];
       if (!ps.kind) continue;
@@ -707,6 +840,18 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       cur = ps.dst;
     }
     d.final_src = cur + (d.copy_needed ? o.final_off : 0);
+    for (uint32_t k = 0; k < kAlphaPoints; k++) {
+      if (!d.aop[k].prog) continue;
+      const int sg = o.aop_stage[k];
+      if (sg < 0) {
+        d.aop[k].buf = decoded;
+        d.aop[k].stride = decoded_stride;
+        d.aop[k].on_decoded = 1;
+      } else {
+        d.aop[k].buf = d.pass[sg].dst;
+        d.aop[k].stride = d.pass[sg].dst_stride;
+      }
+    }
     (void)subs_off;
   }
   // ---- 5. workgroup lists
@@ -715,6 +860,16 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   for (int di = 0; di < (int)b.descs.size(); di++) {
     const ImageDesc &d = b.descs[di];
     const uint32_t I = (uint32_t)di;
+    for (uint32_t k = 0; k < kAlphaPoints; k++)
+      if (d.aop[k].prog) {
+        const uint32_t cnt = d.aop[k].width * d.aop[k].rows;
+        for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_ALPHA0 + k].push_back({I, it});
+      }
+    if (d.fmt == kFmtPng) {
+      b.lists[L_PNG].push_back({I, 0});
+      if (d.png.expand)
+        for (uint32_t it = 0; it < d.width * d.height; it += 256) b.lists[L_EXPAND].push_back({I, it});
+    } else {
     for (uint32_t w = 0; w < d.nsub; w += kSubPerWg) b.lists[L_HUFF].push_back({I, w});
     for (uint32_t w = 0; w < d.nsub; w += kSubPerWg - 1) b.lists[L_SYNC].push_back({I, w});
     for (uint32_t c = 0; c < d.nchunk; c++) b.lists[L_DESTUFF].push_back({I, c});
@@ -726,6 +881,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       uint32_t q = (d.width + 7) / 8 * d.height;
       for (uint32_t it = 0; it < q; it += 256) b.lists[L_COLOR].push_back({I, it});
     }
+    }  // JPEG
     for (int s = 0; s < kStages; s++) {
       const ResizePass &ps = d.pass[s];
       if (!ps.kind) continue;
@@ -747,6 +903,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_COPY].push_back({I, it});
     }
   }
+  for (uint32_t j = 0; j < (uint32_t)b.gjobs.size(); j++)
+    for (uint32_t pc = 0; pc * kGatherPiece < b.gjobs[j].len; pc++) b.lists[L_GATHER].push_back({j, pc});
   for (int h = 0; h < 2; h++)
     for (int c = 0; c < 4; c++) {
       b.hclass[h][c] = (uint32_t)hb[h][c].size();
@@ -758,9 +916,13 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.flags_off = M.take(sizeof(BatchFlags));
   b.desc_off = M.take(b.descs.size() * sizeof(ImageDesc));
   for (int l = 0; l < L_COUNT; l++) b.list_off[l] = M.take(b.lists[l].size() * sizeof(WgItem));
+  b.gjob_off = M.take(b.gjobs.size() * sizeof(GatherJob));
+  b.blob_off = M.take(b.blob.size());
   b.meta_bytes = M.off;
   st = ensure(sl.meta, b.meta_bytes + 256, sl.st);
   if (st) return st;
+  for (ImageDesc &d : b.descs)
+    if (d.fmt == kFmtPng && d.png.pal) d.png.pal = (uint64_t)(uintptr_t)((char *)sl.meta.p + b.blob_off + d.png.pal - 1);
   size_t stage_bytes = b.meta_bytes + (host_io ? IN.off : 0);
   st = ensure_pinned(sl.stage, stage_bytes + 256, sl.st);
   if (st) return st;
@@ -777,6 +939,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   memcpy(P + b.desc_off, b.descs.data(), b.descs.size() * sizeof(ImageDesc));
   for (int l = 0; l < L_COUNT; l++)
     if (!b.lists[l].empty()) memcpy(P + b.list_off[l], b.lists[l].data(), b.lists[l].size() * sizeof(WgItem));
+  if (!b.gjobs.empty()) memcpy(P + b.gjob_off, b.gjobs.data(), b.gjobs.size() * sizeof(GatherJob));
+  if (!b.blob.empty()) memcpy(P + b.blob_off, b.blob.data(), b.blob.size());
   if (host_io) {
     for (int i = 0; i < n; i++)
       if (b.desc_of[i] >= 0) memcpy(P + b.meta_bytes + in_off[i], h_srcs[i], lens[i]);
@@ -816,7 +980,22 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     return DG_OK;
   };
   if (from_fix) HIPCHK(hipMemsetAsync(fl, 0, sizeof(BatchFlags), sl.st));
-  if (ev(1)) return DG_ERR_DEVICE;
+  int evi = 1;  // event i closes stage i-1 (kStageNames)
+  auto next = [&]() -> dg_status { return ev(evi++); };
+  // a resync round re-runs everything downstream of the entropy decode; the
+  // decoded images themselves (PNG, alpha programs on them) are not redone
+  const int alpha_flags = from_fix ? 1 : 0;
+  if (next()) return DG_ERR_DEVICE;
+  if (!from_fix && b.any_png) {
+    launch_png_gather(sl.st, (const GatherJob *)(M + b.gjob_off), lst(L_GATHER), cnt(L_GATHER));
+    launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG));
+  }
+  if (next()) return DG_ERR_DEVICE;
+  if (!from_fix && b.any_png) {
+    launch_png_unfilter(sl.st, dm, lst(L_PNG), cnt(L_PNG));
+    launch_png_expand(sl.st, dd, lst(L_EXPAND), cnt(L_EXPAND));
+  }
+  if (next()) return DG_ERR_DEVICE;
   if (!from_fix) {
     // Lanczos coefficient tables depend only on the plan: compute them on a
     // side stream, overlapped with the entropy decode.
@@ -830,34 +1009,37 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     launch_destuff_scan(sl.st, dm, lst(L_SCAN), cnt(L_SCAN));
     launch_destuff_write(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
   }
-  if (ev(2)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;
   Ckpt *ck = (Ckpt *)((char *)sl.scratch.p + sl.ckpt_off);
   if (!from_fix) launch_huff_sync(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
-  if (ev(3)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;
   launch_huff_fix(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
-  if (ev(4)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;
   launch_huff_scan(sl.st, dm, lst(L_SCAN), cnt(L_SCAN), subs);
-  if (ev(5)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;
   launch_huff_write(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
-  if (ev(6)) return DG_ERR_DEVICE;
-  if (ev(7)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;  // coeffs (side stream)
   launch_idct(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);
-  if (ev(8)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;
   launch_color(sl.st, dd, lst(L_COLOR), cnt(L_COLOR));
-  if (ev(9)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;
   HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_coef, 0));
+  launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
   launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | (debug_flags_ << 8));
-  if (ev(10)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV1), cnt(L_RV1), 1);
-  if (ev(11)) return DG_ERR_DEVICE;
+  launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
+  if (next()) return DG_ERR_DEVICE;
   launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2);
   launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | (debug_flags_ << 8));
-  if (ev(12)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3);
-  if (ev(13)) return DG_ERR_DEVICE;
+  launch_alpha(sl.st, dd, lst(L_ALPHA2), cnt(L_ALPHA2), 2 | (alpha_flags << 8));
+  if (next()) return DG_ERR_DEVICE;
   launch_copy(sl.st, dd, lst(L_COPY), cnt(L_COPY));
-  if (ev(14)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;
   HIPCHK(hipGetLastError());
   // read back flags + per-image status (descs) for finish(), then outputs (host path)
   size_t back = b.desc_off + b.descs.size() * sizeof(ImageDesc);
@@ -877,7 +1059,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
       off += align_up(b.plans[i].out_bytes, 16);
     }
   }
-  if (ev(15)) return DG_ERR_DEVICE;
+  if (next()) return DG_ERR_DEVICE;  // download
   HIPCHK(hipEventRecord(sl.done, sl.st));
   return DG_OK;
 }

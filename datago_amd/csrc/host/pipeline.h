@@ -13,6 +13,7 @@
 #include "../dg_types.h"
 #include "buckets.h"
 #include "jpeg_header.h"
+#include "png_header.h"
 
 namespace dg {
 
@@ -29,7 +30,9 @@ struct PinBuf {
 // Per-image host-side plan (what the host knows before the GPU runs).
 struct ImagePlan {
   int status = DG_OK;
+  uint32_t fmt = kFmtJpeg;
   JpegHeader hdr;
+  PngHeader png;
   int bucket = -1;
   uint32_t out_w = 0, out_h = 0, out_c = 0;
   uint64_t out_bytes = 0;
@@ -44,8 +47,14 @@ struct Batch {
   std::vector<ImageDesc> descs;
   std::vector<int> desc_of;           // image -> desc index or -1
   // workgroup lists (host copies) and their offsets in the device meta buffer
-  std::vector<WgItem> lists[16];
-  size_t list_off[16] = {0};
+  std::vector<WgItem> lists[32];
+  size_t list_off[32] = {0};
+  // PNG: IDAT gather jobs and palettes, uploaded with the descriptors
+  std::vector<GatherJob> gjobs;
+  size_t gjob_off = 0;
+  std::vector<uint8_t> blob;
+  size_t blob_off = 0;
+  bool any_png = false, any_alpha = false;
   // band H lists (L_RH0, L_RH2) are grouped by weight-count class (<=8, <=16,
   // <=32, more): hclass[stage/2][k] items of class k, in that order
   uint32_t hclass[2][4] = {{0}};
@@ -62,6 +71,7 @@ struct Batch {
   BatchFlags flags = {0, 0, 0, 0};
   std::vector<float> stage_ms;
 };
+static_assert(32 >= 20, "list arrays");
 
 // One in-flight batch's device/pinned buffers.  Two slots let the host plan
 // and upload batch k+1 while the GPU still runs batch k.
@@ -85,6 +95,7 @@ struct Slot {
 enum ListId {
   L_HUFF = 0, L_SYNC, L_DESTUFF, L_SCAN, L_IDCT, L_COLOR, L_COEF, L_RH0, L_RV1, L_RH2, L_RV3, L_COPY,
   L_RHX0, L_RHX2,  // H passes whose source segment is too wide for the band kernel
+  L_GATHER, L_PNG, L_EXPAND, L_ALPHA0, L_ALPHA1, L_ALPHA2,  // PNG decode, alpha programs
   L_COUNT
 };
 

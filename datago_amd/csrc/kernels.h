@@ -38,3 +38,16 @@ void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 
 }  // namespace dg
+
+// PNG (dg_png.hip)
+namespace dg {
+void launch_png_gather(hipStream_t st, const GatherJob *jobs, const WgItem *list, uint32_t nwg);
+// one 64-thread workgroup (one wave) per image
+void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+// 256 pixels per workgroup
+void launch_png_expand(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+// alpha program at `point` (0 before call 1, 1 between the calls, 2 after call 2): 256 pixels per workgroup
+void launch_alpha(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int point);
+size_t png_inflate_smem();
+}  // namespace dg

@@ -1133,6 +1133,39 @@ __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ 
   }
 }
 
+// image 0.25 Rgba<u8>::blend of `f` over an opaque (128,128,128,255) pixel,
+// then its RGB: f32 arithmetic in the crate's order, truncating casts.
+// hipcc's f32 division is IEEE correctly rounded and contraction is off, so
+// this matches the CPU restatement (oracle/png_oracle.c) bit for bit.
+__device__ __forceinline__ void blend_over_gray(const DG_GLOBAL uint8_t *f, DG_GLOBAL uint8_t *o) {
+  const uint32_t a = f[3];
+  if (a == 0) {
+    o[0] = o[1] = o[2] = 128;
+    return;
+  }
+  if (a == 255) {
+    o[0] = f[0];
+    o[1] = f[1];
+    o[2] = f[2];
+    return;
+  }
+  const float mx = 255.0f;
+  const float bg = 128.0f / mx, bga = 255.0f / mx;
+  const float fa = (float)a / mx;
+  const float af = bga + fa - bga * fa;
+  if (af == 0.0f) {
+    o[0] = o[1] = o[2] = 128;
+    return;
+  }
+  const float bgm = bg * bga;
+  for (int c = 0; c < 3; c++) {
+    const float fc = (float)f[c] / mx;
+    const float v = (fc * fa + bgm * (1.0f - fa)) / af;
+    const float sv = mx * v;
+    o[c] = (uint8_t)(sv < 0.0f ? 0 : sv > 255.0f ? 255 : (int)sv);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_copy(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
@@ -1141,10 +1174,23 @@ __global__ __launch_bounds__(256) void k_copy(const ImageDesc *__restrict__ imgs
   const uint32_t y = idx / im.out_w, x = idx - y * im.out_w;
   const DG_GLOBAL uint8_t *s = gp<const uint8_t>(im.final_src) + (size_t)y * im.final_src_stride + (size_t)x * im.final_src_c;
   DG_GLOBAL uint8_t *d = gp<uint8_t>(im.out) + (size_t)y * im.out_stride + (size_t)x * im.out_c;
-  if (im.final_src_c == im.out_c) {
-    for (uint32_t c = 0; c < im.out_c; c++) d[c] = s[c];
-  } else {  // L8 -> RGB8 (image::DynamicImage::to_rgb8 replicates luma)
-    d[0] = d[1] = d[2] = s[0];
+  switch (im.copy_mode) {
+    case 0:
+      for (uint32_t c = 0; c < im.out_c; c++) d[c] = s[c];
+      break;
+    case 1:  // L8 -> RGB8 (image::DynamicImage::to_rgb8 replicates luma)
+    case 4:  // unresized LumaA8 -> RGB8: alpha dropped
+      d[0] = d[1] = d[2] = s[0];
+      break;
+    case 2:  // RGBA8 -> RGB8: Pixel::blend over opaque (128,128,128) (image_processing.rs:172-179)
+      blend_over_gray(s, d);
+      break;
+    default: {  // resized LA: image_to_dyn_image made a GrayImage over the LA bytes
+      const uint32_t rb = im.out_w * 2, r = idx / rb, c = idx - r * rb;
+      const uint8_t v = gp<const uint8_t>(im.final_src)[(size_t)r * im.final_src_stride + c];
+      d[0] = d[1] = d[2] = v;
+      break;
+    }
   }
 }
 

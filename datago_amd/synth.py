@@ -129,3 +129,144 @@ def uniform_corpus(seed: int, n: int, w: int = 640, h: int = 480, quality: int =
     if workers > 1:
         return _pool_map(jobs, workers)
     return [_make_one(j) for j in jobs]
+
+
+# ---------------------------------------------------------------- PNG
+
+PNG_KINDS = ("L", "LA", "RGB", "RGBA", "P8", "P8T", "P4", "P2", "P1", "L1", "L2", "L4", "LT", "RGBT")
+
+
+def _png_chunk(t: bytes, data: bytes) -> bytes:
+    import struct
+    import zlib
+    return struct.pack(">I", len(data)) + t + data + struct.pack(">I", zlib.crc32(t + data) & 0xFFFFFFFF)
+
+
+def _paeth(a, b, c):
+    p = a + b - c
+    pa, pb, pc = np.abs(p - a), np.abs(p - b), np.abs(p - c)
+    return np.where((pa <= pb) & (pa <= pc), a, np.where(pb <= pc, b, c))
+
+
+def png_filter_rows(rows: np.ndarray, bpp: int, filters: np.ndarray) -> bytes:
+    """PNG scanline filtering (spec 9.2) of H x rowbytes uint8 with the given
+    per-row filter types; returns the filtered stream (filter byte + row)."""
+    h, rb = rows.shape
+    out = bytearray()
+    prev = np.zeros(rb, np.int32)
+    for y in range(h):
+        r = rows[y].astype(np.int32)
+        a = np.concatenate([np.zeros(bpp, np.int32), r[:-bpp]]) if rb > bpp else np.zeros(rb, np.int32)
+        c = np.concatenate([np.zeros(bpp, np.int32), prev[:-bpp]]) if rb > bpp else np.zeros(rb, np.int32)
+        f = int(filters[y])
+        if f == 0:
+            v = r
+        elif f == 1:
+            v = r - a
+        elif f == 2:
+            v = r - prev
+        elif f == 3:
+            v = r - ((a + prev) >> 1)
+        else:
+            v = r - _paeth(a, prev, c)
+        out.append(f)
+        out += (v & 0xFF).astype(np.uint8).tobytes()
+        prev = r
+    return bytes(out)
+
+
+def encode_png(rows: np.ndarray, w: int, h: int, depth: int, ctype: int, bpp: int, rng: np.random.Generator,
+               level: int = 6, strategy: int = 0, filters: str = "random", idat_max: int = 0,
+               plte: Optional[bytes] = None, trns: Optional[bytes] = None) -> bytes:
+    """PNG writer for test corpora: explicit filter choice ("random" per row,
+    "none", or a filter number), zlib level/strategy (0 = stored blocks,
+    Z_FIXED = fixed Huffman), IDAT split into chunks of at most idat_max."""
+    import struct
+    import zlib
+    if filters == "random":
+        fl = rng.integers(0, 5, size=h)
+    elif filters == "none":
+        fl = np.zeros(h, np.int64)
+    else:
+        fl = np.full(h, int(filters))
+    raw = png_filter_rows(rows, bpp, fl)
+    co = zlib.compressobj(level, zlib.DEFLATED, 15, 8, strategy)
+    z = co.compress(raw) + co.flush()
+    out = b"\x89PNG\r\n\x1a\n" + _png_chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0))
+    if plte is not None:
+        out += _png_chunk(b"PLTE", plte)
+    if trns is not None:
+        out += _png_chunk(b"tRNS", trns)
+    step = idat_max if idat_max > 0 else len(z)
+    for i in range(0, max(len(z), 1), max(step, 1)):
+        out += _png_chunk(b"IDAT", z[i:i + step])
+    return out + _png_chunk(b"IEND", b"")
+
+
+def _pack_bits(idx: np.ndarray, depth: int) -> np.ndarray:
+    h, w = idx.shape
+    per = 8 // depth
+    rb = (w * depth + 7) // 8
+    pad = np.zeros((h, rb * per), np.uint8)
+    pad[:, :w] = idx
+    pad = pad.reshape(h, rb, per)
+    out = np.zeros((h, rb), np.uint8)
+    for k in range(per):
+        out |= (pad[:, :, k] << (8 - depth * (k + 1))).astype(np.uint8)
+    return out
+
+
+def make_png(seed: int, w: int, h: int, kind: str = "RGB", **kw) -> bytes:
+    """Seeded PNG of the given kind (PNG_KINDS).  Pixel content as synth_pixels;
+    alpha is a smooth ramp with fully transparent/opaque patches."""
+    rng = np.random.default_rng(seed)
+    gray = kind[0] == "L" or kind[0] == "P"
+    px = synth_pixels(rng, w, h, gray=gray)
+    px = px.reshape(h, w, -1)
+    alpha = np.clip(np.linspace(-64, 320, w)[None, :] + rng.normal(0, 30, (h, w)), 0, 255).astype(np.uint8)
+    plte = trns = None
+    if kind in ("L", "LA", "RGB", "RGBA"):
+        if kind in ("LA", "RGBA"):
+            px = np.concatenate([px, alpha[:, :, None]], axis=2)
+        depth, ctype = 8, {"L": 0, "LA": 4, "RGB": 2, "RGBA": 6}[kind]
+        c = px.shape[2]
+        rows = px.reshape(h, w * c)
+        bpp = c
+    elif kind.startswith("P"):
+        depth = int(kind[1])
+        ncol = 1 << depth
+        npal = int(rng.integers(max(1, ncol // 2), ncol + 1))
+        pal = rng.integers(0, 256, size=(npal, 3)).astype(np.uint8)
+        idx = (px[:, :, 0].astype(np.int32) * ncol // 256).astype(np.uint8)  # may exceed npal: black
+        plte = pal.tobytes()
+        if kind.endswith("T"):
+            trns = rng.integers(0, 256, size=int(rng.integers(1, npal + 1))).astype(np.uint8).tobytes()
+        ctype = 3
+        rows = idx if depth == 8 else _pack_bits(idx, depth)
+        bpp = 1
+    elif kind in ("L1", "L2", "L4"):
+        depth = int(kind[1])
+        v = (px[:, :, 0].astype(np.int32) >> (8 - depth)).astype(np.uint8)
+        ctype, bpp = 0, 1
+        rows = _pack_bits(v, depth)
+        if kw.pop("trns_key", False):
+            trns = bytes([0, int(v[0, 0])])
+    elif kind == "LT":
+        depth, ctype, bpp = 8, 0, 1
+        rows = px[:, :, 0].copy()
+        trns = bytes([0, int(rows[0, 0])])
+    elif kind == "RGBT":
+        depth, ctype, bpp = 8, 2, 3
+        rows = px.reshape(h, w * 3)
+        trns = bytes([0, int(px[0, 0, 0]), 0, int(px[0, 0, 1]), 0, int(px[0, 0, 2])])
+    else:
+        raise ValueError(kind)
+    return encode_png(rows, w, h, depth, ctype, bpp, rng, plte=plte, trns=trns, **kw)
+
+
+def pil_png(arr: np.ndarray, **kw) -> bytes:
+    """PNG through PIL's own encoder (what most PNGs in the wild look like)."""
+    im = Image.fromarray(arr)
+    buf = io.BytesIO()
+    im.save(buf, format="PNG", **kw)
+    return buf.getvalue()

@@ -116,3 +116,82 @@ def fit_crop(sw: int, sh: int, dw: int, dh: int):
     v = [ctypes.c_double() for _ in range(4)]
     lib().or_fit_crop(sw, sh, dw, dh, *[ctypes.byref(x) for x in v])
     return tuple(x.value for x in v)
+
+
+# ------------------------------------------------------------------ PNG
+PO_OK, PO_UNSUPPORTED, PO_CORRUPT, PO_SMALLBUF = 0, 1, 2, 3
+
+
+def _png_lib():
+    L = lib()
+    if not getattr(L, "_png_ready", False):
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        ip = ctypes.POINTER(ctypes.c_int)
+        L.po_info.argtypes = [u8p, ctypes.c_size_t] + [ip] * 6
+        L.po_decode.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
+        L.po_zlib_inflate.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t,
+                                      ctypes.POINTER(ctypes.c_size_t)]
+        L.po_premultiply.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int]
+        L.po_unpremultiply.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int]
+        L.po_blend_over_gray.argtypes = [u8p, ctypes.c_size_t, u8p]
+        L._png_ready = True
+    return L
+
+
+def png_info(data: bytes):
+    """(status, w, h, channels_after_expand, depth, color_type, interlace)."""
+    v = [ctypes.c_int() for _ in range(6)]
+    st = _png_lib().po_info(_u8(data), len(data), *[ctypes.byref(x) for x in v])
+    return (st,) + tuple(x.value for x in v)
+
+
+def png_decode(data: bytes):
+    """Decode to HWC uint8 (C = 1..4 after EXPAND).  (status, array or None)."""
+    st, w, h, c = png_info(data)[:4]
+    if st != PO_OK:
+        return st, None
+    out = np.empty((h, w, c), np.uint8)
+    st = _png_lib().po_decode(_u8(data), len(data), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), out.nbytes)
+    return st, (out if st == PO_OK else None)
+
+
+def zlib_inflate(z: bytes, want: int):
+    out = np.zeros(max(want, 1), np.uint8)
+    got = ctypes.c_size_t()
+    st = _png_lib().po_zlib_inflate(_u8(z), len(z), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), want,
+                                    ctypes.byref(got))
+    return st, out[:got.value].tobytes()
+
+
+def blend_over_gray(rgba: np.ndarray) -> np.ndarray:
+    """convert_to_rgb8 for RGBA (image_processing.rs:163-186)."""
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    out = np.empty(rgba.shape[:-1] + (3,), np.uint8)
+    _png_lib().po_blend_over_gray(rgba.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), rgba.size // 4,
+                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    return out
+
+
+def decode_any(data: bytes):
+    """JPEG or PNG by magic bytes: (status, HWC array)."""
+    if data[:8] == b"\x89PNG\r\n\x1a\n":
+        return png_decode(data)
+    return jpeg_decode(data)
+
+
+def to_rgb8(arr: np.ndarray, resized: bool) -> np.ndarray:
+    """image_to_payload's img_to_rgb8 step (image_processing.rs:362-372) on the
+    transformed image.  LumaA8 quirk: a resized U8x2 image comes
+    back from image_to_dyn_image as a GrayImage over the LA bytes, so its RGB
+    is the first w*h bytes of the LA buffer as luma; an unresized LumaA8 drops
+    its alpha."""
+    h, w, c = arr.shape
+    if c == 3:
+        return arr
+    if c == 4:
+        return blend_over_gray(arr)
+    if c == 2 and resized:
+        g = np.ascontiguousarray(arr).reshape(-1)[: w * h].reshape(h, w)
+    else:
+        g = arr[:, :, 0]
+    return np.repeat(g[:, :, None], 3, axis=2)

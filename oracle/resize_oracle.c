@@ -276,16 +276,43 @@ void or_fit_crop(int sw, int sh, int dw, int dh, double *l, double *t, double *c
   *ch = h;
 }
 
-/* Whole crop_and_resize for C in {1,3}: src W x H -> dst tw x th. */
+/* fast_image_resize mul_div_alpha: a U8x2/U8x4 convolution call
+ * premultiplies a copy of its source, resamples, and divides the result; a
+ * call that is a plain copy (same size, integral box) touches no alpha.
+ * po_premultiply/po_unpremultiply live in png_oracle.c. */
+void po_premultiply(uint8_t *p, size_t npx, int C);
+void po_unpremultiply(uint8_t *p, size_t npx, int C);
+
+static int resample_call(const uint8_t *src, int sw, int sh, int C, uint8_t *dst, int dw, int dh, double x0,
+                         double y0, double x1, double y1, int mode) {
+  /* a crop box of the destination's size at integral offsets is a copy */
+  const int is_copy = x1 - x0 == (double)dw && y1 - y0 == (double)dh && x0 == floor(x0) && y0 == floor(y0);
+  if (is_copy) {
+    for (int y = 0; y < dh; y++)
+      memcpy(dst + (size_t)y * dw * C, src + ((size_t)(y + (int)y0) * sw + (size_t)x0) * C, (size_t)dw * C);
+    return 0;
+  }
+  if (!(C == 2 || C == 4)) return or_resample(src, sw, sh, C, dst, dw, dh, x0, y0, x1, y1, mode);
+  const size_t n = (size_t)sw * sh;
+  uint8_t *pm = (uint8_t *)malloc(n * C + 1);
+  memcpy(pm, src, n * C);
+  po_premultiply(pm, n, C);
+  int r = or_resample(pm, sw, sh, C, dst, dw, dh, x0, y0, x1, y1, mode);
+  po_unpremultiply(dst, (size_t)dw * dh, C);
+  free(pm);
+  return r;
+}
+
+/* Whole crop_and_resize for C in {1,2,3,4}: src W x H -> dst tw x th. */
 int or_crop_and_resize(const uint8_t *src, int w, int h, int C, int tw, int th, uint8_t *dst, int mode) {
   if (w == tw && h == th) { memcpy(dst, src, (size_t)w * h * C); return 0; }
   int nw, nh;
   or_scaled_size(w, h, tw, th, &nw, &nh);
   uint8_t *mid = (uint8_t *)malloc((size_t)nw * nh * C + 1);
-  or_resample(src, w, h, C, mid, nw, nh, 0.0, 0.0, (double)w, (double)h, mode);
+  resample_call(src, w, h, C, mid, nw, nh, 0.0, 0.0, (double)w, (double)h, mode);
   double l, t, cw, ch;
   or_fit_crop(nw, nh, tw, th, &l, &t, &cw, &ch);
-  or_resample(mid, nw, nh, C, dst, tw, th, l, t, l + cw, t + ch, mode);
+  resample_call(mid, nw, nh, C, dst, tw, th, l, t, l + cw, t + ch, mode);
   free(mid);
   return 0;
 }

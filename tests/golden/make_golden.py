@@ -10,7 +10,14 @@
   BASELINE configs, from oracle/buckets.py (itself pinned by the reference's
   known answers at image_processing.rs:441-478).
 
-Usage: python tests/golden/make_golden.py
+* tests/golden/png/*.png    — small seeded PNGs (every colour type, sub-byte
+  depths, palettes with tRNS, all five filters, stored / fixed / dynamic
+  blocks, split IDAT chunks, PIL's own encoder) plus 16-bit / interlaced /
+  corrupt files
+* tests/golden/png_expected.json — status + sha256 + shape of PIL's decode of
+  each (expanded like png's Transformations::EXPAND)
+
+Usage: python tests/golden/make_golden.py [--png-only]
 """
 import hashlib
 import io
@@ -53,7 +60,80 @@ def sha(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+PNG_CASES = [
+    # name, kind, w, h, encoder kwargs
+    ("rgb_17x9_dyn", "RGB", 17, 9, {}),
+    ("rgba_33x20_dyn", "RGBA", 33, 20, {}),
+    ("l_64x33_paeth", "L", 64, 33, {"filters": "4"}),
+    ("la_31x17_avg", "LA", 31, 17, {"filters": "3"}),
+    ("p8_40x30_stored", "P8", 40, 30, {"level": 0}),
+    ("p8t_25x25_fixed", "P8T", 25, 25, {"strategy": 4}),
+    ("p4_19x7_split", "P4", 19, 7, {"idat_max": 5}),
+    ("p2_13x11", "P2", 13, 11, {}),
+    ("p1_70x3", "P1", 70, 3, {}),
+    ("l1_9x9", "L1", 9, 9, {}),
+    ("l2_21x5", "L2", 21, 5, {}),
+    ("l4_11x13", "L4", 11, 13, {}),
+    ("lt_15x15", "LT", 15, 15, {}),
+    ("rgbt_12x10", "RGBT", 12, 10, {}),
+    ("rgb_1x1", "RGB", 1, 1, {}),
+    ("rgb_300x200_l9", "RGB", 300, 200, {"level": 9}),
+]
+
+
+def png_golden():
+    import zlib
+    os.makedirs(os.path.join(HERE, "png"), exist_ok=True)
+    exp = {}
+
+    def pil_expand(data):
+        im = Image.open(io.BytesIO(data))
+        trns = "transparency" in im.info
+        if im.mode == "P":
+            im = im.convert("RGBA" if trns else "RGB")
+        elif im.mode in ("1", "L"):
+            im = im.convert("LA" if trns else "L")
+        elif im.mode == "RGB" and trns:
+            im = im.convert("RGBA")
+        a = np.asarray(im)
+        return a[:, :, None] if a.ndim == 2 else a
+
+    files = {}
+    for i, (name, kind, w, h, kw) in enumerate(PNG_CASES):
+        files[name] = synth.make_png(2000 + i, w, h, kind, **kw)
+    rng = np.random.default_rng(7)
+    files["pil_rgb_97x61"] = synth.pil_png(synth.synth_pixels(rng, 97, 61))
+    files["pil_rgba_50x40_opt"] = synth.pil_png(
+        np.concatenate([synth.synth_pixels(rng, 50, 40), rng.integers(0, 256, (40, 50, 1), dtype=np.uint8)], 2),
+        optimize=True)
+    rows = rng.integers(0, 256, (5, 16), dtype=np.uint8)
+    files["l16_8x5_unsupported"] = synth.encode_png(rows, 8, 5, 16, 0, 2, rng)
+    ad = bytearray(synth.pil_png(synth.synth_pixels(rng, 40, 30)))
+    ad[28] = 1  # IHDR interlace method = Adam7 (header-only: the GPU path reports UNSUPPORTED)
+    ad[29:33] = zlib.crc32(bytes(ad[12:29])).to_bytes(4, "big")
+    files["rgb_40x30_adam7_unsupported"] = bytes(ad)
+    good = files["rgb_17x9_dyn"]
+    files["truncated_corrupt"] = good[: len(good) - 30]
+    for name, data in files.items():
+        with open(os.path.join(HERE, "png", name + ".png"), "wb") as f:
+            f.write(data)
+        if name.endswith("_unsupported"):
+            exp[name] = {"status": 1}
+            continue
+        if name.endswith("_corrupt"):
+            exp[name] = {"status": 2}
+            continue
+        a = pil_expand(data)
+        exp[name] = {"status": 0, "shape": list(a.shape), "sha256": sha(a)}
+    with open(os.path.join(HERE, "png_expected.json"), "w") as f:
+        json.dump(exp, f, indent=1, sort_keys=True)
+    print("wrote", len(files), "png fixtures")
+
+
 def main():
+    png_golden()
+    if "--png-only" in sys.argv:
+        return
     jexp, rexp = {}, {}
     tr = B.ARAwareTransform(512, 16, 0.5, 2.0)
     for i, (name, w, h, q, ss, gray, rst) in enumerate(CASES):

@@ -169,8 +169,8 @@ def test_status_codes(ctx512):
     buf = _io.BytesIO()
     Image.fromarray(synth.synth_pixels(np.random.default_rng(0), 64, 64)).save(buf, format="JPEG", progressive=True)
     prog = buf.getvalue()
-    png = _io.BytesIO()
-    Image.new("RGB", (8, 8)).save(png, format="PNG")
+    png = _io.BytesIO()  # 16-bit PNG: valid, outside the GPU path (the Rust glue keeps its CPU decode)
+    Image.fromarray(np.arange(64, dtype=np.uint16).reshape(8, 8) * 1000).save(png, format="PNG")
     trunc = synth.make_jpeg(14, 300, 300, 90)[:1500]
     res = ctx512.decode_batch([good, b"This is not a valid image file", prog, png.getvalue(), trunc, good])
     sts = [r[0] for r in res]

@@ -1,0 +1,196 @@
+"""GPU parity for the PNG path (k_png_* kernels through the C ABI) against the
+oracle (oracle/png_oracle.c, pinned to PIL by tests/test_oracle_png.py).
+Tolerance 0 everywhere: inflate/unfilter/expand are exact by spec, the
+resize is the same integer arithmetic as the JPEG path, alpha mul/div and the
+f32 compositing are restated bit for bit."""
+import hashlib
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+from datago_amd import synth
+from oracle import buckets as B
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+
+def _lib():
+    from datago_amd import _lib as L
+    return L
+
+
+@pytest.fixture(scope="module")
+def ctx_dec():
+    return _lib().Context(0)
+
+
+@pytest.fixture(scope="module")
+def ctx_rgb8():
+    return _lib().Context(0, image_to_rgb8=True)
+
+
+@pytest.fixture(scope="module")
+def ctx512():
+    return _lib().Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+                          min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+
+
+@pytest.fixture(scope="module")
+def ctx512_rgb8():
+    return _lib().Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+                          min_aspect_ratio=0.5, max_aspect_ratio=2.0, image_to_rgb8=True)
+
+
+def _cases():
+    out = []
+    i = 0
+    for kind in synth.PNG_KINDS:
+        for (w, h) in [(1, 1), (5, 3), (64, 33), (255, 7), (130, 300)]:
+            for kw in ({}, {"level": 0}, {"strategy": zlib.Z_FIXED}, {"idat_max": 97, "level": 9}, {"filters": "4"}):
+                i += 1
+                if i % 2:
+                    out.append((kind, w, h, kw))
+    return out
+
+
+CASES = _cases()
+
+
+def _png(case):
+    kind, w, h, kw = case
+    return synth.make_png(hash((kind, w, h, str(kw))) & 0xFFFF, w, h, kind, **kw)
+
+
+def test_png_decode_only_bit_exact(ctx_dec):
+    datas = [_png(c) for c in CASES]
+    res = ctx_dec.decode_batch(datas)
+    for c, d, (st, arr, m) in zip(CASES, datas, res):
+        ost, ref = O.png_decode(d)
+        assert ost == 0
+        assert st == 0, (c, st, _lib().last_error())
+        assert arr.shape == ref.shape, c
+        assert np.array_equal(arr, ref), (c, int(np.argwhere(arr != ref)[0][0]))
+        assert (m.original_width, m.original_height, m.channels, m.bit_depth) == (ref.shape[1], ref.shape[0],
+                                                                                 ref.shape[2], 8)
+
+
+def test_png_golden_fixtures(ctx_dec):
+    exp = json.load(open(os.path.join(GOLD, "png_expected.json")))
+    names = sorted(exp)
+    datas = [open(os.path.join(GOLD, "png", n + ".png"), "rb").read() for n in names]
+    res = ctx_dec.decode_batch(datas)
+    for n, (st, arr, m) in zip(names, res):
+        assert st == exp[n]["status"], (n, st)
+        if st == 0:
+            assert list(arr.shape) == exp[n]["shape"], n
+            assert hashlib.sha256(arr.tobytes()).hexdigest() == exp[n]["sha256"], n
+
+
+def test_png_bucket_resize_bit_exact(ctx512):
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    rng = np.random.default_rng(11)
+    datas, kinds = [], []
+    for i in range(36):
+        kind = synth.PNG_KINDS[i % len(synth.PNG_KINDS)]
+        w, h = int(rng.integers(20, 900)), int(rng.integers(20, 900))
+        datas.append(synth.make_png(500 + i, w, h, kind, idat_max=int(rng.integers(0, 3)) * 8192))
+        kinds.append((kind, w, h))
+    res = ctx512.decode_batch(datas)
+    for k, d, (st, arr, m) in zip(kinds, datas, res):
+        assert st == 0, (k, st)
+        _, ref = O.png_decode(d)
+        tw, th = t.target_size(ref.shape[1], ref.shape[0])
+        exp = O.crop_and_resize(ref, tw, th, O.MODE_FIR)
+        assert arr.shape == exp.shape, k
+        diff = np.argwhere(arr != exp)
+        assert diff.size == 0, (k, diff[:3].tolist(), arr[tuple(diff[0])], exp[tuple(diff[0])])
+
+
+def test_png_rgb8_conversions(ctx512_rgb8, ctx_rgb8):
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    datas = [synth.make_png(900 + i, w, h, kind) for i, (kind, w, h) in enumerate(
+        [("RGBA", 200, 150), ("LA", 151, 233), ("L", 90, 300), ("RGB", 640, 480), ("P8T", 120, 70),
+         ("RGBA", 592, 432), ("LA", 592, 432)])]
+    for ctx, resize in ((ctx512_rgb8, True), (ctx_rgb8, False)):
+        res = ctx.decode_batch(datas)
+        for d, (st, arr, m) in zip(datas, res):
+            assert st == 0
+            _, dec = O.png_decode(d)
+            if resize:
+                tw, th = t.target_size(dec.shape[1], dec.shape[0])
+                resized = (tw, th) != (dec.shape[1], dec.shape[0])
+                tr = O.crop_and_resize(dec, tw, th, O.MODE_FIR) if resized else dec
+            else:
+                resized, tr = False, dec
+            exp = O.to_rgb8(tr, resized)
+            assert m.channels == 3 and arr.shape == exp.shape
+            assert np.array_equal(arr, exp), (dec.shape, resized)
+
+
+def test_reference_rgba_composite_known_answers(ctx_rgb8):
+    # worker_files.rs:322-383: 3x1 RGBA PNG through image_payload_from_path with img_to_rgb8
+    rgba = np.array([[[255, 100, 50, 255], [200, 100, 50, 128], [255, 0, 0, 0]]], np.uint8)
+    (st, arr, m), = ctx_rgb8.decode_batch([synth.pil_png(rgba)])
+    assert st == 0 and (m.channels, m.bit_depth, m.width, m.height) == (3, 8, 3, 1)
+    px = arr.reshape(-1).tolist()
+    assert px[0:3] == [255, 100, 50]
+    assert abs(px[3] - 164) <= 2 and abs(px[4] - 114) <= 2 and abs(px[5] - 89) <= 2
+    assert px[6:9] == [128, 128, 128]
+    # worker_files.rs:385-444: gray -> replicated, RGB passthrough
+    (st, arr, m), = ctx_rgb8.decode_batch([synth.pil_png(np.array([[100]], np.uint8))])
+    assert st == 0 and m.channels == 3 and arr.reshape(-1).tolist() == [100, 100, 100]
+    (st, arr, m), = ctx_rgb8.decode_batch([synth.pil_png(np.array([[[255, 100, 50]]], np.uint8))])
+    assert st == 0 and arr.reshape(-1).tolist() == [255, 100, 50]
+
+
+def test_png_status_codes(ctx_dec):
+    L = _lib()
+    exp = json.load(open(os.path.join(GOLD, "png_expected.json")))
+    bad = [n for n in sorted(exp) if exp[n]["status"]]
+    datas = [open(os.path.join(GOLD, "png", n + ".png"), "rb").read() for n in bad]
+    # corrupt inside the zlib stream (header intact): flipped bits in the IDAT payload
+    good = bytearray(synth.make_png(77, 64, 64, "RGB"))
+    i = good.index(b"IDAT") + 4
+    for k in range(i + 2, min(i + 40, len(good) - 16)):
+        good[k] ^= 0x5A
+    datas.append(bytes(good))
+    res = ctx_dec.decode_batch(datas)
+    for n, (st, _, _) in zip(bad, res):
+        assert st == exp[n]["status"], n
+    assert res[-1][0] in (L.DG_ERR_CORRUPT, L.DG_OK)  # the oracle decides which
+    assert res[-1][0] == (L.DG_OK if O.png_decode(bytes(good))[0] == 0 else L.DG_ERR_CORRUPT)
+
+
+def test_mixed_jpeg_png_batch(ctx512):
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    datas = []
+    for i in range(12):
+        if i % 2:
+            datas.append(synth.make_png(300 + i, 100 + 37 * i, 80 + 29 * i, ["RGB", "L", "RGBA", "P8"][i % 4]))
+        else:
+            datas.append(synth.make_jpeg(300 + i, 100 + 37 * i, 80 + 29 * i, 90, "4:2:0"))
+    res = ctx512.decode_batch(datas)
+    for d, (st, arr, m) in zip(datas, res):
+        assert st == 0
+        _, dec = O.decode_any(d)
+        tw, th = t.target_size(dec.shape[1], dec.shape[0])
+        assert np.array_equal(arr, O.crop_and_resize(dec, tw, th, O.MODE_FIR))
+
+
+def test_png_large_full_size_properties(ctx512):
+    # bench-sized PNG: decode equals the oracle; resize output has the bucket's dims
+    d = synth.make_png(4242, 1800, 1200, "RGB")
+    (st, arr, m), = _lib().Context(0).decode_batch([d])
+    assert st == 0
+    _, ref = O.png_decode(d)
+    assert np.array_equal(arr, ref)
+    (st, arr, m), = ctx512.decode_batch([d])
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    assert st == 0 and (arr.shape[1], arr.shape[0]) == t.target_size(1800, 1200)
