@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=3, help="host-memory (PCIe-inclusive) steps")
+    ap.add_argument("--workload", choices=("jpeg", "png"), default="jpeg",
+                    help="jpeg: configs[1] (the headline); png: configs[4]-style RGB PNG + aligned L8 mask pairs "
+                         "(decode + bucket-resize; the mask is forced to the image's bucket, worker_http.rs:186-214)")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 
@@ -75,7 +78,7 @@ def _cpu_work(args):
     from oracle import oracle as O
     data, tw, th = args
     t = time.perf_counter()
-    st, dec = O.jpeg_decode(data)
+    st, dec = O.decode_any(data)
     O.crop_and_resize(dec, tw, th, O.MODE_FIR)
     return dec.shape[0] * dec.shape[1], time.perf_counter() - t
 
@@ -91,7 +94,7 @@ def cpu_baseline(pool, targets, seconds: float):
     # size the sample from a one-image probe so the run takes ~`seconds`
     px, dt = _cpu_work((pool[0], *targets[0]))
     per_px = dt / max(px, 1)
-    mean_px = np.mean([w * h for (w, h) in [O.jpeg_info(d)[1:3] for d in pool[:32]]])
+    mean_px = np.mean([w * h for (w, h) in [image_dims(d)[:2] for d in pool[:32]]])
     n = int(max(cores, min(64 * len(pool), seconds * cores / max(per_px * mean_px, 1e-9))))
     jobs = [(pool[i % len(pool)], *targets[i % len(pool)]) for i in range(n)]
     p = mp.get_context("fork").Pool(cores)
@@ -107,6 +110,90 @@ def cpu_baseline(pool, targets, seconds: float):
     return {"value": round(tot_px / wall / 1e6, 2), "unit": "Mpixel/s", "cores": cores, "kind": "port",
             "sample": f"{n} images of the same pool ({tot_px / 1e6:.1f} Mpx) through oracle/ (scalar C "
                       f"decode + FIR-mode Lanczos3 crop_and_resize), {cores} processes, {wall:.1f} s"}
+
+
+def image_dims(data: bytes):
+    """(w, h, decoded channels) from the header (oracle helpers: bench plumbing)."""
+    from oracle import oracle as O
+    if data[:8] == b"\x89PNG\r\n\x1a\n":
+        st, w, h, c = O.png_info(data)[:4]
+        return w, h, c
+    return tuple(O.jpeg_info(data)[1:4])
+
+
+def png_stage_bytes(data: bytes, dim, target) -> dict:
+    """Algorithmic bytes per stage for one PNG: inflate reads the zlib stream
+    and writes the filtered scanlines; unfilter reads and writes them once;
+    the resize passes as for a non-fused source of C channels."""
+    from oracle import buckets as B
+    from oracle import oracle as O
+    w, h, c = dim
+    tw, th = target
+    info = O.png_info(data)
+    depth, ctype = info[4], info[5]
+    spp = {0: 1, 2: 3, 3: 1, 4: 2, 6: 4}[ctype]
+    rb = (spp * depth * w + 7) // 8
+    b = {"png_inflate": len(data) + h * (rb + 1), "png_unfilter": h * (rb + 1) + h * rb,
+         "resize_h1": 0.0, "resize_v1": 0.0, "resize_h2": 0.0, "resize_v2": 0.0, "copy": 0.0}
+    if (w, h) != (tw, th):
+        nw, nh = B.scaled_size(w, h, tw, th)
+        l, t, bw, bh = B.fit_crop_box(nw, nh, tw, th)
+        fold_x = abs(l - round(l)) <= 1e-6 and abs(bw - tw) <= 1e-6
+        fold_y = abs(t - round(t)) <= 1e-6 and abs(bh - th) <= 1e-6
+        cw, ch = w, h
+        if nw != w:
+            wx = tw if fold_x else nw
+            b["resize_h1"] = c * (w * h + wx * h)
+            cw = wx
+        elif fold_x:
+            cw = tw
+        if nh != h:
+            hy = th if fold_y else nh
+            b["resize_v1"] = c * (cw * h + cw * hy)
+            ch = hy
+        elif fold_y:
+            ch = th
+        if not fold_x:
+            b["resize_h2"] = c * (cw * ch + tw * ch)
+            cw = tw
+        if not fold_y:
+            b["resize_v2"] = c * (cw * ch + cw * th)
+    else:
+        b["copy"] = 2 * c * w * h
+    return b
+
+
+def png_pair(args):
+    """One configs[4] sample: an RGB PNG (PIL encoder: adaptive filters, zlib
+    level 6) and an L8 mask PNG of the same size (seed 5 stream)."""
+    from datago_amd import synth
+    seed, (w, h, _, _, _) = args
+    rng = np.random.default_rng(seed)
+    img = synth.pil_png(synth.synth_pixels(rng, w, h))
+    yy, xx = np.mgrid[0:h, 0:w]
+    cx, cy, r = rng.uniform(0.3, 0.7) * w, rng.uniform(0.3, 0.7) * h, rng.uniform(0.2, 0.45) * min(w, h)
+    mask = (((xx - cx) ** 2 + (yy - cy) ** 2) < r * r).astype(np.uint8) * 255
+    return img, synth.pil_png(mask)
+
+
+def png_corpus(seed: int, n: int, short_min: int, short_max: int, workers: int, lo: int, hi: int):
+    from datago_amd import synth
+    spec = synth.mixed_spec(seed, n, short_min, short_max)
+    jobs = [(seed * 1_000_003 + i, spec[i]) for i in range(lo, hi)]
+    if workers > 1:
+        import multiprocessing as mp
+        p = mp.get_context("fork").Pool(workers)
+        try:
+            pairs = p.map(png_pair, jobs, chunksize=1)
+        finally:
+            p.close()
+            p.join()
+    else:
+        pairs = [png_pair(j) for j in jobs]
+    out = []
+    for img, mask in pairs:
+        out += [img, mask]
+    return out
 
 
 # ------------------------------------------------------------- roofline
@@ -188,20 +275,28 @@ def main() -> int:
     lo, hi = get_data_slice_multirank(a.pool * world, rank, world)
     workers = a.workers or cpu_share()
     t_gen = time.perf_counter()
-    spec_seed = 2  # BASELINE configs[1] seed
-    pool = synth.mixed_corpus(spec_seed, a.pool * world, a.short_min, a.short_max, workers=workers, lo=lo, hi=hi)
+    png = a.workload == "png"
+    if png:  # configs[4]: pairs (image, mask), seed 5; a.pool counts images (2 per pair)
+        npair = max(1, a.pool // 2)
+        plo, phi = get_data_slice_multirank(npair * world, rank, world)
+        pool = png_corpus(5, npair * world, a.short_min, a.short_max, workers, plo, phi)
+    else:
+        spec_seed = 2  # BASELINE configs[1] seed
+        pool = synth.mixed_corpus(spec_seed, a.pool * world, a.short_min, a.short_max, workers=workers, lo=lo,
+                                  hi=hi)
     t_gen = time.perf_counter() - t_gen
     torch.cuda.set_device(local)
     tr = B.ARAwareTransform(a.size, a.ratio, 0.5, 2.0)
-    dims = []
-    from oracle import oracle as O
-    for d in pool:
-        st, w, h, nc = O.jpeg_info(d)
-        dims.append((w, h, nc))
-    targets = [tr.target_size(w, h) for (w, h, _) in dims]
-
+    dims = [image_dims(d) for d in pool]
     ctx = L.Context(local, crop_and_resize=True, default_image_size=a.size, downsampling_ratio=a.ratio,
                     min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+    # multi-payload alignment (worker_wds.rs:68-76, worker_http.rs:186-214): every
+    # payload after the first of a sample takes the first one's bucket
+    forced_pool = [-1] * len(pool)
+    if png:
+        for i in range(1, len(pool), 2):
+            forced_pool[i] = ctx.buckets.closest(dims[i - 1][0], dims[i - 1][1])
+    targets = [tr.target_size(w, h) if f < 0 else ctx.buckets.get(f)[:2] for (w, h, _), f in zip(dims, forced_pool)]
     if a.sub_bits:
         ctx.set_option("sub_bits", a.sub_bits)
     if a.lead_bits >= 0:
@@ -220,7 +315,8 @@ def main() -> int:
     ctx.h2d(d_arena, host_arena)
     h_base = host_arena.ctypes.data
     out_bytes = [tw * th * nc for (tw, th), (_, _, nc) in zip(targets, dims)]
-    img_stage_bytes = [stage_bytes(L, d, dim, tgt) for d, dim, tgt in zip(pool, dims, targets)]
+    img_stage_bytes = [(png_stage_bytes if png else stage_bytes)(*((d, dim, tgt) if png else (L, d, dim, tgt)))
+                       for d, dim, tgt in zip(pool, dims, targets)]
     B_ = min(a.batch, 1 << 16)
     # output arena for one step (reused), sized for the largest B_ outputs
     out_cap = sum(sorted(out_bytes)[-B_:]) + 16 * B_
@@ -237,7 +333,7 @@ def main() -> int:
             outs.append(d_out[slot] + oo)
             caps.append(out_bytes[i])
             oo += (out_bytes[i] + 15) // 16 * 16
-        ticket, metas = ctx.submit_device(hp, dp, lens, outs, caps)
+        ticket, metas = ctx.submit_device(hp, dp, lens, outs, caps, [forced_pool[i] for i in idx])
         return ticket, metas, idx
 
     def complete(pend):
@@ -318,7 +414,7 @@ def main() -> int:
         e2e_px = 0
         for k in range(a.e2e_steps):
             idx = [(k * B_ + j) % len(pool) for j in range(B_)]
-            res = ctx.decode_batch([pool[i] for i in idx])
+            res = ctx.decode_batch([pool[i] for i in idx], [forced_pool[i] for i in idx])
             e2e_px += sum(dims[i][0] * dims[i][1] for i, r in zip(idx, res) if r[0] == 0)
         e2e = e2e_px / (time.perf_counter() - t1) / 1e6
 
@@ -353,7 +449,8 @@ def main() -> int:
                    "stages_alg_GBs": {k: round(ser_alg[k] / ser_n / (v / 1e3) / 1e9, 1)
                                       for k, v in skern.items() if ser_alg.get(k) and v > 0}}
         result = {
-            "metric": "Mpixel/s device-resident JPEG decode+bucket-resize at 1/2/4/8 MI355X",
+            "metric": ("Mpixel/s device-resident JPEG decode+bucket-resize at 1/2/4/8 MI355X" if not png else
+                       "Mpixel/s device-resident PNG decode+bucket-resize (image + aligned mask pairs)"),
             "value": round(px_all / dt_max / 1e6, 2),
             "unit": "Mpixel/s",
             "n_gpus": world,
@@ -364,9 +461,12 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": f"synthetic (seeded PIL JPEG pool of {a.pool} unique images per rank, cycled)",
-            "config": {"workload": "configs[1]: file-source JPEGs, mixed aspect ratios, decode + bucket + "
-                                   "crop/resize to 1024/32 buckets",
+            "data": (f"synthetic (seeded PIL JPEG pool of {a.pool} unique images per rank, cycled)" if not png else
+                     f"synthetic (seeded PIL PNG pool of {len(pool) // 2} RGB image + L8 mask pairs per rank, cycled)"),
+            "config": {"workload": ("configs[1]: file-source JPEGs, mixed aspect ratios, decode + bucket + "
+                                    "crop/resize to 1024/32 buckets") if not png else
+                                   ("configs[4] without re-encode: RGB PNG (PIL, zlib 6) + L8 mask PNG pairs, "
+                                    "mask aligned to the image's bucket, decode + crop/resize to 1024/32"),
                        "images_per_step": B_, "pool_per_rank": a.pool,
                        "short_side": [a.short_min, a.short_max], "buckets": f"{a.size}/{a.ratio}/0.5/2.0",
                        "parallelism": f"dp{world} (sample shards, no collectives)"},
@@ -395,6 +495,9 @@ def main() -> int:
         }
         if world == 1 and not a.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(pool, targets, a.cpu_seconds)
+        if png:  # the PMC file is for the JPEG workload
+            result["roofline"]["traffic"] = None
+            result["roofline"]["traffic_source"] = None
         else:
             result["cpu_baseline"] = None
         line = json.dumps(result)

@@ -229,6 +229,7 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
   const WgItem it = list[blockIdx.x];
   ImageDesc &im = imgs[it.image];
   const PngDesc &pd = im.png;
+  if (pd.nchunks && !pd.serial) return;  // the chunk-parallel path produced this image
   const uint32_t lane = threadIdx.x;
   const DG_GLOBAL uint32_t *z = gp<const uint32_t>(pd.zs);
   DG_GLOBAL uint8_t *out = gp<uint8_t>(pd.raw);
@@ -470,6 +471,525 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
   if (status && lane == 0) im.status = status;
 }
 
+// ------------------------------------------------------------ chunked inflate
+
+// Bits [pos, pos + n) of the stream (n <= 32), LSB-first; zero past the end.
+__device__ __forceinline__ uint32_t zbits(const DG_GLOBAL uint32_t *z, uint32_t zwords, uint32_t pos, uint32_t n) {
+  const uint32_t w = pos >> 5, sh = pos & 31u;
+  const uint64_t lo = w < zwords ? z[w] : 0u, hi = w + 1 < zwords ? z[w + 1] : 0u;
+  const uint64_t v = (lo | (hi << 32)) >> sh;
+  return n >= 32 ? (uint32_t)v : (uint32_t)v & ((1u << n) - 1u);
+}
+
+// Does a dynamic-Huffman block header with valid, complete codes start at bit
+// `pos`?  (The checks zlib's inflate applies: HLIT <= 29, HDIST <= 29, a
+// complete code-length code, a well-formed run of code lengths, an
+// end-of-block code, complete literal/length and distance codes (a single
+// distance code is allowed).)  Per lane, serial; the cheap tests reject
+// almost every position within a few instructions.
+__device__ bool inf_header_ok(const DG_GLOBAL uint32_t *z, uint32_t zwords, uint32_t pos) {
+  // the 17-bit header and up to 19 x 3 code-length bits (74 bits) from 4 words
+  const uint32_t w = pos >> 5, sh = pos & 31u;
+  uint32_t q[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) q[k] = w + k < zwords ? z[w + k] : 0u;
+  const uint64_t a = (uint64_t)q[0] | ((uint64_t)q[1] << 32), b = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
+  const uint64_t lo = sh ? (a >> sh) | (b << (64 - sh)) : a, hi = b >> sh;  // bits [pos, pos + 96)
+  const uint32_t h = (uint32_t)lo & 0x1FFFFu;
+  if (((h >> 1) & 3u) != 2u) return false;
+  const uint32_t nlen = ((h >> 3) & 31u) + 257, ndist = ((h >> 8) & 31u) + 1, ncode = ((h >> 13) & 15u) + 4;
+  if (nlen > 286 || ndist > 30) return false;
+  // code-length code: lengths of up to 19 symbols, 3 bits each, in c_clorder
+  uint32_t clcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t cll = 0;  // 3-bit length of symbol s at bits 3s
+  const uint64_t clbits = (lo >> 17) | (hi << 47);  // bits [pos + 17, pos + 81)
+  for (uint32_t i = 0; i < ncode; i++) {
+    const uint32_t l = (uint32_t)(clbits >> (3 * i)) & 7u;
+    cll |= (uint64_t)l << (3 * c_clorder[i]);
+  }
+  pos += 17 + 3 * ncode;
+  for (uint32_t s = 0; s < 19; s++) {
+    const uint32_t l = (uint32_t)(cll >> (3 * s)) & 7u;
+#pragma unroll
+    for (uint32_t k = 1; k < 8; k++) clcnt[k] += l == k ? 1u : 0u;
+  }
+  int left = 1;
+  uint32_t first[8], offs[8], o = 0, code = 0;
+#pragma unroll
+  for (uint32_t k = 1; k < 8; k++) {
+    left = 2 * left - (int)clcnt[k];
+    if (left < 0) return false;
+    code = (code + (k > 1 ? clcnt[k - 1] : 0u)) << 1;
+    first[k] = k == 1 ? 0u : code;
+    offs[k] = o;
+    o += clcnt[k];
+  }
+  if (left != 0) return false;  // incomplete code-length code
+  // decode the code lengths, counting the litlen / distance codes as we go
+  uint32_t lcnt[16], dcnt[16];
+#pragma unroll
+  for (uint32_t k = 0; k < 16; k++) lcnt[k] = dcnt[k] = 0;
+  uint32_t i = 0, prev = 0, eob = 0;
+  const uint32_t total = nlen + ndist;
+  while (i < total) {
+    // bit-serial canonical decode of the code-length code (max 7 bits)
+    const uint32_t bitsv = zbits(z, zwords, pos, 7);
+    uint32_t sym = 99, len = 0, c = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < 8; k++) {
+      c = (c << 1) | ((bitsv >> (k - 1)) & 1u);
+      if (len == 0 && c - first[k] < clcnt[k]) {
+        len = k;
+        sym = offs[k] + (c - first[k]);  // rank among codes: resolve to symbol below
+      }
+    }
+    if (!len) return false;
+    // rank -> symbol (symbols of equal length in increasing order)
+    uint32_t r = sym, found = 99;
+    for (uint32_t s = 0; s < 19 && found == 99; s++) {
+      if (((uint32_t)(cll >> (3 * s)) & 7u) == len) {
+        if (r == offs[len]) found = s;
+        r--;
+      }
+    }
+    // r counts down from the rank: the symbol is the (rank - offs)th of its length
+    pos += len;
+    uint32_t v = 0, rep = 1;
+    if (found < 16) {
+      v = found;
+    } else if (found == 16) {
+      if (i == 0) return false;
+      v = prev;
+      rep = 3 + zbits(z, zwords, pos, 2);
+      pos += 2;
+    } else if (found == 17) {
+      rep = 3 + zbits(z, zwords, pos, 3);
+      pos += 3;
+    } else if (found == 18) {
+      rep = 11 + zbits(z, zwords, pos, 7);
+      pos += 7;
+    } else {
+      return false;
+    }
+    if (i + rep > total) return false;
+    for (uint32_t k = 0; k < rep; k++, i++) {
+      if (i < nlen) {
+#pragma unroll
+        for (uint32_t q = 1; q < 16; q++) lcnt[q] += v == q ? 1u : 0u;
+        if (i == 256 && v) eob = 1;
+      } else {
+#pragma unroll
+        for (uint32_t q = 1; q < 16; q++) dcnt[q] += v == q ? 1u : 0u;
+      }
+    }
+    prev = v;
+  }
+  if (!eob) return false;
+  int ll = 1, dl = 1;
+  uint32_t dn = 0;
+#pragma unroll
+  for (uint32_t q = 1; q < 16; q++) {
+    ll = 2 * ll - (int)lcnt[q];
+    dl = 2 * dl - (int)dcnt[q];
+    dn += dcnt[q];
+    if (ll < 0 || dl < 0) return false;
+  }
+  if (ll != 0) return false;
+  if (dl != 0 && !(dn == 1 && dcnt[1] == 1) && dn != 0) return false;
+  return true;
+}
+
+// One wave per chunk (but chunk 0): the first candidate block start in the
+// chunk's bit range, 64 consecutive bit positions per step.
+__global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
+                                                 const WgItem *__restrict__ list) {
+  const WgItem it = list[blockIdx.x];
+  InfChunk &c = ch[it.image];
+  const ImageDesc &im = imgs[c.image];
+  const DG_GLOBAL uint32_t *z = gp<const uint32_t>(im.png.zs);
+  const uint32_t zlen = im.png.zlen, zwords = (zlen + 3) / 4;
+  const uint32_t b0 = c.idx * kInfChunk * 8u;
+  const uint32_t b1 = min((c.idx + 1) * kInfChunk * 8u, zlen * 8u);
+  uint32_t found = kInfNone;
+  for (uint32_t p = b0; p < b1; p += 64) {
+    const uint32_t pos = p + threadIdx.x;
+    const bool ok = pos < b1 && inf_header_ok(z, zwords, pos);
+    const uint64_t m = __ballot(ok);
+    if (m) {
+      found = p + (uint32_t)__ffsll((long long)m) - 1u;
+      break;
+    }
+  }
+  if (threadIdx.x == 0) c.start = found;
+}
+
+// Per-lane canonical table in global scratch: lut[1 << B] = (sym << 4) | len
+// for codes of <= B bits, 0 for long-code prefixes / unused entries (then the
+// bit-serial walk over cnt/offs/sym); cnt/offs/sym as in puff.c.
+struct LaneTab {
+  DG_GLOBAL uint16_t *lut;
+  DG_GLOBAL uint16_t *cnt;   // [16]
+  DG_GLOBAL uint16_t *offs;  // [16]
+  DG_GLOBAL uint16_t *sym;   // [n]
+  uint32_t B;
+};
+
+__device__ bool lane_build(const DG_GLOBAL uint8_t *lens, uint32_t n, LaneTab t) {
+  uint32_t cnt[16];
+#pragma unroll
+  for (uint32_t k = 0; k < 16; k++) cnt[k] = 0;
+  for (uint32_t s = 0; s < n; s++) {
+    const uint32_t l = lens[s];
+#pragma unroll
+    for (uint32_t k = 1; k < 16; k++) cnt[k] += l == k ? 1u : 0u;
+  }
+  int left = 1;
+  uint32_t next[16], o = 0, code = 0;
+#pragma unroll
+  for (uint32_t k = 1; k < 16; k++) {
+    left = 2 * left - (int)cnt[k];
+    code = (code + (k > 1 ? cnt[k - 1] : 0u)) << 1;
+    next[k] = k == 1 ? 0u : code;
+    t.cnt[k] = (uint16_t)cnt[k];
+    t.offs[k] = (uint16_t)o;
+    o += cnt[k];
+  }
+  if (left < 0) return false;
+  if (left > 0)  // incomplete: unused prefixes must read as invalid
+    for (uint32_t e = 0; e < (1u << t.B); e++) t.lut[e] = 0;
+  uint32_t pos[16];
+#pragma unroll
+  for (uint32_t k = 1; k < 16; k++) pos[k] = t.offs[k];
+  for (uint32_t s = 0; s < n; s++) {
+    const uint32_t l = lens[s];
+    if (!l) continue;
+    uint32_t cd = 0, ps = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < 16; k++)
+      if (l == k) {
+        cd = next[k]++;
+        ps = pos[k]++;
+      }
+    t.sym[ps] = (uint16_t)s;
+    const uint32_t rv = __builtin_bitreverse32(cd) >> (32 - l);
+    if (l <= t.B) {
+      const uint16_t e = (uint16_t)((s << 4) | l);
+      for (uint32_t x = rv; x < (1u << t.B); x += 1u << l) t.lut[x] = e;
+    } else {
+      t.lut[rv & ((1u << t.B) - 1u)] = 0;  // long code: its B-bit prefix takes the slow path
+    }
+  }
+  return true;
+}
+
+struct LaneBits {
+  uint64_t bb;
+  uint32_t nb, wp, zwords;
+  uint32_t w1;  // next word, loaded one refill ahead
+};
+
+__device__ __forceinline__ void lb_refill(LaneBits &r, const DG_GLOBAL uint32_t *z) {
+  if (r.nb < 32) {
+    r.bb |= (uint64_t)r.w1 << r.nb;
+    r.nb += 32;
+    r.wp++;
+    r.w1 = r.wp < r.zwords ? z[r.wp] : 0u;
+  }
+}
+__device__ __forceinline__ uint32_t lb_get(LaneBits &r, uint32_t k) {
+  const uint32_t v = (uint32_t)r.bb & ((1u << k) - 1u);
+  r.bb >>= k;
+  r.nb -= k;
+  return v;
+}
+// consumed bit position: wp counts the word held in w1
+__device__ __forceinline__ uint32_t lb_pos(const LaneBits &r) { return r.wp * 32u - r.nb; }
+
+__device__ __forceinline__ uint32_t lane_sym(LaneBits &r, const LaneTab &t) {
+  const uint32_t peek = (uint32_t)r.bb;
+  const uint32_t e = t.lut[peek & ((1u << t.B) - 1u)];
+  if (e & 15u) {
+    const uint32_t l = e & 15u;
+    r.bb >>= l;
+    r.nb -= l;
+    return e >> 4;
+  }
+  const uint32_t rv = __builtin_bitreverse32(peek);
+  uint32_t first = 0, index = 0, code = 0;
+  for (uint32_t L = 1; L < 16; L++) {
+    code = rv >> (32 - L);
+    const uint32_t c = t.cnt[L];
+    if (code - first < c) {
+      r.bb >>= L;
+      r.nb -= L;
+      return t.sym[index + code - first];
+    }
+    index += c;
+    first = (first + c) << 1;
+  }
+  return 0xFFFFu;
+}
+
+// One lane per chunk: decode from the chunk's candidate block start until a
+// block ends exactly where a later chunk's candidate starts (or the stream
+// ends), writing uint16 entries: bytes, or 256 + window index for bytes that
+// lie before the chunk (resolved by k_inf_resolve).
+__global__ __launch_bounds__(64) void k_inf_decode(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
+                                                   uint32_t nch) {
+  const uint32_t gi = blockIdx.x * 64 + threadIdx.x;
+  if (gi >= nch) return;
+  InfChunk &c = ch[gi];
+  c.len = 0;
+  c.status = 0;
+  const ImageDesc &im = imgs[c.image];
+  const PngDesc &pd = im.png;
+  const uint32_t n = pd.nchunks;
+  c.stop = n;
+  if (c.start == kInfNone) return;
+  const InfChunk *img_ch = ch + pd.chunk0;
+  const DG_GLOBAL uint32_t *z = gp<const uint32_t>(pd.zs);
+  DG_GLOBAL uint16_t *out = gp<uint16_t>(c.out);
+  DG_GLOBAL uint8_t *tb = gp<uint8_t>(c.tab);
+  DG_GLOBAL uint8_t *lens = tb + 3584;
+  LaneTab tl{(DG_GLOBAL uint16_t *)tb, (DG_GLOBAL uint16_t *)(tb + 2560), (DG_GLOBAL uint16_t *)(tb + 2592),
+             (DG_GLOBAL uint16_t *)(tb + 2624), 10};
+  LaneTab td{(DG_GLOBAL uint16_t *)(tb + 2048), (DG_GLOBAL uint16_t *)(tb + 3200), (DG_GLOBAL uint16_t *)(tb + 3232),
+             (DG_GLOBAL uint16_t *)(tb + 3264), 8};
+  LaneTab tc{(DG_GLOBAL uint16_t *)(tb + 3328), (DG_GLOBAL uint16_t *)(tb + 3456), (DG_GLOBAL uint16_t *)(tb + 3488),
+             (DG_GLOBAL uint16_t *)(tb + 3520), 6};
+  const uint32_t zbits_total = pd.zlen * 8u;
+  LaneBits r;
+  r.zwords = (pd.zlen + 3) / 4;
+  {
+    const uint32_t p = c.start;
+    r.wp = p >> 5;
+    r.bb = 0;
+    r.nb = 0;
+    r.w1 = r.wp < r.zwords ? z[r.wp] : 0u;
+    lb_refill(r, z);
+    lb_get(r, p & 31u);
+  }
+  const uint32_t cap = c.cap;
+  const bool first_chunk = c.idx == 0;
+  uint32_t q = 0;  // entries produced
+  uint32_t nxt = c.idx + 1;
+  uint32_t status = 0;
+  for (;;) {
+    // block boundary: stop if a later chunk starts exactly here
+    const uint32_t bp = lb_pos(r);
+    while (nxt < n && (img_ch[nxt].start == kInfNone || img_ch[nxt].start < bp)) nxt++;
+    if (nxt < n && img_ch[nxt].start == bp && bp != c.start) {
+      c.stop = nxt;
+      break;
+    }
+    if (bp > zbits_total) {
+      status = 1;
+      break;
+    }
+    lb_refill(r, z);
+    const uint32_t last = lb_get(r, 1), type = lb_get(r, 2);
+    if (type == 3) {
+      status = 1;
+      break;
+    }
+    if (type == 0) {
+      lb_get(r, r.nb & 7u);
+      lb_refill(r, z);
+      const uint32_t len = lb_get(r, 16), nlen = lb_get(r, 16);
+      if ((len ^ 0xFFFFu) != nlen) {
+        status = 1;
+        break;
+      }
+      const uint32_t bpos = lb_pos(r) / 8u;
+      if (bpos + len > pd.zlen || q + len > cap) {
+        status = bpos + len > pd.zlen ? 1u : 2u;
+        break;
+      }
+      const DG_GLOBAL uint8_t *zb = (const DG_GLOBAL uint8_t *)z;
+      for (uint32_t j = 0; j < len; j++) out[q + j] = zb[bpos + j];
+      q += len;
+      const uint32_t np = (bpos + len) * 8u;
+      r.wp = np >> 5;
+      r.bb = 0;
+      r.nb = 0;
+      r.w1 = r.wp < r.zwords ? z[r.wp] : 0u;
+      lb_refill(r, z);
+      lb_get(r, np & 31u);
+      if (last) break;
+      continue;
+    }
+    if (type == 1) {
+      for (uint32_t s = 0; s < 320; s++) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+      lane_build(lens, 288, tl);
+      lane_build(lens + 288, 30, td);
+    } else {
+      lb_refill(r, z);
+      const uint32_t nlen = lb_get(r, 5) + 257, ndist = lb_get(r, 5) + 1, ncode = lb_get(r, 4) + 4;
+      if (nlen > 286 || ndist > 30) {
+        status = 1;
+        break;
+      }
+      for (uint32_t s = 0; s < 19; s++) lens[s] = 0;
+      for (uint32_t i = 0; i < ncode; i++) {
+        lb_refill(r, z);
+        lens[c_clorder[i]] = (uint8_t)lb_get(r, 3);
+      }
+      if (!lane_build(lens, 19, tc)) {
+        status = 1;
+        break;
+      }
+      uint32_t i = 0, prev = 0;
+      const uint32_t total = nlen + ndist;
+      while (i < total && !status) {
+        lb_refill(r, z);
+        const uint32_t s = lane_sym(r, tc);
+        uint32_t v = s, rep = 1;
+        if (s < 16) {
+        } else if (s == 16 && i > 0) {
+          v = prev;
+          rep = 3 + lb_get(r, 2);
+        } else if (s == 17) {
+          v = 0;
+          rep = 3 + lb_get(r, 3);
+        } else if (s == 18) {
+          v = 0;
+          rep = 11 + lb_get(r, 7);
+        } else {
+          status = 1;
+          break;
+        }
+        if (i + rep > total) {
+          status = 1;
+          break;
+        }
+        // litlen lengths at [0, nlen), distance lengths at [288, 288 + ndist)
+        for (uint32_t k = 0; k < rep; k++, i++) lens[i < nlen ? i : 288 + (i - nlen)] = (uint8_t)v;
+        prev = v;
+      }
+      if (status) break;
+      if (lens[256] == 0 || !lane_build(lens, nlen, tl) || !lane_build(lens + 288, ndist, td)) {
+        status = 1;
+        break;
+      }
+    }
+    // symbols of the block
+    for (;;) {
+      lb_refill(r, z);
+      const uint32_t s = lane_sym(r, tl);
+      if (s < 256) {
+        if (q >= cap) {
+          status = 2;
+          break;
+        }
+        out[q++] = (uint16_t)s;
+        continue;
+      }
+      if (s == 256) break;
+      if (s > 285) {
+        status = 1;
+        break;
+      }
+      const uint32_t len = c_lbase[s - 257] + lb_get(r, c_lext[s - 257]);
+      lb_refill(r, z);
+      const uint32_t ds = lane_sym(r, td);
+      if (ds >= 30) {
+        status = 1;
+        break;
+      }
+      lb_refill(r, z);
+      const uint32_t dist = c_dbase[ds] + lb_get(r, c_dext[ds]);
+      if (q + len > cap) {
+        status = 2;
+        break;
+      }
+      if (dist > q && first_chunk) {
+        status = 1;
+        break;
+      }
+      // sources lie before q: entries of this chunk, or markers into the
+      // window before it (256 + 32768 + (src - 0) for src < 0)
+      int32_t src = (int32_t)q - (int32_t)dist;
+      const int32_t s0 = src;
+      uint32_t j = 0;
+      for (; j + 4 <= len; j += 4) {
+        uint16_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int32_t sp = s0 + (int32_t)((dist >= len) ? (j + u) : ((j + u) % dist));
+          v[u] = sp >= 0 ? out[sp] : (uint16_t)(256 + 32768 + sp);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) out[q + j + u] = v[u];
+      }
+      for (; j < len; j++) {
+        const int32_t sp = s0 + (int32_t)((dist >= len) ? j : (j % dist));
+        out[q + j] = sp >= 0 ? out[sp] : (uint16_t)(256 + 32768 + sp);
+      }
+      (void)src;
+      q += len;
+    }
+    if (status) break;
+    if (last) break;
+  }
+  c.len = q;
+  c.status = status;
+}
+
+// One workgroup per chunked image: walk the chain of chunks the decode made
+// consistent, resolving each chunk's entries into the scanline buffer in
+// order (a chunk's markers read the 32 KiB written just before it).
+__global__ __launch_bounds__(1024) void k_inf_resolve(ImageDesc *__restrict__ imgs, const InfChunk *__restrict__ ch,
+                                                      const WgItem *__restrict__ list) {
+  const WgItem it = list[blockIdx.x];
+  ImageDesc &im = imgs[it.image];
+  PngDesc &pd = im.png;
+  const uint32_t want = im.height * (pd.rowbytes + 1u);
+  DG_GLOBAL uint8_t *raw = gp<uint8_t>(pd.raw);
+  const InfChunk *c0 = ch + pd.chunk0;
+  uint32_t k = 0, P = 0;
+  bool bad = false;
+  while (k < pd.nchunks && P < want) {
+    const InfChunk &c = c0[k];
+    if (c.status || c.start == kInfNone) {
+      bad = true;
+      break;
+    }
+    const DG_GLOBAL uint16_t *e = gp<const uint16_t>(c.out);
+    const uint32_t n = min(c.len, want - P);
+    uint32_t oob = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) {
+      const uint32_t v = e[i];
+      uint8_t b;
+      if (v < 256) {
+        b = (uint8_t)v;
+      } else {
+        const int64_t sp = (int64_t)P - 32768 + (int64_t)(v - 256);
+        if (sp < 0) {
+          oob = 1;
+          b = 0;
+        } else {
+          b = raw[sp];
+        }
+      }
+      raw[P + i] = b;
+    }
+    if (__syncthreads_or(oob)) {
+      bad = true;
+      break;
+    }
+    __threadfence();
+    __syncthreads();
+    P += n;
+    if (c.stop <= k) {  // cannot go backwards
+      bad = true;
+      break;
+    }
+    k = c.stop;
+  }
+  if (P < want) bad = true;
+  if (bad && threadIdx.x == 0) pd.serial = 1;
+}
+
 // ------------------------------------------------------------ unfilter
 
 // One wave per image.  Rows are taken 64 at a time, lane l owning row y0 + l,
@@ -489,80 +1009,189 @@ __device__ __forceinline__ uint32_t shfl_up1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((threadIdx.x + 63u) & 63u) << 2), (int)v);
 }
 
-__global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
-  const WgItem it = list[blockIdx.x];
-  ImageDesc &im = imgs[it.image];
+// The band's raw bytes are staged through LDS in tiles of kUfTile filter
+// units x 64 rows (coalesced loads; the diagonal then reads and writes LDS
+// only), three tiles in flight: lane 0 enters tile k while lanes 1..63 finish
+// tile k-1; tile k-2 is complete, is stored to HBM, and its buffer receives
+// tile k+1.  Each lane takes kUfU units per step (lane l at step t owns units
+// kUfU*(t-l) ..), so one shuffle round trip serves kUfU units.
+constexpr uint32_t kUfU = 2;
+constexpr uint32_t kUfTile = 64 * kUfU;
+constexpr uint32_t kUfPitch = kUfTile * 4 + 4;  // bytes per tile row (bpp <= 4) + dword misalignment; 129 words: lane rows on distinct banks
+
+struct UnfilterSmem {
+  uint8_t tile[3][64][kUfPitch];
+  uint8_t prow[3][kUfPitch];  // row y0 - 1 (the previous band's last), per tile
+};
+
+template <uint32_t BPP>
+__device__ __forceinline__ uint32_t unfilter_unit(uint32_t f, uint32_t rawv, uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < BPP; k++) {
+    const uint32_t sh = 8 * k;
+    const uint32_t ak = (a >> sh) & 0xFFu, bk = (b >> sh) & 0xFFu, ck = (c >> sh) & 0xFFu;
+    const uint32_t pr = f == 0 ? 0u : f == 1 ? ak : f == 2 ? bk : f == 3 ? (ak + bk) >> 1 : paeth_b(ak, bk, ck);
+    v |= ((((rawv >> sh) & 0xFFu) + pr) & 0xFFu) << sh;
+  }
+  return v;
+}
+
+template <uint32_t BPP>
+__device__ void unfilter_image(UnfilterSmem &sm, ImageDesc &im) {
   const PngDesc &pd = im.png;
-  if (im.status) return;
   const uint32_t lane = threadIdx.x;
-  const uint32_t rb = pd.rowbytes, bpp = pd.bpp, us = pd.ustride, H = im.height;
-  const uint32_t units = (rb + bpp - 1) / bpp;  // rowbytes is a multiple of bpp for 8-bit samples
+  const uint32_t rb = pd.rowbytes, us = pd.ustride, H = im.height;
+  const uint32_t units = rb / BPP;  // BPP == 1 covers sub-byte samples (filter unit = 1 byte)
+  const uint32_t tb = kUfTile * BPP;
+  const uint32_t ntiles = (units + kUfTile - 1) / kUfTile;
   const DG_GLOBAL uint8_t *raw = gp<const uint8_t>(pd.raw);
   DG_GLOBAL uint8_t *unf = gp<uint8_t>(pd.unf);
   int bad = 0;
   for (uint32_t y0 = 0; y0 < H; y0 += 64) {
-    const uint32_t y = y0 + lane;
-    const bool active = y < H;
-    const DG_GLOBAL uint8_t *r = raw + (size_t)y * (rb + 1);
-    DG_GLOBAL uint8_t *o = unf + (size_t)y * us;
-    const DG_GLOBAL uint8_t *prow = y > 0 ? unf + (size_t)(y - 1) * us : nullptr;
-    uint32_t f = active ? r[0] : 0u;
+    const uint32_t nrows = H - y0 < 64 ? H - y0 : 64;
+    const bool active = lane < nrows;
+    uint32_t f = active ? raw[(size_t)(y0 + lane) * (rb + 1)] : 0u;
     if (f > 4) {
       bad = 1;
       f = 0;
     }
-    r++;
-    uint32_t cur = 0, prev = 0, prev2 = 0;  // results of steps t, t-1, t-2 (packed bytes)
-    const uint32_t nsteps = units + 63;
-    for (uint32_t t = 0; t < nsteps; t++) {
-      // neighbour row: lane l-1's results of steps t-1 (above) and t-2 (above-left)
-      uint32_t up = shfl_up1(prev), ul = shfl_up1(prev2);
-      const int32_t x = (int32_t)t - (int32_t)lane;
-      if (active && x >= 0 && (uint32_t)x < units) {
-        const uint32_t b0 = (uint32_t)x * bpp;
-        if (lane == 0) {  // previous band's last row comes from memory
-          up = 0;
-          ul = 0;
-          if (prow) {
-            for (uint32_t k = 0; k < bpp; k++) up |= (uint32_t)prow[b0 + k] << (8 * k);
-            if (x > 0)
-              for (uint32_t k = 0; k < bpp; k++) ul |= (uint32_t)prow[b0 - bpp + k] << (8 * k);
-          }
-        } else if (y == 0) {
-          up = ul = 0;
-        }
-        if (x == 0) ul = 0;
-        const uint32_t left = x > 0 ? prev : 0u;
-        uint32_t v = 0;
-        for (uint32_t k = 0; k < bpp; k++) {
-          const uint32_t sh = 8 * k;
-          const uint32_t a = (left >> sh) & 0xFFu, b = (up >> sh) & 0xFFu, c = (ul >> sh) & 0xFFu;
-          uint32_t pr;
-          switch (f) {
-            case 0: pr = 0; break;
-            case 1: pr = a; break;
-            case 2: pr = b; break;
-            case 3: pr = (a + b) >> 1; break;
-            default: pr = paeth_b(a, b, c); break;
-          }
-          const uint32_t bx = b0 + k;
-          const uint32_t rv = bx < rb ? (uint32_t)r[bx] : 0u;
-          v |= ((rv + pr) & 0xFFu) << sh;
-        }
-        for (uint32_t k = 0; k < bpp; k++)
-          if (b0 + k < rb) o[b0 + k] = (uint8_t)(v >> (8 * k));
-        cur = v;
-      } else {
-        cur = 0;
+    // Tiles arrive by LDS-DMA (global_load_lds_dword, no VGPR round trip,
+    // retired by the vmcnt wait of the next tile boundary's barrier).  Raw
+    // rows are not dword aligned: each row lands whole-word aligned and the
+    // row's first byte sits at roff (0..3) in its LDS row.
+    const uint64_t rbase = pd.raw + (uint64_t)y0 * (rb + 1) + 1;
+    auto roff = [&](uint32_t r) { return (uint32_t)((rbase + (uint64_t)r * (rb + 1)) & 3u); };
+    auto load_tile = [&](uint32_t k) {
+      const uint32_t b0 = k * tb, nb = rb - b0 < tb ? rb - b0 : tb;
+      uint8_t(*T)[kUfPitch] = sm.tile[k % 3];
+      for (uint32_t r = 0; r < nrows; r++) {
+        const uint64_t a = rbase + (uint64_t)r * (rb + 1) + b0, a4 = a & ~(uint64_t)3;
+        const uint32_t nw = (uint32_t)((a - a4 + nb + 3) / 4);
+        for (uint32_t w0 = 0; w0 < nw; w0 += 64)
+          if (w0 + lane < nw)
+            __builtin_amdgcn_global_load_lds((const DG_GLOBAL void *)(uintptr_t)(a4 + 4ull * (w0 + lane)),
+                                             (__attribute__((address_space(3))) void *)(T[r] + 4 * w0), 4, 0, 0);
       }
-      prev2 = prev;
-      prev = cur;
+      if (y0) {
+        const uint64_t a = pd.unf + (uint64_t)(y0 - 1) * us + b0;
+        const uint32_t nw = (nb + 3) / 4;
+        for (uint32_t w0 = 0; w0 < nw; w0 += 64)
+          if (w0 + lane < nw)
+            __builtin_amdgcn_global_load_lds((const DG_GLOBAL void *)(uintptr_t)(a + 4ull * (w0 + lane)),
+                                             (__attribute__((address_space(3))) void *)(sm.prow[k % 3] + 4 * w0), 4,
+                                             0, 0);
+      } else {
+        for (uint32_t c = lane; c < nb; c += 64) sm.prow[k % 3][c] = 0;
+      }
+    };
+    auto store_tile = [&](uint32_t k) {
+      const uint32_t b0 = k * tb, nb = rb - b0 < tb ? rb - b0 : tb;
+      const uint32_t nw = (nb + 3) / 4;  // whole words: the tail lands in the row's stride padding
+      uint8_t(*T)[kUfPitch] = sm.tile[k % 3];
+      for (uint32_t r = 0; r < nrows; r++) {
+        DG_GLOBAL uint32_t *dst = (DG_GLOBAL uint32_t *)(unf + (size_t)(y0 + r) * us + b0);
+        const uint32_t o = roff(r);
+        const uint32_t *src = (const uint32_t *)T[r];
+        for (uint32_t c = lane; c < nw; c += 64) dst[c] = __builtin_amdgcn_alignbyte(src[c + 1], src[c], o);
+      }
+    };
+    const uint32_t myoff = roff(lane < nrows ? lane : 0);
+    load_tile(0);
+    if (ntiles > 1) load_tile(1);
+    uint32_t stored = 0;  // tiles [0, stored) are in HBM
+    __syncthreads();
+    uint32_t prev[kUfU], prev2 = 0;  // this lane's results of step t-1; last unit of step t-2
+#pragma unroll
+    for (uint32_t j = 0; j < kUfU; j++) prev[j] = 0;
+    const uint32_t nsteps = (units + kUfU - 1) / kUfU + 63;
+    for (uint32_t t = 0; t < nsteps; t++) {
+      if ((t & 63) == 0 && t > 0) {
+        const uint32_t k = t / 64;  // lane 0 enters tile k; tile k-2 is complete
+        if (k >= 2) {
+          store_tile(k - 2);
+          stored = k - 1;
+        }
+        if (k + 1 < ntiles) load_tile(k + 1);
+        __syncthreads();
+      }
+      const int32_t x0 = (int32_t)(kUfU * t) - (int32_t)(kUfU * lane);
+      // this step's raw samples (independent of the shuffles below)
+      uint32_t rawv[kUfU];
+      uint8_t *Tp[kUfU];
+#pragma unroll
+      for (uint32_t j = 0; j < kUfU; j++) {
+        const int32_t x = x0 + (int32_t)j;
+        const bool ok = active && x >= 0 && (uint32_t)x < units;
+        const uint32_t xx = ok ? (uint32_t)x : 0u;
+        Tp[j] = sm.tile[(xx / kUfTile) % 3][lane] + myoff + (xx % kUfTile) * BPP;
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < BPP; k++) v |= (uint32_t)Tp[j][k] << (8 * k);
+        rawv[j] = v;
+      }
+      // row above: lane l-1's units of step t-1; above-left of unit 0: its last unit of step t-2
+      uint32_t up[kUfU];
+#pragma unroll
+      for (uint32_t j = 0; j < kUfU; j++) up[j] = shfl_up1(prev[j]);
+      uint32_t ul0 = shfl_up1(prev2);
+      if (lane == 0 && x0 >= 0 && (uint32_t)x0 < units) {  // the previous band's last row
+#pragma unroll
+        for (uint32_t j = 0; j < kUfU; j++) {
+          const uint32_t x = (uint32_t)x0 + j < units ? (uint32_t)x0 + j : (uint32_t)x0;
+          const uint8_t *pr = sm.prow[(x / kUfTile) % 3] + (x % kUfTile) * BPP;
+          uint32_t v = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < BPP; k++) v |= (uint32_t)pr[k] << (8 * k);
+          up[j] = v;
+        }
+        ul0 = 0;
+        if (x0 > 0) {
+          const uint32_t x = (uint32_t)x0 - 1;
+          const uint8_t *pr = sm.prow[(x / kUfTile) % 3] + (x % kUfTile) * BPP;
+#pragma unroll
+          for (uint32_t k = 0; k < BPP; k++) ul0 |= (uint32_t)pr[k] << (8 * k);
+        }
+      }
+      uint32_t cur[kUfU];
+      uint32_t left = x0 > 0 ? prev[kUfU - 1] : 0u, ul = x0 > 0 ? ul0 : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < kUfU; j++) {
+        const int32_t x = x0 + (int32_t)j;
+        const bool ok = active && x >= 0 && (uint32_t)x < units;
+        const uint32_t v = unfilter_unit<BPP>(f, rawv[j], left, up[j], ul);
+        cur[j] = ok ? v : 0u;
+        if (ok) {
+#pragma unroll
+          for (uint32_t k = 0; k < BPP; k++) Tp[j][k] = (uint8_t)(v >> (8 * k));
+        }
+        left = v;
+        ul = up[j];
+      }
+      prev2 = prev[kUfU - 1];
+#pragma unroll
+      for (uint32_t j = 0; j < kUfU; j++) prev[j] = cur[j];
     }
-    // the next band's lane 0 reads this band's last row from memory
+    __syncthreads();
+    for (uint32_t k = stored; k < ntiles; k++) store_tile(k);
+    // the next band's tiles read this band's last row from HBM
     __threadfence();
     __syncthreads();
   }
   if (__ballot(bad) && lane == 0) im.status = 2;
+}
+
+__global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
+  __shared__ __attribute__((aligned(16))) UnfilterSmem sm;
+  const WgItem it = list[blockIdx.x];
+  ImageDesc &im = imgs[it.image];
+  if (im.status) return;
+  switch (im.png.bpp) {
+    case 1: unfilter_image<1>(sm, im); break;
+    case 2: unfilter_image<2>(sm, im); break;
+    case 3: unfilter_image<3>(sm, im); break;
+    default: unfilter_image<4>(sm, im); break;
+  }
 }
 
 // ------------------------------------------------------------ expand
@@ -669,6 +1298,15 @@ void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
   }
   if (nwg)
     hipLaunchKernelGGL(k_png_inflate, dim3(nwg), dim3(64), sizeof(InflateSmem), st, imgs, list);
+}
+void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg) {
+  if (nwg) hipLaunchKernelGGL(k_inf_find, dim3(nwg), dim3(64), 0, st, imgs, ch, list);
+}
+void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch) {
+  if (nch) hipLaunchKernelGGL(k_inf_decode, dim3((nch + 63) / 64), dim3(64), 0, st, imgs, ch, nch);
+}
+void launch_inf_resolve(hipStream_t st, ImageDesc *imgs, const InfChunk *ch, const WgItem *list, uint32_t nwg) {
+  if (nwg) hipLaunchKernelGGL(k_inf_resolve, dim3(nwg), dim3(1024), 0, st, imgs, ch, list);
 }
 void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_png_unfilter, dim3(nwg), dim3(64), 0, st, imgs, list);

@@ -130,8 +130,38 @@ struct PngDesc {
   uint32_t bpp;       // filter unit (bytes)
   uint32_t ctype, depth, expand, has_trns;
   uint32_t trns[3];   // gray / RGB transparency key
+  uint32_t chunk0;    // chunked inflate: first InfChunk of this image
+  uint32_t nchunks;   // 0: serial inflate (small streams)
+  uint32_t serial;    // set by the chunked path when the image must be inflated serially
+  uint32_t pad[2];
+};
+
+// Chunk-parallel inflate.  The zlib stream of a large PNG is cut into
+// kInfChunk-byte chunks.  k_inf_find looks in each chunk (but the first) for
+// the first bit position that parses as a dynamic-Huffman block header with
+// complete codes; k_inf_decode decodes, one lane per chunk, from there until
+// it reaches a block boundary that another chunk starts at (or the end).  A
+// match reaching before the chunk's start yields a marker (256 + index into
+// the 32 KiB window preceding the chunk); k_inf_resolve walks the chain of
+// chunks that the decode proved consistent and writes the bytes.  Anything
+// irregular (no candidate chain, overflow, a decode error) sends the image to
+// the serial inflate kernel.
+constexpr uint32_t kInfChunk = 32768;          // compressed bytes per chunk
+constexpr uint32_t kInfCapPerByte = 8;         // output entries per compressed byte of a chunk
+constexpr uint32_t kInfNone = 0xFFFFFFFFu;
+struct InfChunk {
+  uint64_t out;       // uint16 entries: byte value, or 256 + window index
+  uint64_t tab;       // per-chunk Huffman tables (k_inf_decode scratch)
+  uint32_t image;     // descriptor index
+  uint32_t idx;       // chunk index within the image
+  uint32_t cap;       // capacity of out (entries)
+  uint32_t start;     // bit position of the chunk's first block (kInfNone: no candidate)
+  uint32_t len;       // entries produced
+  uint32_t stop;      // chunk index whose start the decode reached (nchunks: end of stream)
+  uint32_t status;    // 0 ok, 1 decode error, 2 overflow
   uint32_t pad;
 };
+constexpr uint32_t kInfTabBytes = 4096;        // per-chunk table scratch (see k_inf_decode)
 // A gather job: copy `len` bytes (one IDAT payload) from src to dst.
 struct GatherJob {
   uint64_t src, dst;

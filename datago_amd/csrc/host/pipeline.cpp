@@ -177,6 +177,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     side_stream_ = v != 0;
     return DG_OK;
   }
+  if (k == "png_chunked") {  // 0: every PNG inflates serially (test switch)
+    chunked_off_ = v == 0;
+    return DG_OK;
+  }
   if (k == "debug_flags") {
     debug_flags_ = (int)v;
     return DG_OK;
@@ -199,6 +203,8 @@ int64_t Context::get_stat(const std::string &k) {
         if (k == std::string("wg_") + kn[a] + "_" + sn[q]) return (int64_t)(wgstat_[a][q] * 1000.0);
   }
   if (k == "sub_bits") return last_sub_bits_;
+  if (k == "png_serial_fallbacks") return stat_png_serial_;
+  if (k == "png_chunks") return stat_png_chunks_;
   if (k == "hpool") return (int64_t)hpool_.size();
   if (k == "qpool") return (int64_t)qpool_.size();
   return -1;
@@ -333,7 +339,8 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
     }
     // the decoder's working set (raw + unfiltered + expanded) must stay 32-bit addressable
     const uint64_t raw = (uint64_t)p.png.height * (p.png.rowbytes + 1ull);
-    if (raw >= (1ull << 31) || (uint64_t)p.png.width * p.png.height * 4ull >= (1ull << 31)) {
+    if (raw >= (1ull << 31) || (uint64_t)p.png.width * p.png.height * 4ull >= (1ull << 31) ||
+        p.png.zlen >= (1ull << 28)) {
       p.status = DG_ERR_UNSUPPORTED;
       return DG_OK;
     }
@@ -529,6 +536,31 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       for (int k = 0; k < 3; k++) pd.trns[k] = g.trns[k];
       pd.expand = g.ctype == 3 || g.depth < 8 || g.has_trns;
       o.zs = L.take((size_t)g.zlen + 64, 256);
+      // chunk-parallel inflate for streams of at least two chunks (small ones,
+      // e.g. masks, inflate serially in one wave)
+      {
+        const uint64_t want = (uint64_t)H * (g.rowbytes + 1ull);
+        const uint32_t nch = (uint32_t)((g.zlen + kInfChunk - 1) / kInfChunk);
+        if (nch >= 2 && !chunked_off_) {
+          pd.chunk0 = (uint32_t)b.ichunks.size();
+          pd.nchunks = nch;
+          // entries per chunk: 3x the image's average expansion (+64 Ki), at most the whole image;
+          // a chunk that needs more sends the image to the serial kernel
+          const double ratio = (double)want / (double)g.zlen;
+          const uint64_t cap = std::min<uint64_t>(want, (uint64_t)(3.0 * ratio * kInfChunk) + 65536);
+          for (uint32_t k = 0; k < nch; k++) {
+            InfChunk c;
+            memset(&c, 0, sizeof(c));
+            c.image = (uint32_t)b.descs.size();
+            c.idx = k;
+            c.cap = (uint32_t)cap;
+            c.start = k == 0 ? 16u : kInfNone;  // chunk 0: first block after the 2-byte zlib header
+            c.out = L.take(cap * 2, 256);       // offsets: made absolute below
+            c.tab = L.take(kInfTabBytes, 256);
+            b.ichunks.push_back(c);
+          }
+        }
+      }
       o.raw = L.take((size_t)H * (g.rowbytes + 1) + 16, 256);
       o.unf = L.take((size_t)H * pd.ustride, 256);
       if (pd.expand) {
@@ -791,6 +823,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   // ---- 4. patch device addresses
   char *S = (char *)sl.scratch.p;
+  for (InfChunk &c : b.ichunks) {
+    c.out = (uint64_t)(uintptr_t)(S + c.out);
+    c.tab = (uint64_t)(uintptr_t)(S + c.tab);
+  }
   int k = 0;
   for (int i = 0; i < n; i++) {
     if (b.desc_of[i] < 0) continue;
@@ -867,6 +903,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       }
     if (d.fmt == kFmtPng) {
       b.lists[L_PNG].push_back({I, 0});
+      if (d.png.nchunks) {
+        b.lists[L_INF_RES].push_back({I, 0});
+        for (uint32_t k = 1; k < d.png.nchunks; k++) b.lists[L_INF_FIND].push_back({d.png.chunk0 + k, 0});
+      }
       if (d.png.expand)
         for (uint32_t it = 0; it < d.width * d.height; it += 256) b.lists[L_EXPAND].push_back({I, it});
     } else {
@@ -917,6 +957,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.desc_off = M.take(b.descs.size() * sizeof(ImageDesc));
   for (int l = 0; l < L_COUNT; l++) b.list_off[l] = M.take(b.lists[l].size() * sizeof(WgItem));
   b.gjob_off = M.take(b.gjobs.size() * sizeof(GatherJob));
+  b.ichunk_off = M.take(b.ichunks.size() * sizeof(InfChunk));
   b.blob_off = M.take(b.blob.size());
   b.meta_bytes = M.off;
   st = ensure(sl.meta, b.meta_bytes + 256, sl.st);
@@ -940,6 +981,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   for (int l = 0; l < L_COUNT; l++)
     if (!b.lists[l].empty()) memcpy(P + b.list_off[l], b.lists[l].data(), b.lists[l].size() * sizeof(WgItem));
   if (!b.gjobs.empty()) memcpy(P + b.gjob_off, b.gjobs.data(), b.gjobs.size() * sizeof(GatherJob));
+  if (!b.ichunks.empty()) memcpy(P + b.ichunk_off, b.ichunks.data(), b.ichunks.size() * sizeof(InfChunk));
   if (!b.blob.empty()) memcpy(P + b.blob_off, b.blob.data(), b.blob.size());
   if (host_io) {
     for (int i = 0; i < n; i++)
@@ -988,7 +1030,13 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (next()) return DG_ERR_DEVICE;
   if (!from_fix && b.any_png) {
     launch_png_gather(sl.st, (const GatherJob *)(M + b.gjob_off), lst(L_GATHER), cnt(L_GATHER));
-    launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG));
+    if (!b.ichunks.empty()) {
+      InfChunk *ich = (InfChunk *)(M + b.ichunk_off);
+      launch_inf_find(sl.st, dd, ich, lst(L_INF_FIND), cnt(L_INF_FIND));
+      launch_inf_decode(sl.st, dd, ich, (uint32_t)b.ichunks.size());
+      launch_inf_resolve(sl.st, dm, ich, lst(L_INF_RES), cnt(L_INF_RES));
+    }
+    launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG));  // serial: small streams + fallbacks
   }
   if (next()) return DG_ERR_DEVICE;
   if (!from_fix && b.any_png) {
@@ -1116,6 +1164,10 @@ dg_status Context::finish(Slot &sl) {
   for (int i = 0; i < b.n; i++) {
     if (b.desc_of[i] < 0) continue;
     int status = back[b.desc_of[i]].status;
+    if (back[b.desc_of[i]].fmt == kFmtPng && back[b.desc_of[i]].png.nchunks) {
+      stat_png_chunks_ += back[b.desc_of[i]].png.nchunks;
+      stat_png_serial_ += back[b.desc_of[i]].png.serial ? 1 : 0;
+    }
     if (status) b.metas[i].status = status;
     if (b.host_io) {
       if (!status) memcpy(b.host_outs[i], (char *)sl.out.p + off, b.plans[i].out_bytes);

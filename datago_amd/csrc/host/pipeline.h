@@ -52,6 +52,8 @@ struct Batch {
   // PNG: IDAT gather jobs and palettes, uploaded with the descriptors
   std::vector<GatherJob> gjobs;
   size_t gjob_off = 0;
+  std::vector<InfChunk> ichunks;  // chunk-parallel inflate records (kernels fill start/len/stop/status)
+  size_t ichunk_off = 0;
   std::vector<uint8_t> blob;
   size_t blob_off = 0;
   bool any_png = false, any_alpha = false;
@@ -96,6 +98,7 @@ enum ListId {
   L_HUFF = 0, L_SYNC, L_DESTUFF, L_SCAN, L_IDCT, L_COLOR, L_COEF, L_RH0, L_RV1, L_RH2, L_RV3, L_COPY,
   L_RHX0, L_RHX2,  // H passes whose source segment is too wide for the band kernel
   L_GATHER, L_PNG, L_EXPAND, L_ALPHA0, L_ALPHA1, L_ALPHA2,  // PNG decode, alpha programs
+  L_INF_FIND, L_INF_RES,                                    // chunk-parallel inflate
   L_COUNT
 };
 
@@ -180,6 +183,8 @@ class Context {
   bool side_stream_ = true;
   int debug_flags_ = 0;
   bool wg_timing_ = false;
+  bool chunked_off_ = false;  // option "png_chunked" = 0
+  int64_t stat_png_serial_ = 0, stat_png_chunks_ = 0;
   // "wg_timing" summaries of the last batch (microseconds): per kernel {span, mean, p90, max}
   double wgstat_[2][4] = {{0}};
   // stats

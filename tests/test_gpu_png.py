@@ -194,3 +194,29 @@ def test_png_large_full_size_properties(ctx512):
     (st, arr, m), = ctx512.decode_batch([d])
     t = B.ARAwareTransform(512, 16, 0.5, 2.0)
     assert st == 0 and (arr.shape[1], arr.shape[0]) == t.target_size(1800, 1200)
+
+
+def test_chunked_inflate_matches_serial_and_oracle():
+    """Large streams take the chunk-parallel inflate (block-header search,
+    one lane per chunk, window markers); it must equal the oracle and the
+    serial kernel (option png_chunked=0) byte for byte."""
+    L = _lib()
+    rng = np.random.default_rng(31)
+    datas = []
+    for i, (w, h) in enumerate([(1500, 1000), (700, 2100), (2048, 600), (999, 777)]):
+        px = synth.synth_pixels(rng, w, h)
+        if i == 1:  # flat graphics: highly compressible, long matches
+            px = (px // 64) * 64
+        datas.append(synth.pil_png(px, compress_level=[6, 9, 1, 6][i]))
+    datas.append(synth.make_png(77, 1200, 900, "RGBA", level=6))
+    datas.append(synth.make_png(78, 1600, 1000, "L", level=6, filters="random"))
+    a = L.Context(0)
+    b = L.Context(0)
+    b.set_option("png_chunked", 0)
+    ra, rb = a.decode_batch(datas), b.decode_batch(datas)
+    for d, (sa, xa, _), (sb, xb, _) in zip(datas, ra, rb):
+        _, ref = O.png_decode(d)
+        assert sa == 0 and sb == 0
+        assert np.array_equal(xa, ref) and np.array_equal(xb, ref)
+    assert a.stat("png_chunks") > 0
+    print("chunks", a.stat("png_chunks"), "serial fallbacks", a.stat("png_serial_fallbacks"))
