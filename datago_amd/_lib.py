@@ -261,6 +261,9 @@ class Context:
             if m.status != DG_OK:
                 res.append((m.status, None, m))
                 continue
+            if m.is_encoded:  # pre_encode_images: the JPEG bytes
+                res.append((DG_OK, outs[i][: m.nbytes].copy(), m))
+                continue
             c = int(m.nbytes // (m.width * m.height)) if m.width and m.height else 0
             res.append((DG_OK, outs[i][: m.nbytes].reshape(m.height, m.width, c), m))
         return res

@@ -23,6 +23,8 @@ SOURCES = [
     # (source, is_device_code)
     ("kernels.hip", True),
     ("dg_png.hip", True),
+    ("dg_enc.hip", True),
+    ("host/jpeg_enc.cpp", False),
     ("host/png_header.cpp", False),
     ("host/pipeline.cpp", False),
     ("host/capi.cpp", False),

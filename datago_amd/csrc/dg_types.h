@@ -180,6 +180,31 @@ struct AlphaOp {
 };
 constexpr uint32_t kAlphaPoints = 3;  // before call 1, between the calls, after call 2
 
+// ---- JPEG re-encode (pre_encode_images + encode_format jpeg,
+// image_processing.rs:374-395): image 0.25's baseline encoder, 1x1 sampling,
+// Annex K tables scaled by quality.  Per image: k_enc_fdct (colour + FDCT +
+// quantisation per MCU), k_enc_count (bits per block), k_enc_scan (bit
+// offsets), k_enc_write (codes OR-ed into a zeroed bit buffer), k_enc_stuff
+// (header, 0xFF00 stuffing, padding, EOI).
+struct EncTables {
+  uint16_t code[4][256];  // DC luma, AC luma, DC chroma, AC chroma
+  uint8_t len[4][256];
+};
+struct EncDesc {
+  uint64_t src;        // the transformed image (C channels, row stride src_stride)
+  uint64_t coef;       // int16 [nblocks][64], quantised, zigzag order, MCU-interleaved blocks
+  uint64_t bits;       // uint32 [nblocks]: bit length of each block -> exclusive bit offsets
+  uint64_t words;      // scan bit buffer (stream bytes in memory order), zeroed per batch
+  uint64_t out;        // header | stuffed scan | EOI
+  uint64_t hdr;        // header bytes (SOI .. SOS)
+  uint64_t tab;        // EncTables
+  uint32_t src_stride, C, ncomp, mode;  // mode 1: resized LA image read as luma bytes
+  uint32_t w, h, nbx, nby;
+  uint32_t nblocks, hdr_len, total_bits, enc_bytes;
+  uint32_t active, pad[3];
+  uint8_t q[2][64];    // quantisation tables, natural order
+};
+
 struct ImageDesc {
   // ---- entropy stream
   uint64_t scan;            // device address of the first raw entropy-coded byte
@@ -236,6 +261,7 @@ struct ImageDesc {
                             // 4 LA->RGB of an unresized LumaA8 (alpha dropped)
   PngDesc png;
   AlphaOp aop[kAlphaPoints];
+  EncDesc enc;
 };
 
 // One workgroup's work: an image and the first item it handles.

@@ -37,8 +37,8 @@ static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; 
 static const char *kStageNames[] = {"upload",     "png_inflate", "png_unfilter", "destuff",   "huff_sync",
                                     "huff_fix",   "huff_scan",   "huff_write",   "coeffs",    "idct",
                                     "color",      "resize_h1",   "resize_v1",    "resize_h2", "resize_v2",
-                                    "copy",       "download"};
-static const int kNumStages = 17;
+                                    "copy",       "encode",      "download"};
+static const int kNumStages = 18;
 
 Context::Context(int device, const dg_image_config *cfg) : device_(device) {
   if (cfg && cfg->crop_and_resize) {
@@ -381,7 +381,16 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
   p.out_c = cfg_.image_to_rgb8 ? 3 : C;  // convert_to_rgb8 (:163-186)
   if (cfg_.image_to_rgb8) p.channels = 3;  // image_processing.rs:367-372
   p.out_bytes = (uint64_t)ow * oh * p.out_c;
-  if (cfg_.pre_encode_images) p.status = DG_ERR_UNSUPPORTED;
+  p.img_bytes = p.out_bytes;
+  if (cfg_.pre_encode_images) {  // image_processing.rs:374-419
+    if (cfg_.encode_format != 1) {  // PNG re-encode is not on the GPU: the glue keeps its CPU path
+      p.status = DG_ERR_UNSUPPORTED;
+      return DG_OK;
+    }
+    p.encode = true;
+    p.out_bytes = jpeg_enc_bound(ow, oh, p.out_c);
+    p.channels = -1;  // :416
+  }
   return DG_OK;
 }
 
@@ -446,7 +455,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     m.height = p.out_h;
     m.channels = p.channels;
     m.bit_depth = p.bit_depth;
-    m.is_encoded = 0;
+    m.is_encoded = p.encode ? 1 : 0;
     m.nbytes = p.out_bytes;
     if (p.status == DG_OK && caps[i] < p.out_bytes) {
       p.status = DG_ERR_SMALL_BUFFER;
@@ -501,6 +510,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     size_t coef, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], pass_srcoff[kStages];
     size_t final_off, tmp, out, ds, mk, chunk;
     size_t zs, raw, unf, pal;
+    size_t tout, ecoef, ebits, ewords, hdr;  // JPEG re-encode
     // alpha programs: buffer = dst of pass `stage` (-1: the decoded image), byte offset
     int aop_stage[kAlphaPoints];
     size_t aop_off[kAlphaPoints];
@@ -804,12 +814,57 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       b.out_dev_off[i] = o.out;
       out_total += p.out_bytes;
     }
+    if (p.encode) {  // the transform lands in tout; the JPEG goes to the caller's buffer
+      EncDesc &e = d.enc;
+      e.active = 1;
+      e.w = p.out_w;
+      e.h = p.out_h;
+      e.C = p.out_c;
+      e.ncomp = p.out_c <= 2 ? 1 : 3;
+      // a resized LA image is a GrayImage over its LA bytes by now (image_to_dyn_image)
+      e.mode = (p.out_c == 2 && has_cfg_ && !(W == p.out_w && H == p.out_h)) ? 1 : 0;
+      e.src_stride = d.out_stride;
+      e.nbx = (p.out_w + 7) / 8;
+      e.nby = (p.out_h + 7) / 8;
+      e.nblocks = e.nbx * e.nby * e.ncomp;
+      int qual = cfg_.jpeg_quality;
+      uint8_t q[2][64];
+      jpeg_enc_qtables(qual, q);
+      memcpy(e.q, q, sizeof(q));
+      const std::vector<uint8_t> hdr = jpeg_enc_header(p.out_w, p.out_h, (int)e.ncomp, qual);
+      e.hdr_len = (uint32_t)hdr.size();
+      o.hdr = b.blob.size();
+      b.blob.insert(b.blob.end(), hdr.begin(), hdr.end());
+      o.tout = L.take(p.img_bytes + 16, 256);
+      o.ecoef = L.take((size_t)e.nblocks * 128, 256);
+      o.ebits = L.take((size_t)e.nblocks * 4, 256);
+      o.ewords = (size_t)(e.nblocks * 210ull + 64) / 4 * 4 + 16;  // size for now; placed after the loop
+      b.any_enc = true;
+    }
     b.desc_of[i] = (int)b.descs.size();
     b.descs.push_back(d);
     offs.push_back(o);
     (void)last_stage;
   }
   b.total_subs = sub_base;
+  if (b.any_enc) {  // encoder bit buffers: one contiguous region, zeroed with one memset per batch
+    size_t tot = 0;
+    for (Offs &o : offs)
+      if (o.ewords) {
+        const size_t sz = o.ewords;
+        o.ewords = tot;
+        tot += (sz + 255) / 256 * 256;
+      }
+    b.words_off = L.take(tot, 256);
+    b.words_bytes = tot;
+    for (Offs &o : offs)
+      if (o.tout) o.ewords += b.words_off;
+    EncTables et;
+    jpeg_enc_tables(et);
+    while (b.blob.size() % 16) b.blob.push_back(0);
+    b.enctab_off = b.blob.size();
+    b.blob.insert(b.blob.end(), (const uint8_t *)&et, (const uint8_t *)&et + sizeof(et));
+  }
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
   const size_t ckpt_off = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits)) * sizeof(Ckpt));
   st = ensure(sl.scratch, L.off + 256, sl.st);
@@ -834,8 +889,18 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     const Offs &o = offs[k++];
     const JpegHeader &h = b.plans[i].hdr;
     const uint8_t *src = host_io ? (const uint8_t *)sl.input.p + in_off[i] : d_srcs[i];
-    uint64_t out = host_io ? (uint64_t)(uintptr_t)(S + o.out) : (uint64_t)(uintptr_t)outs[i];
+    const uint64_t user_out = host_io ? (uint64_t)(uintptr_t)(S + o.out) : (uint64_t)(uintptr_t)outs[i];
+    const uint64_t out = d.enc.active ? (uint64_t)(uintptr_t)(S + o.tout) : user_out;
     d.out = out;
+    if (d.enc.active) {
+      EncDesc &e = d.enc;
+      e.src = out;
+      e.out = user_out;
+      e.coef = (uint64_t)(uintptr_t)(S + o.ecoef);
+      e.bits = (uint64_t)(uintptr_t)(S + o.ebits);
+      e.words = (uint64_t)(uintptr_t)(S + o.ewords);
+      e.hdr = o.hdr + 1;  // blob offset + 1: made absolute with the meta buffer
+    }
     if (d.fmt == kFmtPng) {
       const PngHeader &g = b.plans[i].png;
       PngDesc &pd = d.png;
@@ -942,6 +1007,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       uint32_t cnt = d.out_w * d.out_h;
       for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_COPY].push_back({I, it});
     }
+    if (d.enc.active) {
+      const EncDesc &e = d.enc;
+      for (uint32_t it = 0; it < e.nbx * e.nby; it += 256) b.lists[L_ENC_MCU].push_back({I, it});
+      for (uint32_t it = 0; it < e.nblocks; it += 256) b.lists[L_ENC_BLK].push_back({I, it});
+      b.lists[L_ENC_IMG].push_back({I, 0});
+    }
   }
   for (uint32_t j = 0; j < (uint32_t)b.gjobs.size(); j++)
     for (uint32_t pc = 0; pc * kGatherPiece < b.gjobs[j].len; pc++) b.lists[L_GATHER].push_back({j, pc});
@@ -962,8 +1033,13 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.meta_bytes = M.off;
   st = ensure(sl.meta, b.meta_bytes + 256, sl.st);
   if (st) return st;
-  for (ImageDesc &d : b.descs)
+  for (ImageDesc &d : b.descs) {
     if (d.fmt == kFmtPng && d.png.pal) d.png.pal = (uint64_t)(uintptr_t)((char *)sl.meta.p + b.blob_off + d.png.pal - 1);
+    if (d.enc.active) {
+      d.enc.hdr = (uint64_t)(uintptr_t)((char *)sl.meta.p + b.blob_off + d.enc.hdr - 1);
+      d.enc.tab = (uint64_t)(uintptr_t)((char *)sl.meta.p + b.blob_off + b.enctab_off);
+    }
+  }
   size_t stage_bytes = b.meta_bytes + (host_io ? IN.off : 0);
   st = ensure_pinned(sl.stage, stage_bytes + 256, sl.st);
   if (st) return st;
@@ -1088,20 +1164,29 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (next()) return DG_ERR_DEVICE;
   launch_copy(sl.st, dd, lst(L_COPY), cnt(L_COPY));
   if (next()) return DG_ERR_DEVICE;
+  if (b.any_enc) {
+    HIPCHK(hipMemsetAsync((char *)sl.scratch.p + b.words_off, 0, b.words_bytes, sl.st));
+    launch_enc_fdct(sl.st, dd, lst(L_ENC_MCU), cnt(L_ENC_MCU));
+    launch_enc_count(sl.st, dd, lst(L_ENC_BLK), cnt(L_ENC_BLK));
+    launch_enc_scan(sl.st, dm, lst(L_ENC_IMG), cnt(L_ENC_IMG));
+    launch_enc_write(sl.st, dd, lst(L_ENC_BLK), cnt(L_ENC_BLK));
+    launch_enc_stuff(sl.st, dm, lst(L_ENC_IMG), cnt(L_ENC_IMG));
+  }
+  if (next()) return DG_ERR_DEVICE;
   HIPCHK(hipGetLastError());
   // read back flags + per-image status (descs) for finish(), then outputs (host path)
   size_t back = b.desc_off + b.descs.size() * sizeof(ImageDesc);
   size_t total = align_up(back, 256);
   if (b.host_io)
     for (int i = 0; i < b.n; i++)
-      if (b.desc_of[i] >= 0) total += align_up(b.plans[i].out_bytes, 16);
+      if (b.desc_of[i] >= 0 && !b.plans[i].encode) total += align_up(b.plans[i].out_bytes, 16);
   dg_status st = ensure_pinned(sl.out, total + 256, sl.st);
   if (st) return st;
   HIPCHK(hipMemcpyAsync(sl.out.p, M, back, hipMemcpyDeviceToHost, sl.st));
   if (b.host_io) {
     size_t off = align_up(back, 256);
     for (int i = 0; i < b.n; i++) {
-      if (b.desc_of[i] < 0) continue;
+      if (b.desc_of[i] < 0 || b.plans[i].encode) continue;  // encoded: exact size copied in finish()
       HIPCHK(hipMemcpyAsync((char *)sl.out.p + off, (char *)sl.scratch.p + b.out_dev_off[i], b.plans[i].out_bytes,
                             hipMemcpyDeviceToHost, sl.st));
       off += align_up(b.plans[i].out_bytes, 16);
@@ -1169,6 +1254,13 @@ dg_status Context::finish(Slot &sl) {
       stat_png_serial_ += back[b.desc_of[i]].png.serial ? 1 : 0;
     }
     if (status) b.metas[i].status = status;
+    if (b.plans[i].encode) {
+      const uint32_t nb = back[b.desc_of[i]].enc.enc_bytes;
+      b.metas[i].nbytes = nb;
+      if (b.host_io && !status && nb)
+        HIPCHK(hipMemcpy(b.host_outs[i], (char *)sl.scratch.p + b.out_dev_off[i], nb, hipMemcpyDeviceToHost));
+      continue;
+    }
     if (b.host_io) {
       if (!status) memcpy(b.host_outs[i], (char *)sl.out.p + off, b.plans[i].out_bytes);
       off += align_up(b.plans[i].out_bytes, 16);

@@ -14,6 +14,7 @@
 #include "buckets.h"
 #include "jpeg_header.h"
 #include "png_header.h"
+#include "jpeg_enc.h"
 
 namespace dg {
 
@@ -37,6 +38,8 @@ struct ImagePlan {
   uint32_t out_w = 0, out_h = 0, out_c = 0;
   uint64_t out_bytes = 0;
   int32_t channels = 0, bit_depth = 8;
+  bool encode = false;     // pre_encode_images + JPEG: out holds a JPEG of at most out_bytes
+  uint64_t img_bytes = 0;  // transformed image bytes (out_w * out_h * out_c)
 };
 
 struct Batch {
@@ -56,7 +59,9 @@ struct Batch {
   size_t ichunk_off = 0;
   std::vector<uint8_t> blob;
   size_t blob_off = 0;
-  bool any_png = false, any_alpha = false;
+  bool any_png = false, any_alpha = false, any_enc = false;
+  size_t words_off = 0, words_bytes = 0;  // contiguous encoder bit buffers (zeroed per batch)
+  size_t enctab_off = 0;                  // EncTables in the blob
   // band H lists (L_RH0, L_RH2) are grouped by weight-count class (<=8, <=16,
   // <=32, more): hclass[stage/2][k] items of class k, in that order
   uint32_t hclass[2][4] = {{0}};
@@ -99,6 +104,7 @@ enum ListId {
   L_RHX0, L_RHX2,  // H passes whose source segment is too wide for the band kernel
   L_GATHER, L_PNG, L_EXPAND, L_ALPHA0, L_ALPHA1, L_ALPHA2,  // PNG decode, alpha programs
   L_INF_FIND, L_INF_RES,                                    // chunk-parallel inflate
+  L_ENC_MCU, L_ENC_BLK, L_ENC_IMG,                          // JPEG re-encode
   L_COUNT
 };
 

@@ -56,3 +56,14 @@ void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const 
 void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch);
 void launch_inf_resolve(hipStream_t st, ImageDesc *imgs, const InfChunk *ch, const WgItem *list, uint32_t nwg);
 }  // namespace dg
+
+// JPEG re-encode (dg_enc.hip)
+namespace dg {
+// fdct: 256 MCUs per workgroup; count / write: 256 blocks per workgroup;
+// scan / stuff: one 1024-thread workgroup per image
+void launch_enc_fdct(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_enc_count(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_enc_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_enc_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_enc_stuff(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+}  // namespace dg

@@ -100,16 +100,19 @@ class ARAwareTransform:
     def get_closest_aspect_ratio(self, image_width: int, image_height: int) -> str:
         return self.table.get(self.table.closest(image_width, image_height))[2]
 
-    def context(self, img_to_rgb8: bool = False) -> "_lib.Context":
-        if img_to_rgb8 not in self._ctx:
+    def context(self, encoding: "ImageEncoding" = None) -> "_lib.Context":
+        enc = encoding if encoding is not None else ImageEncoding()
+        key = (enc.img_to_rgb8, enc.encode_images, int(enc.encode_format), enc.jpeg_quality)
+        if key not in self._ctx:
             c = self.cfg
-            self._ctx[img_to_rgb8] = _lib.Context(self.device, crop_and_resize=True,
-                                                  default_image_size=c.default_image_size,
-                                                  downsampling_ratio=c.downsampling_ratio,
-                                                  min_aspect_ratio=c.min_aspect_ratio,
-                                                  max_aspect_ratio=c.max_aspect_ratio,
-                                                  image_to_rgb8=img_to_rgb8)
-        return self._ctx[img_to_rgb8]
+            self._ctx[key] = _lib.Context(self.device, crop_and_resize=True,
+                                          default_image_size=c.default_image_size,
+                                          downsampling_ratio=c.downsampling_ratio,
+                                          min_aspect_ratio=c.min_aspect_ratio,
+                                          max_aspect_ratio=c.max_aspect_ratio,
+                                          image_to_rgb8=enc.img_to_rgb8, pre_encode_images=enc.encode_images,
+                                          encode_format=int(enc.encode_format), jpeg_quality=enc.jpeg_quality)
+        return self._ctx[key]
 
 
 def aspect_ratio_to_str(size: Tuple[int, int]) -> str:
@@ -140,13 +143,14 @@ class ImagePayload:
         return Image.fromarray(self.to_numpy_array())
 
 
-_plain_ctx: Dict[Tuple[int, bool], _lib.Context] = {}
+_plain_ctx: Dict[tuple, _lib.Context] = {}
 
 
-def _decode_ctx(device: int, rgb8: bool) -> _lib.Context:
-    key = (device, rgb8)
+def _decode_ctx(device: int, enc: "ImageEncoding") -> _lib.Context:
+    key = (device, enc.img_to_rgb8, enc.encode_images, int(enc.encode_format), enc.jpeg_quality)
     if key not in _plain_ctx:
-        _plain_ctx[key] = _lib.Context(device, image_to_rgb8=rgb8)
+        _plain_ctx[key] = _lib.Context(device, image_to_rgb8=enc.img_to_rgb8, pre_encode_images=enc.encode_images,
+                                       encode_format=int(enc.encode_format), jpeg_quality=enc.jpeg_quality)
     return _plain_ctx[key]
 
 
@@ -157,10 +161,8 @@ def images_to_payloads(datas: List[bytes], img_tfm: Optional[ARAwareTransform], 
     (status, payload) per image; status != 0 means the reference would have
     returned an ImageError (CORRUPT) or the format is outside the GPU path
     (UNSUPPORTED, the caller's CPU path keeps it)."""
-    if encoding.encode_images:
-        return [(_lib.DG_ERR_UNSUPPORTED, None) for _ in datas]
     if img_tfm is not None:
-        ctx = img_tfm.context(encoding.img_to_rgb8)
+        ctx = img_tfm.context(encoding)
         forced = []
         for ar in aspect_ratios:
             if not ar:
@@ -171,7 +173,7 @@ def images_to_payloads(datas: List[bytes], img_tfm: Optional[ARAwareTransform], 
                 raise KeyError("Aspect ratio not found in aspect ratio to size map")  # :334-336
             forced.append(k)
     else:
-        ctx = _decode_ctx(device, encoding.img_to_rgb8)
+        ctx = _decode_ctx(device, encoding)
         forced = [-1] * len(datas)
     out = []
     for st, arr, m in ctx.decode_batch(datas, forced):
@@ -180,7 +182,7 @@ def images_to_payloads(datas: List[bytes], img_tfm: Optional[ARAwareTransform], 
             continue
         out.append((st, ImagePayload(data=arr.tobytes(), original_height=m.original_height,
                                      original_width=m.original_width, height=m.height, width=m.width,
-                                     channels=m.channels, bit_depth=m.bit_depth, is_encoded=False)))
+                                     channels=m.channels, bit_depth=m.bit_depth, is_encoded=bool(m.is_encoded))))
     return out
 
 

@@ -195,3 +195,43 @@ def to_rgb8(arr: np.ndarray, resized: bool) -> np.ndarray:
     else:
         g = arr[:, :, 0]
     return np.repeat(g[:, :, None], 3, axis=2)
+
+
+# ------------------------------------------------------------------ JPEG encode
+def _enc_lib():
+    L = lib()
+    if not getattr(L, "_enc_ready", False):
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.oe_encode.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t]
+        L.oe_encode.restype = ctypes.c_size_t
+        L.oe_bound.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oe_bound.restype = ctypes.c_size_t
+        L.oe_qtables.argtypes = [ctypes.c_int, u8p]
+        L.oe_fdct.argtypes = [u8p, ctypes.POINTER(ctypes.c_int32)]
+        L._enc_ready = True
+    return L
+
+
+def jpeg_encode(arr: np.ndarray, quality: int = 92) -> bytes:
+    """image 0.25 JpegEncoder::new_with_quality restated (image_processing.rs:374-395)."""
+    arr = np.ascontiguousarray(arr, np.uint8)
+    if arr.ndim == 2:
+        arr = arr[:, :, None]
+    h, w, c = arr.shape
+    L = _enc_lib()
+    cap = L.oe_bound(w, h, c)
+    out = np.empty(cap, np.uint8)
+    n = L.oe_encode(arr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), w, h, c, quality,
+                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), cap)
+    assert n > 0
+    return out[:n].tobytes()
+
+
+def jpeg_qtables(quality: int) -> np.ndarray:
+    q = np.empty((2, 64), np.uint8)
+    _enc_lib().oe_qtables(quality, q.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    return q
+
+
+def jpeg_encode_bound(w: int, h: int, c: int) -> int:
+    return int(_enc_lib().oe_bound(w, h, c))
