@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--workload", choices=("jpeg", "png"), default="jpeg",
                     help="jpeg: configs[1] (the headline); png: configs[4]-style RGB PNG + aligned L8 mask pairs "
                          "(decode + bucket-resize; the mask is forced to the image's bucket, worker_http.rs:186-214)")
+    ap.add_argument("--encode", action="store_true",
+                    help="pre_encode_images with encode_format jpeg, quality 92 (configs[4]: every payload "
+                         "re-encoded on the GPU, WebDataset semantics worker_wds.rs:47-52)")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 
@@ -76,14 +79,16 @@ def cpu_share() -> int:
 
 def _cpu_work(args):
     from oracle import oracle as O
-    data, tw, th = args
+    data, tw, th, enc = args
     t = time.perf_counter()
     st, dec = O.decode_any(data)
-    O.crop_and_resize(dec, tw, th, O.MODE_FIR)
+    out = O.crop_and_resize(dec, tw, th, O.MODE_FIR) if (dec.shape[1], dec.shape[0]) != (tw, th) else dec
+    if enc:
+        O.jpeg_encode(out, 92)
     return dec.shape[0] * dec.shape[1], time.perf_counter() - t
 
 
-def cpu_baseline(pool, targets, seconds: float):
+def cpu_baseline(pool, targets, seconds: float, encode: bool = False):
     """Oracle (scalar C restatement of the reference path: decode +
     crop_and_resize) on the host cores, one image per task like the
     reference's tokio worker (worker_files.rs:74-141)."""
@@ -92,11 +97,11 @@ def cpu_baseline(pool, targets, seconds: float):
     O.lib()
     cores = cpu_share()
     # size the sample from a one-image probe so the run takes ~`seconds`
-    px, dt = _cpu_work((pool[0], *targets[0]))
+    px, dt = _cpu_work((pool[0], *targets[0], encode))
     per_px = dt / max(px, 1)
     mean_px = np.mean([w * h for (w, h) in [image_dims(d)[:2] for d in pool[:32]]])
     n = int(max(cores, min(64 * len(pool), seconds * cores / max(per_px * mean_px, 1e-9))))
-    jobs = [(pool[i % len(pool)], *targets[i % len(pool)]) for i in range(n)]
+    jobs = [(pool[i % len(pool)], *targets[i % len(pool)], encode) for i in range(n)]
     p = mp.get_context("fork").Pool(cores)
     try:
         p.map(_cpu_work, jobs[:cores], chunksize=1)  # workers up and the oracle loaded
@@ -109,7 +114,8 @@ def cpu_baseline(pool, targets, seconds: float):
     tot_px = sum(r[0] for r in res)
     return {"value": round(tot_px / wall / 1e6, 2), "unit": "Mpixel/s", "cores": cores, "kind": "port",
             "sample": f"{n} images of the same pool ({tot_px / 1e6:.1f} Mpx) through oracle/ (scalar C "
-                      f"decode + FIR-mode Lanczos3 crop_and_resize), {cores} processes, {wall:.1f} s"}
+                      f"decode + FIR-mode Lanczos3 crop_and_resize{' + JPEG q92 encode' if encode else ''}), "
+                      f"{cores} processes, {wall:.1f} s"}
 
 
 def image_dims(data: bytes):
@@ -289,7 +295,8 @@ def main() -> int:
     tr = B.ARAwareTransform(a.size, a.ratio, 0.5, 2.0)
     dims = [image_dims(d) for d in pool]
     ctx = L.Context(local, crop_and_resize=True, default_image_size=a.size, downsampling_ratio=a.ratio,
-                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0, pre_encode_images=a.encode, encode_format=1,
+                    jpeg_quality=92)
     # multi-payload alignment (worker_wds.rs:68-76, worker_http.rs:186-214): every
     # payload after the first of a sample takes the first one's bucket
     forced_pool = [-1] * len(pool)
@@ -314,7 +321,10 @@ def main() -> int:
     d_arena = ctx.alloc(o)
     ctx.h2d(d_arena, host_arena)
     h_base = host_arena.ctypes.data
-    out_bytes = [tw * th * nc for (tw, th), (_, _, nc) in zip(targets, dims)]
+    if a.encode:  # caller buffers sized by the encoder bound (datago_hip.h dg_output_size)
+        out_bytes = [ctx.output_size(d, f)[1] for d, f in zip(pool, forced_pool)]
+    else:
+        out_bytes = [tw * th * nc for (tw, th), (_, _, nc) in zip(targets, dims)]
     img_stage_bytes = [(png_stage_bytes if png else stage_bytes)(*((d, dim, tgt) if png else (L, d, dim, tgt)))
                        for d, dim, tgt in zip(pool, dims, targets)]
     B_ = min(a.batch, 1 << 16)
@@ -465,8 +475,10 @@ def main() -> int:
                      f"synthetic (seeded PIL PNG pool of {len(pool) // 2} RGB image + L8 mask pairs per rank, cycled)"),
             "config": {"workload": ("configs[1]: file-source JPEGs, mixed aspect ratios, decode + bucket + "
                                     "crop/resize to 1024/32 buckets") if not png else
-                                   ("configs[4] without re-encode: RGB PNG (PIL, zlib 6) + L8 mask PNG pairs, "
-                                    "mask aligned to the image's bucket, decode + crop/resize to 1024/32"),
+                                   (f"configs[4]{'' if a.encode else ' without re-encode'}: RGB PNG (PIL, zlib 6) "
+                                    "+ L8 mask PNG pairs, mask aligned to the image's bucket, decode + crop/resize "
+                                    f"to 1024/32{' + JPEG q92 re-encode of every payload' if a.encode else ''}"),
+                       "pre_encode_images": bool(a.encode),
                        "images_per_step": B_, "pool_per_rank": a.pool,
                        "short_side": [a.short_min, a.short_max], "buckets": f"{a.size}/{a.ratio}/0.5/2.0",
                        "parallelism": f"dp{world} (sample shards, no collectives)"},
@@ -494,7 +506,7 @@ def main() -> int:
                               for q in ("span", "mean", "p90", "max")} if a.wg_timing else None),
         }
         if world == 1 and not a.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(pool, targets, a.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(pool, targets, a.cpu_seconds, a.encode)
         if png:  # the PMC file is for the JPEG workload
             result["roofline"]["traffic"] = None
             result["roofline"]["traffic_source"] = None

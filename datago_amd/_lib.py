@@ -37,7 +37,7 @@ EXPORTS = [
     "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_buckets", "dg_output_size", "dg_submit", "dg_wait",
     "dg_poll", "dg_decode_one", "dg_submit_device", "dg_device_alloc", "dg_device_free",
     "dg_memcpy_h2d", "dg_memcpy_d2h", "dg_synchronize", "dg_last_batch_timings",
-    "dg_ctx_set_option", "dg_ctx_get_stat", "dg_last_error", "dg_abi_version",
+    "dg_ctx_set_option", "dg_ctx_get_stat", "dg_last_error", "dg_abi_version", "dg_sample_align",
 ]
 
 
@@ -117,6 +117,7 @@ def load() -> ctypes.CDLL:
     L.dg_ctx_get_stat.argtypes = [vp, ctypes.c_char_p]
     L.dg_ctx_get_stat.restype = ctypes.c_int64
     L.dg_last_error.restype = ctypes.c_char_p
+    L.dg_sample_align.argtypes = [vp, i32, u8pp, ctypes.POINTER(sz), i32, ctypes.POINTER(i32)]
     _lib = L
     return L
 
@@ -182,6 +183,18 @@ def probe(data: bytes) -> Tuple[int, ProbeInfo]:
     return st, info
 
 
+def sample_align(table: Optional["BucketTable"], datas: Sequence[bytes], forced_first: int = -1) -> List[int]:
+    """dg_sample_align: forced bucket per payload of one sample (reference
+    first; worker_wds.rs:68-76).  table None = no image_config."""
+    n = len(datas)
+    bufs = [ctypes.create_string_buffer(d, len(d)) for d in datas]
+    srcs = _as_ptr_array([ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_size_t * max(1, n))(*[len(d) for d in datas])
+    out = (ctypes.c_int32 * max(1, n))()
+    _check(load().dg_sample_align(table._h if table is not None else None, n, srcs, lens, forced_first, out))
+    return [out[i] for i in range(n)]
+
+
 # ------------------------------------------------------------------ context
 
 def _as_ptr_array(ptrs: Sequence[int]):
@@ -234,6 +247,9 @@ class Context:
         n = ctypes.c_uint64()
         st = load().dg_output_size(self._h, data, len(data), forced_bucket, ctypes.byref(n))
         return st, n.value
+
+    def sample_align(self, datas: Sequence[bytes], forced_first: int = -1) -> List[int]:
+        return sample_align(self.buckets, datas, forced_first)
 
     # -- host memory in, host memory out (the Rust workers' path)
     def decode_batch(self, datas: Sequence[bytes], forced: Optional[Sequence[int]] = None

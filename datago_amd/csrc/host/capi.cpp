@@ -158,6 +158,36 @@ const dg_bucket_table *dg_ctx_buckets(const dg_ctx *ctx) {
   return &ctx->view;
 }
 
+dg_status dg_sample_align(const dg_bucket_table *t, int32_t n, const uint8_t *const *srcs, const size_t *lens,
+                          int32_t forced_first, int32_t *forced_out) {
+  if (n < 0 || (n > 0 && (!srcs || !lens || !forced_out))) return DG_ERR_INVALID;
+  for (int32_t i = 0; i < n; i++) forced_out[i] = -1;
+  if (!t) return DG_OK;  // no image_config: the aspect ratio is never used
+  const dg::BucketTable *bt = &t->t;
+  // the reference payload: the first one whose header gives dimensions (a payload
+  // that fails to load is skipped, worker_wds.rs:134-137)
+  int32_t ref = -1;
+  uint32_t w = 0, h = 0;
+  for (int32_t i = 0; i < n && ref < 0; i++) {
+    dg_probe_info pi;
+    if (dg_probe(srcs[i], lens[i], &pi) == DG_OK && pi.width && pi.height) {
+      ref = i;
+      w = pi.width;
+      h = pi.height;
+    }
+  }
+  if (ref < 0) return DG_OK;
+  const int nb = (int)bt->buckets().size();
+  if (forced_first >= nb || forced_first < -1) return DG_ERR_BAD_BUCKET;
+  const int b = forced_first >= 0 ? forced_first : bt->closest((int32_t)w, (int32_t)h);
+  forced_out[ref] = forced_first;
+  // aspect_ratio_to_str(first payload's output size) -> the key the others are forced to
+  const dg::Bucket &bk = bt->buckets()[b];
+  const int k = bt->find_key(dg::aspect_ratio_to_str(bk.w, bk.h));
+  for (int32_t i = ref + 1; i < n; i++) forced_out[i] = k < 0 ? -2 : k;
+  return DG_OK;
+}
+
 dg_status dg_output_size(dg_ctx *ctx, const uint8_t *bytes, size_t len, int32_t forced, uint64_t *nbytes) {
   if (!ctx || !nbytes) return DG_ERR_INVALID;
   return ctx->c.output_size(bytes, len, forced, nbytes);

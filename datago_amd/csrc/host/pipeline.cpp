@@ -366,9 +366,9 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
   uint32_t ow = W, oh = H;
   if (has_cfg_) {
     int b = forced;
-    if (b < 0) {
+    if (b == -1) {
       b = buckets_->closest((int32_t)W, (int32_t)H);
-    } else if (b >= (int)buckets_->buckets().size()) {
+    } else if (b < -1 || b >= (int)buckets_->buckets().size()) {  // -2: "NaN" key (dg_sample_align)
       p.status = DG_ERR_BAD_BUCKET;
       return DG_OK;
     }

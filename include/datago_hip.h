@@ -20,6 +20,8 @@
  *       worker_wds.rs:45-66, worker_http.rs:64,129-137       dg_submit / dg_wait (batched)
  *   ImagePayload {data, original_*, height, width, channels, bit_depth, is_encoded}
  *       structs.rs:52-71                                     dg_payload_meta (+ caller-owned data buffer)
+ *   reference-first AR propagation of a sample
+ *       worker_wds.rs:33,68-76, worker_http.rs:126-214       dg_sample_align
  *   ImageError -> sample dropped (worker_files.rs:63-70)     DG_ERR_CORRUPT
  *   panic!/assert! (Cargo.toml:54 panic="abort")             DG_ERR_BAD_BUCKET / DG_ERR_INVALID (never abort)
  *
@@ -64,7 +66,7 @@ typedef struct dg_image_config {
   uint32_t downsampling_ratio;  /* e.g. 32 */
   double min_aspect_ratio;      /* e.g. 0.5 */
   double max_aspect_ratio;      /* e.g. 2.0 */
-  int32_t pre_encode_images;    /* not yet supported on the GPU path: DG_ERR_UNSUPPORTED */
+  int32_t pre_encode_images;    /* re-encode: JPEG on the GPU; PNG -> DG_ERR_UNSUPPORTED (CPU path) */
   int32_t image_to_rgb8;        /* gray -> RGB expansion after resize (:367-372) */
   int32_t encode_format;        /* 0 = PNG, 1 = JPEG (EncodeFormat, :16-22) */
   int32_t jpeg_quality;         /* default 92 (:14) */
@@ -131,6 +133,18 @@ typedef struct dg_payload_meta {
   int32_t bucket;         /* bucket index used, -1 without transform */
   uint64_t nbytes;        /* bytes written (or needed) in the output buffer */
 } dg_payload_meta;
+
+/* Multi-payload alignment of one sample (worker_wds.rs:33,68-76; worker_http.rs:126-152,159-214):
+ * the reference payload (the first whose header gives dimensions; the generator
+ * sorts it first, generator_wds.rs:154-166) takes the closest bucket (or
+ * forced_first >= 0); every later payload is forced to the bucket whose key is
+ * aspect_ratio_to_str(reference output size).  Header-only, so all payloads
+ * of a sample go to the GPU in one batch.  forced_out[i]: -1 = closest
+ * (payloads before the reference, and everything without an image_config),
+ * -2 = no such key (the reference panics; dg_submit reports DG_ERR_BAD_BUCKET). */
+dg_status dg_sample_align(const dg_bucket_table *t /* dg_ctx_buckets(ctx); NULL = no image_config */,
+                          int32_t n, const uint8_t *const *srcs, const size_t *lens, int32_t forced_first,
+                          int32_t *forced_out);
 
 /* Bytes needed for image `bytes` (after probe + bucket choice). */
 dg_status dg_output_size(dg_ctx *ctx, const uint8_t *bytes, size_t len, int32_t forced_bucket,
