@@ -934,8 +934,10 @@ __device__ __forceinline__ void hfill_bytes4(const DG_GLOBAL uint8_t *row, uint3
   *(u32x4 *)d = u32x4{v[0], v[1], v[2], v[3]};
 }
 
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
 template <int KMAX, int C>
-__device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, const int32_t *kw,
+__device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, const uint32_t *kw2,
                                            const DG_GLOBAL int16_t *kp, uint32_t ksize, uint32_t n, uint32_t r0,
                                            uint32_t nrows, int32_t prec, uint8_t *ob, uint32_t col) {
   constexpr uint32_t R = kHBandRows / 2;  // rows r0, r0 + 2, ...
@@ -945,20 +947,37 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
   for (uint32_t r = 0; r < R; r++)
 #pragma unroll
     for (int c = 0; c < C; c++) a[r][c] = bias;
-  auto tap = [&](uint32_t i, int32_t w) {
-#pragma unroll
-    for (uint32_t r = 0; r < R; r++) {
-      const uint32_t v = seg[(r0 + 2 * r) * kHSegStride + off + i];
-#pragma unroll
-      for (int c = 0; c < C; c++) a[r][c] += (int32_t)((v >> (8 * c)) & 0xFF) * w;
-    }
-  };
   if (KMAX > 0) {
+    // two taps per v_dot2_i32_i16: the channel-c bytes of pixels i and i+1
+    // packed as i16 x 2 (one v_perm) against the packed weights (w_i, w_i+1);
+    // an odd last tap pairs with a zero weight.  Integer sums: bit-exact
+    // with tap-by-tap accumulation.
 #pragma unroll
-    for (int i = 0; i < (KMAX > 0 ? KMAX : 1); i++)
-      if ((uint32_t)i < ksize) tap((uint32_t)i, kw[i]);
+    for (int j = 0; j < (KMAX > 0 ? (KMAX + 1) / 2 : 1); j++) {
+      if ((uint32_t)(2 * j) >= ksize) break;
+      const s16x2 w = __builtin_bit_cast(s16x2, kw2[j]);
+#pragma unroll
+      for (uint32_t r = 0; r < R; r++) {
+        const uint32_t *row = seg + (r0 + 2 * r) * kHSegStride + off + 2 * j;
+        const uint32_t v0 = row[0], v1 = row[1];
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+          const uint32_t sel = 0x0C000C00u | ((4u + (uint32_t)c) << 16) | (uint32_t)c;  // [v0.c, 0, v1.c, 0]
+          const uint32_t pr = __builtin_amdgcn_perm(v1, v0, sel);
+          a[r][c] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pr), w, a[r][c], false);
+        }
+      }
+    }
   } else {
-    for (uint32_t i = 0; i < n; i++) tap(i, kp[i]);
+    for (uint32_t i = 0; i < n; i++) {
+      const int32_t w = kp[i];
+#pragma unroll
+      for (uint32_t r = 0; r < R; r++) {
+        const uint32_t v = seg[(r0 + 2 * r) * kHSegStride + off + i];
+#pragma unroll
+        for (int c = 0; c < C; c++) a[r][c] += (int32_t)((v >> (8 * c)) & 0xFF) * w;
+      }
+    }
   }
 #pragma unroll
   for (uint32_t r = 0; r < R; r++)
@@ -1021,11 +1040,15 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
         hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * u, seg + fr * kHSegStride + 4 * u);
     }
   }
-  int32_t kw[KMAX > 0 ? KMAX : 1];
+  uint32_t kw2[KMAX > 0 ? (KMAX + 1) / 2 : 1];  // weights (w_2j, w_2j+1) as i16 x 2
   const DG_GLOBAL int16_t *kp = coef + (size_t)(valid ? x : x0) * ksize;
   if (KMAX > 0) {
 #pragma unroll
-    for (int i = 0; i < (KMAX > 0 ? KMAX : 1); i++) kw[i] = (valid && (uint32_t)i < n) ? (int32_t)kp[i] : 0;
+    for (int j = 0; j < (KMAX > 0 ? (KMAX + 1) / 2 : 1); j++) {
+      const uint32_t lo = (valid && (uint32_t)(2 * j) < n) ? (uint16_t)kp[2 * j] : 0u;
+      const uint32_t hi = (valid && (uint32_t)(2 * j + 1) < n) ? (uint16_t)kp[2 * j + 1] : 0u;
+      kw2[j] = lo | (hi << 16);
+    }
   }
   __syncthreads();
   // phase 2: convolve (thread: column col, rows r0, r0 + 2, ...)
@@ -1033,13 +1056,13 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
     const uint32_t off = st - p0, r0 = t / kHBandCols;
     const int32_t prec = ps.precision;
     if (C == 3)
-      hconv_rows<KMAX, 3>(seg, off, kw, kp, ksize, n, r0, nrows, prec, ob, col);
+      hconv_rows<KMAX, 3>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
     else if (C == 1)
-      hconv_rows<KMAX, 1>(seg, off, kw, kp, ksize, n, r0, nrows, prec, ob, col);
+      hconv_rows<KMAX, 1>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
     else if (C == 4)
-      hconv_rows<KMAX, 4>(seg, off, kw, kp, ksize, n, r0, nrows, prec, ob, col);
+      hconv_rows<KMAX, 4>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
     else
-      hconv_rows<KMAX, 2>(seg, off, kw, kp, ksize, n, r0, nrows, prec, ob, col);
+      hconv_rows<KMAX, 2>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
   }
   __syncthreads();
   // phase 3: store the band's rows, 16 bytes per thread per step
@@ -1093,7 +1116,24 @@ __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ 
   for (int j = 0; j < 16; j++) a[j] = bias;
   const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(start - (int32_t)ps.row0) * ps.src_stride + b0;
   if (nb == 16 && (ps.src_stride & 15) == 0) {
-    for (int32_t i = 0; i < n; i++) {
+    // two taps (source rows i, i+1) per v_dot2_i32_i16, as in hconv_rows
+    int32_t i = 0;
+    for (; i + 1 < n; i += 2) {
+      const uint32_t w2 = (uint32_t)(uint16_t)k[i] | ((uint32_t)(uint16_t)k[i + 1] << 16);
+      const s16x2 w = __builtin_bit_cast(s16x2, w2);
+      const u32x4 v0 = *(const DG_GLOBAL u32x4 *)(src + (size_t)i * ps.src_stride);
+      const u32x4 v1 = *(const DG_GLOBAL u32x4 *)(src + (size_t)(i + 1) * ps.src_stride);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t sel = 0x0C000C00u | ((4u + (uint32_t)b) << 16) | (uint32_t)b;  // [v0.b, 0, v1.b, 0]
+          const uint32_t pr = __builtin_amdgcn_perm(v1[j], v0[j], sel);
+          a[4 * j + b] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pr), w, a[4 * j + b], false);
+        }
+      }
+    }
+    if (i < n) {
       const int32_t w = k[i];
       const u32x4 v = *(const DG_GLOBAL u32x4 *)(src + (size_t)i * ps.src_stride);
 #pragma unroll
