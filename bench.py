@@ -58,7 +58,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=3, help="host-memory (PCIe-inclusive) steps")
-    ap.add_argument("--workload", choices=("jpeg", "png"), default="jpeg",
+    ap.add_argument("--shards", type=int, default=8, help="wds workload: shards of 1000 samples")
+    ap.add_argument("--workload", choices=("jpeg", "png", "wds"), default="jpeg",
                     help="jpeg: configs[1] (the headline); png: configs[4]-style RGB PNG + aligned L8 mask pairs "
                          "(decode + bucket-resize; the mask is forced to the image's bucket, worker_http.rs:186-214)")
     ap.add_argument("--encode", action="store_true",
@@ -282,7 +283,21 @@ def main() -> int:
     workers = a.workers or cpu_share()
     t_gen = time.perf_counter()
     png = a.workload == "png"
-    if png:  # configs[4]: pairs (image, mask), seed 5; a.pool counts images (2 per pair)
+    wds = a.workload == "wds"
+    tar_arena = None
+    if wds:  # configs[2]: WebDataset shards held in memory, indexed by dg_wds_index (zero-copy members)
+        tars = [synth.make_wds_shard(3 * 1000 + k, 1000, first_key=1000 * k, workers=workers)
+                for k in range(a.shards)]
+        t_idx = time.perf_counter()
+        tar_arena = np.frombuffer(b"".join(tars), np.uint8)
+        members, base = [], 0
+        for t_ in tars:  # this rank's samples (SipHash-1-3 of the key % world, generator_wds.rs:133-148)
+            for smp in L.wds_index(t_, rank, world, "jpg"):
+                members += [(base + off, n) for (name, off, n) in smp if name.endswith(".jpg")]
+            base += len(t_)
+        wds_index_s = time.perf_counter() - t_idx
+        pool = [tar_arena[off:off + n].tobytes() for off, n in members]
+    elif png:  # configs[4]: pairs (image, mask), seed 5; a.pool counts images (2 per pair)
         npair = max(1, a.pool // 2)
         plo, phi = get_data_slice_multirank(npair * world, rank, world)
         pool = png_corpus(5, npair * world, a.short_min, a.short_max, workers, plo, phi)
@@ -310,14 +325,19 @@ def main() -> int:
         ctx.set_option("lead_bits", a.lead_bits)
     if a.wg_timing:
         ctx.set_option("wg_timing", 1)
-    # ---- pool -> HBM (one arena, 16-byte aligned entries)
-    offs, o = [], 0
-    for d in pool:
-        offs.append(o)
-        o += (len(d) + 16 + 15) // 16 * 16
-    host_arena = np.zeros(o, np.uint8)
-    for d, of in zip(pool, offs):
-        host_arena[of:of + len(d)] = np.frombuffer(d, np.uint8)
+    # ---- pool -> HBM (one arena, 16-byte aligned entries; wds: the shards themselves)
+    if wds:
+        host_arena = np.concatenate([tar_arena, np.zeros(64, np.uint8)])
+        offs = [off for off, _ in members]
+        o = host_arena.nbytes
+    else:
+        offs, o = [], 0
+        for d in pool:
+            offs.append(o)
+            o += (len(d) + 16 + 15) // 16 * 16
+        host_arena = np.zeros(o, np.uint8)
+        for d, of in zip(pool, offs):
+            host_arena[of:of + len(d)] = np.frombuffer(d, np.uint8)
     d_arena = ctx.alloc(o)
     ctx.h2d(d_arena, host_arena)
     h_base = host_arena.ctypes.data
@@ -459,8 +479,8 @@ def main() -> int:
                    "stages_alg_GBs": {k: round(ser_alg[k] / ser_n / (v / 1e3) / 1e9, 1)
                                       for k, v in skern.items() if ser_alg.get(k) and v > 0}}
         result = {
-            "metric": ("Mpixel/s device-resident JPEG decode+bucket-resize at 1/2/4/8 MI355X" if not png else
-                       "Mpixel/s device-resident PNG decode+bucket-resize (image + aligned mask pairs)"),
+            "metric": ("Mpixel/s device-resident PNG decode+bucket-resize (image + aligned mask pairs)" if png else
+                       "Mpixel/s device-resident JPEG decode+bucket-resize at 1/2/4/8 MI355X"),
             "value": round(px_all / dt_max / 1e6, 2),
             "unit": "Mpixel/s",
             "n_gpus": world,
@@ -471,9 +491,13 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": (f"synthetic (seeded PIL JPEG pool of {a.pool} unique images per rank, cycled)" if not png else
-                     f"synthetic (seeded PIL PNG pool of {len(pool) // 2} RGB image + L8 mask pairs per rank, cycled)"),
-            "config": {"workload": ("configs[1]: file-source JPEGs, mixed aspect ratios, decode + bucket + "
+            "data": (f"synthetic (seeded PIL PNG pool of {len(pool) // 2} RGB image + L8 mask pairs per rank, cycled)"
+                     if png else f"synthetic ({a.shards} seeded WebDataset shards, {len(pool)} .jpg members on this "
+                     f"rank, indexed in {wds_index_s * 1e3:.1f} ms by dg_wds_index, cycled)" if wds else
+                     f"synthetic (seeded PIL JPEG pool of {a.pool} unique images per rank, cycled)"),
+            "config": {"workload": ("configs[2]: WebDataset shards (fake-imagenet-like {key}.jpg + {key}.cls, "
+                                    f"W U[300,500] H U[250,500] q90), decode + bucket-resize to {a.size}/{a.ratio}")
+                       if wds else ("configs[1]: file-source JPEGs, mixed aspect ratios, decode + bucket + "
                                     "crop/resize to 1024/32 buckets") if not png else
                                    (f"configs[4]{'' if a.encode else ' without re-encode'}: RGB PNG (PIL, zlib 6) "
                                     "+ L8 mask PNG pairs, mask aligned to the image's bucket, decode + crop/resize "

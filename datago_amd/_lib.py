@@ -38,6 +38,7 @@ EXPORTS = [
     "dg_poll", "dg_decode_one", "dg_submit_device", "dg_device_alloc", "dg_device_free",
     "dg_memcpy_h2d", "dg_memcpy_d2h", "dg_synchronize", "dg_last_batch_timings",
     "dg_ctx_set_option", "dg_ctx_get_stat", "dg_last_error", "dg_abi_version", "dg_sample_align",
+    "dg_wds_index", "dg_wds_key_hash",
 ]
 
 
@@ -118,6 +119,10 @@ def load() -> ctypes.CDLL:
     L.dg_ctx_get_stat.restype = ctypes.c_int64
     L.dg_last_error.restype = ctypes.c_char_p
     L.dg_sample_align.argtypes = [vp, i32, u8pp, ctypes.POINTER(sz), i32, ctypes.POINTER(i32)]
+    L.dg_wds_index.argtypes = [vp, sz, i32, i32, ctypes.c_char_p, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                               vp, sz, ctypes.POINTER(sz), vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+    L.dg_wds_key_hash.argtypes = [ctypes.c_char_p, sz]
+    L.dg_wds_key_hash.restype = ctypes.c_uint64
     _lib = L
     return L
 
@@ -193,6 +198,44 @@ def sample_align(table: Optional["BucketTable"], datas: Sequence[bytes], forced_
     out = (ctypes.c_int32 * max(1, n))()
     _check(load().dg_sample_align(table._h if table is not None else None, n, srcs, lens, forced_first, out))
     return [out[i] for i in range(n)]
+
+
+class WdsMember(ctypes.Structure):
+    _fields_ = [("name_off", ctypes.c_uint64), ("data_off", ctypes.c_uint64), ("data_len", ctypes.c_uint64),
+                ("name_len", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+class WdsSample(ctypes.Structure):
+    _fields_ = [("first", ctypes.c_uint32), ("count", ctypes.c_uint32)]
+
+
+def wds_index(tar, rank: int = 0, world_size: int = 1, reference_ext: str = "jpg"):
+    """dg_wds_index over a shard in memory (bytes or a uint8 numpy array).
+    Returns [[(name, data_off, data_len), ...] per sample]."""
+    L = load()
+    buf = np.frombuffer(tar, np.uint8) if not isinstance(tar, np.ndarray) else tar
+    ptr = buf.ctypes.data
+    nm, nn, ns = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_int64()
+    st = L.dg_wds_index(ptr, buf.nbytes, rank, world_size, reference_ext.encode(), None, 0, ctypes.byref(nm), None,
+                        0, ctypes.byref(nn), None, 0, ctypes.byref(ns))
+    if st not in (DG_OK, DG_ERR_SMALL_BUFFER):
+        _check(st)
+    mem = (WdsMember * max(1, nm.value))()
+    names = ctypes.create_string_buffer(max(1, nn.value))
+    sam = (WdsSample * max(1, ns.value))()
+    _check(L.dg_wds_index(ptr, buf.nbytes, rank, world_size, reference_ext.encode(), mem, nm.value, ctypes.byref(nm),
+                          names, nn.value, ctypes.byref(nn), sam, ns.value, ctypes.byref(ns)))
+    raw = names.raw
+    out = []
+    for s in sam[: ns.value]:
+        out.append([(raw[m.name_off:m.name_off + m.name_len].decode("utf-8", "replace"), m.data_off, m.data_len)
+                    for m in mem[s.first:s.first + s.count]])
+    return out
+
+
+def wds_key_hash(key: str) -> int:
+    b = key.encode()
+    return load().dg_wds_key_hash(b, len(b))
 
 
 # ------------------------------------------------------------------ context

@@ -25,6 +25,7 @@ SOURCES = [
     ("dg_png.hip", True),
     ("dg_enc.hip", True),
     ("host/jpeg_enc.cpp", False),
+    ("host/wds.cpp", False),
     ("host/png_header.cpp", False),
     ("host/pipeline.cpp", False),
     ("host/capi.cpp", False),

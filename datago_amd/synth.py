@@ -270,3 +270,44 @@ def pil_png(arr: np.ndarray, **kw) -> bytes:
     buf = io.BytesIO()
     im.save(buf, format="PNG", **kw)
     return buf.getvalue()
+
+
+# ---------------------------------------------------------------- WebDataset shards
+
+def imagenet_like_spec(seed: int, n: int):
+    """BASELINE configs[2]: fake-imagenet-like members, W U[300,500], H U[250,500], q90."""
+    rng = np.random.default_rng(seed)
+    return [(int(rng.integers(300, 501)), int(rng.integers(250, 501)), int(rng.integers(0, 1000))) for _ in range(n)]
+
+
+def _wds_member(args):
+    seed, (w, h, cls) = args
+    return make_jpeg(seed, w, h, 90, "4:2:0"), str(cls).encode()
+
+
+def make_wds_shard(seed: int, n: int, first_key: int = 0, workers: int = 1, fmt: str = "gnu") -> bytes:
+    """A WebDataset tar: {key}.jpg + {key}.cls per sample (tarfile, GNU format)."""
+    import tarfile
+    spec = imagenet_like_spec(seed, n)
+    jobs = [(seed * 1_000_003 + i, spec[i]) for i in range(n)]
+    if workers > 1:
+        import multiprocessing as mp
+        p = mp.get_context("fork").Pool(workers)
+        try:
+            members = p.map(_wds_member, jobs, chunksize=4)
+        finally:
+            p.close()
+            p.join()
+    else:
+        members = [_wds_member(j) for j in jobs]
+    buf = io.BytesIO()
+    tf_fmt = {"gnu": tarfile.GNU_FORMAT, "pax": tarfile.PAX_FORMAT, "ustar": tarfile.USTAR_FORMAT}[fmt]
+    with tarfile.open(fileobj=buf, mode="w", format=tf_fmt) as tf:
+        for i, (jpg, cls) in enumerate(members):
+            key = f"n{first_key + i:08d}"
+            for name, data in ((f"{key}.jpg", jpg), (f"{key}.cls", cls)):
+                ti = tarfile.TarInfo(name)
+                ti.size = len(data)
+                ti.mtime = 0
+                tf.addfile(ti, io.BytesIO(data))
+    return buf.getvalue()

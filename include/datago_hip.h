@@ -206,6 +206,32 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
 dg_status dg_ctx_set_option(dg_ctx *ctx, const char *key, int64_t value);
 int64_t dg_ctx_get_stat(dg_ctx *ctx, const char *key);
 
+/* ------------------------------------------------------------ WebDataset shards */
+
+/* One tar member: its bytes are tar[data_off, data_off + data_len) (zero-copy);
+ * its path is names[name_off, name_off + name_len) (NUL-terminated). */
+typedef struct dg_wds_member {
+  uint64_t name_off, data_off, data_len;
+  uint32_t name_len, pad;
+} dg_wds_member;
+/* One sample: members[first, first + count), the reference extension first. */
+typedef struct dg_wds_sample {
+  uint32_t first, count;
+} dg_wds_sample;
+
+/* Index a WebDataset shard held in memory (pull_tarballs, generator_wds.rs:56-204):
+ * regular-file entries (ustar, GNU long names, pax paths), sample key =
+ * Path::file_stem of the path, kept when world_size <= 1 or
+ * dg_wds_key_hash(key) % world_size == rank (:133-148), consecutive equal keys
+ * grouped, members ending with reference_ext first (:154-166).  Call with
+ * NULL/0 capacities to get the counts (DG_ERR_SMALL_BUFFER), then again. */
+dg_status dg_wds_index(const uint8_t *tar, size_t len, int32_t rank, int32_t world_size, const char *reference_ext,
+                       dg_wds_member *members, int64_t members_cap, int64_t *n_members, char *names,
+                       size_t names_cap, size_t *names_len, dg_wds_sample *samples, int64_t samples_cap,
+                       int64_t *n_samples);
+/* Rust's DefaultHasher (SipHash-1-3, keys 0/0) of a &str: hash_fn (generator_wds.rs:50-54). */
+uint64_t dg_wds_key_hash(const char *key, size_t len);
+
 const char *dg_last_error(void);
 int32_t dg_abi_version(void);
 
