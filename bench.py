@@ -531,11 +531,11 @@ def main() -> int:
         }
         if world == 1 and not a.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(pool, targets, a.cpu_seconds, a.encode)
-        if png:  # the PMC file is for the JPEG workload
-            result["roofline"]["traffic"] = None
-            result["roofline"]["traffic_source"] = None
         else:
             result["cpu_baseline"] = None
+        if png or wds:  # the PMC file is for the configs[1] workload
+            result["roofline"]["traffic"] = None
+            result["roofline"]["traffic_source"] = None
         line = json.dumps(result)
         print(line, flush=True)
         if a.out:
