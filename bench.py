@@ -438,7 +438,7 @@ def main() -> int:
         ctx.set_option("timing", 0)
 
     # ---- end-to-end (host memory in and out: PCIe-inclusive), reported only
-    e2e = None
+    e2e = e2e_dev = None
     if a.e2e_steps > 0 and rank == 0:
         t1 = time.perf_counter()
         e2e_px = 0
@@ -447,6 +447,16 @@ def main() -> int:
             res = ctx.decode_batch([pool[i] for i in idx], [forced_pool[i] for i in idx])
             e2e_px += sum(dims[i][0] * dims[i][1] for i, r in zip(idx, res) if r[0] == 0)
         e2e = e2e_px / (time.perf_counter() - t1) / 1e6
+        # host coded bytes in -> HBM tensors out (the training-loop hand-off: PCIe carries the
+        # compressed stream only)
+        t1 = time.perf_counter()
+        e2e_px = 0
+        for k in range(a.e2e_steps):
+            idx = [(k * B_ + j) % len(pool) for j in range(B_)]
+            res = ctx.decode_batch_torch([pool[i] for i in idx], [forced_pool[i] for i in idx])
+            e2e_px += sum(dims[i][0] * dims[i][1] for i, r in zip(idx, res) if r[0] == 0)
+            del res
+        e2e_dev = e2e_px / (time.perf_counter() - t1) / 1e6
 
     result = None
     if rank == 0:
@@ -522,6 +532,7 @@ def main() -> int:
             "output_mpix_s": round(outpx_all / dt_max / 1e6, 2),
             "images_per_s": round(B_ * a.steps * world / dt_max, 1),
             "e2e_host_mpix_s": round(e2e, 2) if e2e else None,
+            "e2e_host_in_hbm_out_mpix_s": round(e2e_dev, 2) if e2e_dev else None,
             "corpus_gen_s": round(t_gen, 1),
             "stats": {"resync_rounds": ctx.stat("resync_rounds"), "fix_workgroups": ctx.stat("fix_workgroups"),
                       "write_mismatch": ctx.stat("write_mismatch"), "sync_iters_max": ctx.stat("sync_iters_max"),

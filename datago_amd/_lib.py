@@ -342,6 +342,47 @@ class Context:
         c = int(m.nbytes // (m.width * m.height)) if m.width and m.height else 0
         return DG_OK, out[: m.nbytes].reshape(m.height, m.width, c), m
 
+    # -- host bytes in, HBM out (a training loop consumes the tensors where they are)
+    def decode_batch_torch(self, datas: Sequence[bytes], forced: Optional[Sequence[int]] = None):
+        """Coded bytes go up once (PCIe carries the compressed stream, ~10x
+        less than the decoded pixels); outputs are torch uint8 CUDA tensors
+        the kernels write directly (no D2H, no host copy).  Returns
+        [(status, tensor or None, meta)]; HWC tensors, or 1-D bytes when
+        re-encoded."""
+        import torch as _t
+        n = len(datas)
+        fb = list(forced) if forced else [-1] * n
+        dev = _t.device("cuda", self.device)
+        offs, o = [], 0
+        for d in datas:
+            offs.append(o)
+            o += (len(d) + 16 + 15) // 16 * 16
+        host = _t.zeros(max(o, 16), dtype=_t.uint8).pin_memory()
+        hv = host.numpy()
+        for d, of in zip(datas, offs):
+            hv[of:of + len(d)] = np.frombuffer(d, np.uint8)
+        dev_in = host.to(dev, non_blocking=False)
+        sizes = [self.output_size(d, f)[1] for d, f in zip(datas, fb)]
+        outs = [_t.empty(max(nb, 1), dtype=_t.uint8, device=dev) for nb in sizes]
+        _t.cuda.current_stream(dev).synchronize()  # inputs resident before the library's streams read them
+        hbase, dbase = host.data_ptr(), dev_in.data_ptr()
+        ticket, metas = self.submit_device([hbase + of for of in offs], [dbase + of for of in offs],
+                                           [len(d) for d in datas], [t.data_ptr() for t in outs],
+                                           [max(nb, 1) for nb in sizes], fb)
+        self.wait(ticket)
+        res = []
+        for i in range(n):
+            m = metas[i]
+            if m.status != DG_OK:
+                res.append((m.status, None, m))
+            elif m.is_encoded:
+                res.append((DG_OK, outs[i][: m.nbytes], m))
+            else:
+                c = int(m.nbytes // (m.width * m.height)) if m.width and m.height else 0
+                res.append((DG_OK, outs[i][: m.nbytes].view(m.height, m.width, c), m))
+        del dev_in, host
+        return res
+
     # -- device-resident path (bench): coded bytes already in HBM
     def alloc(self, nbytes: int) -> int:
         p = ctypes.c_void_p()

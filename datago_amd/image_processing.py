@@ -194,3 +194,24 @@ def image_to_payload(data: bytes, img_tfm: Optional[ARAwareTransform], aspect_ra
     if st != _lib.DG_OK:
         raise ValueError(f"image decode failed: {_lib.STATUS_NAMES.get(st, st)}")
     return p
+
+
+def images_to_tensors(datas: List[bytes], img_tfm: Optional[ARAwareTransform], aspect_ratios: List[str],
+                      encoding: ImageEncoding = ImageEncoding(), device: int = 0):
+    """images_to_payloads for a GPU training loop: the
+    payload data stays in HBM as torch uint8 tensors written by the kernels,
+    without the D2H copy and the two to three host copies of the Python
+    hand-off (structs.rs:103-188).  Returns (status, tensor, meta) per image."""
+    if img_tfm is not None:
+        ctx = img_tfm.context(encoding)
+        forced = []
+        for ar in aspect_ratios:
+            k = img_tfm.table.find_key(ar) if ar else -1
+            if ar and k < 0:
+                raise KeyError("Aspect ratio not found in aspect ratio to size map")  # :334-336
+            forced.append(k)
+    else:
+        ctx = _decode_ctx(device, encoding)
+        forced = [-1] * len(datas)
+    return ctx.decode_batch_torch(datas, forced)
+

@@ -72,3 +72,21 @@ def test_db_sample_masks_and_reencode():
     s = process_db_sample("id", img, {"mask": mask}, {}, tfm, ImageEncoding(encode_images=True, encode_format=1))
     assert s.image.is_encoded and s.image.channels == -1
     assert s.unsupported == {"mask": 1}
+
+
+def test_torch_handoff_equals_host_path():
+    """images_to_tensors: outputs written into CUDA tensors (no D2H) equal the host path."""
+    import torch
+    from datago_amd.image_processing import images_to_payloads, images_to_tensors
+    tfm = _tfm()
+    datas = [synth.make_jpeg(40 + i, 300 + 50 * i, 200 + 70 * i, 90) for i in range(6)]
+    datas.append(synth.make_png(99, 333, 222, "RGBA"))
+    host = images_to_payloads(datas, tfm, [""] * len(datas))
+    dev = images_to_tensors(datas, tfm, [""] * len(datas))
+    for (st, p), (st2, t, m) in zip(host, dev):
+        assert st == 0 and st2 == 0 and t.is_cuda
+        assert t.cpu().numpy().tobytes() == p.data and (m.width, m.height) == (p.width, p.height)
+    enc = images_to_tensors(datas[:2], tfm, ["", ""], ImageEncoding(encode_images=True, encode_format=1))
+    ref = images_to_payloads(datas[:2], tfm, ["", ""], ImageEncoding(encode_images=True, encode_format=1))
+    for (st, t, m), (_, p) in zip(enc, ref):
+        assert st == 0 and m.is_encoded and t.cpu().numpy().tobytes() == p.data
