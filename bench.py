@@ -55,6 +55,8 @@ def parse():
                                                        "pmc_traffic.json"),
                     help="per-stage HBM bytes from a PMC run of this configuration (tools/pmc_traffic.py)")
     ap.add_argument("--wg-timing", action="store_true", help="debug: per-workgroup timing of the entropy kernels")
+    ap.add_argument("--inflight", type=int, default=2, help="batches in flight (context slots / output arenas)")
+    ap.add_argument("--hb-bands", type=int, default=0, help="band H kernel: 8-row bands per workgroup (0 = default)")
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=3, help="host-memory (PCIe-inclusive) steps")
@@ -325,6 +327,10 @@ def main() -> int:
         ctx.set_option("lead_bits", a.lead_bits)
     if a.wg_timing:
         ctx.set_option("wg_timing", 1)
+    if a.hb_bands:
+        ctx.set_option("hb_bands", a.hb_bands)
+    if a.inflight != 2:
+        ctx.set_option("slots", a.inflight)
     # ---- pool -> HBM (one arena, 16-byte aligned entries; wds: the shards themselves)
     if wds:
         host_arena = np.concatenate([tar_arena, np.zeros(64, np.uint8)])
@@ -350,7 +356,7 @@ def main() -> int:
     B_ = min(a.batch, 1 << 16)
     # output arena for one step (reused), sized for the largest B_ outputs
     out_cap = sum(sorted(out_bytes)[-B_:]) + 16 * B_
-    d_out = [ctx.alloc(out_cap), ctx.alloc(out_cap)]
+    d_out = [ctx.alloc(out_cap) for _ in range(a.inflight)]
 
     def submit(k: int):
         idx = [(k * B_ + j) % len(pool) for j in range(B_)]
@@ -358,7 +364,7 @@ def main() -> int:
         dp = [d_arena + offs[i] for i in idx]
         lens = [len(pool[i]) for i in idx]
         outs, caps, oo = [], [], 0
-        slot = k & 1  # two output arenas: batch k+1 is planned while batch k runs
+        slot = k % a.inflight  # one output arena per batch in flight
         for i in idx:
             outs.append(d_out[slot] + oo)
             caps.append(out_bytes[i])
@@ -375,16 +381,17 @@ def main() -> int:
         return idx
 
     def run(k0: int, n: int, on_done=None):
-        pend = submit(k0)
-        for k in range(k0 + 1, k0 + n):
-            nxt = submit(k)
-            idx = complete(pend)
+        pend = []  # batch k + inflight - 1 is submitted before batch k is waited on
+        for k in range(k0, k0 + n):
+            pend.append(submit(k))
+            if len(pend) >= a.inflight:
+                idx = complete(pend.pop(0))
+                if on_done:
+                    on_done(idx)
+        while pend:
+            idx = complete(pend.pop(0))
             if on_done:
                 on_done(idx)
-            pend = nxt
-        idx = complete(pend)
-        if on_done:
-            on_done(idx)
 
     run(0, max(1, a.warmup))
     # ---- timed region

@@ -98,7 +98,7 @@ struct ResizePass {
   uint32_t src_stride, dst_stride;  // bytes per row
   uint32_t width, rows;     // output extent of this pass (pixels, rows)
   uint32_t out0;            // first output (of out_size) computed: integral crops fold into the pass
-  uint32_t pad0;
+  uint32_t bands;           // band H kernel: kHBandRows-row bands per workgroup (option "hb_bands")
   uint32_t row0;            // H pass: first source row; V pass: source row of temp row 0
   uint32_t C;               // channels
   uint32_t kind;            // 0 none, 1 horizontal, 2 vertical
@@ -109,6 +109,7 @@ constexpr uint32_t kHFused = 1, kHDirect = 2;
 constexpr uint32_t kHBandRows = 8;    // rows per workgroup of the band H kernel
 constexpr uint32_t kHBandCols = 128;  // output columns per workgroup
 constexpr uint32_t kHSegPx = 640;     // LDS source segment (pixels) per row
+constexpr uint32_t kHBandsDefault = 4;  // default ResizePass::bands
 
 constexpr int kStages = 4;  // R1.H, R1.V, R2.H, R2.V
 

@@ -177,6 +177,17 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     side_stream_ = v != 0;
     return DG_OK;
   }
+  if (k == "slots") {
+    if (v < 1 || v > (int64_t)kMaxInflight) return DG_ERR_INVALID;
+    nslots_ = (int)v;
+    next_slot_ %= nslots_;
+    return DG_OK;
+  }
+  if (k == "hb_bands") {  // band H kernel: 8-row bands per workgroup
+    if (v < 1 || v > 64) return DG_ERR_INVALID;
+    hb_bands_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "png_chunked") {  // 0: every PNG inflates serially (test switch)
     chunked_off_ = v == 0;
     return DG_OK;
@@ -701,6 +712,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       ps.width = width;
       ps.rows = rows;
       ps.row0 = row0;
+      ps.bands = hb_bands_;
       ps.C = C;
       ps.dst_stride = (uint32_t)align_up((size_t)width * C, 16);
       o.pass_srcoff[stage] = (size_t)xoff * C;  // column window of the source (V passes)
@@ -995,7 +1007,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         uint32_t cnt = ps.rows * ((ps.width + 511) / 512);
         for (uint32_t it = 0; it < cnt; it++) b.lists[s == 0 ? L_RHX0 : L_RHX2].push_back({I, it});
       } else if (ps.kind == 1) {  // one workgroup per (band of rows, column tile)
-        uint32_t cnt = ((ps.rows + kHBandRows - 1) / kHBandRows) * ((ps.width + kHBandCols - 1) / kHBandCols);
+        const uint32_t rows_per_wg = kHBandRows * ps.bands;
+        uint32_t cnt = ((ps.rows + rows_per_wg - 1) / rows_per_wg) * ((ps.width + kHBandCols - 1) / kHBandCols);
         const int cls = ps.ksize <= 8 ? 0 : ps.ksize <= 16 ? 1 : ps.ksize <= 32 ? 2 : 3;
         for (uint32_t it = 0; it < cnt; it++) hb[s / 2][cls].push_back({I, it});
       } else {
@@ -1078,7 +1091,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   if (st) return st;
   stat_batches_++;
   *ticket = sl.batch->ticket;
-  next_slot_ ^= 1;
+  next_slot_ = (next_slot_ + 1) % nslots_;
   return DG_OK;
 }
 
@@ -1343,7 +1356,7 @@ dg_status Context::decode_one(const uint8_t *src, size_t len, int32_t forced, ui
     const bool ready = !pending_.empty() &&
                        ((int)pending_.size() >= coalesce_max_ || (int)pending_.size() >= callers_ - inflight_reqs_ ||
                         std::chrono::steady_clock::now() >= deadline);
-    if (ready && inflight_ < 2 && std::find(pending_.begin(), pending_.end(), &r) != pending_.end()) {
+    if (ready && inflight_ < nslots_ && std::find(pending_.begin(), pending_.end(), &r) != pending_.end()) {
       std::vector<OneReq *> batch;
       const size_t take = std::min(pending_.size(), (size_t)coalesce_max_);
       batch.assign(pending_.begin(), pending_.begin() + take);

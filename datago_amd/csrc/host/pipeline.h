@@ -80,8 +80,10 @@ struct Batch {
 };
 static_assert(32 >= 20, "list arrays");
 
-// One in-flight batch's device/pinned buffers.  Two slots let the host plan
-// and upload batch k+1 while the GPU still runs batch k.
+// One in-flight batch's device/pinned buffers.  Two (or, option "slots", up
+// to kMaxInflight) slots let the host plan and upload batch k+1 while the GPU
+// still runs batch k.
+constexpr int kMaxInflight = 4;
 struct Slot {
   DevBuf scratch, meta, input;
   DevBuf wgt;  // debug: per-workgroup timestamps of the entropy kernels (option "wg_timing")
@@ -178,7 +180,8 @@ class Context {
   size_t hpool_uploaded_ = 0, qpool_uploaded_ = 0;
   DevBuf d_hpool_, d_qpool_;
 
-  Slot slots_[2];
+  Slot slots_[kMaxInflight];
+  int nslots_ = 2;  // option "slots": batches in flight (each slot: own streams + scratch)
   int next_slot_ = 0;
   uint64_t next_ticket_ = 1;
 
@@ -190,6 +193,7 @@ class Context {
   int debug_flags_ = 0;
   bool wg_timing_ = false;
   bool chunked_off_ = false;  // option "png_chunked" = 0
+  uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
   int64_t stat_png_serial_ = 0, stat_png_chunks_ = 0;
   // "wg_timing" summaries of the last batch (microseconds): per kernel {span, mean, p90, max}
   double wgstat_[2][4] = {{0}};

@@ -991,10 +991,11 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
 template <int KMAX>
 __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps, uint32_t item, uint32_t *seg,
                                       uint8_t *ob, uint32_t *ext) {
+  // one workgroup: a tile of kHBandCols output columns x ps.bands bands of
+  // kHBandRows rows; the column tile's weights, source extent and descriptor
+  // reads are set up once and reused for every band
   const uint32_t tiles = (ps.width + kHBandCols - 1) / kHBandCols;
-  const uint32_t band = item / tiles, tile = item - band * tiles;
-  const uint32_t y0 = band * kHBandRows;
-  const uint32_t nrows = ps.rows - y0 < kHBandRows ? ps.rows - y0 : kHBandRows;
+  const uint32_t group = item / tiles, tile = item - group * tiles;
   const uint32_t x0 = tile * kHBandCols;
   const uint32_t x1 = x0 + kHBandCols < ps.width ? x0 + kHBandCols : ps.width;
   // coefficient tables cover all out_size outputs; this pass computes [out0, out0 + width)
@@ -1024,22 +1025,6 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
   uint32_t p1 = ext[1];
   if (p1 - p0 > kHSegPx) p1 = p0 + kHSegPx;  // host sizing guarantees this never triggers
   const uint32_t pe = p1 < ps.in_size ? p1 : ps.in_size;
-  // phase 1: fill
-  // fill: 32 threads per row (kHBandRows * 32 == 256), no divisions
-  static_assert(kHBandRows * 32 == 256, "fill mapping");
-  const uint32_t fr = t >> 5, fl = t & 31;
-  if (fr < nrows) {
-    if (ps.mode & kHFused) {
-      const uint32_t noct = (pe - p0 + 7) >> 3;
-      for (uint32_t q = fl; q < noct; q += 32)
-        hfill_color8(im, ps.row0 + y0 + fr, p0 + 8 * q, seg + fr * kHSegStride + 8 * q);
-    } else {
-      const uint32_t nu = (pe - p0 + 3) >> 2;
-      const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0 + fr) * ps.src_stride;
-      for (uint32_t u = fl; u < nu; u += 32)
-        hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * u, seg + fr * kHSegStride + 4 * u);
-    }
-  }
   uint32_t kw2[KMAX > 0 ? (KMAX + 1) / 2 : 1];  // weights (w_2j, w_2j+1) as i16 x 2
   const DG_GLOBAL int16_t *kp = coef + (size_t)(valid ? x : x0) * ksize;
   if (KMAX > 0) {
@@ -1050,33 +1035,56 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
       kw2[j] = lo | (hi << 16);
     }
   }
-  __syncthreads();
-  // phase 2: convolve (thread: column col, rows r0, r0 + 2, ...)
-  if (valid) {
-    const uint32_t off = st - p0, r0 = t / kHBandCols;
-    const int32_t prec = ps.precision;
-    if (C == 3)
-      hconv_rows<KMAX, 3>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
-    else if (C == 1)
-      hconv_rows<KMAX, 1>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
-    else if (C == 4)
-      hconv_rows<KMAX, 4>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
-    else
-      hconv_rows<KMAX, 2>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
-  }
-  __syncthreads();
-  // phase 3: store the band's rows, 16 bytes per thread per step
+  static_assert(kHBandRows * 32 == 256, "fill mapping");
+  const uint32_t fr = t >> 5, fl = t & 31;  // fill: 32 threads per row, no divisions
+  const uint32_t off = st - p0, r0 = t / kHBandCols;
+  const int32_t prec = ps.precision;
   const uint32_t rb = (x1 - x0) * C;  // <= kHBandCols * 4 = 512 bytes: 32 chunks of 16
-  DG_GLOBAL uint8_t *dst = gp<uint8_t>(ps.dst) + (size_t)y0 * ps.dst_stride + (size_t)x0 * C;
-  if (fr < nrows && fl * 16 < rb) {
-    const uint32_t r = fr, b = fl * 16;
-    DG_GLOBAL uint8_t *d = dst + (size_t)r * ps.dst_stride + b;
-    const uint8_t *o = ob + r * (kHBandCols * 4) + b;
-    if (b + 16 <= rb && (((uintptr_t)d) & 15) == 0) {
-      *(DG_GLOBAL u32x4 *)d = *(const u32x4 *)o;
-    } else {
-      const uint32_t e = b + 16 < rb ? 16 : rb - b;
-      for (uint32_t i = 0; i < e; i++) d[i] = o[i];
+  const uint32_t ybeg = group * kHBandRows * ps.bands;
+  for (uint32_t bi = 0; bi < ps.bands; bi++) {
+    const uint32_t y0 = ybeg + bi * kHBandRows;
+    if (y0 >= ps.rows) break;
+    const uint32_t nrows = ps.rows - y0 < kHBandRows ? ps.rows - y0 : kHBandRows;
+    // phase 1: fill
+    if (fr < nrows) {
+      if (ps.mode & kHFused) {
+        const uint32_t noct = (pe - p0 + 7) >> 3;
+        for (uint32_t q = fl; q < noct; q += 32)
+          hfill_color8(im, ps.row0 + y0 + fr, p0 + 8 * q, seg + fr * kHSegStride + 8 * q);
+      } else {
+        const uint32_t nu = (pe - p0 + 3) >> 2;
+        const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0 + fr) * ps.src_stride;
+        for (uint32_t u = fl; u < nu; u += 32)
+          hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * u, seg + fr * kHSegStride + 4 * u);
+      }
+    }
+    __syncthreads();
+    // phase 2: convolve (thread: column col, rows r0, r0 + 2, ...)
+    if (valid) {
+      if (C == 3)
+        hconv_rows<KMAX, 3>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
+      else if (C == 1)
+        hconv_rows<KMAX, 1>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
+      else if (C == 4)
+        hconv_rows<KMAX, 4>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
+      else
+        hconv_rows<KMAX, 2>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
+    }
+    __syncthreads();
+    // phase 3: store the band's rows, 16 bytes per thread per step (the next
+    // band's fill only touches seg; its barrier orders these ob reads before
+    // the next convolution writes ob)
+    DG_GLOBAL uint8_t *dst = gp<uint8_t>(ps.dst) + (size_t)y0 * ps.dst_stride + (size_t)x0 * C;
+    if (fr < nrows && fl * 16 < rb) {
+      const uint32_t r = fr, b = fl * 16;
+      DG_GLOBAL uint8_t *d = dst + (size_t)r * ps.dst_stride + b;
+      const uint8_t *o = ob + r * (kHBandCols * 4) + b;
+      if (b + 16 <= rb && (((uintptr_t)d) & 15) == 0) {
+        *(DG_GLOBAL u32x4 *)d = *(const u32x4 *)o;
+      } else {
+        const uint32_t e = b + 16 < rb ? 16 : rb - b;
+        for (uint32_t i = 0; i < e; i++) d[i] = o[i];
+      }
     }
   }
 }
