@@ -109,7 +109,7 @@ constexpr uint32_t kHFused = 1, kHDirect = 2;
 constexpr uint32_t kHBandRows = 8;    // rows per workgroup of the band H kernel
 constexpr uint32_t kHBandCols = 128;  // output columns per workgroup
 constexpr uint32_t kHSegPx = 640;     // LDS source segment (pixels) per row
-constexpr uint32_t kHBandsDefault = 4;  // default ResizePass::bands
+constexpr uint32_t kHBandsDefault = 8;  // default ResizePass::bands
 
 constexpr int kStages = 4;  // R1.H, R1.V, R2.H, R2.V
 

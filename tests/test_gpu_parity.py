@@ -145,6 +145,32 @@ def test_subsequence_sizes_agree(ctx_dec):
         assert ctx.stat("write_mismatch") == 0
 
 
+@pytest.mark.parametrize("bands,slots", [(1, 1), (3, 2), (8, 3), (64, 4)])
+def test_band_and_slot_options_bit_exact(bands, slots):
+    # the band H kernel's rows per workgroup (hb_bands) and the batches in
+    # flight (slots) change only the partitioning: outputs stay bit-exact
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=1024, downsampling_ratio=32,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+    ctx.set_option("hb_bands", bands)
+    ctx.set_option("slots", slots)
+    datas = _rand_jpegs(5, 6, maxdim=1300)
+    t = B.ARAwareTransform(1024, 32, 0.5, 2.0)
+    for _ in range(2):  # consecutive batches cycle through the slots
+        for data, (st, arr, meta) in zip(datas, ctx.decode_batch(datas)):
+            assert st == 0
+            w, h = O.jpeg_info(data)[1:3]
+            assert np.array_equal(arr, _oracle_resized(data, *t.target_size(w, h))), (bands, slots, (w, h))
+
+
+def test_band_and_slot_options_validated():
+    L = _lib()
+    ctx = L.Context(0)
+    for k, v in (("hb_bands", 0), ("hb_bands", 65), ("slots", 0), ("slots", 5)):
+        with pytest.raises(Exception):
+            ctx.set_option(k, v)
+
+
 def test_forced_bucket_alignment(ctx512):
     # worker_wds.rs:68-76: later members are forced into the first image's bucket
     t = ctx512.buckets
