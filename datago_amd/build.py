@@ -24,6 +24,7 @@ SOURCES = [
     ("kernels.hip", True),
     ("dg_png.hip", True),
     ("dg_enc.hip", True),
+    ("dg_prog.hip", True),
     ("host/jpeg_enc.cpp", False),
     ("host/wds.cpp", False),
     ("host/png_header.cpp", False),

@@ -257,6 +257,8 @@ struct ImageDesc {
   uint32_t color_fused;     // 1: pass[0] converts colour itself, pix is never written
   // ---- format, PNG, alpha handling, final conversion
   uint32_t fmt;             // kFmtJpeg / kFmtPng
+  uint32_t prog;            // progressive JPEG: scans decoded by k_prog_scan (0: sequential)
+  uint32_t prog_pad;
   uint32_t copy_mode;       // k_copy: 0 same channels, 1 L->RGB, 2 RGBA->RGB blend over gray,
                             // 3 LA->RGB of a resized LA image (GrayImage over the LA bytes, B3),
                             // 4 LA->RGB of an unresized LumaA8 (alpha dropped)
@@ -264,6 +266,27 @@ struct ImageDesc {
   AlphaOp aop[kAlphaPoints];
   EncDesc enc;
 };
+
+// ---- progressive JPEG (ImageDesc::prog > 0).  The coefficient blocks are
+// zeroed (k_prog_zero), then every scan is decoded by one lane of k_prog_scan
+// straight from the stuffed bytes.  Scans that touch disjoint (component,
+// coefficient band) sets are independent; the host groups them into levels
+// (a scan's level = 1 + the highest level of an earlier overlapping scan),
+// one launch per level.
+struct ProgScan {
+  uint64_t data;        // device address of the scan's first entropy-coded byte
+  uint32_t len;         // entropy-coded bytes (up to the next non-RST marker)
+  uint32_t image;       // descriptor index
+  uint32_t ns;          // components in the scan
+  uint32_t comp[4];     // their component indices
+  uint16_t dc[4];       // DC-first scans: Huffman pool index per scan component
+  uint16_t ac;          // AC scans: Huffman pool index
+  uint16_t pad0;
+  uint32_t ss, se, ah, al;
+  uint32_t restart;     // restart interval (MCUs; blocks when ns == 1), 0 = none
+  uint32_t level;
+};
+constexpr uint32_t kProgZeroBytes = 65536;  // coefficient bytes zeroed per k_prog_zero workgroup
 
 // One workgroup's work: an image and the first item it handles.
 struct WgItem {

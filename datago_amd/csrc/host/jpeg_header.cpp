@@ -118,6 +118,51 @@ void parse_jpeg_header(const uint8_t *d, size_t n, JpegHeader &h) {
         if (h.comp[c].td > 3 || h.comp[c].ta > 3) return fail(h, JH_CORRUPT, "bad table selector");
       }
       h.scan_off = p + (size_t)L;
+      if (h.progressive) {
+        // T.81 G.1.2 scan parameters (libjpeg jdphuff.c start_pass_phuff_decoder checks)
+        JpegScan sc;
+        sc.ns = ns;
+        sc.ss = s[1 + 2 * ns];
+        sc.se = s[2 + 2 * ns];
+        sc.ah = s[3 + 2 * ns] >> 4;
+        sc.al = s[3 + 2 * ns] & 15;
+        sc.restart = h.restart;
+        if (sc.ss == 0 ? sc.se != 0 : (sc.se < sc.ss || sc.se > 63 || ns != 1))
+          return fail(h, JH_CORRUPT, "bad progressive scan band");
+        if ((sc.ah != 0 && sc.al != sc.ah - 1) || sc.al > 13) return fail(h, JH_CORRUPT, "bad successive approximation");
+        for (int i = 0; i < ns; i++) {
+          const JpegComponent &k = h.comp[h.scan_comp[i]];
+          sc.comp[i] = h.scan_comp[i];
+          if (sc.ss == 0 && sc.ah == 0) {
+            if (!h.dc[k.td].present) return fail(h, JH_CORRUPT, "missing Huffman table");
+            sc.dc_tab[i] = (int)h.tables.size();
+            h.tables.push_back(h.dc[k.td]);
+          }
+        }
+        if (sc.ss > 0) {
+          const JpegComponent &k = h.comp[h.scan_comp[0]];
+          if (!h.ac[k.ta].present) return fail(h, JH_CORRUPT, "missing Huffman table");
+          sc.ac_tab = (int)h.tables.size();
+          h.tables.push_back(h.ac[k.ta]);
+        }
+        // the scan's data ends at the first marker that is not RSTn
+        size_t q = h.scan_off;
+        for (;;) {
+          const uint8_t *f = (const uint8_t *)memchr(d + q, 0xFF, n - q);
+          if (!f || (size_t)(f - d) + 1 >= n) return fail(h, JH_CORRUPT, "truncated progressive scan");
+          q = (size_t)(f - d);
+          const uint8_t c = d[q + 1];
+          if (c != 0x00 && c != 0xFF && !(c >= 0xD0 && c <= 0xD7)) break;
+          q++;
+        }
+        sc.off = h.scan_off;
+        sc.end = q;
+        h.scans.push_back(sc);
+        if (h.scans.size() > 256) return fail(h, JH_UNSUPPORTED, "more than 256 progressive scans");
+        p = q;
+        if (d[q + 1] == 0xD9) break;  // EOI
+        continue;
+      }
       h.scan_end = n;
       if (n >= 2 && d[n - 2] == 0xFF && d[n - 1] == 0xD9) {
         h.scan_end = n - 2;
@@ -135,12 +180,25 @@ void parse_jpeg_header(const uint8_t *d, size_t n, JpegHeader &h) {
     p += (size_t)L;
   }
   // ---- what the GPU path decodes
-  if (h.progressive) return fail(h, JH_UNSUPPORTED, "progressive JPEG");
   if (h.arithmetic) return fail(h, JH_UNSUPPORTED, "arithmetic-coded JPEG");
-  if (h.lossless || (h.sof != 0xC0 && h.sof != 0xC1)) return fail(h, JH_UNSUPPORTED, "unsupported SOF type");
+  if (h.lossless || (h.sof != 0xC0 && h.sof != 0xC1 && h.sof != 0xC2)) return fail(h, JH_UNSUPPORTED, "unsupported SOF type");
   if (h.precision != 8) return fail(h, JH_UNSUPPORTED, "12/16-bit JPEG");
   if (h.ncomp != 1 && h.ncomp != 3) return fail(h, JH_UNSUPPORTED, "CMYK/2-component JPEG");
-  if (h.scan_ncomp != h.ncomp) return fail(h, JH_UNSUPPORTED, "non-interleaved multi-scan JPEG");
+  if (!h.progressive && h.scan_ncomp != h.ncomp) return fail(h, JH_UNSUPPORTED, "non-interleaved multi-scan JPEG");
+  if (h.progressive) {
+    // coefficient precision after the last scan (libjpeg coef_bits): the DC and
+    // AC 1..9 must end exact, or libjpeg would smooth blocks (jdcoefct.c smoothing_ok)
+    int bits[4][64];
+    for (int c = 0; c < 4; c++)
+      for (int k = 0; k < 64; k++) bits[c][k] = -1;
+    for (const JpegScan &sc : h.scans)
+      for (int i = 0; i < sc.ns; i++)
+        for (int k = sc.ss; k <= sc.se; k++) bits[sc.comp[i]][k] = sc.al;
+    for (int c = 0; c < h.ncomp; c++)
+      for (int k = 0; k < 10; k++)
+        if (bits[c][k] != 0) return fail(h, JH_UNSUPPORTED, "incomplete progressive refinement (block smoothing)");
+    h.scan_end = h.scans.empty() ? h.scan_off : h.scans.back().end;
+  }
   h.hmax = h.vmax = 1;
   for (int c = 0; c < h.ncomp; c++) {
     if (h.comp[c].h > h.hmax) h.hmax = h.comp[c].h;
@@ -160,7 +218,7 @@ void parse_jpeg_header(const uint8_t *d, size_t n, JpegHeader &h) {
   }
   for (int c = 0; c < h.ncomp; c++) {
     if (!h.qpresent[h.comp[c].tq]) return fail(h, JH_CORRUPT, "missing quantisation table");
-    if (!h.dc[h.comp[c].td].present || !h.ac[h.comp[c].ta].present)
+    if (!h.progressive && (!h.dc[h.comp[c].td].present || !h.ac[h.comp[c].ta].present))
       return fail(h, JH_CORRUPT, "missing Huffman table");
   }
   // colour space guess (libjpeg jdapimin.c default_decompress_parms)

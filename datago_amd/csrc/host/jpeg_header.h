@@ -3,11 +3,14 @@
 // Replaces the header half of `ImageReader::with_guessed_format().decode()`
 // (reference worker_files.rs:14-16; image 0.25.9 -> zune-jpeg 0.5.12): it
 // validates the stream, decides whether the GPU path can decode it (baseline /
-// extended sequential Huffman, 8-bit, 1 or 3 components, h2v1/h2v2/1x1 chroma,
-// single interleaved scan) and gathers everything the kernels need.
+// extended sequential Huffman with a single interleaved scan, or progressive
+// Huffman; 8-bit, 1 or 3 components, h2v1/h2v2/1x1 chroma) and gathers
+// everything the kernels need.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
+
+#include <vector>
 
 #include "../dg_types.h"
 
@@ -18,6 +21,19 @@ struct HuffSpec {
   uint8_t bits[17] = {0};
   uint8_t vals[256] = {0};
   int nvals = 0;
+};
+
+// One scan of a progressive JPEG (T.81 G.1.2): its components, spectral
+// band [ss, se], successive-approximation bits ah/al, the Huffman tables in
+// force when it starts and its entropy-coded bytes [off, end).
+struct JpegScan {
+  int ns = 0;
+  int comp[4] = {0, 0, 0, 0};
+  int dc_tab[4] = {-1, -1, -1, -1};  // index into JpegHeader::tables (DC first scans)
+  int ac_tab = -1;                    // AC scans (ns == 1)
+  int ss = 0, se = 0, ah = 0, al = 0;
+  int restart = 0;
+  size_t off = 0, end = 0;
 };
 
 struct JpegComponent {
@@ -47,6 +63,9 @@ struct JpegHeader {
   size_t scan_end = 0;   // end of entropy data (EOI position if found at the end)
   int hmax = 1, vmax = 1;
   int colorspace = CS_YCC;
+  // progressive files: every scan, and snapshots of the Huffman tables they use
+  std::vector<JpegScan> scans;
+  std::vector<HuffSpec> tables;
 };
 
 // Parse up to (and including) the SOS header.  Only touches bytes before the

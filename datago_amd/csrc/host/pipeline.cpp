@@ -34,11 +34,11 @@ void set_error(const std::string &s) { g_last_error = s; }
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-static const char *kStageNames[] = {"upload",     "png_inflate", "png_unfilter", "destuff",   "huff_sync",
-                                    "huff_fix",   "huff_scan",   "huff_write",   "coeffs",    "idct",
-                                    "color",      "resize_h1",   "resize_v1",    "resize_h2", "resize_v2",
-                                    "copy",       "encode",      "download"};
-static const int kNumStages = 18;
+static const char *kStageNames[] = {"upload",     "png_inflate", "png_unfilter", "destuff",   "prog_scans",
+                                    "huff_sync",  "huff_fix",    "huff_scan",    "huff_write", "coeffs",
+                                    "idct",       "color",       "resize_h1",    "resize_v1", "resize_h2",
+                                    "resize_v2",  "copy",        "encode",       "download"};
+static const int kNumStages = 19;
 
 Context::Context(int device, const dg_image_config *cfg) : device_(device) {
   if (cfg && cfg->crop_and_resize) {
@@ -482,10 +482,17 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     ImagePlan &p = b.plans[i];
     if (p.status || p.fmt != kFmtJpeg) continue;
     bool ok = true;
-    for (int c = 0; c < p.hdr.ncomp; c++) {
-      if (pool_huff(p.hdr.dc[p.hdr.comp[c].td]) < 0 || pool_huff(p.hdr.ac[p.hdr.comp[c].ta]) < 0 ||
-          pool_quant(p.hdr.q[p.hdr.comp[c].tq]) < 0)
-        ok = false;
+    if (p.hdr.progressive) {  // the tables each scan uses
+      for (const HuffSpec &t : p.hdr.tables)
+        if (pool_huff(t) < 0) ok = false;
+      for (int c = 0; c < p.hdr.ncomp; c++)
+        if (pool_quant(p.hdr.q[p.hdr.comp[c].tq]) < 0) ok = false;
+    } else {
+      for (int c = 0; c < p.hdr.ncomp; c++) {
+        if (pool_huff(p.hdr.dc[p.hdr.comp[c].td]) < 0 || pool_huff(p.hdr.ac[p.hdr.comp[c].ta]) < 0 ||
+            pool_quant(p.hdr.q[p.hdr.comp[c].tq]) < 0)
+          ok = false;
+      }
     }
     if (!ok) {
       p.status = DG_ERR_CORRUPT;
@@ -504,7 +511,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   if (!sub_bits) {
     uint64_t coded = 0;
     for (int i = 0; i < n; i++)
-      if (!b.plans[i].status && b.plans[i].fmt == kFmtJpeg) coded += b.plans[i].hdr.scan_end - b.plans[i].hdr.scan_off;
+      if (!b.plans[i].status && b.plans[i].fmt == kFmtJpeg && !b.plans[i].hdr.progressive)
+        coded += b.plans[i].hdr.scan_end - b.plans[i].hdr.scan_off;
     sub_bits = coded >= (64ull << 20) ? 4096 : 2048;
   }
   last_sub_bits_ = sub_bits;
@@ -647,11 +655,17 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     };
     d.slotmap = 0;
     for (int c = 0; c < h.ncomp; c++) {
-      d.slotmap |= (uint32_t)slot_of(pool_huff(h.dc[h.comp[c].td])) << ((2 * c) * 4);
-      d.slotmap |= (uint32_t)slot_of(pool_huff(h.ac[h.comp[c].ta])) << ((2 * c + 1) * 4);
+      if (!h.progressive) {
+        d.slotmap |= (uint32_t)slot_of(pool_huff(h.dc[h.comp[c].td])) << ((2 * c) * 4);
+        d.slotmap |= (uint32_t)slot_of(pool_huff(h.ac[h.comp[c].ta])) << ((2 * c + 1) * 4);
+      }
       d.qpool[c] = (uint16_t)pool_quant(h.q[h.comp[c].tq]);
     }
     d.nslots = (uint8_t)nslots;
+    if (h.progressive) {  // scans decoded by k_prog_scan (records built once the source address is known)
+      d.prog = (uint32_t)h.scans.size();
+      if (host_io) in_off[i] = IN.take(lens[i] + 16, 16);
+    } else {
     // entropy data
     d.scan_len = (uint32_t)(h.scan_end - h.scan_off);
     d.sub_bits = sub_bits;
@@ -671,6 +685,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     o.mk = L.take((size_t)d.mk_cap * 4, 16);
     o.chunk = L.take((size_t)d.nchunk * 16, 16);
     if (host_io) in_off[i] = IN.take(lens[i] + 16, 16);
+    }  // sequential
     // buffers
     o.coef = CO.take((size_t)d.total_blocks * 128);
     for (int c = 0; c < h.ncomp; c++) o.plane[c] = L.take((size_t)d.cbw[c] * 8 * d.cbh[c] * 8);
@@ -934,9 +949,45 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     } else {
     d.scan = (uint64_t)(uintptr_t)(src + h.scan_off);
     d.coef = (uint64_t)(uintptr_t)((char *)sl.coef.p + o.coef);
+    if (d.prog) {
+      // one record per scan; level = 1 + the highest level of an earlier scan
+      // sharing a component and an overlapping coefficient band
+      const size_t first = b.pscans.size();
+      for (size_t j = 0; j < h.scans.size(); j++) {
+        const JpegScan &sc = h.scans[j];
+        ProgScan r;
+        memset(&r, 0, sizeof(r));
+        r.data = (uint64_t)(uintptr_t)(src + sc.off);
+        r.len = (uint32_t)(sc.end - sc.off);
+        r.image = (uint32_t)b.desc_of[i];
+        r.ns = (uint32_t)sc.ns;
+        for (int q = 0; q < sc.ns; q++) {
+          r.comp[q] = (uint32_t)sc.comp[q];
+          r.dc[q] = sc.dc_tab[q] >= 0 ? (uint16_t)pool_huff(h.tables[sc.dc_tab[q]]) : 0;
+        }
+        r.ac = sc.ac_tab >= 0 ? (uint16_t)pool_huff(h.tables[sc.ac_tab]) : 0;
+        r.ss = (uint32_t)sc.ss;
+        r.se = (uint32_t)sc.se;
+        r.ah = (uint32_t)sc.ah;
+        r.al = (uint32_t)sc.al;
+        r.restart = (uint32_t)sc.restart;
+        uint32_t lvl = 0;
+        for (size_t e = 0; e < j; e++) {
+          const JpegScan &pr = h.scans[e];
+          if (pr.se < sc.ss || sc.se < pr.ss) continue;
+          bool share = false;
+          for (int x = 0; x < pr.ns; x++)
+            for (int y = 0; y < sc.ns; y++) share |= pr.comp[x] == sc.comp[y];
+          if (share) lvl = std::max(lvl, b.pscans[first + e].level + 1);
+        }
+        r.level = lvl;
+        b.pscans.push_back(r);
+      }
+    } else {
     d.ds = (uint64_t)(uintptr_t)(S + o.ds);
     d.mk = (uint64_t)(uintptr_t)(S + o.mk);
     d.chunk = (uint64_t)(uintptr_t)(S + o.chunk);
+    }
     for (int c = 0; c < h.ncomp; c++) d.plane[c] = (uint64_t)(uintptr_t)(S + o.plane[c]);
     d.pix = h.ncomp == 3 && !d.color_fused ? (uint64_t)(uintptr_t)(S + o.pix) : 0;
     }  // JPEG
@@ -987,10 +1038,15 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       if (d.png.expand)
         for (uint32_t it = 0; it < d.width * d.height; it += 256) b.lists[L_EXPAND].push_back({I, it});
     } else {
+    if (d.prog) {
+      const uint64_t bytes = (uint64_t)d.total_blocks * 128;
+      for (uint32_t c = 0; (uint64_t)c * kProgZeroBytes < bytes; c++) b.lists[L_PROG_ZERO].push_back({I, c});
+    } else {
     for (uint32_t w = 0; w < d.nsub; w += kSubPerWg) b.lists[L_HUFF].push_back({I, w});
     for (uint32_t w = 0; w < d.nsub; w += kSubPerWg - 1) b.lists[L_SYNC].push_back({I, w});
     for (uint32_t c = 0; c < d.nchunk; c++) b.lists[L_DESTUFF].push_back({I, c});
     b.lists[L_SCAN].push_back({I, 0});
+    }
     uint32_t items = 0;
     for (uint32_t c = 0; c < d.ncomp; c++) items += d.cbh[c] * ((d.cbw[c] + 63) / 64);  // kIdctBlocks
     for (uint32_t it = 0; it < items; it++) b.lists[L_IDCT].push_back({I, it});
@@ -1029,6 +1085,19 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   for (uint32_t j = 0; j < (uint32_t)b.gjobs.size(); j++)
     for (uint32_t pc = 0; pc * kGatherPiece < b.gjobs[j].len; pc++) b.lists[L_GATHER].push_back({j, pc});
+  b.prog_level_n.clear();
+  for (uint32_t j = 0; j < (uint32_t)b.pscans.size(); j++) {  // L_PROG: scans grouped by level
+    const uint32_t lv = b.pscans[j].level;
+    if (lv >= b.prog_level_n.size()) b.prog_level_n.resize(lv + 1, 0);
+    b.prog_level_n[lv]++;
+  }
+  {
+    std::vector<uint32_t> at(b.prog_level_n.size(), 0);
+    for (size_t lv = 1; lv < at.size(); lv++) at[lv] = at[lv - 1] + b.prog_level_n[lv - 1];
+    b.lists[L_PROG].resize(b.pscans.size());
+    for (uint32_t j = 0; j < (uint32_t)b.pscans.size(); j++)
+      b.lists[L_PROG][at[b.pscans[j].level]++] = WgItem{b.pscans[j].image, j};
+  }
   for (int h = 0; h < 2; h++)
     for (int c = 0; c < 4; c++) {
       b.hclass[h][c] = (uint32_t)hb[h][c].size();
@@ -1042,6 +1111,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   for (int l = 0; l < L_COUNT; l++) b.list_off[l] = M.take(b.lists[l].size() * sizeof(WgItem));
   b.gjob_off = M.take(b.gjobs.size() * sizeof(GatherJob));
   b.ichunk_off = M.take(b.ichunks.size() * sizeof(InfChunk));
+  b.pscan_off = M.take(b.pscans.size() * sizeof(ProgScan));
   b.blob_off = M.take(b.blob.size());
   b.meta_bytes = M.off;
   st = ensure(sl.meta, b.meta_bytes + 256, sl.st);
@@ -1071,6 +1141,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     if (!b.lists[l].empty()) memcpy(P + b.list_off[l], b.lists[l].data(), b.lists[l].size() * sizeof(WgItem));
   if (!b.gjobs.empty()) memcpy(P + b.gjob_off, b.gjobs.data(), b.gjobs.size() * sizeof(GatherJob));
   if (!b.ichunks.empty()) memcpy(P + b.ichunk_off, b.ichunks.data(), b.ichunks.size() * sizeof(InfChunk));
+  if (!b.pscans.empty()) memcpy(P + b.pscan_off, b.pscans.data(), b.pscans.size() * sizeof(ProgScan));
   if (!b.blob.empty()) memcpy(P + b.blob_off, b.blob.data(), b.blob.size());
   if (host_io) {
     for (int i = 0; i < n; i++)
@@ -1145,6 +1216,16 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     launch_destuff_count(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
     launch_destuff_scan(sl.st, dm, lst(L_SCAN), cnt(L_SCAN));
     launch_destuff_write(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
+  }
+  if (next()) return DG_ERR_DEVICE;
+  if (!from_fix && !b.pscans.empty()) {  // progressive JPEG: zero, then the scans level by level
+    launch_prog_zero(sl.st, dd, lst(L_PROG_ZERO), cnt(L_PROG_ZERO));
+    const ProgScan *ps = (const ProgScan *)(M + b.pscan_off);
+    uint32_t at = 0;
+    for (uint32_t nl : b.prog_level_n) {
+      launch_prog_scan(sl.st, dd, ps, lst(L_PROG) + at, nl, hp);
+      at += nl;
+    }
   }
   if (next()) return DG_ERR_DEVICE;
   Ckpt *ck = (Ckpt *)((char *)sl.scratch.p + sl.ckpt_off);

@@ -62,6 +62,9 @@ struct Batch {
   bool any_png = false, any_alpha = false, any_enc = false;
   size_t words_off = 0, words_bytes = 0;  // contiguous encoder bit buffers (zeroed per batch)
   size_t enctab_off = 0;                  // EncTables in the blob
+  std::vector<ProgScan> pscans;           // progressive JPEG scans of the batch
+  size_t pscan_off = 0;
+  std::vector<uint32_t> prog_level_n;     // L_PROG holds the scans level by level: counts
   // band H lists (L_RH0, L_RH2) are grouped by weight-count class (<=8, <=16,
   // <=32, more): hclass[stage/2][k] items of class k, in that order
   uint32_t hclass[2][4] = {{0}};
@@ -78,7 +81,6 @@ struct Batch {
   BatchFlags flags = {0, 0, 0, 0};
   std::vector<float> stage_ms;
 };
-static_assert(32 >= 20, "list arrays");
 
 // One in-flight batch's device/pinned buffers.  Two (or, option "slots", up
 // to kMaxInflight) slots let the host plan and upload batch k+1 while the GPU
@@ -107,8 +109,10 @@ enum ListId {
   L_GATHER, L_PNG, L_EXPAND, L_ALPHA0, L_ALPHA1, L_ALPHA2,  // PNG decode, alpha programs
   L_INF_FIND, L_INF_RES,                                    // chunk-parallel inflate
   L_ENC_MCU, L_ENC_BLK, L_ENC_IMG,                          // JPEG re-encode
+  L_PROG_ZERO, L_PROG,                                      // progressive JPEG
   L_COUNT
 };
+static_assert((int)L_COUNT <= 32, "Batch::lists");
 
 class Context {
  public:

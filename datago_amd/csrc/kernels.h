@@ -36,6 +36,11 @@ void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage);
 // final copy / gray->RGB expansion: 256 output pixels per workgroup
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+// progressive JPEG (dg_prog.hip): zero coefficients (kProgZeroBytes per
+// workgroup), then one lane per scan of one dependency level
+void launch_prog_zero(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_prog_scan(hipStream_t st, const ImageDesc *imgs, const ProgScan *scans, const WgItem *list, uint32_t n,
+                      const HuffTable *pool);
 
 }  // namespace dg
 

@@ -51,10 +51,10 @@ def synth_pixels(rng: np.random.Generator, w: int, h: int, gray: bool = False) -
 
 
 def encode_jpeg(arr: np.ndarray, quality: int = 90, subsampling: str = "4:2:0",
-                restart_marker_rows: int = 0, restart_marker_blocks: int = 0) -> bytes:
+                restart_marker_rows: int = 0, restart_marker_blocks: int = 0, progressive: bool = False) -> bytes:
     im = Image.fromarray(arr)
     buf = io.BytesIO()
-    kw = dict(quality=int(quality))
+    kw = dict(quality=int(quality), progressive=bool(progressive))
     if im.mode == "RGB":
         kw["subsampling"] = SUBSAMPLING[subsampling]
     if restart_marker_rows:
@@ -66,9 +66,18 @@ def encode_jpeg(arr: np.ndarray, quality: int = 90, subsampling: str = "4:2:0",
 
 
 def make_jpeg(seed: int, w: int, h: int, quality: int = 90, subsampling: str = "4:2:0",
-              gray: bool = False, restart_marker_rows: int = 0) -> bytes:
+              gray: bool = False, restart_marker_rows: int = 0, progressive: bool = False) -> bytes:
     rng = np.random.default_rng(seed)
-    return encode_jpeg(synth_pixels(rng, w, h, gray), quality, subsampling, restart_marker_rows)
+    return encode_jpeg(synth_pixels(rng, w, h, gray), quality, subsampling, restart_marker_rows,
+                       progressive=progressive)
+
+
+def make_cmyk_jpeg(seed: int, w: int, h: int, quality: int = 90) -> bytes:
+    """A 4-component (Adobe CMYK) JPEG: valid, outside the GPU path."""
+    rng = np.random.default_rng(seed)
+    buf = io.BytesIO()
+    Image.fromarray(synth_pixels(rng, w, h)).convert("CMYK").save(buf, format="JPEG", quality=int(quality))
+    return buf.getvalue()
 
 
 def mixed_spec(seed: int, n: int, short_min: int = 256, short_max: int = 2048,

@@ -3,10 +3,14 @@
  * bench.py's cpu_baseline leg may load this file's library; the product path
  * (datago_amd/csrc) never links or calls it.
  *
- * A plain-C, scalar restatement of baseline/extended-sequential Huffman JPEG
- * decoding, written from ITU-T T.81 and following libjpeg-turbo's
- * decompression semantics (the decoder PIL uses in this image):
+ * A plain-C, scalar restatement of baseline/extended-sequential and
+ * progressive Huffman JPEG decoding, written from ITU-T T.81 and following
+ * libjpeg-turbo's decompression semantics (the decoder PIL uses in this image):
  *   - Huffman decode + HUFF_EXTEND per T.81 F.2.2 (libjpeg jdhuff.c),
+ *   - progressive scans per T.81 G.1.2 (libjpeg jdphuff.c: DC first/refine,
+ *     AC first with EOB runs, AC refine with correction bits); files whose
+ *     coefficients 1..9 stay incomplete after the last scan (libjpeg would
+ *     apply block smoothing, jdcoefct.c smoothing_ok) are UNSUPPORTED,
  *   - ISLOW integer IDCT (libjpeg jidctint.c, CONST_BITS=13, PASS1_BITS=2) with
  *     the SIMD build's saturating output (clamp to [-128,127] + 128),
  *   - "fancy" triangular chroma upsampling h2v1 / h2v2 (libjpeg jdsample.c),
@@ -71,7 +75,11 @@ typedef struct {
   int scan_comp[4];
   size_t scan_off;     /* offset of the first entropy-coded byte */
   int saw_sof, saw_sos;
+  int progressive;
+  int ss, se, ah, al;  /* spectral selection / successive approximation of the current scan */
 } oj_jpeg;
+
+#define OJ_EOI 100 /* parse_markers reached EOI (internal) */
 
 /* ---------------------------------------------------------------- markers */
 
@@ -95,10 +103,9 @@ static int build_huff(oj_huff *t) {
 
 static int rd16(const uint8_t *p) { return (p[0] << 8) | p[1]; }
 
-static int parse_headers(oj_jpeg *j, const uint8_t *d, size_t n) {
-  memset(j, 0, sizeof(*j));
-  if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return OJ_CORRUPT;
-  size_t p = 2;
+/* Process markers from offset p up to the next SOS (OJ_OK, scan fields set)
+ * or EOI (OJ_EOI). */
+static int parse_markers(oj_jpeg *j, const uint8_t *d, size_t n, size_t p) {
   for (;;) {
     /* find marker */
     while (p < n && d[p] != 0xFF) p++;
@@ -106,7 +113,7 @@ static int parse_headers(oj_jpeg *j, const uint8_t *d, size_t n) {
     if (p >= n) return OJ_CORRUPT;
     int m = d[p++];
     if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
-    if (m == 0xD9) return OJ_CORRUPT; /* EOI before SOS */
+    if (m == 0xD9) return OJ_EOI;
     if (p + 2 > n) return OJ_CORRUPT;
     int L = rd16(d + p);
     if (L < 2 || p + L > n) return OJ_CORRUPT;
@@ -116,9 +123,11 @@ static int parse_headers(oj_jpeg *j, const uint8_t *d, size_t n) {
       case 0xC0: case 0xC1: /* baseline / extended sequential Huffman */
       case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7:
       case 0xC9: case 0xCA: case 0xCB: case 0xCD: case 0xCE: case 0xCF: {
-        if (m != 0xC0 && m != 0xC1) return OJ_UNSUPPORTED;
+        if (m != 0xC0 && m != 0xC1 && m != 0xC2) return OJ_UNSUPPORTED;
         if (len < 6) return OJ_CORRUPT;
+        if (j->saw_sof) return OJ_CORRUPT; /* second SOF */
         j->sof = m;
+        j->progressive = (m == 0xC2);
         j->precision = s[0];
         j->H = rd16(s + 1);
         j->W = rd16(s + 3);
@@ -194,9 +203,24 @@ static int parse_headers(oj_jpeg *j, const uint8_t *d, size_t n) {
           if (j->comp[c].td > 3 || j->comp[c].ta > 3) return OJ_CORRUPT;
         }
         int ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ahal = s[3 + 2 * ns];
-        if (ss != 0 || se != 63 || ahal != 0) return OJ_CORRUPT;
-        /* only single-scan images are in scope (all components interleaved) */
-        if (ns != j->ncomp) return OJ_UNSUPPORTED;
+        j->ss = ss;
+        j->se = se;
+        j->ah = ahal >> 4;
+        j->al = ahal & 15;
+        if (j->progressive) {
+          /* libjpeg jdphuff.c start_pass_phuff_decoder: bad progression -> error */
+          if (ss == 0) {
+            if (se != 0) return OJ_CORRUPT;
+          } else {
+            if (se < ss || se > 63 || ns != 1) return OJ_CORRUPT;
+          }
+          if (j->ah != 0 && j->al != j->ah - 1) return OJ_CORRUPT;
+          if (j->al > 13) return OJ_CORRUPT;
+        } else {
+          if (ss != 0 || se != 63 || ahal != 0) return OJ_CORRUPT;
+          /* only single-scan sequential images are in scope (all components interleaved) */
+          if (ns != j->ncomp) return OJ_UNSUPPORTED;
+        }
         j->scan_off = p + L;
         j->saw_sos = 1;
         return OJ_OK;
@@ -206,6 +230,13 @@ static int parse_headers(oj_jpeg *j, const uint8_t *d, size_t n) {
     }
     p += L;
   }
+}
+
+static int parse_headers(oj_jpeg *j, const uint8_t *d, size_t n) {
+  memset(j, 0, sizeof(*j));
+  if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return OJ_CORRUPT;
+  int st = parse_markers(j, d, n, 2);
+  return st == OJ_EOI ? OJ_CORRUPT : st; /* EOI before SOS */
 }
 
 /* ---------------------------------------------------------- bit reader */
@@ -334,7 +365,7 @@ static int setup_geometry(oj_jpeg *j) {
     k->plane = (uint8_t *)malloc((size_t)k->bw * 8 * k->bh * 8);
     if (!k->coef || !k->plane) return OJ_SMALLBUF;
     if (!j->qpresent[k->tq]) return OJ_CORRUPT;
-    if (!j->dc[k->td].present || !j->ac[k->ta].present) return OJ_CORRUPT;
+    if (!j->progressive && (!j->dc[k->td].present || !j->ac[k->ta].present)) return OJ_CORRUPT;
   }
   return OJ_OK;
 }
@@ -378,6 +409,172 @@ static int decode_scan(oj_jpeg *j, const uint8_t *d, size_t n) {
       }
       since_restart++;
     }
+  return OJ_OK;
+}
+
+/* ------------------------------------------------------- progressive scans */
+
+/* Block (bx, by) of component c in a non-interleaved scan covers the
+ * component's ceil(dsw/8) x ceil(dsh/8) blocks (libjpeg jdinput.c
+ * per_scan_setup); interleaved scans walk MCUs like the sequential scan. */
+typedef struct {
+  int eobrun;
+  int pred[4];
+} oj_pstate;
+
+static int prog_block(oj_jpeg *j, oj_bits *b, oj_pstate *ps, int ci, int16_t *blk) {
+  const int ss = j->ss, se = j->se, ah = j->ah, al = j->al;
+  oj_comp *k = &j->comp[j->scan_comp[ci]];
+  if (ss == 0) {
+    if (ah == 0) { /* DC first: jdphuff.c decode_mcu_DC_first */
+      int s = decode_sym(b, &j->dc[k->td]);
+      if (s < 0 || s > 15) return OJ_CORRUPT;
+      int diff = s ? extend(getbits(b, s), s) : 0;
+      ps->pred[ci] += diff;
+      blk[0] = (int16_t)((uint32_t)ps->pred[ci] << al);
+    } else { /* DC refine: decode_mcu_DC_refine */
+      if (getbits(b, 1)) blk[0] = (int16_t)(blk[0] | (1 << al));
+    }
+    return OJ_OK;
+  }
+  const oj_huff *ac = &j->ac[k->ta];
+  if (ah == 0) { /* AC first: decode_mcu_AC_first */
+    if (ps->eobrun > 0) {
+      ps->eobrun--;
+      return OJ_OK;
+    }
+    for (int kk = ss; kk <= se; kk++) {
+      int rs = decode_sym(b, ac);
+      if (rs < 0) return OJ_CORRUPT;
+      int r = rs >> 4, s = rs & 15;
+      if (s) {
+        kk += r;
+        int v = extend(getbits(b, s), s);
+        blk[kNatural[kk]] = (int16_t)((uint32_t)v << al);
+      } else if (r == 15) {
+        kk += 15;
+      } else {
+        ps->eobrun = 1 << r;
+        if (r) ps->eobrun += getbits(b, r);
+        ps->eobrun--;
+        break;
+      }
+    }
+    return OJ_OK;
+  }
+  /* AC refine: decode_mcu_AC_refine */
+  const int p1 = 1 << al, m1 = -(1 << al);
+  int kk = ss;
+  if (ps->eobrun == 0) {
+    for (; kk <= se; kk++) {
+      int rs = decode_sym(b, ac);
+      if (rs < 0) return OJ_CORRUPT;
+      int r = rs >> 4, s = rs & 15;
+      if (s) {
+        s = getbits(b, 1) ? p1 : m1; /* size must be 1 (a warning in libjpeg otherwise) */
+      } else if (r != 15) {
+        ps->eobrun = 1 << r;
+        if (r) ps->eobrun += getbits(b, r);
+        break; /* the rest of the block is handled by the EOB run below */
+      }
+      /* advance over already-nonzero coefficients (appending correction bits)
+       * and r still-zero ones */
+      do {
+        int16_t *c = &blk[kNatural[kk]];
+        if (*c != 0) {
+          if (getbits(b, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
+        } else {
+          if (--r < 0) break; /* reached the target zero coefficient */
+        }
+        kk++;
+      } while (kk <= se);
+      if (s) blk[kNatural[kk]] = (int16_t)s;
+    }
+  }
+  if (ps->eobrun > 0) {
+    /* scan the rest of the band for correction bits of nonzero coefficients */
+    for (; kk <= se; kk++) {
+      int16_t *c = &blk[kNatural[kk]];
+      if (*c != 0 && getbits(b, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
+    }
+    ps->eobrun--;
+  }
+  return OJ_OK;
+}
+
+/* Decode the current progressive scan; *end = reader position afterwards. */
+static int prog_scan(oj_jpeg *j, const uint8_t *d, size_t n, size_t *end) {
+  oj_bits b = {d, n, j->scan_off, 0, 0, 0};
+  oj_pstate ps;
+  memset(&ps, 0, sizeof(ps));
+  int since_restart = 0;
+  /* tables the scan needs */
+  for (int i = 0; i < j->scan_ncomp; i++) {
+    oj_comp *k = &j->comp[j->scan_comp[i]];
+    if (j->ss == 0 && j->ah == 0 && !j->dc[k->td].present) return OJ_CORRUPT;
+    if (j->ss > 0 && !j->ac[k->ta].present) return OJ_CORRUPT;
+  }
+  if (j->scan_ncomp == 1) {
+    oj_comp *k = &j->comp[j->scan_comp[0]];
+    int bx_n = (k->dsw + 7) / 8, by_n = (k->dsh + 7) / 8;
+    for (int by = 0; by < by_n; by++)
+      for (int bx = 0; bx < bx_n; bx++) {
+        if (j->restart && since_restart == j->restart) {
+          restart_reader(&b);
+          memset(&ps, 0, sizeof(ps));
+          since_restart = 0;
+        }
+        if (prog_block(j, &b, &ps, 0, k->coef + ((size_t)by * k->bw + bx) * 64)) return OJ_CORRUPT;
+        since_restart++;
+      }
+  } else {
+    for (int my = 0; my < j->mcuy; my++)
+      for (int mx = 0; mx < j->mcux; mx++) {
+        if (j->restart && since_restart == j->restart) {
+          restart_reader(&b);
+          memset(&ps, 0, sizeof(ps));
+          since_restart = 0;
+        }
+        for (int i = 0; i < j->scan_ncomp; i++) {
+          oj_comp *k = &j->comp[j->scan_comp[i]];
+          for (int v = 0; v < k->v; v++)
+            for (int h = 0; h < k->h; h++) {
+              int by = my * k->v + v, bx = mx * k->h + h;
+              if (prog_block(j, &b, &ps, i, k->coef + ((size_t)by * k->bw + bx) * 64)) return OJ_CORRUPT;
+            }
+        }
+        since_restart++;
+      }
+  }
+  *end = b.p;
+  return OJ_OK;
+}
+
+/* Every scan of a progressive file, then the completeness check. */
+static int decode_progressive(oj_jpeg *j, const uint8_t *d, size_t n) {
+  int bits[4][64];
+  for (int c = 0; c < 4; c++)
+    for (int k = 0; k < 64; k++) bits[c][k] = -1;
+  for (;;) {
+    for (int i = 0; i < j->scan_ncomp; i++)
+      for (int k = j->ss; k <= j->se; k++) bits[j->scan_comp[i]][k] = j->al;
+    size_t end;
+    int st = prog_scan(j, d, n, &end);
+    if (st) return st;
+    /* the scan's data ends at the first marker that is not RSTn */
+    size_t q = end < j->scan_off ? j->scan_off : end;
+    while (q + 1 < n && !(d[q] == 0xFF && d[q + 1] != 0x00 && d[q + 1] != 0xFF && !(d[q + 1] >= 0xD0 && d[q + 1] <= 0xD7)))
+      q++;
+    if (q + 1 >= n) return OJ_CORRUPT; /* no EOI */
+    st = parse_markers(j, d, n, q);
+    if (st == OJ_EOI) break;
+    if (st) return st;
+  }
+  for (int c = 0; c < j->ncomp; c++) {
+    if (bits[c][0] != 0) return OJ_UNSUPPORTED; /* DC incomplete */
+    for (int k = 1; k < 10; k++)
+      if (bits[c][k] != 0) return OJ_UNSUPPORTED; /* libjpeg would smooth blocks */
+  }
   return OJ_OK;
 }
 
@@ -558,12 +755,13 @@ static int decode_to_coefs(oj_jpeg *j, const uint8_t *d, size_t n) {
   if (!supported_sampling(j)) { free_jpeg(j); return OJ_UNSUPPORTED; }
   for (int c = 0; c < j->ncomp; c++) {
     if (!j->comp[c].coef || !j->comp[c].plane) { free_jpeg(j); return OJ_SMALLBUF; }
-    if (!j->qpresent[j->comp[c].tq] || !j->dc[j->comp[c].td].present || !j->ac[j->comp[c].ta].present) {
+    if (!j->qpresent[j->comp[c].tq] ||
+        (!j->progressive && (!j->dc[j->comp[c].td].present || !j->ac[j->comp[c].ta].present))) {
       free_jpeg(j);
       return OJ_CORRUPT;
     }
   }
-  st = decode_scan(j, d, n);
+  st = j->progressive ? decode_progressive(j, d, n) : decode_scan(j, d, n);
   if (st) { free_jpeg(j); return st; }
   return OJ_OK;
 }
@@ -584,8 +782,8 @@ int oj_decode_coefs(const uint8_t *d, size_t n, int16_t *out, size_t out_blocks,
   } else {
     for (int my = 0; my < j.mcuy; my++)
       for (int mx = 0; mx < j.mcux; mx++)
-        for (int i = 0; i < j.scan_ncomp; i++) {
-          oj_comp *k = &j.comp[j.scan_comp[i]];
+        for (int i = 0; i < (j.progressive ? j.ncomp : j.scan_ncomp); i++) {
+          oj_comp *k = &j.comp[j.progressive ? i : j.scan_comp[i]];
           for (int v = 0; v < k->v; v++)
             for (int h = 0; h < k->h; h++, nb++) {
               int by = my * k->v + v, bx = mx * k->h + h;

@@ -96,7 +96,9 @@ def test_probe(L):
     buf = io.BytesIO()
     Image.fromarray(synth.synth_pixels(np.random.default_rng(0), 40, 30)).save(buf, format="JPEG", progressive=True)
     st, info = _lib.probe(buf.getvalue())
-    assert st == 0 and info.progressive == 1 and info.gpu_supported == 0
+    assert st == 0 and info.progressive == 1 and info.gpu_supported == 1
+    st, info = _lib.probe(synth.make_cmyk_jpeg(0, 40, 30))
+    assert st == 0 and info.components == 4 and info.gpu_supported == 0
     buf = io.BytesIO()
     Image.new("RGB", (7, 5)).save(buf, format="PNG")
     st, info = _lib.probe(buf.getvalue())

@@ -192,13 +192,11 @@ def test_status_codes(ctx512):
     import io as _io
     L = _lib()
     good = synth.make_jpeg(13, 64, 64, 90)
-    buf = _io.BytesIO()
-    Image.fromarray(synth.synth_pixels(np.random.default_rng(0), 64, 64)).save(buf, format="JPEG", progressive=True)
-    prog = buf.getvalue()
+    cmyk = synth.make_cmyk_jpeg(0, 64, 64)  # valid, outside the GPU path
     png = _io.BytesIO()  # 16-bit PNG: valid, outside the GPU path (the Rust glue keeps its CPU decode)
     Image.fromarray(np.arange(64, dtype=np.uint16).reshape(8, 8) * 1000).save(png, format="PNG")
     trunc = synth.make_jpeg(14, 300, 300, 90)[:1500]
-    res = ctx512.decode_batch([good, b"This is not a valid image file", prog, png.getvalue(), trunc, good])
+    res = ctx512.decode_batch([good, b"This is not a valid image file", cmyk, png.getvalue(), trunc, good])
     sts = [r[0] for r in res]
     assert sts == [L.DG_OK, L.DG_ERR_CORRUPT, L.DG_ERR_UNSUPPORTED, L.DG_ERR_UNSUPPORTED, L.DG_ERR_CORRUPT, L.DG_OK]
     assert np.array_equal(res[0][1], res[5][1])

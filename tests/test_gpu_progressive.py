@@ -1,0 +1,86 @@
+"""GPU parity for progressive JPEG (zune-jpeg decodes
+"baseline + progressive"): k_prog_zero + k_prog_scan through the C ABI vs
+the oracle's jdphuff.c restatement, bit-exact, and vs PIL/libjpeg-turbo.
+Scripts are libjpeg's default progression (jpeg_simple_progression), which
+is what PIL writes; sizes, samplings, gray, quality and restart intervals
+vary."""
+import io
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from datago_amd import synth
+from oracle import buckets as B
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from datago_amd import _lib as L
+    return L
+
+
+def _prog(seed, w, h, q=85, ss="4:2:0", gray=False, rst=0):
+    rng = np.random.default_rng(seed)
+    return synth.encode_jpeg(synth.synth_pixels(rng, w, h, gray), q, ss, restart_marker_blocks=rst, progressive=True)
+
+
+def _cases(seed, n, maxdim):
+    out = []
+    for i in range(n):
+        rng = np.random.default_rng(seed * 1000 + i)
+        w, h = int(rng.integers(1, maxdim)), int(rng.integers(1, maxdim))
+        out.append(_prog(seed * 1000 + i, w, h, int(rng.integers(20, 101)), ["4:2:0", "4:2:2", "4:4:4"][i % 3],
+                         i % 7 == 6, int(rng.integers(1, 12)) if i % 4 == 1 else 0))
+    return out
+
+
+def test_progressive_decode_bit_exact():
+    L = _lib()
+    ctx = L.Context(0)
+    datas = _cases(31, 24, 500)
+    for i, (data, (st, arr, meta)) in enumerate(zip(datas, ctx.decode_batch(datas))):
+        assert st == 0, (i, L.last_error())
+        ost, ref = O.jpeg_decode(data)
+        assert ost == 0
+        assert np.array_equal(arr.reshape(ref.shape), ref), i
+        pil = np.asarray(Image.open(io.BytesIO(data)))
+        assert np.array_equal(arr.reshape(pil.shape), pil), i
+
+
+def test_progressive_mixed_with_baseline_and_resized():
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+    datas = []
+    for i in range(8):
+        datas.append(synth.make_jpeg(700 + i, 200 + 97 * i, 640 - 53 * i, 80 + i, ["4:2:0", "4:2:2", "4:4:4"][i % 3],
+                                     progressive=bool(i % 2)))
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    for i, (data, (st, arr, meta)) in enumerate(zip(datas, ctx.decode_batch(datas))):
+        assert st == 0
+        w, h = O.jpeg_info(data)[1:3]
+        tw, th = t.target_size(w, h)
+        ost, dec = O.jpeg_decode(data)
+        ref = O.crop_and_resize(dec, tw, th, O.MODE_FIR)
+        assert np.array_equal(arr, ref), i
+
+
+def test_progressive_large_and_restarts():
+    L = _lib()
+    ctx = L.Context(0)
+    datas = [_prog(41, 1600, 1100, 92), _prog(42, 1333, 777, 75, "4:4:4", rst=3), _prog(43, 900, 1201, 60, gray=True, rst=5)]
+    for data, (st, arr, meta) in zip(datas, ctx.decode_batch(datas)):
+        assert st == 0
+        ost, ref = O.jpeg_decode(data)
+        assert np.array_equal(arr.reshape(ref.shape), ref)
+
+
+def test_progressive_truncated_is_corrupt():
+    L = _lib()
+    ctx = L.Context(0)
+    data = _prog(44, 300, 200)
+    res = ctx.decode_batch([data[: len(data) // 2], data])
+    assert res[0][0] == L.DG_ERR_CORRUPT and res[1][0] == L.DG_OK

@@ -64,12 +64,26 @@ def test_oracle_restart_markers_vs_pil(rst):
     assert np.array_equal(arr, np.asarray(Image.open(io.BytesIO(data))))
 
 
-def test_oracle_rejects_progressive_and_garbage():
-    arr = synth.synth_pixels(np.random.default_rng(0), 64, 64)
-    buf = io.BytesIO()
-    Image.fromarray(arr).save(buf, format="JPEG", progressive=True)
-    assert O.jpeg_decode(buf.getvalue())[0] == O.OJ_UNSUPPORTED
+def test_oracle_rejects_cmyk_and_garbage():
+    assert O.jpeg_decode(synth.make_cmyk_jpeg(0, 64, 64))[0] == O.OJ_UNSUPPORTED
     assert O.jpeg_decode(b"This is not a valid image file")[0] == O.OJ_CORRUPT
+
+
+@pytest.mark.parametrize("i", range(24))
+def test_oracle_progressive_matches_pil(i):
+    # libjpeg's default progressive script (jpeg_simple_progression: DC first
+    # Al=1, AC bands with successive approximation, refinements); sizes,
+    # samplings, gray and restart intervals vary
+    rng = np.random.default_rng(900 + i)
+    w, h = int(rng.integers(1, 420)), int(rng.integers(1, 420))
+    gray = i % 6 == 5
+    data = synth.encode_jpeg(synth.synth_pixels(rng, w, h, gray), int(rng.integers(20, 101)),
+                             ["4:2:0", "4:2:2", "4:4:4"][i % 3], restart_marker_blocks=(i % 4 == 1) * int(rng.integers(1, 9)),
+                             progressive=True)
+    st, arr = O.jpeg_decode(data)
+    assert st == O.OJ_OK
+    ref = np.asarray(Image.open(io.BytesIO(data)))
+    assert np.array_equal(arr.reshape(ref.shape), ref)
 
 
 def test_coefs_layout_counts():
