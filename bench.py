@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--encode", action="store_true",
                     help="pre_encode_images with encode_format jpeg, quality 92 (configs[4]: every payload "
                          "re-encoded on the GPU, WebDataset semantics worker_wds.rs:47-52)")
+    ap.add_argument("--progressive-frac", type=float, default=0.0,
+                    help="jpeg workload: share of the pool written as progressive JPEGs (not the headline config)")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 
@@ -306,6 +308,7 @@ def main() -> int:
     else:
         spec_seed = 2  # BASELINE configs[1] seed
         pool = synth.mixed_corpus(spec_seed, a.pool * world, a.short_min, a.short_max, workers=workers, lo=lo,
+                                  progressive_frac=a.progressive_frac,
                                   hi=hi)
     t_gen = time.perf_counter() - t_gen
     torch.cuda.set_device(local)
@@ -329,6 +332,8 @@ def main() -> int:
         ctx.set_option("wg_timing", 1)
     if a.hb_bands:
         ctx.set_option("hb_bands", a.hb_bands)
+    if a.progressive_frac > 0:
+        ctx.set_option("progressive", 1)
     if a.inflight != 2:
         ctx.set_option("slots", a.inflight)
     # ---- pool -> HBM (one arena, 16-byte aligned entries; wds: the shards themselves)
@@ -520,6 +525,7 @@ def main() -> int:
                                     "+ L8 mask PNG pairs, mask aligned to the image's bucket, decode + crop/resize "
                                     f"to 1024/32{' + JPEG q92 re-encode of every payload' if a.encode else ''}"),
                        "pre_encode_images": bool(a.encode),
+                       "progressive_frac": a.progressive_frac,
                        "images_per_step": B_, "pool_per_rank": a.pool,
                        "short_side": [a.short_min, a.short_max], "buckets": f"{a.size}/{a.ratio}/0.5/2.0",
                        "parallelism": f"dp{world} (sample shards, no collectives)"},

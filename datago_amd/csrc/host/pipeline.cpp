@@ -183,6 +183,14 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     next_slot_ %= nslots_;
     return DG_OK;
   }
+  if (k == "progressive") {
+    // Progressive JPEGs on the GPU (dg_prog.hip).  Off by default: a
+    // refinement scan decodes serially in one wave, so one large progressive
+    // image holds its whole batch for ~0.1-2 s; the default
+    // returns DG_ERR_UNSUPPORTED and the caller's CPU decoder takes them.
+    progressive_ = v != 0;
+    return DG_OK;
+  }
   if (k == "hb_bands") {  // band H kernel: 8-row bands per workgroup
     if (v < 1 || v > 64) return DG_ERR_INVALID;
     hb_bands_ = (uint32_t)v;
@@ -366,6 +374,11 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
     parse_jpeg_header(h, len, p.hdr);
     if (p.hdr.status != JH_OK) {
       p.status = p.hdr.status == JH_UNSUPPORTED ? DG_ERR_UNSUPPORTED : DG_ERR_CORRUPT;
+      return DG_OK;
+    }
+    if (p.hdr.progressive && !progressive_) {  // see option "progressive"
+      p.hdr.why = "progressive JPEG (context option \"progressive\" decodes it on the GPU)";
+      p.status = DG_ERR_UNSUPPORTED;
       return DG_OK;
     }
     W = p.hdr.width;

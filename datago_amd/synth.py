@@ -103,8 +103,9 @@ def mixed_spec(seed: int, n: int, short_min: int = 256, short_max: int = 2048,
 
 
 def _make_one(args):
-    seed, (w, h, q, ss, gray), rst = args
-    return make_jpeg(seed, w, h, q, ss, gray, rst)
+    seed, (w, h, q, ss, gray), rst = args[:3]
+    prog = args[3] if len(args) > 3 else False
+    return make_jpeg(seed, w, h, q, ss, gray, rst, progressive=prog)
 
 
 def _pool_map(jobs, workers):
@@ -121,12 +122,16 @@ def _pool_map(jobs, workers):
 
 
 def mixed_corpus(seed: int, n: int, short_min: int = 256, short_max: int = 2048,
-                 workers: int = 1, restart_marker_rows: int = 0, lo: int = 0, hi: int | None = None) -> List[bytes]:
+                 workers: int = 1, restart_marker_rows: int = 0, lo: int = 0, hi: int | None = None,
+                 progressive_frac: float = 0.0) -> List[bytes]:
     """Images [lo, hi) of the logical n-image stream for `seed` (a rank's
-    slice of a sharded corpus is generated without building the rest)."""
+    slice of a sharded corpus is generated without building the rest).
+    progressive_frac: share of images written as progressive JPEGs (libjpeg's
+    default script), every 1/frac-th image of the stream."""
     spec = mixed_spec(seed, n, short_min, short_max)
     hi = n if hi is None else hi
-    jobs = [(seed * 1_000_003 + i, spec[i], restart_marker_rows) for i in range(lo, hi)]
+    step = int(round(1.0 / progressive_frac)) if progressive_frac > 0 else 0
+    jobs = [(seed * 1_000_003 + i, spec[i], restart_marker_rows, bool(step) and i % step == 0) for i in range(lo, hi)]
     if workers > 1:
         return _pool_map(jobs, workers)
     return [_make_one(j) for j in jobs]

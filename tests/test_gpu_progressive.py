@@ -40,6 +40,7 @@ def _cases(seed, n, maxdim):
 def test_progressive_decode_bit_exact():
     L = _lib()
     ctx = L.Context(0)
+    ctx.set_option("progressive", 1)
     datas = _cases(31, 24, 500)
     for i, (data, (st, arr, meta)) in enumerate(zip(datas, ctx.decode_batch(datas))):
         assert st == 0, (i, L.last_error())
@@ -54,6 +55,7 @@ def test_progressive_mixed_with_baseline_and_resized():
     L = _lib()
     ctx = L.Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
                     min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+    ctx.set_option("progressive", 1)
     datas = []
     for i in range(8):
         datas.append(synth.make_jpeg(700 + i, 200 + 97 * i, 640 - 53 * i, 80 + i, ["4:2:0", "4:2:2", "4:4:4"][i % 3],
@@ -71,6 +73,7 @@ def test_progressive_mixed_with_baseline_and_resized():
 def test_progressive_large_and_restarts():
     L = _lib()
     ctx = L.Context(0)
+    ctx.set_option("progressive", 1)
     datas = [_prog(41, 1600, 1100, 92), _prog(42, 1333, 777, 75, "4:4:4", rst=3), _prog(43, 900, 1201, 60, gray=True, rst=5)]
     for data, (st, arr, meta) in zip(datas, ctx.decode_batch(datas)):
         assert st == 0
@@ -81,6 +84,14 @@ def test_progressive_large_and_restarts():
 def test_progressive_truncated_is_corrupt():
     L = _lib()
     ctx = L.Context(0)
+    ctx.set_option("progressive", 1)
     data = _prog(44, 300, 200)
     res = ctx.decode_batch([data[: len(data) // 2], data])
     assert res[0][0] == L.DG_ERR_CORRUPT and res[1][0] == L.DG_OK
+
+
+def test_progressive_off_by_default_is_unsupported():
+    L = _lib()
+    ctx = L.Context(0)
+    res = ctx.decode_batch([_prog(45, 64, 48), synth.make_jpeg(46, 64, 48)])
+    assert res[0][0] == L.DG_ERR_UNSUPPORTED and res[1][0] == L.DG_OK
