@@ -233,7 +233,7 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
   const uint32_t lane = threadIdx.x;
   const DG_GLOBAL uint32_t *z = gp<const uint32_t>(pd.zs);
   DG_GLOBAL uint8_t *out = gp<uint8_t>(pd.raw);
-  const uint32_t want = uni(im.height * (pd.rowbytes + 1u));
+  const uint32_t want = uni(pd.rawlen);
   const uint32_t zlen = uni(pd.zlen);
   BitReader br;
   br.bb = 0;
@@ -943,7 +943,7 @@ __global__ __launch_bounds__(1024) void k_inf_resolve(ImageDesc *__restrict__ im
   const WgItem it = list[blockIdx.x];
   ImageDesc &im = imgs[it.image];
   PngDesc &pd = im.png;
-  const uint32_t want = im.height * (pd.rowbytes + 1u);
+  const uint32_t want = pd.rawlen;
   DG_GLOBAL uint8_t *raw = gp<uint8_t>(pd.raw);
   const InfChunk *c0 = ch + pd.chunk0;
   uint32_t k = 0, P = 0;
@@ -1037,16 +1037,17 @@ __device__ __forceinline__ uint32_t unfilter_unit(uint32_t f, uint32_t rawv, uin
   return v;
 }
 
+// One filtered plane (the image, or one Adam7 pass): H rows of 1 + rb bytes
+// at raw_a -> H rows of rb bytes at stride us at unf_a.
 template <uint32_t BPP>
-__device__ void unfilter_image(UnfilterSmem &sm, ImageDesc &im) {
-  const PngDesc &pd = im.png;
+__device__ void unfilter_image(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, uint64_t unf_a, uint32_t rb,
+                               uint32_t us, uint32_t H) {
   const uint32_t lane = threadIdx.x;
-  const uint32_t rb = pd.rowbytes, us = pd.ustride, H = im.height;
   const uint32_t units = rb / BPP;  // BPP == 1 covers sub-byte samples (filter unit = 1 byte)
   const uint32_t tb = kUfTile * BPP;
   const uint32_t ntiles = (units + kUfTile - 1) / kUfTile;
-  const DG_GLOBAL uint8_t *raw = gp<const uint8_t>(pd.raw);
-  DG_GLOBAL uint8_t *unf = gp<uint8_t>(pd.unf);
+  const DG_GLOBAL uint8_t *raw = gp<const uint8_t>(raw_a);
+  DG_GLOBAL uint8_t *unf = gp<uint8_t>(unf_a);
   int bad = 0;
   for (uint32_t y0 = 0; y0 < H; y0 += 64) {
     const uint32_t nrows = H - y0 < 64 ? H - y0 : 64;
@@ -1060,7 +1061,7 @@ __device__ void unfilter_image(UnfilterSmem &sm, ImageDesc &im) {
     // retired by the vmcnt wait of the next tile boundary's barrier).  Raw
     // rows are not dword aligned: each row lands whole-word aligned and the
     // row's first byte sits at roff (0..3) in its LDS row.
-    const uint64_t rbase = pd.raw + (uint64_t)y0 * (rb + 1) + 1;
+    const uint64_t rbase = raw_a + (uint64_t)y0 * (rb + 1) + 1;
     auto roff = [&](uint32_t r) { return (uint32_t)((rbase + (uint64_t)r * (rb + 1)) & 3u); };
     auto load_tile = [&](uint32_t k) {
       const uint32_t b0 = k * tb, nb = rb - b0 < tb ? rb - b0 : tb;
@@ -1074,7 +1075,7 @@ __device__ void unfilter_image(UnfilterSmem &sm, ImageDesc &im) {
                                              (__attribute__((address_space(3))) void *)(T[r] + 4 * w0), 4, 0, 0);
       }
       if (y0) {
-        const uint64_t a = pd.unf + (uint64_t)(y0 - 1) * us + b0;
+        const uint64_t a = unf_a + (uint64_t)(y0 - 1) * us + b0;
         const uint32_t nw = (nb + 3) / 4;
         for (uint32_t w0 = 0; w0 < nw; w0 += 64)
           if (w0 + lane < nw)
@@ -1186,11 +1187,27 @@ __global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ img
   const WgItem it = list[blockIdx.x];
   ImageDesc &im = imgs[it.image];
   if (im.status) return;
-  switch (im.png.bpp) {
-    case 1: unfilter_image<1>(sm, im); break;
-    case 2: unfilter_image<2>(sm, im); break;
-    case 3: unfilter_image<3>(sm, im); break;
-    default: unfilter_image<4>(sm, im); break;
+  const PngDesc &pd = im.png;
+  const uint32_t np = pd.interlace ? 7u : 1u;
+  const uint32_t spp = pd.ctype == 2 ? 3u : pd.ctype == 4 ? 2u : pd.ctype == 6 ? 4u : 1u;
+  for (uint32_t p = 0; p < np; p++) {
+    uint64_t ra = pd.raw, ua = pd.unf;
+    uint32_t rb = pd.rowbytes, us = pd.ustride, H = im.height;
+    if (pd.interlace) {  // Adam7 pass p: a sub-image of its own (PNG spec 8.2)
+      const A7Pass a = png_adam7(im.width, im.height, spp * pd.depth, p);
+      if (!a.pw || !a.ph) continue;
+      ra += a.raw_off;
+      ua += a.unf_off;
+      rb = a.rb;
+      us = a.us;
+      H = a.ph;
+    }
+    switch (pd.bpp) {
+      case 1: unfilter_image<1>(sm, im, ra, ua, rb, us, H); break;
+      case 2: unfilter_image<2>(sm, im, ra, ua, rb, us, H); break;
+      case 3: unfilter_image<3>(sm, im, ra, ua, rb, us, H); break;
+      default: unfilter_image<4>(sm, im, ra, ua, rb, us, H); break;
+    }
   }
 }
 
@@ -1206,12 +1223,26 @@ __global__ __launch_bounds__(256) void k_png_expand(const ImageDesc *__restrict_
   const uint32_t idx = it.item0 + threadIdx.x;
   const uint32_t W = im.width;
   if (idx >= W * im.height) return;
-  const uint32_t y = idx / W, x = idx - y * W;
-  const DG_GLOBAL uint8_t *r = gp<const uint8_t>(pd.unf) + (size_t)y * pd.ustride;
+  const uint32_t y = idx / W, xo = idx - y * W;
   const uint32_t C = im.dec_c;
-  DG_GLOBAL uint8_t *o = gp<uint8_t>(im.pix) + (size_t)y * im.pix_stride + (size_t)x * C;
+  DG_GLOBAL uint8_t *o = gp<uint8_t>(im.pix) + (size_t)y * im.pix_stride + (size_t)xo * C;
+  const DG_GLOBAL uint8_t *r;
+  uint32_t x = xo;  // sample index in the source row
+  if (pd.interlace) {  // Adam7: the pass holding (x, y) and the pixel's place in it
+    const uint32_t spp = pd.ctype == 2 ? 3u : pd.ctype == 4 ? 2u : pd.ctype == 6 ? 4u : 1u;
+    const uint32_t xm = xo & 7u, ym = y & 7u;
+    const uint32_t p = (ym & 1u) ? 6u : (xm & 1u) ? 5u : (ym & 2u) ? 4u : (xm & 2u) ? 3u : (ym & 4u) ? 2u
+                     : (xm & 4u) ? 1u : 0u;
+    const A7Pass a = png_adam7(W, im.height, spp * pd.depth, p);
+    x = (xo - png_a7(p, 0)) / png_a7(p, 2);
+    r = gp<const uint8_t>(pd.unf) + a.unf_off + (size_t)((y - png_a7(p, 1)) / png_a7(p, 3)) * a.us;
+  } else {
+    r = gp<const uint8_t>(pd.unf) + (size_t)y * pd.ustride;
+  }
   const uint32_t dp = pd.depth;
-  if (pd.ctype == 0 || pd.ctype == 3) {
+  if (dp == 8 && !pd.has_trns && pd.ctype != 3) {  // de-interlace only: copy the pixel
+    for (uint32_t c = 0; c < C; c++) o[c] = r[(size_t)x * C + c];
+  } else if (pd.ctype == 0 || pd.ctype == 3) {
     uint32_t v;
     if (dp == 8) {
       v = r[x];

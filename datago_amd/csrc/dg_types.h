@@ -134,8 +134,46 @@ struct PngDesc {
   uint32_t chunk0;    // chunked inflate: first InfChunk of this image
   uint32_t nchunks;   // 0: serial inflate (small streams)
   uint32_t serial;    // set by the chunked path when the image must be inflated serially
-  uint32_t pad[2];
+  uint32_t interlace; // Adam7: raw/unf hold the 7 passes back to back (png_adam7_*)
+  uint32_t rawlen;    // inflated bytes expected
 };
+
+// Adam7 pass p of a W x H image (PNG spec 8.2): origin (x0, y0), spacing (dx, dy)
+DG_HD uint32_t png_a7(uint32_t p, uint32_t k) {
+  // x0, y0, dx, dy of the pass, 4 bits each (no table: no scratch on the device)
+  const uint32_t t = p == 0 ? 0x8800u : p == 1 ? 0x8804u : p == 2 ? 0x8440u : p == 3 ? 0x4402u
+                   : p == 4 ? 0x4220u : p == 5 ? 0x2201u : 0x2110u;
+  return (t >> (4 * k)) & 15u;
+}
+DG_HD void png_adam7_pass(uint32_t W, uint32_t H, uint32_t p, uint32_t &pw, uint32_t &ph) {
+  const uint32_t x0 = png_a7(p, 0), y0 = png_a7(p, 1), dx = png_a7(p, 2), dy = png_a7(p, 3);
+  pw = W > x0 ? (W - x0 + dx - 1) / dx : 0;
+  ph = H > y0 ? (H - y0 + dy - 1) / dy : 0;
+}
+// Geometry of pass p of an interlaced image: size, unfiltered row bytes and
+// 16-byte-aligned stride, offsets of its rows in raw and unf
+struct A7Pass {
+  uint32_t pw, ph, rb, us;
+  uint64_t raw_off, unf_off;
+};
+DG_HD A7Pass png_adam7(uint32_t W, uint32_t H, uint32_t bitspp, uint32_t p) {
+  A7Pass r = {0, 0, 0, 0, 0, 0};
+  for (uint32_t q = 0; q <= p; q++) {
+    uint32_t pw, ph;
+    png_adam7_pass(W, H, q, pw, ph);
+    const uint32_t rb = (uint32_t)(((uint64_t)bitspp * pw + 7) / 8), us = (rb + 15) / 16 * 16;
+    if (q == p) {
+      r.pw = pw;
+      r.ph = ph;
+      r.rb = rb;
+      r.us = us;
+    } else if (pw && ph) {
+      r.raw_off += (uint64_t)ph * (rb + 1);
+      r.unf_off += (uint64_t)ph * us;
+    }
+  }
+  return r;
+}
 
 // Chunk-parallel inflate.  The zlib stream of a large PNG is cut into
 // kInfChunk-byte chunks.  k_inf_find looks in each chunk (but the first) for

@@ -357,7 +357,7 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
       return DG_OK;
     }
     // the decoder's working set (raw + unfiltered + expanded) must stay 32-bit addressable
-    const uint64_t raw = (uint64_t)p.png.height * (p.png.rowbytes + 1ull);
+    const uint64_t raw = p.png.rawlen;
     if (raw >= (1ull << 31) || (uint64_t)p.png.width * p.png.height * 4ull >= (1ull << 31) ||
         p.png.zlen >= (1ull << 28)) {
       p.status = DG_ERR_UNSUPPORTED;
@@ -576,12 +576,14 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       pd.depth = (uint32_t)g.depth;
       pd.has_trns = (uint32_t)g.has_trns;
       for (int k = 0; k < 3; k++) pd.trns[k] = g.trns[k];
-      pd.expand = g.ctype == 3 || g.depth < 8 || g.has_trns;
+      pd.interlace = (uint32_t)g.interlace;
+      pd.rawlen = (uint32_t)g.rawlen;
+      pd.expand = g.ctype == 3 || g.depth < 8 || g.has_trns || g.interlace;  // k_png_expand also de-interlaces
       o.zs = L.take((size_t)g.zlen + 64, 256);
       // chunk-parallel inflate for streams of at least two chunks (small ones,
       // e.g. masks, inflate serially in one wave)
       {
-        const uint64_t want = (uint64_t)H * (g.rowbytes + 1ull);
+        const uint64_t want = g.rawlen;
         const uint32_t nch = (uint32_t)((g.zlen + kInfChunk - 1) / kInfChunk);
         if (nch >= 2 && !chunked_off_) {
           pd.chunk0 = (uint32_t)b.ichunks.size();
@@ -603,8 +605,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
           }
         }
       }
-      o.raw = L.take((size_t)H * (g.rowbytes + 1) + 16, 256);
-      o.unf = L.take((size_t)H * pd.ustride, 256);
+      o.raw = L.take((size_t)g.rawlen + 16, 256);
+      o.unf = L.take(g.interlace ? (size_t)g.unflen + 16 : (size_t)H * pd.ustride, 256);
       if (pd.expand) {
         d.pix_stride = (uint32_t)align_up((size_t)W * C, 16);
         o.pix = L.take((size_t)d.pix_stride * H);

@@ -8,6 +8,8 @@
 // (ignore_adler32), neither is the zlib Adler-32 trailer.
 #include "png_header.h"
 
+#include "../dg_types.h"
+
 #include <string.h>
 
 namespace dg {
@@ -97,7 +99,16 @@ void parse_png_header(const uint8_t *d, size_t n, PngHeader &h) {
   h.rowbytes = (uint32_t)((bits + 7) / 8);
   h.bpp = (int)(((uint64_t)h.spp * dp + 7) / 8);
   if (dp == 16) return fail(h, PH_UNSUPPORTED, "PNG: 16-bit samples (CPU path)");
-  if (h.interlace) return fail(h, PH_UNSUPPORTED, "PNG: Adam7 interlacing (CPU path)");
+  // Adam7 (PNG spec 8.2): seven sub-images back to back, empty ones absent
+  h.rawlen = h.unflen = 0;
+  for (uint32_t p = 0; p < (h.interlace ? 7u : 1u); p++) {
+    uint32_t pw = h.width, ph = h.height;
+    if (h.interlace) png_adam7_pass(h.width, h.height, p, pw, ph);
+    if (!pw || !ph) continue;
+    const uint64_t rb = ((uint64_t)h.spp * dp * pw + 7) / 8;
+    h.rawlen += (uint64_t)ph * (rb + 1);
+    h.unflen += (uint64_t)ph * ((rb + 15) / 16 * 16);
+  }
   h.status = PH_OK;
 }
 

@@ -31,6 +31,8 @@ struct PngHeader {
   uint16_t trns[3] = {0, 0, 0};  // gray / RGB transparency key (file sample values)
   std::vector<uint32_t> idat_off, idat_len;  // IDAT payload positions in the file
   uint64_t zlen = 0;     // total zlib bytes
+  uint64_t rawlen = 0;   // inflated bytes: filtered rows (+1 filter byte each) of the image or of its 7 Adam7 passes
+  uint64_t unflen = 0;   // unfiltered bytes at 16-byte row strides (per pass when interlaced)
 };
 
 bool is_png(const uint8_t *d, size_t n);

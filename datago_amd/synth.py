@@ -189,24 +189,46 @@ def png_filter_rows(rows: np.ndarray, bpp: int, filters: np.ndarray) -> bytes:
     return bytes(out)
 
 
+ADAM7 = ((0, 0, 8, 8), (4, 0, 8, 8), (0, 4, 4, 8), (2, 0, 4, 4), (0, 2, 2, 4), (1, 0, 2, 2), (0, 1, 1, 2))
+
+
+def _filters(n: int, filters: str, rng: np.random.Generator) -> np.ndarray:
+    if filters == "random":
+        return rng.integers(0, 5, size=n)
+    if filters == "none":
+        return np.zeros(n, np.int64)
+    return np.full(n, int(filters))
+
+
 def encode_png(rows: np.ndarray, w: int, h: int, depth: int, ctype: int, bpp: int, rng: np.random.Generator,
                level: int = 6, strategy: int = 0, filters: str = "random", idat_max: int = 0,
-               plte: Optional[bytes] = None, trns: Optional[bytes] = None) -> bytes:
+               plte: Optional[bytes] = None, trns: Optional[bytes] = None, samples: Optional[np.ndarray] = None,
+               interlace: bool = False) -> bytes:
     """PNG writer for test corpora: explicit filter choice ("random" per row,
     "none", or a filter number), zlib level/strategy (0 = stored blocks,
-    Z_FIXED = fixed Huffman), IDAT split into chunks of at most idat_max."""
+    Z_FIXED = fixed Huffman), IDAT split into chunks of at most idat_max.
+    interlace: Adam7 (PNG spec 8.2) from `samples` (h, w, spp) -- 8-bit
+    samples, or sample values for depths 1/2/4 -- each pass filtered on its own."""
     import struct
     import zlib
-    if filters == "random":
-        fl = rng.integers(0, 5, size=h)
-    elif filters == "none":
-        fl = np.zeros(h, np.int64)
+    if interlace:
+        parts = []
+        for x0, y0, dx, dy in ADAM7:
+            sub = samples[y0::dy, x0::dx]
+            if sub.shape[0] == 0 or sub.shape[1] == 0:
+                continue
+            if depth < 8:
+                prow = _pack_bits(sub[:, :, 0], depth)
+            else:
+                prow = sub.reshape(sub.shape[0], -1)
+            parts.append(png_filter_rows(prow, bpp, _filters(sub.shape[0], filters, rng)))
+        raw = b"".join(parts)
     else:
-        fl = np.full(h, int(filters))
-    raw = png_filter_rows(rows, bpp, fl)
+        raw = png_filter_rows(rows, bpp, _filters(h, filters, rng))
     co = zlib.compressobj(level, zlib.DEFLATED, 15, 8, strategy)
     z = co.compress(raw) + co.flush()
-    out = b"\x89PNG\r\n\x1a\n" + _png_chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0))
+    out = b"\x89PNG\r\n\x1a\n" + _png_chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0,
+                                                                     1 if interlace else 0))
     if plte is not None:
         out += _png_chunk(b"PLTE", plte)
     if trns is not None:
@@ -245,6 +267,7 @@ def make_png(seed: int, w: int, h: int, kind: str = "RGB", **kw) -> bytes:
         depth, ctype = 8, {"L": 0, "LA": 4, "RGB": 2, "RGBA": 6}[kind]
         c = px.shape[2]
         rows = px.reshape(h, w * c)
+        samples = px
         bpp = c
     elif kind.startswith("P"):
         depth = int(kind[1])
@@ -257,25 +280,29 @@ def make_png(seed: int, w: int, h: int, kind: str = "RGB", **kw) -> bytes:
             trns = rng.integers(0, 256, size=int(rng.integers(1, npal + 1))).astype(np.uint8).tobytes()
         ctype = 3
         rows = idx if depth == 8 else _pack_bits(idx, depth)
+        samples = idx[:, :, None]
         bpp = 1
     elif kind in ("L1", "L2", "L4"):
         depth = int(kind[1])
         v = (px[:, :, 0].astype(np.int32) >> (8 - depth)).astype(np.uint8)
         ctype, bpp = 0, 1
         rows = _pack_bits(v, depth)
+        samples = v[:, :, None]
         if kw.pop("trns_key", False):
             trns = bytes([0, int(v[0, 0])])
     elif kind == "LT":
         depth, ctype, bpp = 8, 0, 1
         rows = px[:, :, 0].copy()
+        samples = rows[:, :, None]
         trns = bytes([0, int(rows[0, 0])])
     elif kind == "RGBT":
         depth, ctype, bpp = 8, 2, 3
         rows = px.reshape(h, w * 3)
+        samples = px
         trns = bytes([0, int(px[0, 0, 0]), 0, int(px[0, 0, 1]), 0, int(px[0, 0, 2])])
     else:
         raise ValueError(kind)
-    return encode_png(rows, w, h, depth, ctype, bpp, rng, plte=plte, trns=trns, **kw)
+    return encode_png(rows, w, h, depth, ctype, bpp, rng, plte=plte, trns=trns, samples=samples, **kw)
 
 
 def pil_png(arr: np.ndarray, **kw) -> bytes:

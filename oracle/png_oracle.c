@@ -17,8 +17,10 @@
  *     RGB(A) (tRNS entries become alpha, missing palette entries are black),
  *     gray of 1/2/4 bits -> 8 bits scaled by 255/(2^d-1), tRNS on gray/RGB ->
  *     an alpha channel (0 where the sample equals the tRNS key, else 255).
- *     16-bit and Adam7-interlaced images report PO_UNSUPPORTED (the GPU path
- *     reports DG_ERR_UNSUPPORTED for them, the Rust glue keeps its CPU path).
+ *   - Adam7 interlacing (PNG spec 8.2): the seven passes' filtered rows back
+ *     to back, each pass unfiltered on its own, then scattered.
+ *     16-bit images report PO_UNSUPPORTED (the GPU path reports
+ *     DG_ERR_UNSUPPORTED for them, the Rust glue keeps its CPU path).
  *   - fast_image_resize 5.5.0 alpha handling for U8x2/U8x4 (ResizeOptions
  *     mul_div_alpha = true): multiply colour by alpha
  *     before a convolution call, divide after.  Restated from the crate's
@@ -302,7 +304,7 @@ static int parse(const uint8_t *d, size_t n, pnginfo *pi, int want_data) {
     case 4: pi->out_c = 2; break;
     default: pi->out_c = 4; break;
   }
-  if (dp == 16 || pi->interlace) return PO_UNSUPPORTED;
+  if (dp == 16) return PO_UNSUPPORTED;
   return PO_OK;
 }
 
@@ -354,7 +356,44 @@ int po_unfilter(uint8_t *raw, uint32_t h, size_t rowbytes, int bpp, uint8_t *out
   return PO_OK;
 }
 
-/* Decode to HWC u8 with out_c channels (po_info). */
+/* One pixel: sample x of an unfiltered row -> out_c channels (png EXPAND). */
+static void put_pixel(const pnginfo *pi, const uint8_t *r, uint32_t x, uint8_t *o) {
+  const int C = pi->out_c, dp = pi->depth;
+  if (pi->ctype == 0 || pi->ctype == 3) {
+    uint32_t v;
+    if (dp == 8) {
+      v = r[x];
+    } else {
+      const size_t bit = (size_t)x * dp;
+      v = (r[bit >> 3] >> (8 - dp - (bit & 7))) & ((1u << dp) - 1);
+    }
+    if (pi->ctype == 3) { /* entries past PLTE are black; alpha from tRNS, else 255 */
+      o[0] = pi->pal[v][0];
+      o[1] = pi->pal[v][1];
+      o[2] = pi->pal[v][2];
+      if (C == 4) o[3] = pi->pal[v][3];
+    } else {
+      const uint32_t scale = 255u / ((1u << dp) - 1u);
+      o[0] = (uint8_t)(v * scale);
+      if (C == 2) o[1] = v == pi->trns[0] ? 0 : 255;
+    }
+  } else if (pi->ctype == 2) {
+    const uint8_t *p = r + 3 * (size_t)x;
+    o[0] = p[0];
+    o[1] = p[1];
+    o[2] = p[2];
+    if (C == 4) o[3] = (p[0] == pi->trns[0] && p[1] == pi->trns[1] && p[2] == pi->trns[2]) ? 0 : 255;
+  } else {
+    memcpy(o, r + (size_t)x * C, (size_t)C);
+  }
+}
+
+/* Adam7 pass p (PNG spec 8.2): origin and spacing */
+static const int kA7[7][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4}, {0, 2, 2, 4}, {1, 0, 2, 2}, {0, 1, 1, 2}};
+
+/* Decode to HWC u8 with out_c channels (po_info).  Interlaced images: the
+ * inflated stream holds the seven passes' filtered rows back to back (empty
+ * passes contribute nothing), each pass unfiltered on its own. */
 int po_decode(const uint8_t *d, size_t n, uint8_t *out, size_t cap) {
   pnginfo pi;
   int st = parse(d, n, &pi, 1);
@@ -364,56 +403,57 @@ int po_decode(const uint8_t *d, size_t n, uint8_t *out, size_t cap) {
   }
   const int spp = pi.ctype == 2 ? 3 : pi.ctype == 4 ? 2 : pi.ctype == 6 ? 4 : 1;
   const size_t bitspp = (size_t)spp * pi.depth;
-  const size_t rowbytes = (bitspp * pi.w + 7) / 8;
   const int bpp = (int)((bitspp + 7) / 8);
-  const size_t want = (size_t)pi.h * (rowbytes + 1);
+  uint32_t pw[7], ph[7];
+  size_t prb[7], want = 0, unfn = 0;
+  const int np = pi.interlace ? 7 : 1;
+  for (int p = 0; p < np; p++) {
+    if (pi.interlace) {
+      pw[p] = pi.w > (uint32_t)kA7[p][0] ? (pi.w - kA7[p][0] + kA7[p][2] - 1) / kA7[p][2] : 0;
+      ph[p] = pi.h > (uint32_t)kA7[p][1] ? (pi.h - kA7[p][1] + kA7[p][3] - 1) / kA7[p][3] : 0;
+    } else {
+      pw[p] = pi.w;
+      ph[p] = pi.h;
+    }
+    prb[p] = (bitspp * pw[p] + 7) / 8;
+    if (pw[p] && ph[p]) {
+      want += (size_t)ph[p] * (prb[p] + 1);
+      unfn += (size_t)ph[p] * prb[p];
+    }
+  }
   if (cap < (size_t)pi.w * pi.h * pi.out_c) {
     free(pi.z);
     return PO_SMALLBUF;
   }
   uint8_t *raw = (uint8_t *)malloc(want + 1);
-  uint8_t *unf = (uint8_t *)malloc((size_t)pi.h * rowbytes + 1);
+  uint8_t *unf = (uint8_t *)malloc(unfn + 1);
   st = po_zlib_inflate(pi.z, pi.zn, raw, want, NULL);
   free(pi.z);
-  if (!st) st = po_unfilter(raw, pi.h, rowbytes, bpp, unf);
+  size_t ro = 0, uo = 0;
+  for (int p = 0; p < np && !st; p++) {
+    if (!pw[p] || !ph[p]) continue;
+    st = po_unfilter(raw + ro, ph[p], prb[p], bpp, unf + uo);
+    ro += (size_t)ph[p] * (prb[p] + 1);
+    uo += (size_t)ph[p] * prb[p];
+  }
   free(raw);
   if (st) {
     free(unf);
     return st;
   }
-  const int C = pi.out_c, dp = pi.depth;
-  for (uint32_t y = 0; y < pi.h; y++) {
-    const uint8_t *r = unf + (size_t)y * rowbytes;
-    uint8_t *o = out + (size_t)y * pi.w * C;
-    for (uint32_t x = 0; x < pi.w; x++) {
-      if (pi.ctype == 0 || pi.ctype == 3) {
-        uint32_t v;
-        if (dp == 8) {
-          v = r[x];
-        } else {
-          const size_t bit = (size_t)x * dp;
-          v = (r[bit >> 3] >> (8 - dp - (bit & 7))) & ((1u << dp) - 1);
-        }
-        if (pi.ctype == 3) {  /* entries past PLTE are black; alpha from tRNS, else 255 */
-          o[x * C] = pi.pal[v][0];
-          o[x * C + 1] = pi.pal[v][1];
-          o[x * C + 2] = pi.pal[v][2];
-          if (C == 4) o[x * C + 3] = pi.pal[v][3];
-        } else {
-          const uint32_t scale = 255u / ((1u << dp) - 1u);
-          o[x * C] = (uint8_t)(v * scale);
-          if (C == 2) o[x * C + 1] = v == pi.trns[0] ? 0 : 255;
-        }
-      } else if (pi.ctype == 2) {
-        const uint8_t *p = r + 3 * (size_t)x;
-        o[x * C] = p[0];
-        o[x * C + 1] = p[1];
-        o[x * C + 2] = p[2];
-        if (C == 4) o[x * C + 3] = (p[0] == pi.trns[0] && p[1] == pi.trns[1] && p[2] == pi.trns[2]) ? 0 : 255;
-      } else {
-        memcpy(o + (size_t)x * C, r + (size_t)x * C, (size_t)C);
-      }
+  const int C = pi.out_c;
+  uo = 0;
+  for (int p = 0; p < np; p++) {
+    if (!pw[p] || !ph[p]) continue;
+    const int x0 = pi.interlace ? kA7[p][0] : 0, y0 = pi.interlace ? kA7[p][1] : 0;
+    const int dx = pi.interlace ? kA7[p][2] : 1, dy = pi.interlace ? kA7[p][3] : 1;
+    for (uint32_t py = 0; py < ph[p]; py++) {
+      const uint8_t *r = unf + uo + (size_t)py * prb[p];
+      const size_t y = (size_t)y0 + (size_t)py * dy;
+      for (uint32_t px = 0; px < pw[p]; px++)
+        put_pixel(&pi, r, px, out + (y * pi.w + (size_t)x0 + (size_t)px * dx) * C);
     }
+    uo += (size_t)ph[p] * prb[p];
   }
   free(unf);
   return PO_OK;

@@ -108,10 +108,10 @@ def png_golden():
         optimize=True)
     rows = rng.integers(0, 256, (5, 16), dtype=np.uint8)
     files["l16_8x5_unsupported"] = synth.encode_png(rows, 8, 5, 16, 0, 2, rng)
-    ad = bytearray(synth.pil_png(synth.synth_pixels(rng, 40, 30)))
-    ad[28] = 1  # IHDR interlace method = Adam7 (header-only: the GPU path reports UNSUPPORTED)
-    ad[29:33] = zlib.crc32(bytes(ad[12:29])).to_bytes(4, "big")
-    files["rgb_40x30_adam7_unsupported"] = bytes(ad)
+    # Adam7-interlaced (PNG spec 8.2), expected pixels from PIL
+    files["rgb_40x30_adam7"] = synth.make_png(2100, 40, 30, "RGB", interlace=True)
+    files["p2_13x11_adam7"] = synth.make_png(2101, 13, 11, "P2", interlace=True)
+    files["la_5x3_adam7"] = synth.make_png(2102, 5, 3, "LA", interlace=True)
     good = files["rgb_17x9_dyn"]
     files["truncated_corrupt"] = good[: len(good) - 30]
     for name, data in files.items():

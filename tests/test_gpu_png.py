@@ -220,3 +220,26 @@ def test_chunked_inflate_matches_serial_and_oracle():
         assert np.array_equal(xa, ref) and np.array_equal(xb, ref)
     assert a.stat("png_chunks") > 0
     print("chunks", a.stat("png_chunks"), "serial fallbacks", a.stat("png_serial_fallbacks"))
+
+
+A7_CASES = [(k, w, h) for k in synth.PNG_KINDS for (w, h) in [(1, 1), (2, 3), (5, 9), (8, 8), (33, 17), (257, 130)]]
+
+
+def test_png_adam7_bit_exact(ctx_dec, ctx512):
+    """Adam7-interlaced PNGs (PNG spec 8.2): seven passes inflated together,
+    each unfiltered as its own sub-image, scattered by k_png_expand; tiny
+    sizes leave passes empty.  Oracle pinned vs PIL (test_oracle_png)."""
+    datas = [synth.make_png(hash((k, w, h, "a7")) & 0xFFFF, w, h, k, interlace=True) for (k, w, h) in A7_CASES]
+    for c, d, (st, arr, m) in zip(A7_CASES, datas, ctx_dec.decode_batch(datas)):
+        ost, ref = O.png_decode(d)
+        assert ost == 0 and st == 0, (c, st, _lib().last_error())
+        assert arr.shape == ref.shape and np.array_equal(arr, ref), c
+    # large (chunk-parallel inflate) and resized
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    big = [synth.make_png(61, 1400, 900, "RGB", interlace=True), synth.make_png(62, 700, 1300, "RGBA", interlace=True),
+           synth.make_png(63, 1000, 1000, "P4", interlace=True)]
+    for d, (st, arr, m) in zip(big, ctx512.decode_batch(big)):
+        assert st == 0
+        _, ref = O.png_decode(d)
+        tw, th = t.target_size(ref.shape[1], ref.shape[0])
+        assert np.array_equal(arr, O.crop_and_resize(ref, tw, th, O.MODE_FIR))

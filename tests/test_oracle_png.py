@@ -46,6 +46,20 @@ def test_png_oracle_bit_exact_vs_pil(case):
     assert arr.shape == ref.shape and np.array_equal(arr, ref)
 
 
+ADAM7_CASES = [(k, w, h) for k in synth.PNG_KINDS for (w, h) in [(1, 1), (2, 3), (5, 9), (8, 8), (33, 17), (70, 41)]]
+
+
+@pytest.mark.parametrize("case", ADAM7_CASES, ids=lambda c: f"{c[0]}-{c[1]}x{c[2]}")
+def test_png_oracle_adam7_vs_pil(case):
+    # Adam7 (PNG spec 8.2): tiny sizes leave passes empty (no filter bytes)
+    kind, w, h = case
+    data = synth.make_png(hash((kind, w, h, "a7")) & 0xFFFF, w, h, kind, interlace=True)
+    st, arr = O.png_decode(data)
+    assert st == O.PO_OK
+    ref = _pil_expand(data)
+    assert arr.shape == ref.shape and np.array_equal(arr, ref)
+
+
 def test_png_oracle_pil_encoder():
     rng = np.random.default_rng(5)
     for mode, c in (("L", 1), ("LA", 2), ("RGB", 3), ("RGBA", 4)):
