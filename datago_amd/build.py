@@ -25,6 +25,7 @@ SOURCES = [
     ("dg_png.hip", True),
     ("dg_enc.hip", True),
     ("dg_prog.hip", True),
+    ("dg_penc.hip", True),
     ("host/jpeg_enc.cpp", False),
     ("host/wds.cpp", False),
     ("host/png_header.cpp", False),

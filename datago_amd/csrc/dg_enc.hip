@@ -254,6 +254,7 @@ __global__ __launch_bounds__(1024) void k_enc_stuff(ImageDesc *__restrict__ imgs
   ImageDesc &im = imgs[it.image];
   if (im.status) return;
   EncDesc &e = im.enc;
+  if (e.png) return;  // PNG re-encode: k_penc_final
   const uint32_t t = threadIdx.x;
   DG_GLOBAL uint8_t *out = gp<uint8_t>(e.out);
   const DG_GLOBAL uint8_t *hdr = gp<const uint8_t>(e.hdr);

@@ -240,7 +240,9 @@ struct EncDesc {
   uint32_t src_stride, C, ncomp, mode;  // mode 1: resized LA image read as luma bytes
   uint32_t w, h, nbx, nby;
   uint32_t nblocks, hdr_len, total_bits, enc_bytes;
-  uint32_t active, pad[3];
+  uint32_t active, png, pad[2];  // png: PNG re-encode (dg_penc.hip): coef = filtered stream,
+                                 // nblocks = 1 KiB pieces, bits = piece bit lengths
+  uint64_t aux;                  // png: Adler-32 partials per piece (uint32 x 2)
   uint8_t q[2][64];    // quantisation tables, natural order
 };
 

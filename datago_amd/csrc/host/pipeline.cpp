@@ -407,12 +407,11 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
   p.out_bytes = (uint64_t)ow * oh * p.out_c;
   p.img_bytes = p.out_bytes;
   if (cfg_.pre_encode_images) {  // image_processing.rs:374-419
-    if (cfg_.encode_format != 1) {  // PNG re-encode is not on the GPU: the glue keeps its CPU path
-      p.status = DG_ERR_UNSUPPORTED;
-      return DG_OK;
-    }
     p.encode = true;
-    p.out_bytes = jpeg_enc_bound(ow, oh, p.out_c);
+    p.enc_png = cfg_.encode_format == 0;
+    // a resized LA image is a GrayImage over its LA bytes by now (image_to_dyn_image)
+    p.enc_la_gray = p.out_c == 2 && has_cfg_ && !(W == p.out_w && H == p.out_h);
+    p.out_bytes = p.enc_png ? png_enc_bound(ow, oh, p.enc_la_gray ? 1 : p.out_c) : jpeg_enc_bound(ow, oh, p.out_c);
     p.channels = -1;  // :416
   }
   return DG_OK;
@@ -542,7 +541,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     size_t coef, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], pass_srcoff[kStages];
     size_t final_off, tmp, out, ds, mk, chunk;
     size_t zs, raw, unf, pal;
-    size_t tout, ecoef, ebits, ewords, hdr;  // JPEG re-encode
+    size_t tout, ecoef, ebits, ewords, hdr, eaux;  // JPEG / PNG re-encode
     // alpha programs: buffer = dst of pass `stage` (-1: the decoded image), byte offset
     int aop_stage[kAlphaPoints];
     size_t aop_off[kAlphaPoints];
@@ -856,15 +855,34 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       b.out_dev_off[i] = o.out;
       out_total += p.out_bytes;
     }
-    if (p.encode) {  // the transform lands in tout; the JPEG goes to the caller's buffer
+    if (p.encode && p.enc_png) {  // PNG re-encode (dg_penc.hip): the transform lands in tout
+      EncDesc &e = d.enc;
+      e.active = 1;
+      e.png = 1;
+      e.w = p.out_w;
+      e.h = p.out_h;
+      e.C = p.enc_la_gray ? 1 : p.out_c;
+      e.src_stride = p.enc_la_gray ? p.out_w : d.out_stride;
+      const uint64_t nf = (uint64_t)e.h * ((uint64_t)e.w * e.C + 1);
+      e.nblocks = (uint32_t)((nf + 1023) / 1024);
+      const std::vector<uint8_t> hdr = png_enc_header(e.w, e.h, e.C);
+      e.hdr_len = (uint32_t)hdr.size();
+      o.hdr = b.blob.size();
+      b.blob.insert(b.blob.end(), hdr.begin(), hdr.end());
+      o.tout = L.take(p.img_bytes + 16, 256);
+      o.ecoef = L.take((size_t)nf + 16, 256);
+      o.ebits = L.take((size_t)e.nblocks * 4, 256);
+      o.eaux = L.take((size_t)e.nblocks * 8, 256);
+      o.ewords = (size_t)((3 + 9 * nf + 7 + 64) / 8 + 64) / 4 * 4;  // size for now; placed after the loop
+      b.any_enc = true;
+    } else if (p.encode) {  // the transform lands in tout; the JPEG goes to the caller's buffer
       EncDesc &e = d.enc;
       e.active = 1;
       e.w = p.out_w;
       e.h = p.out_h;
       e.C = p.out_c;
       e.ncomp = p.out_c <= 2 ? 1 : 3;
-      // a resized LA image is a GrayImage over its LA bytes by now (image_to_dyn_image)
-      e.mode = (p.out_c == 2 && has_cfg_ && !(W == p.out_w && H == p.out_h)) ? 1 : 0;
+      e.mode = p.enc_la_gray ? 1 : 0;
       e.src_stride = d.out_stride;
       e.nbx = (p.out_w + 7) / 8;
       e.nby = (p.out_h + 7) / 8;
@@ -941,6 +959,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       e.coef = (uint64_t)(uintptr_t)(S + o.ecoef);
       e.bits = (uint64_t)(uintptr_t)(S + o.ebits);
       e.words = (uint64_t)(uintptr_t)(S + o.ewords);
+      e.aux = o.eaux ? (uint64_t)(uintptr_t)(S + o.eaux) : 0;
       e.hdr = o.hdr + 1;  // blob offset + 1: made absolute with the meta buffer
     }
     if (d.fmt == kFmtPng) {
@@ -1091,7 +1110,13 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       uint32_t cnt = d.out_w * d.out_h;
       for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_COPY].push_back({I, it});
     }
-    if (d.enc.active) {
+    if (d.enc.active && d.enc.png) {
+      const EncDesc &e = d.enc;
+      for (uint32_t it = 0; it < e.h; it += 4) b.lists[L_PENC_ROW].push_back({I, it});
+      for (uint32_t it = 0; it < e.nblocks; it += 256) b.lists[L_PENC_PIECE].push_back({I, it});
+      b.lists[L_ENC_IMG].push_back({I, 0});  // k_enc_scan: piece offsets
+      b.lists[L_PENC_IMG].push_back({I, 0});
+    } else if (d.enc.active) {
       const EncDesc &e = d.enc;
       for (uint32_t it = 0; it < e.nbx * e.nby; it += 256) b.lists[L_ENC_MCU].push_back({I, it});
       for (uint32_t it = 0; it < e.nblocks; it += 256) b.lists[L_ENC_BLK].push_back({I, it});
@@ -1277,9 +1302,13 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     HIPCHK(hipMemsetAsync((char *)sl.scratch.p + b.words_off, 0, b.words_bytes, sl.st));
     launch_enc_fdct(sl.st, dd, lst(L_ENC_MCU), cnt(L_ENC_MCU));
     launch_enc_count(sl.st, dd, lst(L_ENC_BLK), cnt(L_ENC_BLK));
+    launch_penc_filter(sl.st, dd, lst(L_PENC_ROW), cnt(L_PENC_ROW));
+    launch_penc_count(sl.st, dd, lst(L_PENC_PIECE), cnt(L_PENC_PIECE));
     launch_enc_scan(sl.st, dm, lst(L_ENC_IMG), cnt(L_ENC_IMG));
     launch_enc_write(sl.st, dd, lst(L_ENC_BLK), cnt(L_ENC_BLK));
+    launch_penc_write(sl.st, dd, lst(L_PENC_PIECE), cnt(L_PENC_PIECE));
     launch_enc_stuff(sl.st, dm, lst(L_ENC_IMG), cnt(L_ENC_IMG));
+    launch_penc_final(sl.st, dm, lst(L_PENC_IMG), cnt(L_PENC_IMG));
   }
   if (next()) return DG_ERR_DEVICE;
   HIPCHK(hipGetLastError());

@@ -38,7 +38,9 @@ struct ImagePlan {
   uint32_t out_w = 0, out_h = 0, out_c = 0;
   uint64_t out_bytes = 0;
   int32_t channels = 0, bit_depth = 8;
-  bool encode = false;     // pre_encode_images + JPEG: out holds a JPEG of at most out_bytes
+  bool encode = false;     // pre_encode_images: out holds a JPEG / PNG of at most out_bytes
+  bool enc_png = false;    // encode_format png (dg_penc.hip)
+  bool enc_la_gray = false;  // resized LA: encoded as the GrayImage over its bytes
   uint64_t img_bytes = 0;  // transformed image bytes (out_w * out_h * out_c)
 };
 
@@ -110,6 +112,7 @@ enum ListId {
   L_INF_FIND, L_INF_RES,                                    // chunk-parallel inflate
   L_ENC_MCU, L_ENC_BLK, L_ENC_IMG,                          // JPEG re-encode
   L_PROG_ZERO, L_PROG,                                      // progressive JPEG
+  L_PENC_ROW, L_PENC_PIECE, L_PENC_IMG,                     // PNG re-encode
   L_COUNT
 };
 static_assert((int)L_COUNT <= 32, "Batch::lists");

@@ -112,4 +112,38 @@ void parse_png_header(const uint8_t *d, size_t n, PngHeader &h) {
   h.status = PH_OK;
 }
 
+static uint32_t crc32_bytes(const uint8_t *p, size_t n) {
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) {
+    c ^= p[i];
+    for (int k = 0; k < 8; k++) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+  }
+  return ~c;
+}
+
+std::vector<uint8_t> png_enc_header(uint32_t w, uint32_t h, uint32_t C) {
+  static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
+  std::vector<uint8_t> o(sig, sig + 8);
+  auto be32 = [&](uint32_t v) {
+    for (int s = 24; s >= 0; s -= 8) o.push_back((uint8_t)(v >> s));
+  };
+  be32(13);
+  const size_t t0 = o.size();
+  for (char c : {'I', 'H', 'D', 'R'}) o.push_back((uint8_t)c);
+  be32(w);
+  be32(h);
+  o.push_back(8);                                                // bit depth
+  o.push_back((uint8_t)(C == 1 ? 0 : C == 2 ? 4 : C == 3 ? 2 : 6));  // colour type
+  o.push_back(0);                                                // deflate
+  o.push_back(0);                                                // adaptive filtering
+  o.push_back(0);                                                // no interlace
+  be32(crc32_bytes(o.data() + t0, o.size() - t0));
+  return o;
+}
+
+uint64_t png_enc_bound(uint32_t w, uint32_t h, uint32_t C) {
+  const uint64_t n = (uint64_t)h * ((uint64_t)w * C + 1);  // filtered stream
+  return 33 + 8 + 2 + (3 + 9 * n + 7 + 7) / 8 + 4 + 4 + 12 + 16;
+}
+
 }  // namespace dg

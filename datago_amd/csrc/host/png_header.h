@@ -36,6 +36,10 @@ struct PngHeader {
 };
 
 bool is_png(const uint8_t *d, size_t n);
+// PNG re-encode (dg_penc.hip): signature + IHDR chunk (8-bit, C = 1/2/3/4
+// channels -> colour type 0/4/2/6, no interlace) and the output size bound.
+std::vector<uint8_t> png_enc_header(uint32_t w, uint32_t h, uint32_t C);
+uint64_t png_enc_bound(uint32_t w, uint32_t h, uint32_t C);
 // Walks every chunk header (reads 8 bytes per chunk plus IHDR/PLTE/tRNS payloads).
 void parse_png_header(const uint8_t *d, size_t n, PngHeader &h);
 

@@ -71,4 +71,9 @@ void launch_enc_count(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
 void launch_enc_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 void launch_enc_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 void launch_enc_stuff(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+// PNG re-encode (dg_penc.hip): 4 rows / 256 pieces / 1 image per workgroup
+void launch_penc_filter(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_penc_count(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_penc_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_penc_final(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 }  // namespace dg

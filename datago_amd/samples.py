@@ -12,7 +12,8 @@ whole sample goes to the GPU at once.  A reference payload whose body turns
 out corrupt (known only after decoding) is skipped as the reference skips a
 failed load (worker_wds.rs:134-137) and the remaining payloads are re-run
 against the next reference.  Payloads outside the GPU path
-(DG_ERR_UNSUPPORTED: progressive JPEG, 16-bit PNG, PNG re-encode ...) are
+(DG_ERR_UNSUPPORTED: 16-bit PNG, CMYK JPEG, progressive JPEG unless the
+context option is set ...) are
 returned with that status for the caller's CPU path; there is no CPU pixel
 path here.
 """

@@ -87,8 +87,62 @@ def test_encode_round_trip_quality():
     assert psnr > 30
 
 
-def test_png_reencode_unsupported():
+def _png_check(data: bytes):
+    """Container checks independent of PIL: chunk CRCs, zlib stream, Adler-32."""
+    import binascii
+    import struct
+    import zlib
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, types = 8, b"", []
+    while pos < len(data):
+        n, = struct.unpack(">I", data[pos:pos + 4])
+        t = data[pos + 4:pos + 8]
+        body = data[pos + 8:pos + 8 + n]
+        crc, = struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])
+        assert binascii.crc32(t + body) & 0xFFFFFFFF == crc, t
+        types.append(t)
+        if t == b"IDAT":
+            idat += body
+        pos += 12 + n
+    assert types[0] == b"IHDR" and types[-1] == b"IEND" and pos == len(data)
+    return zlib.decompress(idat)  # checks the Adler-32
+
+
+@pytest.mark.parametrize("rgb8", [False, True])
+def test_png_reencode_lossless(rgb8):
+    """pre_encode_images + encode_format png (image_processing.rs:396-413):
+    the GPU's PNG (adaptive filters, fixed-Huffman DEFLATE with run matches)
+    must decode -- with PIL, zlib and the oracle -- to exactly the image the
+    same context computes without encoding.  The bytes are not the png
+    crate's (fdeflate is not vendored): parity is on the pixels."""
     L = _lib()
-    ctx = _ctx(92, False, True, fmt=0)
-    (st, _, _), = ctx.decode_batch([synth.make_jpeg(8, 64, 64, 90)])
-    assert st == L.DG_ERR_UNSUPPORTED
+    kw = dict(crop_and_resize=True, default_image_size=512, downsampling_ratio=16, min_aspect_ratio=0.5,
+              max_aspect_ratio=2.0, image_to_rgb8=rgb8)
+    enc = L.Context(0, pre_encode_images=True, encode_format=0, **kw)
+    raw = L.Context(0, **kw)
+    datas = [synth.make_jpeg(30, 640, 480, 90), synth.make_jpeg(31, 300, 700, 85, gray=True),
+             synth.make_png(32, 512, 512, "RGBA"), synth.make_png(33, 200, 150, "LA"),
+             synth.make_png(34, 333, 444, "L"), synth.make_png(35, 700, 300, "P8T"),
+             synth.make_png(36, 1, 1, "RGB"), synth.make_png(37, 512, 512, "LA")]
+    # a flat mask: long runs compress through the distance-1 matches
+    m = np.zeros((600, 800), np.uint8)
+    m[100:400, 200:650] = 255
+    datas.append(synth.pil_png(m))
+    er, rr = enc.decode_batch(datas), raw.decode_batch(datas)
+    for i, (d, (se, pe, me), (sr, pr, mr)) in enumerate(zip(datas, er, rr)):
+        assert se == 0 and sr == 0, (i, se, sr, L.last_error())
+        assert me.is_encoded == 1 and me.channels == -1 and me.nbytes == len(pe.tobytes())
+        png = pe.tobytes()
+        filt = _png_check(png)
+        st, dec = O.png_decode(png)
+        assert st == 0
+        ref = pr.reshape(mr.height, mr.width, -1)
+        if ref.shape[2] == 2 and (mr.original_width, mr.original_height) != (mr.width, mr.height):
+            # resized LA: a GrayImage over the first w*h LA bytes (SURVEY B3)
+            ref = ref.reshape(-1)[: mr.width * mr.height].reshape(mr.height, mr.width, 1)
+        assert dec.shape == ref.shape and np.array_equal(dec, ref), i
+        pil = np.asarray(Image.open(io.BytesIO(png)))
+        assert np.array_equal(pil.reshape(ref.shape), ref), i
+        assert len(filt) == ref.shape[0] * (ref.shape[1] * ref.shape[2] + 1)
+    # the flat mask compresses well
+    assert er[-1][2].nbytes < 0.05 * 800 * 600
