@@ -191,6 +191,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     progressive_ = v != 0;
     return DG_OK;
   }
+  if (k == "entropy_lpt") {
+    entropy_lpt_ = v != 0;
+    return DG_OK;
+  }
   if (k == "hb_bands") {  // band H kernel: 8-row bands per workgroup
     if (v < 1 || v > 64) return DG_ERR_INVALID;
     hb_bands_ = (uint32_t)v;
@@ -1122,6 +1126,21 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       for (uint32_t it = 0; it < e.nblocks; it += 256) b.lists[L_ENC_BLK].push_back({I, it});
       b.lists[L_ENC_IMG].push_back({I, 0});
     }
+  }
+  if (entropy_lpt_) {
+    // Entropy workgroups decode a fixed number of bits, but their time follows
+    // the symbol count: images with few coded bits per block (low quality,
+    // flat content: short EOB-heavy codes) run up to 2x the mean.  Dispatch
+    // those first (workgroups start in list order) so they do not form the
+    // kernel's tail.
+    auto cost_sort = [&](std::vector<WgItem> &l) {
+      std::stable_sort(l.begin(), l.end(), [&](const WgItem &x, const WgItem &y) {
+        const ImageDesc &a = b.descs[x.image], &c = b.descs[y.image];
+        return (uint64_t)a.scan_len * c.total_blocks < (uint64_t)c.scan_len * a.total_blocks;
+      });
+    };
+    cost_sort(b.lists[L_SYNC]);
+    cost_sort(b.lists[L_HUFF]);
   }
   for (uint32_t j = 0; j < (uint32_t)b.gjobs.size(); j++)
     for (uint32_t pc = 0; pc * kGatherPiece < b.gjobs[j].len; pc++) b.lists[L_GATHER].push_back({j, pc});

@@ -202,6 +202,7 @@ class Context {
   bool chunked_off_ = false;  // option "png_chunked" = 0
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
   bool progressive_ = false;            // option "progressive"
+  bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first
   int64_t stat_png_serial_ = 0, stat_png_chunks_ = 0;
   // "wg_timing" summaries of the last batch (microseconds): per kernel {span, mean, p90, max}
   double wgstat_[2][4] = {{0}};
