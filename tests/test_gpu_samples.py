@@ -68,10 +68,17 @@ def test_db_sample_masks_and_reencode():
     _check(s.image, img, target)
     _check(s.masks["mask"], mask, target)
     assert (s.additional_images["masked_image"].width, s.additional_images["masked_image"].height) == target
-    # pre_encode_images: the image is JPEG-encoded on the GPU, the PNG mask goes back to the CPU path
+    # pre_encode_images: the image is JPEG-encoded and the mask PNG-encoded on the GPU
+    # (worker_http.rs:186-192 forces PNG for masks); the mask decodes to the same pixels
     s = process_db_sample("id", img, {"mask": mask}, {}, tfm, ImageEncoding(encode_images=True, encode_format=1))
     assert s.image.is_encoded and s.image.channels == -1
-    assert s.unsupported == {"mask": 1}
+    assert s.unsupported == {}
+    m = s.masks["mask"]
+    assert m.is_encoded and m.channels == -1
+    plain = process_db_sample("id", img, {"mask": mask}, {}, tfm, ImageEncoding()).masks["mask"]
+    st, dec = O.png_decode(bytes(m.data))
+    assert st == 0 and dec.shape == (plain.height, plain.width, 1)
+    assert np.array_equal(dec.reshape(-1), np.frombuffer(bytes(plain.data), np.uint8))
 
 
 def test_torch_handoff_equals_host_path():
