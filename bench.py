@@ -363,7 +363,10 @@ def main() -> int:
                        for d, dim, tgt in zip(pool, dims, targets)]
     B_ = min(a.batch, 1 << 16)
     # output arena for one step (reused), sized for the largest B_ outputs
-    out_cap = sum(sorted(out_bytes)[-B_:]) + 16 * B_
+    # one arena per batch in flight: the B_ largest outputs (images repeat when
+    # the batch is larger than the pool), each padded to 16 bytes
+    reps = -(-B_ // len(pool))
+    out_cap = sum(sorted(out_bytes * reps)[-B_:]) + 16 * B_
     d_out = [ctx.alloc(out_cap) for _ in range(a.inflight)]
 
     def submit(k: int):
