@@ -1090,7 +1090,7 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
 }
 
 template <int KMAX>
-__global__ __launch_bounds__(256) void k_resize_hb(const ImageDesc *__restrict__ imgs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_resize_hb(const ImageDesc *__restrict__ imgs,
                                                    const WgItem *__restrict__ list, int stage) {
   __shared__ __attribute__((aligned(16))) uint32_t seg[kHBandRows * kHSegStride];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kHBandRows * kHBandCols * 4];
