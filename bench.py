@@ -56,6 +56,7 @@ def parse():
                     help="per-stage HBM bytes from a PMC run of this configuration (tools/pmc_traffic.py)")
     ap.add_argument("--wg-timing", action="store_true", help="debug: per-workgroup timing of the entropy kernels")
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight (context slots / output arenas)")
+    ap.add_argument("--entropy-once", type=int, default=-1, help="decode-once entropy staging (-1 = library default)")
     ap.add_argument("--entropy-lpt", type=int, default=-1, help="slow entropy workgroups first (-1 = library default)")
     ap.add_argument("--hb-bands", type=int, default=0, help="band H kernel: 8-row bands per workgroup (0 = default)")
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
@@ -337,6 +338,8 @@ def main() -> int:
         ctx.set_option("progressive", 1)
     if a.entropy_lpt >= 0:
         ctx.set_option("entropy_lpt", a.entropy_lpt)
+    if a.entropy_once >= 0:
+        ctx.set_option("entropy_once", a.entropy_once)
     if a.inflight != 2:
         ctx.set_option("slots", a.inflight)
     # ---- pool -> HBM (one arena, 16-byte aligned entries; wds: the shards themselves)

@@ -157,6 +157,60 @@ DG_HD void wc_flush(WriteCtx &w, uint32_t ze) {
   w.cur = -1;
 }
 
+// Decode-once staging (option "entropy_once").  The sync decode records
+// every coefficient it produces, so k_huff_scatter writes the blocks without
+// decoding the range a second time.  Entries are 32-bit:
+//   coefficient  bit 31 = 0 | zz:6 @25 | j:13 @12 | value:12 (signed) @0
+//   RST marker   bit 31 = 1 | owned @30 | z:6 @24 | j:13 @11
+// j = blocks started in the range so far (0: the block carried in from the
+// previous range), z = zigzag position when the marker was reached.  DC
+// differences of 0 are not recorded.  Groups of four entries are stored
+// interleaved over 64 consecutive ranges (group g of range s at
+// ((s / 64) * cap + g) * 64 + s % 64, 16 bytes each) so that a wave's loads
+// and stores of its g-th groups coalesce.
+struct StageCtx {
+  DG_GLOBAL uint32_t *base;  // this range's group 0
+  uint32_t on;               // this thread stages (decode_range checks it; the context itself is always passed
+                             // by the staging kernels, so it stays in registers)
+  uint32_t n, started;       // entries, blocks started
+  uint32_t g0, g1, g2, g3;   // pending group
+};
+DG_HD uint32_t stage_coef(uint32_t zz, uint32_t j, int32_t v) {
+  return (zz << 25) | ((j & 0x1FFFu) << 12) | ((uint32_t)v & 0xFFFu);
+}
+DG_HD uint32_t stage_marker(uint32_t owned, uint32_t z, uint32_t j) {
+  return 0x80000000u | (owned << 30) | ((z & 63u) << 24) | ((j & 0x1FFFu) << 11);
+}
+DG_HD DG_GLOBAL uint32_t *stage_range(uint64_t stage, uint32_t cap, uint32_t s) {
+  return (DG_GLOBAL uint32_t *)(uintptr_t)stage + ((((size_t)(s >> 6) * cap) << 6) + (s & 63u)) * 4;
+}
+DG_HD void stage_push(StageCtx &c, uint32_t e) {
+  const uint32_t k = c.n & 3u;
+  c.g0 = k == 0 ? e : c.g0;
+  c.g1 = k == 1 ? e : c.g1;
+  c.g2 = k == 2 ? e : c.g2;
+  c.g3 = k == 3 ? e : c.g3;
+  c.n++;
+  if (k == 3) {
+    DG_GLOBAL uint32_t *p = c.base + (size_t)((c.n >> 2) - 1) * 256;  // 64 ranges x 4 dwords per group row
+#if defined(DG_DEVICE)
+    *(DG_GLOBAL u32x4 *)p = u32x4{c.g0, c.g1, c.g2, c.g3};
+#else
+    p[0] = c.g0, p[1] = c.g1, p[2] = c.g2, p[3] = c.g3;
+#endif
+  }
+}
+DG_HD void stage_finish(StageCtx &c) {
+  if (c.n & 3u) {
+    DG_GLOBAL uint32_t *p = c.base + (size_t)(c.n >> 2) * 256;
+#if defined(DG_DEVICE)
+    *(DG_GLOBAL u32x4 *)p = u32x4{c.g0, c.g1, c.g2, c.g3};
+#else
+    p[0] = c.g0, p[1] = c.g1, p[2] = c.g2, p[3] = c.g3;
+#endif
+  }
+}
+
 // Checkpoints for early merging.  A decode records, at the first symbol
 // boundary at/after every kCkptBits-th bit of its range, the state there and
 // the accumulator *tail* from that point to the end of the range.  A later
@@ -253,7 +307,7 @@ template <bool WRITE, class TAB>
 DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uint8_t *stream,
                         const DG_GLOBAL uint32_t *mk,
                         uint32_t s, uint32_t in, RangeAcc &acc, WriteCtx *w, DG_GLOBAL Ckpt *ck = nullptr,
-                        bool merge = false, uint32_t old_out = 0) {
+                        bool merge = false, uint32_t old_out = 0, StageCtx *stg = nullptr) {
   const uint32_t S = im.sub_bits, total = im.ds_bits;
   const uint32_t a0 = s * S;
   const uint32_t a1 = (a0 + S < total) ? a0 + S : total;
@@ -262,6 +316,11 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
   acc.m = 0;
   acc.n = 0;
   acc.dc[0] = acc.dc[1] = acc.dc[2] = 0;
+  const bool stage = stg && stg->on;
+  if (stage) {
+    stg->n = 0;
+    stg->started = 0;
+  }
   if (a0 >= total) {  // empty trailing subsequence (nsub is sized from the raw length):
     acc.out = pack_state(0, 0, 0);  // constant exit, so state changes do not ripple through it
     return;
@@ -300,6 +359,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       if (pos >= mpos) {  // restart marker: hard resync
         bool owned = mpos < a1;
         if (WRITE && z > 0) wc_flush(*w, z);
+        if (stage) stage_push(*stg, stage_marker(owned ? 1u : 0u, z, stg->started));
         pos = mpos;
         r = 0;
         z = 0;
@@ -365,6 +425,10 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
     if (isdc) {
       acc.n++;
       add3(acc.dc, comp, v);
+      if (stage) {
+        stg->started++;
+        if (v) stage_push(*stg, stage_coef(0, stg->started, v));
+      }
       if (WRITE) {
         add3(w->pred, comp, v);
         wc_begin(*w, wc_index(*w, w->nin), 0);
@@ -378,6 +442,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
         uint32_t zz = z + run;
         if (zz < 64) w->blk[zz] = (int16_t)v;
       }
+      if (stage && size && z + run < 64) stage_push(*stg, stage_coef(z + run, stg->started, v));
       z = eob ? 64u : z + run + 1u;
     }
     if (z >= 64) {
@@ -389,6 +454,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
     }
   }
   if (WRITE && z > 0) wc_flush(*w, z);
+  if (stage) stage_finish(*stg);
   if (!merged) {
     uint32_t rel = pos - a1;
     acc.out = pack_state(rel > 255 ? 255 : rel, r, z);

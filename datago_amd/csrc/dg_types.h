@@ -81,7 +81,8 @@ struct SubState {
   uint32_t seg;     // exclusive segmented scan: restart segment at start
   uint32_t nin;     //   blocks already started in that segment
   int32_t dcin[3];  //   DC predictors at start
-  uint32_t pad[2];
+  uint32_t nstart;  // decode-once staging: blocks started in the range (all segments)
+  uint32_t nent;    //   staged entries
 };
 
 enum Colorspace : uint32_t { CS_YCC = 0, CS_RGB = 1, CS_GRAY = 2 };
@@ -263,7 +264,7 @@ struct ImageDesc {
   uint32_t mk_cap;          // capacity of the marker list
   uint32_t lead_bits;       // k_huff_sync lead-in before each subsequence (lead_in)
   uint32_t ds_lsw;          // log2(32-bit words per subsequence) of the interleaved stream
-  uint32_t pad_ds;
+  uint32_t stage_cap;       // decode-once: staging capacity per subsequence (groups of 4 entries), 0 = off
   uint32_t restart;         // restart interval (MCUs), 0 = none
   uint32_t blocks_per_seg;  // restart * bpm, 0 = unlimited
   uint32_t total_blocks;
@@ -275,6 +276,7 @@ struct ImageDesc {
   uint16_t qpool[3];
   uint16_t pad1;
   uint64_t coef;            // device address of block 0 (int16 zigzag[64] per block, decode order)
+  uint64_t stage;           // decode-once staging (dg_entropy.h StageCtx), 0 = off
   // ---- geometry
   uint32_t width, height;
   uint32_t mcux, mcuy;

@@ -191,6 +191,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     progressive_ = v != 0;
     return DG_OK;
   }
+  if (k == "entropy_once") {  // decode-once: k_huff_sync stages coefficients, k_huff_scatter writes them
+    entropy_once_ = v != 0;
+    return DG_OK;
+  }
   if (k == "entropy_lpt") {
     entropy_lpt_ = v != 0;
     return DG_OK;
@@ -543,7 +547,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   // first pass: sizes only (pointers are patched after allocation)
   struct Offs {
     size_t coef, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], pass_srcoff[kStages];
-    size_t final_off, tmp, out, ds, mk, chunk;
+    size_t final_off, tmp, out, ds, mk, chunk, stage;
     size_t zs, raw, unf, pal;
     size_t tout, ecoef, ebits, ewords, hdr, eaux;  // JPEG / PNG re-encode
     // alpha programs: buffer = dst of pass `stage` (-1: the decoded image), byte offset
@@ -700,6 +704,11 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     d.ds_lsw = 0;
     while ((32u << d.ds_lsw) < sub_bits) d.ds_lsw++;
     o.ds = L.take((size_t)ds_words_alloc(d.nsub, d.ds_lsw) * 4, 256);
+    if (entropy_once_ && sub_bits <= 8192) {  // decode-once staging (dg_entropy.h StageCtx)
+      d.stage_cap = (sub_bits / 2 + sub_bits / 8 + 64 + 3) / 4;
+      o.stage = L.take((size_t)((d.nsub + 63) / 64) * d.stage_cap * 64 * 16, 256);
+      b.stage_on = true;
+    }
     o.mk = L.take((size_t)d.mk_cap * 4, 16);
     o.chunk = L.take((size_t)d.nchunk * 16, 16);
     if (host_io) in_off[i] = IN.take(lens[i] + 16, 16);
@@ -1023,6 +1032,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       }
     } else {
     d.ds = (uint64_t)(uintptr_t)(S + o.ds);
+    d.stage = d.stage_cap ? (uint64_t)(uintptr_t)(S + o.stage) : 0;
     d.mk = (uint64_t)(uintptr_t)(S + o.mk);
     d.chunk = (uint64_t)(uintptr_t)(S + o.chunk);
     }
@@ -1288,13 +1298,16 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   }
   if (next()) return DG_ERR_DEVICE;
   Ckpt *ck = (Ckpt *)((char *)sl.scratch.p + sl.ckpt_off);
-  if (!from_fix) launch_huff_sync(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
+  if (!from_fix) launch_huff_sync(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on);
   if (next()) return DG_ERR_DEVICE;
-  launch_huff_fix(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl);
+  launch_huff_fix(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on);
   if (next()) return DG_ERR_DEVICE;
   launch_huff_scan(sl.st, dm, lst(L_SCAN), cnt(L_SCAN), subs);
   if (next()) return DG_ERR_DEVICE;
-  launch_huff_write(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+  if (b.stage_on)
+    launch_huff_scatter(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), subs);
+  else
+    launch_huff_write(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
   if (next()) return DG_ERR_DEVICE;
   if (next()) return DG_ERR_DEVICE;  // coeffs (side stream)
   launch_idct(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);

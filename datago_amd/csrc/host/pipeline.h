@@ -62,6 +62,7 @@ struct Batch {
   std::vector<uint8_t> blob;
   size_t blob_off = 0;
   bool any_png = false, any_alpha = false, any_enc = false;
+  bool stage_on = false;  // decode-once staging (option "entropy_once")
   size_t words_off = 0, words_bytes = 0;  // contiguous encoder bit buffers (zeroed per batch)
   size_t enctab_off = 0;                  // EncTables in the blob
   std::vector<ProgScan> pscans;           // progressive JPEG scans of the batch
@@ -203,6 +204,7 @@ class Context {
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
   bool progressive_ = false;            // option "progressive"
   bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first
+  bool entropy_once_ = false;           // option "entropy_once": decode-once staging + k_huff_scatter
   int64_t stat_png_serial_ = 0, stat_png_chunks_ = 0;
   // "wg_timing" summaries of the last batch (microseconds): per kernel {span, mean, p90, max}
   double wgstat_[2][4] = {{0}};

@@ -13,14 +13,18 @@ void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *l
 // Entropy decode (one 256-thread workgroup per 256 subsequences of one image)
 // (sync/fix: 255 useful subsequences per workgroup, see kernels.hip)
 struct Ckpt;
+// stage: decode-once staging (ImageDesc::stage), see k_huff_scatter
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags);
+                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage = false);
 void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                     const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags);
+                     const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage = false);
 // one workgroup per image
 void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs);
 void launch_huff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                        const HuffTable *pool, const SubState *subs, BatchFlags *flags);
+// decode-once: blocks from the staged coefficients (replaces k_huff_write when ImageDesc::stage is set)
+void launch_huff_scatter(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+                         const SubState *subs);
 // dequant + IDCT: 64 blocks of one block row per workgroup
 void launch_idct(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                  const QuantTable *qpool);

@@ -264,7 +264,8 @@ __device__ __forceinline__ void wg_time_store(const BatchFlags *flags, uint32_t 
 // step with the true decode and k_huff_fix finds nothing to repair.
 constexpr uint32_t kUseful = kSubPerWg - 1;
 
-__device__ __forceinline__ void store_sub(SubState &o, uint32_t in, uint32_t out, const RangeAcc &a) {
+__device__ __forceinline__ void store_sub(SubState &o, uint32_t in, uint32_t out, const RangeAcc &a,
+                                          const StageCtx *stg = nullptr) {
   o.in = in;
   o.out = out;
   o.m = a.m;
@@ -272,8 +273,13 @@ __device__ __forceinline__ void store_sub(SubState &o, uint32_t in, uint32_t out
   o.dc[0] = a.dc[0];
   o.dc[1] = a.dc[1];
   o.dc[2] = a.dc[2];
+  if (stg && stg->on) {
+    o.nstart = stg->started;
+    o.nent = stg->n;
+  }
 }
 
+template <bool STAGE>
 __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__ imgs,
                                                    const WgItem *__restrict__ list,
                                                    const HuffTable *__restrict__ pool,
@@ -293,13 +299,22 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   const bool head = (t == 0) || (s0 == 0 && t == 1);
   const uint32_t s = active ? (uint32_t)si : 0u;
   const uint32_t nck = num_ckpt(im.sub_bits);
-  DG_GLOBAL Ckpt *ck = (t > 0 && active && nck) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck : nullptr;
+  // decode-once: record the coefficients (no checkpoint merging: a re-decode
+  // must stage its whole range); thread 0's lead-in range belongs to the
+  // previous workgroup and is not staged
+  const bool stage = STAGE && im.stage != 0;
+  DG_GLOBAL Ckpt *ck =
+      (!stage && t > 0 && active && nck) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck : nullptr;
+  StageCtx sc;
+  sc.on = stage && t > 0 && active;
+  sc.base = sc.on ? stage_range(im.stage, im.stage_cap, s) : nullptr;
+  StageCtx *stg = STAGE ? &sc : nullptr;
   const DG_GLOBAL uint8_t *scan = gp<const uint8_t>(im.ds);
   const DG_GLOBAL uint32_t *mkp = gp<const uint32_t>(im.mk);
   RangeAcc acc = {0, 0, 0, {0, 0, 0}};
   // entry state: exact for s == 0, otherwise the lead-in decode's guess
   uint32_t in = active ? lead_in(im, tabs, scan, mkp, s, im.lead_bits) : pack_state(0, 0, 0);
-  if (active) decode_range<false>(im, tabs, scan, mkp, s, in, acc, nullptr, ck);
+  if (active) decode_range<false>(im, tabs, scan, mkp, s, in, acc, nullptr, ck, false, 0, stg);
   ex[t] = active ? acc.out : 0u;
   ins[t] = in;
   __syncthreads();
@@ -309,18 +324,19 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
     uint32_t pin = redo ? ex[t - 1] : 0u;
     __syncthreads();
     if (redo) {
-      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr, ck, true, ex[t]);
+      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr, ck, true, ex[t], stg);
       ex[t] = acc.out;
       ins[t] = pin;
     }
     iters++;
     if (!__syncthreads_or(redo)) break;
   }
-  if (active && t > 0) store_sub(subs[im.sub_base + s], ins[t], ex[t], acc);
+  if (active && t > 0) store_sub(subs[im.sub_base + s], ins[t], ex[t], acc, stg);
   if (t == 0) atomicMax(&flags->sync_iters_max, iters);
   wg_time_store(flags, blockIdx.x, t_start);
 }
 
+template <bool STAGE>
 __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ imgs,
                                                   const WgItem *__restrict__ list,
                                                   const HuffTable *__restrict__ pool,
@@ -340,7 +356,12 @@ __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ 
   const uint32_t s = s0 + t;
   const bool active = t < (int)kUseful && s < im.nsub;
   const uint32_t nck = num_ckpt(im.sub_bits);
-  DG_GLOBAL Ckpt *ck = (active && nck) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck : nullptr;
+  const bool stage = STAGE && im.stage != 0;
+  DG_GLOBAL Ckpt *ck = (!stage && active && nck) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck : nullptr;
+  StageCtx sc;
+  sc.on = stage && active;
+  sc.base = sc.on ? stage_range(im.stage, im.stage_cap, s) : nullptr;
+  StageCtx *stg = STAGE ? &sc : nullptr;
   const DG_GLOBAL uint8_t *scan = gp<const uint8_t>(im.ds);
   const DG_GLOBAL uint32_t *mkp = gp<const uint32_t>(im.mk);
   RangeAcc acc = {0, 0, 0, {0, 0, 0}};
@@ -366,7 +387,7 @@ __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ 
     uint32_t pin = redo ? (t == 0 ? first_in : ex[t - 1]) : 0u;
     __syncthreads();
     if (redo) {
-      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr, ck, true, ex[t]);
+      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr, ck, true, ex[t], stg);
       ex[t] = acc.out;
       ins[t] = pin;
       mine = true;
@@ -374,7 +395,7 @@ __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ 
     if (!__syncthreads_or(redo)) break;
   }
   if (active && mine) {
-    store_sub(base[s], ins[t], ex[t], acc);
+    store_sub(base[s], ins[t], ex[t], acc, stg);
     bool last = (t == (int)kUseful - 1) && (s + 1 < im.nsub);
     if (last && ex[t] != orig_out) atomicAdd(&flags->chain_changed, 1u);
   }
@@ -465,6 +486,85 @@ __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict_
     __syncthreads();
     wg_time_store(flags, flags->wgtime_write + blockIdx.x, t_start);
   }
+}
+
+// Decode-once (option "entropy_once"): the blocks from k_huff_sync's staged
+// coefficients -- what k_huff_write writes, without decoding the range again.
+// One thread per range, its block in LDS as in k_huff_write: blocks are
+// started in order (j), carry their DC predictor, and are flushed over the
+// zigzag span this range owns (the carried-in block from its entry z, a
+// block cut by a marker or by the range end up to that z).
+__global__ __launch_bounds__(256) void k_huff_scatter(const ImageDesc *__restrict__ imgs,
+                                                      const WgItem *__restrict__ list,
+                                                      const SubState *__restrict__ subs) {
+  __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][64];
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  const int t = threadIdx.x;
+  const uint32_t s = it.item0 + t;
+  if (s >= im.nsub) return;
+  const SubState ss = subs[im.sub_base + s];
+  WriteCtx w;
+  w.blk = blk[t];
+  w.coef = gp<int16_t>(im.coef);
+  w.seg = ss.seg;
+  w.nin = ss.nin;
+  w.pred[0] = ss.dcin[0];
+  w.pred[1] = ss.dcin[1];
+  w.pred[2] = ss.dcin[2];
+  w.blocks_per_seg = im.blocks_per_seg;
+  w.total_blocks = im.total_blocks;
+  w.cur = -1;
+  w.zs = 0;
+  if (s * im.sub_bits >= im.ds_bits) return;  // empty trailing range: decodes nothing
+  const uint32_t bpm = im.bpm, cbits = im.comp_bits;
+  const uint32_t zin = st_z(ss.in);
+  uint32_t rn = st_r(ss.in);  // block-in-MCU of the next block to start
+  if (zin > 0) {
+    wc_begin(w, w.nin > 0 ? wc_index(w, w.nin - 1) : -1, zin);
+    rn = rn + 1 == bpm ? 0 : rn + 1;
+  }
+  uint32_t started = 0, comp = 0;
+  auto start_next = [&]() {
+    wc_flush(w, 64);  // the open block completed
+    comp = (cbits >> (2 * rn)) & 3u;
+    rn = rn + 1 == bpm ? 0 : rn + 1;
+    wc_begin(w, wc_index(w, w.nin), 0);
+    w.nin++;
+    w.blk[0] = (int16_t)sel3(w.pred, comp);
+    started++;
+  };
+  const DG_GLOBAL u32x4 *g = (const DG_GLOBAL u32x4 *)stage_range(im.stage, im.stage_cap, s);
+  u32x4 grp = {0u, 0u, 0u, 0u};
+  for (uint32_t e = 0; e < ss.nent; e++) {
+    if ((e & 3u) == 0) grp = g[(size_t)(e >> 2) * 64];
+    const uint32_t k = e & 3u;
+    const uint32_t v = k == 0 ? grp.x : k == 1 ? grp.y : k == 2 ? grp.z : grp.w;
+    if (v & 0x80000000u) {  // RST marker
+      const uint32_t zm = (v >> 24) & 63u, j = (v >> 11) & 0x1FFFu;
+      while (started < j) start_next();
+      wc_flush(w, zm > 0 ? zm : 64);
+      if (v & 0x40000000u) {
+        w.seg++;
+        w.nin = 0;
+        w.pred[0] = w.pred[1] = w.pred[2] = 0;
+      }
+      rn = 0;
+      continue;
+    }
+    const uint32_t zz = v >> 25, j = (v >> 12) & 0x1FFFu;
+    const int32_t val = (int32_t)(v << 20) >> 20;
+    while (started < j) start_next();
+    if (zz == 0) {
+      add3(w.pred, comp, val);
+      w.blk[0] = (int16_t)sel3(w.pred, comp);
+    } else {
+      w.blk[zz] = (int16_t)val;
+    }
+  }
+  while (started < ss.nstart) start_next();
+  const uint32_t zout = st_z(ss.out);
+  wc_flush(w, zout > 0 ? zout : 64);
 }
 
 // ------------------------------------------------------------ IDCT
@@ -1259,12 +1359,18 @@ void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *l
   DG_LAUNCH(k_destuff_write, nwg, st, imgs, list);
 }
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags) {
-  DG_LAUNCH(k_huff_sync, nwg, st, imgs, list, pool, subs, ck, flags);
+                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage) {
+  if (stage)
+    DG_LAUNCH(k_huff_sync<true>, nwg, st, imgs, list, pool, subs, ck, flags);
+  else
+    DG_LAUNCH(k_huff_sync<false>, nwg, st, imgs, list, pool, subs, ck, flags);
 }
 void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                     const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags) {
-  DG_LAUNCH(k_huff_fix, nwg, st, imgs, list, pool, subs, ck, flags);
+                     const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage) {
+  if (stage)
+    DG_LAUNCH(k_huff_fix<true>, nwg, st, imgs, list, pool, subs, ck, flags);
+  else
+    DG_LAUNCH(k_huff_fix<false>, nwg, st, imgs, list, pool, subs, ck, flags);
 }
 void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs) {
   DG_LAUNCH(k_huff_scan, nwg, st, imgs, list, subs);
@@ -1272,6 +1378,10 @@ void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint3
 void launch_huff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                        const HuffTable *pool, const SubState *subs, BatchFlags *flags) {
   DG_LAUNCH(k_huff_write, nwg, st, imgs, list, pool, subs, flags);
+}
+void launch_huff_scatter(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+                         const SubState *subs) {
+  DG_LAUNCH(k_huff_scatter, nwg, st, imgs, list, subs);
 }
 void launch_idct(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, const QuantTable *qpool) {
   DG_LAUNCH(k_idct, nwg, st, imgs, list, qpool);

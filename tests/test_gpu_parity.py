@@ -163,6 +163,25 @@ def test_band_and_slot_options_bit_exact(bands, slots):
             assert np.array_equal(arr, _oracle_resized(data, *t.target_size(w, h))), (bands, slots, (w, h))
 
 
+@pytest.mark.parametrize("sub_bits", [0, 512, 2048, 8192])
+def test_entropy_decode_once_matches(sub_bits):
+    """Option entropy_once: k_huff_sync stages every coefficient and
+    k_huff_scatter writes the blocks (no second decode).  Outputs must equal
+    the default two-pass path and the oracle bit for bit, with restart
+    markers (owned / unowned at range ends), gray, 4:2:2 and 4:4:4."""
+    L = _lib()
+    datas = _rand_jpegs(8, 10, maxdim=1200) + _rand_jpegs(9, 8, maxdim=900, rst=True)
+    datas.append(synth.make_jpeg(88, 2000, 1500, 95, "4:2:0", False, restart_marker_rows=1))
+    ctx = L.Context(0)
+    ctx.set_option("entropy_once", 1)
+    if sub_bits:
+        ctx.set_option("sub_bits", sub_bits)
+    for i, (d, (st, arr, _)) in enumerate(zip(datas, ctx.decode_batch(datas))):
+        assert st == 0, i
+        ost, ref = O.jpeg_decode(d)
+        assert np.array_equal(arr.reshape(ref.shape), ref), (i, sub_bits)
+
+
 def test_band_and_slot_options_validated():
     L = _lib()
     ctx = L.Context(0)
