@@ -39,12 +39,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="images per step")
+    ap.add_argument("--batch", type=int, default=0, help="images per step (0: 256, or 1024 for wds's ImageNet-size JPEGs)")
     ap.add_argument("--pool", type=int, default=256, help="unique images per rank held in HBM")
     ap.add_argument("--short-min", type=int, default=256)
     ap.add_argument("--short-max", type=int, default=2048)
-    ap.add_argument("--size", type=int, default=1024)
-    ap.add_argument("--ratio", type=int, default=32)
+    ap.add_argument("--size", type=int, default=0, help="bucket default_image_size (0: 1024, or 512 for wds)")
+    ap.add_argument("--ratio", type=int, default=0, help="bucket downsampling_ratio (0: 32, or 16 for wds)")
     ap.add_argument("--sub-bits", type=int, default=0)
     ap.add_argument("--workers", type=int, default=0, help="corpus generation processes")
     ap.add_argument("--lead-bits", type=int, default=-1, help="entropy lead-in bits (-1 = library default)")
@@ -77,6 +77,12 @@ def parse():
     a = ap.parse_args()
     if a.inflight <= 0:
         a.inflight = 4 if a.workload == "png" else 2
+    if a.batch <= 0:
+        a.batch = 1024 if a.workload == "wds" else 256
+    if a.size <= 0:  # BASELINE.json configs[2]: "decode + resize to 512"
+        a.size = 512 if a.workload == "wds" else 1024
+    if a.ratio <= 0:
+        a.ratio = 16 if a.workload == "wds" else 32
     return a
 
 
