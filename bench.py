@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_T = 256 * 4 * 2.4e9 / 2 / 1e12  # VALU wave-instructions/s: 256 CUs x 4 SIMDs, one per 2 cycles, 2.4 GHz
 
 
 def parse():
@@ -501,13 +502,16 @@ def main() -> int:
         dom_alg = stage_alg[dom] / steps if dom in stage_alg else 0.0
         achieved = dom_alg / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
         gpu_ms = sum(kern.values()) / steps
-        traffic, traffic_src = None, None
+        traffic, traffic_src, valu = None, None, None
         try:
             with open(a.pmc_json) as f:
                 pmc = json.load(f)
             if pmc.get("config") == pmc_config_key(a) and dom in pmc.get("bytes_per_batch", {}):
                 traffic = pmc["bytes_per_batch"][dom] * (B_ / pmc.get("images_per_batch", B_))
                 traffic_src = f"{os.path.relpath(a.pmc_json)} ({pmc.get('correction', '')})"
+            if pmc.get("config") == pmc_config_key(a):
+                valu = {k: v * (B_ / pmc.get("images_per_batch", B_))
+                        for k, v in pmc.get("valu_wave_insts_per_batch", {}).items()}
         except (OSError, ValueError):
             pass
         iso = None
@@ -556,6 +560,15 @@ def main() -> int:
                          "note": "per step (one batch); kernel times from HIP events on the slot stream over the "
                                  "timed region, where consecutive batches overlap"},
             "roofline_isolated": iso,
+            # The pixel and entropy kernels are integer VALU / latency work, not HBM-bound: their VALU
+            # issue rate (PMC SQ_INSTS_VALU per batch over the isolated kernel time) against the
+            # MI355X peak of 256 CUs x 4 SIMDs x one wave-instruction per 2 cycles x 2.4 GHz.
+            "roofline_valu": ({k: {"wave_insts": round(valu[k]),
+                                   "achieved_T_per_s": round(valu[k] / (iso["stages_ms"][k] / 1e3) / 1e12, 4),
+                                   "peak_T_per_s": VALU_PEAK_T,
+                                   "frac": round(valu[k] / (iso["stages_ms"][k] / 1e3) / 1e12 / VALU_PEAK_T, 4)}
+                               for k in valu if iso and iso["stages_ms"].get(k, 0) > 0.05}
+                              if valu and iso else None),
             "roofline_pipeline": {"alg_bytes_per_step": round(per_step_alg), "gpu_ms_per_step": round(gpu_ms, 4),
                                   "achieved_GBs": round(per_step_alg / (gpu_ms / 1e3) / 1e9, 2),
                                   "frac": round(per_step_alg / (gpu_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)},

@@ -28,7 +28,7 @@ def stage_sequence(rows):
         k = r["Kernel_Name"]
         if "dg::" not in k:
             continue
-        name = k.split("(")[0].replace("void ", "").replace("dg::", "")
+        name = k.split("(")[0].replace("void ", "").replace("dg::", "").split("<")[0]
         if name.startswith("k_huff_sync"):
             nv = 0
             phase = "h1"
@@ -61,6 +61,18 @@ def main(root, config=None, images_per_batch=None):
             if d in seq:
                 per[seq[d]] += float(r["Counter_Value"]) * 1024.0
         res[counter] = ({k: v / max(nbatch, 1) for k, v in per.items()}, nbatch)
+    # VALU wave-instructions per stage (the "sq" pass), for the compute-side roofline
+    files = glob.glob(os.path.join(root, "sq", "**", "*counter_collection.csv"), recursive=True)
+    rows = [r for f in files for r in csv.DictReader(open(f)) if r["Counter_Name"] == "SQ_INSTS_VALU"]
+    valu = defaultdict(float)
+    if rows:
+        seq = dict(stage_sequence(rows))
+        nbv = sum(1 for r in rows if "k_huff_sync" in r["Kernel_Name"])
+        for r in rows:
+            d = int(r["Dispatch_Id"])
+            if d in seq:
+                valu[seq[d]] += float(r["Counter_Value"])
+        valu = {k: v / max(nbv, 1) for k, v in valu.items()}
     fetch, nb = res["FETCH_SIZE"]
     write, _ = res["WRITE_SIZE"]
     stages = sorted(set(fetch) | set(write))
@@ -73,6 +85,7 @@ def main(root, config=None, images_per_batch=None):
         "bytes_per_batch": {s: round(2.0 * fetch.get(s, 0.0) + write.get(s, 0.0)) for s in stages},
         "fetch_bytes_per_batch_x2": {s: round(2.0 * fetch.get(s, 0.0)) for s in stages},
         "write_bytes_per_batch": {s: round(write.get(s, 0.0)) for s in stages},
+        "valu_wave_insts_per_batch": {s: round(v) for s, v in sorted(valu.items())},
     }
     json.dump(out, sys.stdout, indent=1)
     print()
