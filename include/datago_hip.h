@@ -201,8 +201,16 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "timing"      1 = record per-kernel HIP events (dg_last_batch_timings)
  *   "side_stream" 1 = Lanczos tables on a second stream (default 1)
  *   "debug_flags" internal switches for kernel bisection
+ *   "progressive" 1 = decode progressive JPEGs on the GPU (default 0: DG_ERR_UNSUPPORTED, the
+ *                 caller's CPU decoder takes them; refinement scans decode serially)
+ *   "slots"       batches in flight, 1..4 (default 2)
+ *   "hb_bands"    band H kernel: 8-row bands per workgroup, 1..64 (default 8)
+ *   "entropy_lpt" 1 = dispatch the slowest entropy workgroups first (default 1)
+ *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)
+ *   "png_chunked" 0 = inflate every PNG with the serial kernel (test switch; default 1)
  * Stats: "batches", "coalesced_batches", "coalesced_images", "resync_rounds", "fix_workgroups", "write_mismatch",
- * "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool"; -1 if unknown. */
+ * "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool", "png_chunks", "png_serial_fallbacks";
+ * -1 if unknown. */
 dg_status dg_ctx_set_option(dg_ctx *ctx, const char *key, int64_t value);
 int64_t dg_ctx_get_stat(dg_ctx *ctx, const char *key);
 
