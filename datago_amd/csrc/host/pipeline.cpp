@@ -684,6 +684,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       d.qpool[c] = (uint16_t)pool_quant(h.q[h.comp[c].tq]);
     }
     d.nslots = (uint8_t)nslots;
+    b.max_slots = std::max<uint32_t>(b.max_slots, (uint32_t)nslots);
     if (h.progressive) {  // scans decoded by k_prog_scan (records built once the source address is known)
       d.prog = (uint32_t)h.scans.size();
       if (host_io) in_off[i] = IN.take(lens[i] + 16, 16);
@@ -1298,9 +1299,9 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   }
   if (next()) return DG_ERR_DEVICE;
   Ckpt *ck = (Ckpt *)((char *)sl.scratch.p + sl.ckpt_off);
-  if (!from_fix) launch_huff_sync(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on);
+  if (!from_fix) launch_huff_sync(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on, b.max_slots);
   if (next()) return DG_ERR_DEVICE;
-  launch_huff_fix(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on);
+  launch_huff_fix(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on, b.max_slots);
   if (next()) return DG_ERR_DEVICE;
   launch_huff_scan(sl.st, dm, lst(L_SCAN), cnt(L_SCAN), subs);
   if (next()) return DG_ERR_DEVICE;

@@ -63,6 +63,7 @@ struct Batch {
   size_t blob_off = 0;
   bool any_png = false, any_alpha = false, any_enc = false;
   bool stage_on = false;  // decode-once staging (option "entropy_once")
+  uint32_t max_slots = 1; // largest Huffman table count of an image (dynamic LDS of k_huff_sync/fix)
   size_t words_off = 0, words_bytes = 0;  // contiguous encoder bit buffers (zeroed per batch)
   size_t enctab_off = 0;                  // EncTables in the blob
   std::vector<ProgScan> pscans;           // progressive JPEG scans of the batch

@@ -14,10 +14,13 @@ void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *l
 // (sync/fix: 255 useful subsequences per workgroup, see kernels.hip)
 struct Ckpt;
 // stage: decode-once staging (ImageDesc::stage), see k_huff_scatter
+// max_slots: the largest ImageDesc::nslots in the batch (dynamic LDS for the tables)
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage = false);
+                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
+                      uint32_t max_slots);
 void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                     const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage = false);
+                     const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
+                     uint32_t max_slots);
 // one workgroup per image
 void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs);
 void launch_huff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,

@@ -285,7 +285,8 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
                                                    const HuffTable *__restrict__ pool,
                                                    SubState *__restrict__ subs, Ckpt *__restrict__ ckpt,
                                                    BatchFlags *flags) {
-  __shared__ HuffTable tabs[kMaxSlots];
+  extern __shared__ __attribute__((aligned(16))) uint8_t huff_dyn[];  // im.nslots tables (launch: batch max)
+  HuffTable *tabs = (HuffTable *)huff_dyn;
   __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
   const uint64_t t_start = wg_clock();
   const WgItem it = list[blockIdx.x];
@@ -342,7 +343,8 @@ __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ 
                                                   const HuffTable *__restrict__ pool,
                                                   SubState *__restrict__ subs, Ckpt *__restrict__ ckpt,
                                                   BatchFlags *flags) {
-  __shared__ HuffTable tabs[kMaxSlots];
+  extern __shared__ __attribute__((aligned(16))) uint8_t huff_dyn[];
+  HuffTable *tabs = (HuffTable *)huff_dyn;
   __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
   const WgItem it = list[blockIdx.x];
   const uint32_t s0 = it.item0;
@@ -1358,19 +1360,28 @@ void launch_destuff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, ui
 void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   DG_LAUNCH(k_destuff_write, nwg, st, imgs, list);
 }
+// sync / fix hold only the batch's largest table count in LDS (4 for a
+// typical colour JPEG instead of kMaxSlots = 6): 16 KiB instead of 23 KiB
+// per workgroup, 8 resident workgroups per CU instead of 6
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage) {
+                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
+                      uint32_t max_slots) {
+  if (!nwg) return;
+  const size_t lds = (size_t)max_slots * sizeof(HuffTable);
   if (stage)
-    DG_LAUNCH(k_huff_sync<true>, nwg, st, imgs, list, pool, subs, ck, flags);
+    hipLaunchKernelGGL(k_huff_sync<true>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags);
   else
-    DG_LAUNCH(k_huff_sync<false>, nwg, st, imgs, list, pool, subs, ck, flags);
+    hipLaunchKernelGGL(k_huff_sync<false>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags);
 }
 void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                     const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage) {
+                     const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
+                     uint32_t max_slots) {
+  if (!nwg) return;
+  const size_t lds = (size_t)max_slots * sizeof(HuffTable);
   if (stage)
-    DG_LAUNCH(k_huff_fix<true>, nwg, st, imgs, list, pool, subs, ck, flags);
+    hipLaunchKernelGGL(k_huff_fix<true>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags);
   else
-    DG_LAUNCH(k_huff_fix<false>, nwg, st, imgs, list, pool, subs, ck, flags);
+    hipLaunchKernelGGL(k_huff_fix<false>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags);
 }
 void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs) {
   DG_LAUNCH(k_huff_scan, nwg, st, imgs, list, subs);
