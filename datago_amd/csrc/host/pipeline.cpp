@@ -421,6 +421,12 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
     p.enc_la_gray = p.out_c == 2 && has_cfg_ && !(W == p.out_w && H == p.out_h);
     p.out_bytes = p.enc_png ? png_enc_bound(ow, oh, p.enc_la_gray ? 1 : p.out_c) : jpeg_enc_bound(ow, oh, p.out_c);
     p.channels = -1;  // :416
+    // the encoders count bits in 32-bit offsets (~400 MB of output): larger
+    // images stay on the caller's CPU encoder
+    if (p.out_bytes >= (1ull << 29)) {
+      p.status = DG_ERR_UNSUPPORTED;
+      return DG_OK;
+    }
   }
   return DG_OK;
 }
