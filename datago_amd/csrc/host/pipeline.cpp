@@ -1314,7 +1314,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (b.stage_on)
     launch_huff_scatter(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), subs);
   else
-    launch_huff_write(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl);
+    launch_huff_write(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots);
   if (next()) return DG_ERR_DEVICE;
   if (next()) return DG_ERR_DEVICE;  // coeffs (side stream)
   launch_idct(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);

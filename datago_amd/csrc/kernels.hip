@@ -453,12 +453,19 @@ __global__ __launch_bounds__(256) void k_huff_scan(ImageDesc *__restrict__ imgs,
   }
 }
 
+// Per-thread coefficient blocks in LDS, 72 int16 (36 dwords) apart: the
+// 16-byte zeroing stores and flush loads of consecutive lanes then cover
+// distinct banks (a 64-coefficient stride put all lanes of a group on the same
+// four banks), and single-coefficient stores spread over banks by lane.
+constexpr int kBlkStride = 72;
+
 __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict__ imgs,
                                                     const WgItem *__restrict__ list,
                                                     const HuffTable *__restrict__ pool,
                                                     const SubState *__restrict__ subs, BatchFlags *flags) {
-  __shared__ HuffTable tabs[kMaxSlots];
-  __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][64];
+  extern __shared__ __attribute__((aligned(16))) uint8_t huff_dyn[];  // im.nslots tables (launch: batch max)
+  HuffTable *tabs = (HuffTable *)huff_dyn;
+  __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][kBlkStride];
   const uint64_t t_start = wg_clock();
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
@@ -499,7 +506,7 @@ __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict_
 __global__ __launch_bounds__(256) void k_huff_scatter(const ImageDesc *__restrict__ imgs,
                                                       const WgItem *__restrict__ list,
                                                       const SubState *__restrict__ subs) {
-  __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][64];
+  __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][kBlkStride];
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
   const int t = threadIdx.x;
@@ -581,7 +588,12 @@ constexpr uint32_t kIdctBlocks = 64;
 
 __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
                                               const QuantTable *__restrict__ qpool) {
-  constexpr int LD = 65;  // padded block stride (dwords): breaks the 64-dword bank period
+  // Block layout in LDS: element (row r, column c) at r * RS + c, blocks LD
+  // dwords apart.  With 4 blocks x 8 lanes per 32-lane bank group, the column
+  // accesses of pass 1 (r fixed) and the row reads of pass 2 (c fixed) are
+  // conflict-free and the zigzag scatter is at most 2-way (a 64-dword block
+  // stride made them 4-, 2- and 3-way).
+  constexpr int LD = 72, RS = 9;
   __shared__ int32_t blkv[kIdctBlocks * LD];
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
@@ -621,24 +633,25 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int n = kZigzagToNatural[lane * 8 + i];
-      bv0[n] = a[i];
-      bv1[n] = b[i];
+      const int e = (n >> 3) * RS + (n & 7);
+      bv0[e] = a[i];
+      bv1[e] = b[i];
     }
   }
   __syncthreads();
   int32_t o0[8], o1[8];
   // pass 1: column `lane`, dequantised on the way in
-  idct_1d(bv0[0 * 8 + lane] * qc[0], bv0[1 * 8 + lane] * qc[1], bv0[2 * 8 + lane] * qc[2],
-          bv0[3 * 8 + lane] * qc[3], bv0[4 * 8 + lane] * qc[4], bv0[5 * 8 + lane] * qc[5],
-          bv0[6 * 8 + lane] * qc[6], bv0[7 * 8 + lane] * qc[7], o0);
-  idct_1d(bv1[0 * 8 + lane] * qc[0], bv1[1 * 8 + lane] * qc[1], bv1[2 * 8 + lane] * qc[2],
-          bv1[3 * 8 + lane] * qc[3], bv1[4 * 8 + lane] * qc[4], bv1[5 * 8 + lane] * qc[5],
-          bv1[6 * 8 + lane] * qc[6], bv1[7 * 8 + lane] * qc[7], o1);
+  idct_1d(bv0[0 * RS + lane] * qc[0], bv0[1 * RS + lane] * qc[1], bv0[2 * RS + lane] * qc[2],
+          bv0[3 * RS + lane] * qc[3], bv0[4 * RS + lane] * qc[4], bv0[5 * RS + lane] * qc[5],
+          bv0[6 * RS + lane] * qc[6], bv0[7 * RS + lane] * qc[7], o0);
+  idct_1d(bv1[0 * RS + lane] * qc[0], bv1[1 * RS + lane] * qc[1], bv1[2 * RS + lane] * qc[2],
+          bv1[3 * RS + lane] * qc[3], bv1[4 * RS + lane] * qc[4], bv1[5 * RS + lane] * qc[5],
+          bv1[6 * RS + lane] * qc[6], bv1[7 * RS + lane] * qc[7], o1);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 8; r++) {
-    bv0[r * 8 + lane] = descale(o0[r], kConstBits - kPass1Bits);
-    bv1[r * 8 + lane] = descale(o1[r], kConstBits - kPass1Bits);
+    bv0[r * RS + lane] = descale(o0[r], kConstBits - kPass1Bits);
+    bv1[r * RS + lane] = descale(o1[r], kConstBits - kPass1Bits);
   }
   __syncthreads();
   // pass 2: row `lane`
@@ -646,7 +659,7 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
   DG_GLOBAL uint8_t *plane = gp<uint8_t>(im.plane[c]) + (size_t)(by * 8 + lane) * pst;
 #pragma unroll
   for (int h = 0; h < 2; h++) {
-    const int32_t *w = (h ? bv1 : bv0) + lane * 8;
+    const int32_t *w = (h ? bv1 : bv0) + lane * RS;
     const bool v = h ? v1 : v0;
     int32_t o[8];
     idct_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
@@ -1387,8 +1400,10 @@ void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint3
   DG_LAUNCH(k_huff_scan, nwg, st, imgs, list, subs);
 }
 void launch_huff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                       const HuffTable *pool, const SubState *subs, BatchFlags *flags) {
-  DG_LAUNCH(k_huff_write, nwg, st, imgs, list, pool, subs, flags);
+                       const HuffTable *pool, const SubState *subs, BatchFlags *flags, uint32_t max_slots) {
+  if (!nwg) return;
+  hipLaunchKernelGGL(k_huff_write, dim3(nwg), dim3(256), (size_t)max_slots * sizeof(HuffTable), st, imgs, list,
+                     pool, subs, flags);
 }
 void launch_huff_scatter(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                          const SubState *subs) {
