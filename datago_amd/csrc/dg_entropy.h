@@ -118,6 +118,13 @@ struct WriteCtx {
   uint32_t blocks_per_seg, total_blocks;
   int32_t cur;   // global index of the block being filled (-1 = none / dropped)
   uint32_t zs;   // first zigzag index this thread owns in the current block
+#if defined(DG_DEVICE)
+  // wave-cooperative flush (k_huff_write): this wave's lane-0 block, block
+  // stride (int16), and a 128-dword LDS table of the wave
+  int16_t *wave_blk;
+  uint32_t stride;
+  uint32_t *tab;
+#endif
 };
 
 DG_HD int32_t wc_index(const WriteCtx &w, uint32_t in_seg) {
@@ -155,6 +162,74 @@ DG_HD void wc_flush(WriteCtx &w, uint32_t ze) {
     for (uint32_t i = w.zs; i < ze; i++) dst[i] = w.blk[i];
   }
   w.cur = -1;
+}
+
+#if defined(DG_DEVICE)
+// Full blocks completed by lanes of a wave are written out together: a lane
+// whose block ends only marks it pending, and at the top of the next symbol
+// step the wave's active lanes copy every pending block with one 16-byte
+// chunk each (8 lanes per block, 128 contiguous bytes) and zero it in LDS for
+// its owner's next block.  A per-lane flush costs every lane 8 LDS loads, 8
+// global stores and 8 LDS stores whenever any lane of the wave ends a block,
+// which with ~8 symbols per block is nearly every step.  Blocks are zero
+// whenever a lane has none open, so a block start only sets its index.
+__device__ __forceinline__ void wc_coop_flush(WriteCtx &w, bool pending) {
+  const uint64_t pm = __ballot(pending);
+  if (!pm) return;
+  const uint64_t am = __ballot(1);
+  if (pending) {
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+    w.tab[rank] = __lane_id();
+    w.tab[64 + rank] = (uint32_t)w.cur;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t wr = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+  const uint32_t na = (uint32_t)__popcll(am), nc = 8u * (uint32_t)__popcll(pm);
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  for (uint32_t c = wr; c < nc; c += na) {
+    const uint32_t k = c >> 3, part = c & 7u;
+    const int32_t idx = (int32_t)w.tab[64 + k];
+    u32x4 *src = (u32x4 *)(w.wave_blk + w.tab[k] * w.stride) + part;
+    if (idx >= 0) *(DG_GLOBAL u32x4 *)(w.coef + (size_t)idx * 64 + part * 8) = *src;
+    *src = zero;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// rare paths (partial blocks at range ends and restart markers): flush, then
+// restore the all-zero block
+__device__ __forceinline__ void wc_flush_zero(WriteCtx &w, uint32_t ze) {
+  wc_flush(w, ze);
+  u32x4 *p = (u32x4 *)w.blk;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < 8; i++) p[i] = zero;
+}
+#endif
+
+// Block flush / start inside decode_range: wave-cooperative on the device
+// when the context provides the table (COOP), per lane otherwise.
+template <bool COOP>
+DG_HD void wc_end_block(WriteCtx &w, bool &pending) {
+#if defined(DG_DEVICE)
+  if (COOP) {
+    if (w.zs == 0) pending = true;
+    else wc_flush_zero(w, 64);
+    return;
+  }
+#endif
+  (void)pending;
+  wc_flush(w, 64);
+}
+template <bool COOP>
+DG_HD void wc_partial(WriteCtx &w, uint32_t ze) {
+#if defined(DG_DEVICE)
+  if (COOP) {
+    wc_flush_zero(w, ze);
+    return;
+  }
+#endif
+  wc_flush(w, ze);
 }
 
 // Decode-once staging (option "entropy_once").  The sync decode records
@@ -303,7 +378,7 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
 //   tabs: Huffman tables indexed by slot (im.dc_slot / im.ac_slot)
 //   ck: this subsequence's checkpoint records (nullptr: none); merge: the
 //   records hold a previous decode of this range whose exit state was old_out.
-template <bool WRITE, class TAB>
+template <bool WRITE, class TAB, bool COOP = false>
 DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uint8_t *stream,
                         const DG_GLOBAL uint32_t *mk,
                         uint32_t s, uint32_t in, RangeAcc &acc, WriteCtx *w, DG_GLOBAL Ckpt *ck = nullptr,
@@ -336,6 +411,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
   const uint32_t nck = ck ? num_ckpt(S) : 0;
   uint32_t k = 0, cpos = a0 + kCkptBits;
   bool merged = false;
+  bool pending = false;  // COOP: a completed block awaits the wave's flush
   if (WRITE) {
     w->cur = -1;
     if (z > 0) wc_begin(*w, w->nin > 0 ? wc_index(*w, w->nin - 1) : -1, z);
@@ -355,10 +431,16 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
   block_tables(tdc, tac);
   uint32_t ev = next_event();
   for (;;) {
+#if defined(DG_DEVICE)
+    if (WRITE && COOP) {
+      wc_coop_flush(*w, pending);
+      pending = false;
+    }
+#endif
     if (pos >= ev) {
       if (pos >= mpos) {  // restart marker: hard resync
         bool owned = mpos < a1;
-        if (WRITE && z > 0) wc_flush(*w, z);
+        if (WRITE && z > 0) wc_partial<COOP>(*w, z);
         if (stage) stage_push(*stg, stage_marker(owned ? 1u : 0u, z, stg->started));
         pos = mpos;
         r = 0;
@@ -431,7 +513,12 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       }
       if (WRITE) {
         add3(w->pred, comp, v);
-        wc_begin(*w, wc_index(*w, w->nin), 0);
+        if (COOP) {
+          w->cur = wc_index(*w, w->nin);
+          w->zs = 0;
+        } else {
+          wc_begin(*w, wc_index(*w, w->nin), 0);
+        }
         w->nin++;
         w->blk[0] = (int16_t)sel3(w->pred, comp);
       }
@@ -446,14 +533,14 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       z = eob ? 64u : z + run + 1u;
     }
     if (z >= 64) {
-      if (WRITE) wc_flush(*w, 64);
+      if (WRITE) wc_end_block<COOP>(*w, pending);
       z = 0;
       r = (r + 1 == bpm) ? 0 : r + 1;
       comp = (cbits >> (2 * r)) & 3u;
       block_tables(tdc, tac);
     }
   }
-  if (WRITE && z > 0) wc_flush(*w, z);
+  if (WRITE && z > 0) wc_partial<COOP>(*w, z);
   if (stage) stage_finish(*stg);
   if (!merged) {
     uint32_t rel = pos - a1;

@@ -466,6 +466,7 @@ __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict_
   extern __shared__ __attribute__((aligned(16))) uint8_t huff_dyn[];  // im.nslots tables (launch: batch max)
   HuffTable *tabs = (HuffTable *)huff_dyn;
   __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][kBlkStride];
+  __shared__ uint32_t wtab[kSubPerWg / 64][128];  // wc_coop_flush tables, one per wave
   const uint64_t t_start = wg_clock();
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
@@ -487,8 +488,18 @@ __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict_
     w.total_blocks = im.total_blocks;
     w.cur = -1;
     w.zs = 0;
+    w.wave_blk = blk[t & ~63];
+    w.stride = kBlkStride;
+    w.tab = wtab[t >> 6];
+    {  // blocks are all-zero whenever none is open (wc_coop_flush)
+      u32x4 *p = (u32x4 *)w.blk;
+      const u32x4 zero = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int i = 0; i < 8; i++) p[i] = zero;
+    }
     RangeAcc acc;
-    decode_range<true>(im, tabs, gp<const uint8_t>(im.ds), gp<const uint32_t>(im.mk), s, ss.in, acc, &w);
+    decode_range<true, HuffTable, true>(im, tabs, gp<const uint8_t>(im.ds), gp<const uint32_t>(im.mk), s, ss.in,
+                                        acc, &w);
     if (acc.out != ss.out) atomicAdd(&flags->write_mismatch, 1u);
   }
   if (flags->wgtime) {
