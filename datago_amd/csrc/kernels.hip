@@ -714,20 +714,31 @@ __device__ __forceinline__ void upsample8(P pl, uint32_t stride, uint32_t hr, ui
     for (int k = 0; k < 4; k++) cs[k + 1] = (v >> (8 * k)) & 0xFF;
     cs[5] = in[cr];
     // clamp interior samples past the downsampled width (replicate the edge)
+    if (c0 + 5 > dsw) {
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (c0 + k >= dsw) cs[k + 1] = cs[dsw - c0];
+      for (int k = 0; k < 4; k++)
+        if (c0 + k >= dsw) cs[k + 1] = cs[dsw - c0];
+    }
     if (!fancy) {
 #pragma unroll
       for (int k = 0; k < 8; k++) o[k] = cs[1 + (k >> 1)];
       return;
     }
+    if (c0 + 5 <= dsw) {  // interior lanes: every right neighbour exists
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      int32_t a = cs[k + 1] * 3;
-      int32_t nl = (c0 + k + 1 < dsw) ? cs[k + 2] : cs[k + 1];
-      o[2 * k] = (a + cs[k] + 1) >> 2;
-      o[2 * k + 1] = (a + nl + 2) >> 2;
+      for (int k = 0; k < 4; k++) {
+        int32_t a = cs[k + 1] * 3;
+        o[2 * k] = (a + cs[k] + 1) >> 2;
+        o[2 * k + 1] = (a + cs[k + 2] + 2) >> 2;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        int32_t a = cs[k + 1] * 3;
+        int32_t nl = (c0 + k + 1 < dsw) ? cs[k + 2] : cs[k + 1];
+        o[2 * k] = (a + cs[k] + 1) >> 2;
+        o[2 * k + 1] = (a + nl + 2) >> 2;
+      }
     }
     if (c0 == 0) o[0] = (cs[1] * 3 + cs[1] + 1) >> 2;
     return;
@@ -752,14 +763,22 @@ __device__ __forceinline__ void upsample8(P pl, uint32_t stride, uint32_t hr, ui
 #pragma unroll
   for (int k = 0; k < 4; k++) cs[k + 1] = (int32_t)((v0 >> (8 * k)) & 0xFF) * 3 + (int32_t)((v1 >> (8 * k)) & 0xFF);
   cs[5] = i0[cr] * 3 + i1[cr];
+  if (c0 + 5 <= dsw) {  // interior lanes: no clamping, every right neighbour exists
 #pragma unroll
-  for (int k = 0; k < 4; k++)
-    if (c0 + k >= dsw) cs[k + 1] = cs[dsw - c0];
+    for (int k = 0; k < 4; k++) {
+      o[2 * k] = (cs[k + 1] * 3 + cs[k] + 8) >> 4;
+      o[2 * k + 1] = (cs[k + 1] * 3 + cs[k + 2] + 7) >> 4;
+    }
+  } else {
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    int32_t nl = (c0 + k + 1 < dsw) ? cs[k + 2] : cs[k + 1];
-    o[2 * k] = (cs[k + 1] * 3 + cs[k] + 8) >> 4;
-    o[2 * k + 1] = (cs[k + 1] * 3 + nl + 7) >> 4;
+    for (int k = 0; k < 4; k++)
+      if (c0 + k >= dsw) cs[k + 1] = cs[dsw - c0];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int32_t nl = (c0 + k + 1 < dsw) ? cs[k + 2] : cs[k + 1];
+      o[2 * k] = (cs[k + 1] * 3 + cs[k] + 8) >> 4;
+      o[2 * k + 1] = (cs[k + 1] * 3 + nl + 7) >> 4;
+    }
   }
 }
 
