@@ -91,9 +91,17 @@ DG_HD void ycc_to_rgb(int32_t y, int32_t cb, int32_t cr, uint8_t &r, uint8_t &g,
   const int32_t F071414 = 46802;
   const int32_t F034414 = 22554;
   int32_t xcr = cr - 128, xcb = cb - 128;
+#if defined(DG_DEVICE)
+  // |x| <= 128 and the constants are < 2^17: 24-bit multiplies are exact and
+  // full rate (hipcc otherwise emits the quarter-rate v_mul_lo_u32 here)
+  int32_t crr = (__mul24(F140200, xcr) + 32768) >> 16;
+  int32_t cbb = (__mul24(F177200, xcb) + 32768) >> 16;
+  int32_t g_ = (__mul24(-F034414, xcb) + 32768 + __mul24(-F071414, xcr)) >> 16;
+#else
   int32_t crr = (F140200 * xcr + 32768) >> 16;
   int32_t cbb = (F177200 * xcb + 32768) >> 16;
   int32_t g_ = (-F034414 * xcb + 32768 + -F071414 * xcr) >> 16;
+#endif
   r = clamp255(y + crr);
   g = clamp255(y + g_);
   b = clamp255(y + cbb);

@@ -392,6 +392,13 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
     W = p.hdr.width;
     H = p.hdr.height;
     C = p.hdr.ncomp == 1 ? 1 : 3;
+    // component planes (padded to whole MCUs) must stay below 4 GiB: the
+    // upsampling kernels address rows with 24-bit multiplies.  The reference's
+    // decoder refuses far smaller images already (image's 512 MiB max_alloc).
+    if ((uint64_t)(W + 32) * (H + 32) >= (1ull << 32)) {
+      p.status = DG_ERR_UNSUPPORTED;
+      return DG_OK;
+    }
   }
   p.channels = (int32_t)C;  // pre-transform (image_processing.rs:349-351)
   p.bit_depth = 8;

@@ -690,11 +690,13 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
 // x0..x0+7 (x0 a multiple of 8), with libjpeg's fancy filters (see
 // upsample_at, which this vectorises: one aligned load per source row plus
 // the two edge samples instead of four byte loads per pixel).
+// Row offsets use 24-bit multiplies (full rate, v_mul_lo_u32 is quarter rate):
+// the host keeps every JPEG plane below 4 GiB (pipeline.cpp, plan_image).
 template <class P>
 __device__ __forceinline__ void upsample8(P pl, uint32_t stride, uint32_t hr, uint32_t vr,
                                           uint32_t dsw, uint32_t dsh, uint32_t x0, uint32_t y, int32_t o[8]) {
   if (hr == 1) {  // 4:4:4 component (vr is 1 too for the supported samplings)
-    u32x2 v = *(const DG_GLOBAL u32x2 *)(pl + (size_t)y * stride + x0);
+    u32x2 v = *(const DG_GLOBAL u32x2 *)(pl + (size_t)__umul24(y, stride) + x0);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       o[k] = (v.x >> (8 * k)) & 0xFF;
@@ -707,7 +709,7 @@ __device__ __forceinline__ void upsample8(P pl, uint32_t stride, uint32_t hr, ui
   int32_t cs[6];                // column sums (or plain samples for h2v1) at c0-1 .. c0+4
   const uint32_t cl = c0 > 0 ? c0 - 1 : 0, cr = c0 + 4 < dsw ? c0 + 4 : dsw - 1;
   if (vr == 1) {
-    P in = pl + (size_t)y * stride;
+    P in = pl + (size_t)__umul24(y, stride);
     uint32_t v = *(const DG_GLOBAL uint32_t *)(in + c0);
     cs[0] = in[cl];
 #pragma unroll
@@ -746,7 +748,7 @@ __device__ __forceinline__ void upsample8(P pl, uint32_t stride, uint32_t hr, ui
   // h2v2
   const uint32_t r = y >> 1;
   if (!fancy) {
-    P in = pl + (size_t)r * stride;
+    P in = pl + (size_t)__umul24(r, stride);
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       uint32_t c = c0 + (k >> 1);
@@ -756,8 +758,8 @@ __device__ __forceinline__ void upsample8(P pl, uint32_t stride, uint32_t hr, ui
   }
   int32_t rn = (y & 1) ? (int32_t)r + 1 : (int32_t)r - 1;
   rn = rn < 0 ? 0 : (rn > (int32_t)dsh - 1 ? (int32_t)dsh - 1 : rn);
-  P i0 = pl + (size_t)r * stride;
-  P i1 = pl + (size_t)rn * stride;
+  P i0 = pl + (size_t)__umul24(r, stride);
+  P i1 = pl + (size_t)__umul24((uint32_t)rn, stride);
   uint32_t v0 = *(const DG_GLOBAL uint32_t *)(i0 + c0), v1 = *(const DG_GLOBAL uint32_t *)(i1 + c0);
   cs[0] = i0[cl] * 3 + i1[cl];
 #pragma unroll
