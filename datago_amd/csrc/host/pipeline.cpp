@@ -1127,7 +1127,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       } else if (ps.kind == 1) {  // one workgroup per (band of rows, column tile)
         const uint32_t rows_per_wg = kHBandRows * ps.bands;
         uint32_t cnt = ((ps.rows + rows_per_wg - 1) / rows_per_wg) * ((ps.width + kHBandCols - 1) / kHBandCols);
-        const int cls = ps.ksize <= 8 ? 0 : ps.ksize <= 16 ? 1 : ps.ksize <= 32 ? 2 : 3;
+        // k_resize_hb<K> reads taps in even-aligned pairs: a window starting
+        // at an odd segment position spans ksize + 1 positions
+        const uint32_t kk = ps.ksize + 1;
+        const int cls = kk <= 8 ? 0 : kk <= 16 ? 1 : kk <= 32 ? 2 : 3;
         for (uint32_t it = 0; it < cnt; it++) hb[s / 2][cls].push_back({I, it});
       } else {
         uint32_t cnt = (ps.width * ps.C + 15) / 16 * ps.rows;

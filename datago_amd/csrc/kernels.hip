@@ -1098,15 +1098,20 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
     // two taps per v_dot2_i32_i16: the channel-c bytes of pixels i and i+1
     // packed as i16 x 2 (one v_perm) against the packed weights (w_i, w_i+1);
     // an odd last tap pairs with a zero weight.  Integer sums: bit-exact
-    // with tap-by-tap accumulation.
+    // with tap-by-tap accumulation.  Pairs start at the even position at or
+    // below the window start (kw2 carries a leading zero weight for odd
+    // starts), so each pair is one 8-byte-aligned ds_read_b64: half the LDS
+    // instructions, and banked over 64 dwords instead of 32, so the lanes'
+    // stride-s reads (s = the downscale factor) stop conflicting up to s = 2.
+    const uint32_t offe = off & ~1u;
 #pragma unroll
     for (int j = 0; j < (KMAX > 0 ? (KMAX + 1) / 2 : 1); j++) {
-      if ((uint32_t)(2 * j) >= ksize) break;
+      if ((uint32_t)(2 * j) >= ksize + 1) break;
       const s16x2 w = __builtin_bit_cast(s16x2, kw2[j]);
 #pragma unroll
       for (uint32_t r = 0; r < R; r++) {
-        const uint32_t *row = seg + (r0 + 2 * r) * kHSegStride + off + 2 * j;
-        const uint32_t v0 = row[0], v1 = row[1];
+        const u32x2 vv = *(const u32x2 *)(seg + (r0 + 2 * r) * kHSegStride + offe + 2 * j);
+        const uint32_t v0 = vv.x, v1 = vv.y;
 #pragma unroll
         for (int c = 0; c < C; c++) {
           const uint32_t sel = 0x0C000C00u | ((4u + (uint32_t)c) << 16) | (uint32_t)c;  // [v0.c, 0, v1.c, 0]
@@ -1175,10 +1180,13 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
   uint32_t kw2[KMAX > 0 ? (KMAX + 1) / 2 : 1];  // weights (w_2j, w_2j+1) as i16 x 2
   const DG_GLOBAL int16_t *kp = coef + (size_t)(valid ? x : x0) * ksize;
   if (KMAX > 0) {
+    // pair j covers segment positions offe + 2j, offe + 2j + 1 = taps 2j - sh, 2j + 1 - sh
+    const uint32_t sh = (st - p0) & 1u;
 #pragma unroll
     for (int j = 0; j < (KMAX > 0 ? (KMAX + 1) / 2 : 1); j++) {
-      const uint32_t lo = (valid && (uint32_t)(2 * j) < n) ? (uint16_t)kp[2 * j] : 0u;
-      const uint32_t hi = (valid && (uint32_t)(2 * j + 1) < n) ? (uint16_t)kp[2 * j + 1] : 0u;
+      const int32_t tl = 2 * j - (int32_t)sh, th = tl + 1;
+      const uint32_t lo = (valid && tl >= 0 && (uint32_t)tl < n) ? (uint16_t)kp[tl] : 0u;
+      const uint32_t hi = (valid && (uint32_t)th < n) ? (uint16_t)kp[th] : 0u;
       kw2[j] = lo | (hi << 16);
     }
   }
