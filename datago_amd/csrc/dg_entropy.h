@@ -336,6 +336,9 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
   uint32_t mpos = im.nmk ? first_marker(mk, im.nmk, pos, midx) : kInf;
   const uint32_t bpm = im.bpm, slotmap = im.slotmap, cbits = im.comp_bits;
   uint32_t comp = cbits & 3u;
+  // the current block's DC/AC tables, resolved when the block changes
+  const TAB *tdc = &tabs[(slotmap >> ((comp << 1) << 2)) & 15u];
+  const TAB *tac = &tabs[(slotmap >> (((comp << 1) | 1u) << 2)) & 15u];
   BitWin b;
   bw_init(b, stream, im.ds_lsw, pos);
   for (;;) {
@@ -344,6 +347,8 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
       r = 0;
       z = 0;
       comp = cbits & 3u;
+      tdc = &tabs[(slotmap >> ((comp << 1) << 2)) & 15u];
+      tac = &tabs[(slotmap >> (((comp << 1) | 1u) << 2)) & 15u];
       midx++;
       mpos = midx < im.nmk ? mk[midx] : kInf;
       bw_seek(b, pos);
@@ -351,8 +356,7 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
     if (pos >= a0) break;
     const uint32_t bits = bw_peek(b, pos);
     const bool isdc = (z == 0);
-    const uint32_t slot = (slotmap >> (((comp << 1) | (isdc ? 0u : 1u)) << 2)) & 15u;
-    const uint32_t e = huff_lookup(tabs[slot], bits);
+    const uint32_t e = huff_lookup(*(isdc ? tdc : tac), bits);
     const uint32_t len = e >> 8, sym = e & 0xFFu;
     const uint32_t size = sym & 15u;
     pos += len + size;
@@ -367,6 +371,8 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
       z = 0;
       r = (r + 1 == bpm) ? 0 : r + 1;
       comp = (cbits >> (2 * r)) & 3u;
+      tdc = &tabs[(slotmap >> ((comp << 1) << 2)) & 15u];
+      tac = &tabs[(slotmap >> (((comp << 1) | 1u) << 2)) & 15u];
     }
   }
   const uint32_t rel = pos - a0;
