@@ -11,6 +11,8 @@
 // uploaded to HBM once, to dg_submit_device).
 #include <string.h>
 
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -55,9 +57,19 @@ uint64_t siphash13_str(const uint8_t *p, size_t n) {
 
 namespace {
 uint64_t octal(const uint8_t *f, size_t n, bool &ok) {
-  if (f[0] & 0x80) {  // GNU base-256
-    uint64_t v = f[0] & 0x7F;
-    for (size_t i = 1; i < n; i++) v = (v << 8) | f[i];
+  if (f[0] & 0x80) {  // GNU base-256 (two's complement, big-endian; tar 0.4 rejects what does not fit u64)
+    if (f[0] & 0x40) {  // negative
+      ok = false;
+      return 0;
+    }
+    uint64_t v = f[0] & 0x3F;
+    for (size_t i = 1; i < n; i++) {
+      if (v >> 56) {  // would overflow 64 bits
+        ok = false;
+        return 0;
+      }
+      v = (v << 8) | f[i];
+    }
     return v;
   }
   uint64_t v = 0;
@@ -81,8 +93,9 @@ bool pax_path(const uint8_t *d, size_t n, std::string &path) {
   bool found = false;
   while (i < n) {
     size_t j = i, len = 0;
-    while (j < n && d[j] >= '0' && d[j] <= '9') len = len * 10 + (d[j++] - '0');
-    if (j >= n || d[j] != ' ' || len == 0 || i + len > n) break;
+    while (j < n && d[j] >= '0' && d[j] <= '9' && len <= n) len = len * 10 + (d[j++] - '0');
+    // a record holds at least its length digits, the space and the trailing newline
+    if (j >= n || d[j] != ' ' || len < (j + 1 - i) + 1 || len > n - i) break;
     const std::string rec((const char *)d + j + 1, len - (j + 1 - i) - 1);
     const size_t eq = rec.find('=');
     if (eq != std::string::npos && rec.compare(0, eq, "path") == 0) {
@@ -116,9 +129,10 @@ extern "C" {
 
 uint64_t dg_wds_key_hash(const char *key, size_t len) { return dg::siphash13_str((const uint8_t *)key, len); }
 
-dg_status dg_wds_index(const uint8_t *tar, size_t len, int32_t rank, int32_t world_size, const char *reference_ext,
-                       dg_wds_member *members, int64_t mcap, int64_t *nmembers, char *names, size_t ncap,
-                       size_t *nnames, dg_wds_sample *samples, int64_t scap, int64_t *nsamples) {
+static dg_status wds_index_impl(const uint8_t *tar, size_t len, int32_t rank, int32_t world_size,
+                                const char *reference_ext, dg_wds_member *members, int64_t mcap, int64_t *nmembers,
+                                char *names, size_t ncap, size_t *nnames, dg_wds_sample *samples, int64_t scap,
+                                int64_t *nsamples) {
   if (!tar || !nmembers || !nsamples || !nnames || world_size < 0 || (world_size > 1 && (rank < 0 || rank >= world_size)))
     return DG_ERR_INVALID;
   struct M {
@@ -143,7 +157,7 @@ dg_status dg_wds_index(const uint8_t *tar, size_t len, int32_t rank, int32_t wor
       return DG_ERR_CORRUPT;
     }
     const uint64_t data = pos + 512;
-    if (data + size > len) {
+    if (size > len - data) {  // data <= len here; never form data + size (it can wrap)
       dg::set_error("wds: truncated tar entry");
       return DG_ERR_CORRUPT;
     }
@@ -220,6 +234,24 @@ dg_status dg_wds_index(const uint8_t *tar, size_t len, int32_t rank, int32_t wor
   }
   memcpy(samples, groups.data(), groups.size() * sizeof(dg_wds_sample));
   return DG_OK;
+}
+
+// No C++ exception may cross the C ABI (the Rust caller would abort): a
+// malformed shard that trips one (e.g. an allocation for a hostile length)
+// reports DG_ERR_CORRUPT like any other bad header.
+dg_status dg_wds_index(const uint8_t *tar, size_t len, int32_t rank, int32_t world_size, const char *reference_ext,
+                       dg_wds_member *members, int64_t mcap, int64_t *nmembers, char *names, size_t ncap,
+                       size_t *nnames, dg_wds_sample *samples, int64_t scap, int64_t *nsamples) {
+  try {
+    return wds_index_impl(tar, len, rank, world_size, reference_ext, members, mcap, nmembers, names, ncap, nnames,
+                          samples, scap, nsamples);
+  } catch (const std::bad_alloc &) {
+    dg::set_error("wds: out of host memory");
+    return DG_ERR_OOM;
+  } catch (const std::exception &e) {
+    dg::set_error(std::string("wds: malformed shard (") + e.what() + ")");
+    return DG_ERR_CORRUPT;
+  }
 }
 
 }  // extern "C"

@@ -79,3 +79,54 @@ def test_synthetic_imagenet_shard():
     for s in samples:
         name, off, n = s[0]
         assert tar[off:off + 2] == b"\xff\xd8"
+
+
+def _raw_header(name: bytes, size_field: bytes, typeflag: bytes) -> bytes:
+    """One 512-byte tar header with a caller-chosen 12-byte size field and a
+    valid checksum (so only the size/record logic can reject it)."""
+    h = bytearray(512)
+    h[0:len(name)] = name
+    h[100:108] = b"0000644\0"
+    h[124:136] = size_field
+    h[136:148] = b"00000000000\0"
+    h[156:157] = typeflag
+    h[257:263] = b"ustar\0"
+    h[263:265] = b"00"
+    h[148:156] = b" " * 8
+    h[148:156] = b"%06o\0 " % sum(h)
+    return bytes(h)
+
+
+def _status(tar: bytes) -> int:
+    import ctypes
+    import numpy as np
+    lib = L.load()
+    buf = np.frombuffer(tar, np.uint8)
+    nm, ns, nn = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_size_t()
+    return lib.dg_wds_index(buf.ctypes.data, buf.nbytes, 0, 1, b"jpg", None, 0, ctypes.byref(nm), None, 0,
+                            ctypes.byref(nn), None, 0, ctypes.byref(ns))
+
+
+@pytest.mark.parametrize("size_field", [
+    b"\x80" + b"\xff" * 11,                      # base-256, ~2^88: does not fit 64 bits
+    b"\x80\x00\x00\x00" + b"\xff" * 7 + b"\x00",  # base-256 2^64-256: data + size would wrap
+    b"\xff" * 12,                                # base-256 negative
+    b"77777777777\0",                            # octal 8 GiB, past the buffer
+])
+def test_hostile_size_field_is_corrupt(size_field):
+    tar = _raw_header(b"a.jpg", size_field, b"0") + b"\0" * 2048
+    assert _status(tar) == L.DG_ERR_CORRUPT
+
+
+def test_truncated_long_name_is_corrupt():
+    # GNU 'L' entry claiming 4 KiB of name where the buffer ends after 512 bytes
+    tar = _raw_header(b"././@LongLink", b"%011o\0" % 4096, b"L") + b"x" * 512
+    assert _status(tar) == L.DG_ERR_CORRUPT
+
+
+@pytest.mark.parametrize("record", [b"2 x", b"3 ab", b"1 ", b"9999999999999999999999 path=a"])
+def test_malformed_pax_record_does_not_abort(record):
+    body = record + b"\0" * (512 - len(record))
+    tar = (_raw_header(b"PaxHeader", b"%011o\0" % len(record), b"x") + body +
+           _raw_header(b"a.jpg", b"%011o\0" % 3, b"0") + b"JPG" + b"\0" * 509 + b"\0" * 1024)
+    assert L.wds_index(tar, 0, 1, "jpg") == [[("a.jpg", 1536, 3)]]
