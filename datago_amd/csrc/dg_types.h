@@ -344,7 +344,13 @@ struct BatchFlags {
   uint32_t sync_iters_max;  // longest intra-workgroup sync loop
   uint64_t wgtime;          // debug: device array of {start, end} s_memrealtime per workgroup, 0 = off
   uint32_t wgtime_write;    // first record of k_huff_write's workgroups
-  uint32_t pad;
+  uint32_t debug;           // test switches (kDbg*), kept across resync rounds
 };
+// The counters a resync round clears (everything before `wgtime`).
+constexpr size_t kFlagCounters = 16;
+// BatchFlags::debug: force the failure paths a valid stream never takes, so
+// tests can check that they surface as a per-image status.
+constexpr uint32_t kDbgForceWriteMismatch = 1u;  // k_huff_write: subsequence 0 of every image disagrees
+constexpr uint32_t kDbgForceChainChange = 2u;    // k_huff_fix: the chain never settles
 
 }  // namespace dg

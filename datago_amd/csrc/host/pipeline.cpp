@@ -222,6 +222,8 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "resync_rounds") return stat_resync_;
   if (k == "fix_workgroups") return stat_fix_;
   if (k == "write_mismatch") return stat_mismatch_;
+  if (k == "unsettled_batches") return stat_unsettled_;
+  if (k == "pool_flushes") return stat_pool_flush_;
   if (k == "sync_iters_max") return stat_iters_;
   {  // wg_timing summaries, in nanoseconds: wg_{sync,write}_{span,mean,p90,max}
     static const char *kn[2] = {"sync", "write"}, *sn[4] = {"span", "mean", "p90", "max"};
@@ -294,6 +296,35 @@ dg_status Context::ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user) {
   return DG_OK;
 }
 
+// Table pools.  Huffman and quantisation tables are de-duplicated by content
+// into per-context pools that the kernels index with 16-bit slots.  Pools are
+// not grow-only: once a pool holds more than kPoolKeep tables (a long-running
+// loader over per-image-optimised JPEGs adds ~4 new tables per image), the
+// next submit drains the batches in flight and starts the pools over, so a
+// valid image never fails for lack of pool space.  Only a single batch that
+// alone needs more than kPoolMax tables sends its overflow images back as
+// DG_ERR_UNSUPPORTED (the caller's CPU path), never as CORRUPT.
+static constexpr size_t kPoolKeep = 4096;
+static constexpr size_t kPoolMax = 65535;
+
+dg_status Context::flush_pools() {
+  for (int s = 0; s < nslots_; s++) {  // batches in flight still read (and may resync with) the pools
+    Slot &o = slots_[s];
+    if (o.batch && !o.batch->done) {
+      dg_status st = finish(o);
+      if (st) return st;
+    }
+  }
+  if (dg_status st = sync_all()) return st;
+  hpool_.clear();
+  hpool_idx_.clear();
+  qpool_.clear();
+  qpool_idx_.clear();
+  hpool_uploaded_ = qpool_uploaded_ = 0;
+  stat_pool_flush_++;
+  return DG_OK;
+}
+
 int Context::pool_huff(const HuffSpec &s) {
   std::string key((const char *)s.bits, 17);
   key.append((const char *)s.vals, (size_t)s.nvals);
@@ -301,7 +332,7 @@ int Context::pool_huff(const HuffSpec &s) {
   if (it != hpool_idx_.end()) return it->second;
   HuffTable t;
   if (!build_huff_table(s, t)) return -1;
-  if (hpool_.size() >= 65535) return -1;
+  if (hpool_.size() >= kPoolMax) return -2;
   hpool_.push_back(t);
   int idx = (int)hpool_.size() - 1;
   hpool_idx_[key] = idx;
@@ -314,7 +345,7 @@ int Context::pool_quant(const uint16_t *q) {
   if (it != qpool_idx_.end()) return it->second;
   QuantTable t;
   memcpy(t.q, q, 128);
-  if (qpool_.size() >= 65535) return -1;
+  if (qpool_.size() >= kPoolMax) return -2;
   qpool_.push_back(t);
   int idx = (int)qpool_.size() - 1;
   qpool_idx_[key] = idx;
@@ -511,23 +542,29 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     }
   }
   // ---- 2. table pools
+  if (hpool_.size() > kPoolKeep || qpool_.size() > kPoolKeep) {
+    dg_status st = flush_pools();
+    if (st) return st;
+  }
   for (int i = 0; i < n; i++) {
     ImagePlan &p = b.plans[i];
     if (p.status || p.fmt != kFmtJpeg) continue;
-    bool ok = true;
+    int worst = 0;  // -1: a table that does not build (corrupt), -2: pools full for this batch
+    auto use = [&](int idx) { worst = std::min(worst, idx); };
     if (p.hdr.progressive) {  // the tables each scan uses
-      for (const HuffSpec &t : p.hdr.tables)
-        if (pool_huff(t) < 0) ok = false;
-      for (int c = 0; c < p.hdr.ncomp; c++)
-        if (pool_quant(p.hdr.q[p.hdr.comp[c].tq]) < 0) ok = false;
+      for (const HuffSpec &t : p.hdr.tables) use(pool_huff(t));
+      for (int c = 0; c < p.hdr.ncomp; c++) use(pool_quant(p.hdr.q[p.hdr.comp[c].tq]));
     } else {
       for (int c = 0; c < p.hdr.ncomp; c++) {
-        if (pool_huff(p.hdr.dc[p.hdr.comp[c].td]) < 0 || pool_huff(p.hdr.ac[p.hdr.comp[c].ta]) < 0 ||
-            pool_quant(p.hdr.q[p.hdr.comp[c].tq]) < 0)
-          ok = false;
+        use(pool_huff(p.hdr.dc[p.hdr.comp[c].td]));
+        use(pool_huff(p.hdr.ac[p.hdr.comp[c].ta]));
+        use(pool_quant(p.hdr.q[p.hdr.comp[c].tq]));
       }
     }
-    if (!ok) {
+    if (worst == -2) {
+      p.status = DG_ERR_UNSUPPORTED;
+      metas[i].status = DG_ERR_UNSUPPORTED;
+    } else if (worst < 0) {
       p.status = DG_ERR_CORRUPT;
       metas[i].status = DG_ERR_CORRUPT;
     }
@@ -1222,6 +1259,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     bf->wgtime = (uint64_t)(uintptr_t)sl.wgt.p;
     bf->wgtime_write = (uint32_t)b.lists[L_SYNC].size();
   }
+  ((BatchFlags *)(P + b.flags_off))->debug = (uint32_t)(debug_flags_ >> 16) & 3u;
   memcpy(P + b.desc_off, b.descs.data(), b.descs.size() * sizeof(ImageDesc));
   for (int l = 0; l < L_COUNT; l++)
     if (!b.lists[l].empty()) memcpy(P + b.list_off[l], b.lists[l].data(), b.lists[l].size() * sizeof(WgItem));
@@ -1267,7 +1305,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     if (timing_) HIPCHK(hipEventRecord(sl.ev[i], sl.st));
     return DG_OK;
   };
-  if (from_fix) HIPCHK(hipMemsetAsync(fl, 0, sizeof(BatchFlags), sl.st));
+  if (from_fix) HIPCHK(hipMemsetAsync(fl, 0, kFlagCounters, sl.st));
   int evi = 1;  // event i closes stage i-1 (kStageNames)
   auto next = [&]() -> dg_status { return ev(evi++); };
   // a resync round re-runs everything downstream of the entropy decode; the
@@ -1324,7 +1362,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (b.stage_on)
     launch_huff_scatter(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), subs);
   else
-    launch_huff_write(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots);
+    launch_huff_write(sl.st, dm, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots);
   if (next()) return DG_ERR_DEVICE;
   if (next()) return DG_ERR_DEVICE;  // coeffs (side stream)
   launch_idct(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);
@@ -1392,7 +1430,18 @@ dg_status Context::finish(Slot &sl) {
     stat_fix_ += b.flags.fix_count;
     stat_mismatch_ += b.flags.write_mismatch;
     stat_iters_ = std::max<int64_t>(stat_iters_, b.flags.sync_iters_max);
-    if (b.flags.chain_changed == 0 || b.resync_rounds >= 64) break;
+    if (b.flags.chain_changed == 0) break;
+    if (b.resync_rounds >= kMaxResyncRounds) {
+      // The boundary repair did not settle: some entropy chain of this batch
+      // may be wrong, and nothing tells which image it belongs to.  Every
+      // sequential JPEG not already failed goes back to the caller's CPU
+      // decoder (DG_ERR_UNSUPPORTED) instead of returning pixels that may
+      // be wrong.
+      stat_unsettled_++;
+      b.unsettled = true;
+      set_error("entropy resync did not converge: the batch's JPEGs are returned DG_ERR_UNSUPPORTED");
+      break;
+    }
     // a workgroup's last exit state changed during the boundary repair: repeat
     // repair + everything downstream until the chain is stable
     b.resync_rounds++;
@@ -1440,6 +1489,8 @@ dg_status Context::finish(Slot &sl) {
       stat_png_chunks_ += back[b.desc_of[i]].png.nchunks;
       stat_png_serial_ += back[b.desc_of[i]].png.serial ? 1 : 0;
     }
+    if (!status && b.unsettled && b.plans[i].fmt == kFmtJpeg && !b.plans[i].hdr.progressive)
+      status = DG_ERR_UNSUPPORTED;
     if (status) b.metas[i].status = status;
     if (b.plans[i].encode) {
       const uint32_t nb = back[b.desc_of[i]].enc.enc_bytes;

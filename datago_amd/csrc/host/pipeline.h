@@ -82,6 +82,7 @@ struct Batch {
   dg_payload_meta *metas = nullptr;
   bool done = false;
   int resync_rounds = 0;
+  bool unsettled = false;  // resync hit kMaxResyncRounds: JPEGs go back as DG_ERR_UNSUPPORTED
   BatchFlags flags = {0, 0, 0, 0};
   std::vector<float> stage_ms;
 };
@@ -147,6 +148,7 @@ class Context {
  private:
   dg_status plan_image(const uint8_t *h, size_t len, int32_t forced, ImagePlan &p);
   int pool_huff(const HuffSpec &s);
+  dg_status flush_pools();
   int pool_quant(const uint16_t *q);
   dg_status ensure(DevBuf &b, size_t bytes, hipStream_t user = nullptr);
   dg_status ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user = nullptr);
@@ -211,6 +213,7 @@ class Context {
   double wgstat_[2][4] = {{0}};
   // stats
   int64_t stat_batches_ = 0, stat_resync_ = 0, stat_fix_ = 0, stat_mismatch_ = 0, stat_iters_ = 0;
+  int64_t stat_unsettled_ = 0, stat_pool_flush_ = 0;
   std::vector<float> last_ms_;
 };
 

@@ -23,7 +23,7 @@ void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
                      uint32_t max_slots);
 // one workgroup per image
 void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs);
-void launch_huff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+void launch_huff_write(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                        const HuffTable *pool, const SubState *subs, BatchFlags *flags, uint32_t max_slots);
 // decode-once: blocks from the staged coefficients (replaces k_huff_write when ImageDesc::stage is set)
 void launch_huff_scatter(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,

@@ -346,6 +346,8 @@ __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ 
   extern __shared__ __attribute__((aligned(16))) uint8_t huff_dyn[];
   HuffTable *tabs = (HuffTable *)huff_dyn;
   __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
+  if ((flags->debug & kDbgForceChainChange) && blockIdx.x == 0 && threadIdx.x == 0)
+    atomicAdd(&flags->chain_changed, 1u);
   const WgItem it = list[blockIdx.x];
   const uint32_t s0 = it.item0;
   if (s0 == 0) return;
@@ -459,7 +461,7 @@ __global__ __launch_bounds__(256) void k_huff_scan(ImageDesc *__restrict__ imgs,
 // four banks), and single-coefficient stores spread over banks by lane.
 constexpr int kBlkStride = 72;
 
-__global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict__ imgs,
+__global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs,
                                                     const WgItem *__restrict__ list,
                                                     const HuffTable *__restrict__ pool,
                                                     const SubState *__restrict__ subs, BatchFlags *flags) {
@@ -500,7 +502,14 @@ __global__ __launch_bounds__(256) void k_huff_write(const ImageDesc *__restrict_
     RangeAcc acc;
     decode_range<true, HuffTable, true>(im, tabs, gp<const uint8_t>(im.ds), gp<const uint32_t>(im.mk), s, ss.in,
                                         acc, &w);
-    if (acc.out != ss.out) atomicAdd(&flags->write_mismatch, 1u);
+    if (acc.out != ss.out || (s == 0 && (flags->debug & kDbgForceWriteMismatch))) {
+      // the write pass left this range in another state than the sync pass
+      // proved: the blocks after it are not trustworthy.  The image goes back
+      // to the caller's CPU decoder (DG_ERR_UNSUPPORTED) unless it is already
+      // known corrupt (k_huff_scan).
+      atomicAdd(&flags->write_mismatch, 1u);
+      if (imgs[it.image].status == 0) imgs[it.image].status = 1;
+    }
   }
   if (flags->wgtime) {
     __syncthreads();
@@ -1439,7 +1448,7 @@ void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
 void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs) {
   DG_LAUNCH(k_huff_scan, nwg, st, imgs, list, subs);
 }
-void launch_huff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
+void launch_huff_write(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                        const HuffTable *pool, const SubState *subs, BatchFlags *flags, uint32_t max_slots) {
   if (!nwg) return;
   hipLaunchKernelGGL(k_huff_write, dim3(nwg), dim3(256), (size_t)max_slots * sizeof(HuffTable), st, imgs, list,

@@ -145,6 +145,268 @@ def uniform_corpus(seed: int, n: int, w: int = 640, h: int = 480, quality: int =
     return [_make_one(j) for j in jobs]
 
 
+# ------------------------------------------------- JPEG with chosen Huffman tables
+#
+# PIL always writes libjpeg's Annex K Huffman tables unless optimize=True, and
+# even its optimised tables stay shallow on synthetic content.  Real corpora
+# (mozjpeg, per-image optimised web JPEGs) carry tables with long (10..16-bit)
+# codes spread over many 9-bit prefixes -- the decoder's second-level and
+# fallback lookups.  This small baseline encoder (T.81 sequential Huffman,
+# 8-bit, gray / 4:4:4 / 4:2:0, optional restart interval) writes the same
+# coefficients with either optimal length-limited tables (Annex K.2/K.3, as
+# optimize=True) or deliberately deep ones.  Test data only: the decoded
+# pixels are checked against the oracle and PIL, never against this encoder.
+
+_STD_LUMA_Q = [16, 11, 10, 16, 24, 40, 51, 61, 12, 12, 14, 19, 26, 58, 60, 55, 14, 13, 16, 24, 40, 57, 69, 56,
+               14, 17, 22, 29, 51, 87, 80, 62, 18, 22, 37, 56, 68, 109, 103, 77, 24, 35, 55, 64, 81, 104, 113, 92,
+               49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99]
+_STD_CHROMA_Q = [17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99, 24, 26, 56, 99, 99, 99, 99, 99,
+                 47, 66, 99, 99, 99, 99, 99, 99] + [99] * 32
+_ZIGZAG = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6, 7,
+           14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39,
+           46, 53, 60, 61, 54, 47, 55, 62, 63]
+
+
+def _scaled_q(base, quality):
+    scale = 5000 // quality if quality < 50 else 200 - 2 * quality
+    return [min(255, max(1, (b * scale + 50) // 100)) for b in base]
+
+
+def _huff_optimal(freq):
+    """Annex K.2 code sizes + K.3 16-bit limit: (bits[1..16], vals)."""
+    freq = list(freq) + [1]  # reserved symbol 256: no code of all ones
+    n = len(freq)
+    size = [0] * n
+    others = [-1] * n
+    f = [x if x > 0 else 0 for x in freq]
+    while True:
+        c1 = c2 = -1
+        for i in range(n):  # least frequency, highest index on ties (libjpeg jchuff)
+            if f[i] and (c1 < 0 or f[i] <= f[c1]):
+                c1 = i
+        for i in range(n):
+            if f[i] and i != c1 and (c2 < 0 or f[i] <= f[c2]):
+                c2 = i
+        if c2 < 0:
+            break
+        f[c1] += f[c2]
+        f[c2] = 0
+        size[c1] += 1
+        while others[c1] >= 0:
+            c1 = others[c1]
+            size[c1] += 1
+        others[c1] = c2
+        size[c2] += 1
+        while others[c2] >= 0:
+            c2 = others[c2]
+            size[c2] += 1
+    bits = [0] * 33
+    for i in range(n):
+        if size[i]:
+            bits[size[i]] += 1
+    for i in range(32, 16, -1):
+        while bits[i] > 0:
+            j = i - 2
+            while bits[j] == 0:
+                j -= 1
+            bits[i] -= 2
+            bits[i - 1] += 1
+            bits[j + 1] += 2
+            bits[j] -= 1
+    i = 16
+    while bits[i] == 0:
+        i -= 1
+    bits[i] -= 1  # drop the reserved code
+    vals = [s for L in range(1, 33) for s in range(n - 1) if size[s] == L]
+    return [0] + bits[1:17], vals
+
+
+def _huff_deep(freq, short, mid_len, mid_n):
+    """Deliberately deep table over every symbol with nonzero frequency (and
+    the rest of `universe`): the `short` most frequent get 1..short-bit codes,
+    the next mid_n get mid_len-bit codes, the rest 16-bit codes."""
+    order = sorted(range(len(freq)), key=lambda s: (-freq[s], s))
+    order = [s for s in order if freq[s] > 0] + [s for s in order if freq[s] == 0]
+    bits = [0] * 17
+    vals = []
+    for k, sym in enumerate(order):
+        L = (k + 1) if k < short else (mid_len if k < short + mid_n else 16)
+        bits[L] += 1
+        vals.append(sym)
+    by_len = sorted(zip([((k + 1) if k < short else (mid_len if k < short + mid_n else 16))
+                         for k in range(len(order))], range(len(order))))
+    return bits, [order[i] for _, i in by_len]
+
+
+def _huff_codes(bits, vals):
+    codes, code, k = {}, 0, 0
+    for L in range(1, 17):
+        for _ in range(bits[L]):
+            codes[vals[k]] = (code, L)
+            code += 1
+            k += 1
+        code <<= 1
+    return codes
+
+
+class _BitWriter:
+    def __init__(self):
+        self.out = bytearray()
+        self.acc = 0
+        self.n = 0
+
+    def put(self, v, n):
+        self.acc = (self.acc << n) | (v & ((1 << n) - 1))
+        self.n += n
+        while self.n >= 8:
+            b = (self.acc >> (self.n - 8)) & 0xFF
+            self.out.append(b)
+            if b == 0xFF:
+                self.out.append(0)
+            self.n -= 8
+        self.acc &= (1 << self.n) - 1
+
+    def pad(self):
+        if self.n:
+            self.put((1 << (8 - self.n)) - 1, 8 - self.n)
+
+
+def _category(v):
+    return 0 if v == 0 else int(abs(v)).bit_length()
+
+
+def encode_jpeg_tables(arr: np.ndarray, quality: int = 75, subsampling: str = "4:2:0", tables: str = "optimal",
+                       restart_interval: int = 0) -> bytes:
+    """Baseline JPEG of `arr` (HW gray or HWC RGB) with Huffman tables
+    `tables` = "optimal" (per-image, as optimize=True / mozjpeg) or "deep"
+    (10- and 16-bit codes over many 9-bit prefixes: the decoder's sub-table
+    overflow path)."""
+    arr = np.asarray(arr)
+    gray = arr.ndim == 2
+    h, w = arr.shape[:2]
+    if gray:
+        planes = [arr.astype(np.float64)]
+        samp = [(1, 1)]
+    else:
+        r, g, b = [arr[:, :, i].astype(np.float64) for i in range(3)]
+        planes = [0.299 * r + 0.587 * g + 0.114 * b,
+                  -0.168735892 * r - 0.331264108 * g + 0.5 * b + 128,
+                  0.5 * r - 0.418687589 * g - 0.081312411 * b + 128]
+        samp = [(2, 2), (1, 1), (1, 1)] if subsampling == "4:2:0" else [(1, 1)] * 3
+    hmax, vmax = max(s[0] for s in samp), max(s[1] for s in samp)
+    mx, my = -(-w // (8 * hmax)), -(-h // (8 * vmax))
+    qt = [_scaled_q(_STD_LUMA_Q, quality), _scaled_q(_STD_CHROMA_Q, quality)]
+    k = np.arange(8)
+    C = np.sqrt(2 / 8) * np.cos((2 * k[None, :] + 1) * k[:, None] * np.pi / 16)
+    C[0, :] = np.sqrt(1 / 8)
+    comps = []
+    for ci, (p, (hs, vs)) in enumerate(zip(planes, samp)):
+        if (hs, vs) != (hmax, vmax):  # 2x2 box average, edge replicated
+            pp = np.pad(p, ((0, h % 2), (0, w % 2)), mode="edge")
+            p = (pp[0::2, 0::2] + pp[1::2, 0::2] + pp[0::2, 1::2] + pp[1::2, 1::2]) / 4
+        bw, bh = mx * hs, my * vs
+        p = np.pad(p, ((0, bh * 8 - p.shape[0]), (0, bw * 8 - p.shape[1])), mode="edge") - 128.0
+        blk = p.reshape(bh, 8, bw, 8).transpose(0, 2, 1, 3)
+        d = np.einsum("ij,abjk,lk->abil", C, blk, C)
+        q = np.array(qt[0 if ci == 0 else 1], np.float64).reshape(8, 8)
+        zz = np.rint(d / q).astype(np.int64).reshape(bh, bw, 64)[:, :, _ZIGZAG]
+        comps.append(zz)
+    # symbol streams: MCU order, per component (DC diff, AC run/size), RST resets
+    seq = []  # (component, kind 0=dc 1=ac, symbol, extra value, extra bits) or ("rst", n)
+    pred = [0] * len(comps)
+    nmcu = 0
+    for my_ in range(my):
+        for mx_ in range(mx):
+            if restart_interval and nmcu and nmcu % restart_interval == 0:
+                seq.append(("rst", (nmcu // restart_interval - 1) & 7))
+                pred = [0] * len(comps)
+            nmcu += 1
+            for ci, (hs, vs) in enumerate(samp):
+                for by in range(vs):
+                    for bx in range(hs):
+                        z = comps[ci][my_ * vs + by, mx_ * hs + bx]
+                        diff = int(z[0]) - pred[ci]
+                        pred[ci] = int(z[0])
+                        s_ = _category(diff)
+                        seq.append((ci, 0, s_, diff, s_))
+                        run = 0
+                        last = 63
+                        while last > 0 and z[last] == 0:
+                            last -= 1
+                        for kk in range(1, last + 1):
+                            v = int(z[kk])
+                            if v == 0:
+                                run += 1
+                                continue
+                            while run > 15:
+                                seq.append((ci, 1, 0xF0, 0, 0))
+                                run -= 16
+                            s_ = _category(v)
+                            seq.append((ci, 1, (run << 4) | s_, v, s_))
+                            run = 0
+                        if last < 63:
+                            seq.append((ci, 1, 0x00, 0, 0))
+    # tables: 0 = luma, 1 = chroma
+    freqs = [[[0] * 256 for _ in range(2)] for _ in range(2)]  # [kind][table][symbol]
+    for e in seq:
+        if e[0] != "rst":
+            freqs[e[1]][0 if e[0] == 0 else 1][e[2]] += 1
+    specs = [[None, None], [None, None]]
+    for kind in range(2):
+        for t in range(1 if gray else 2):
+            f = freqs[kind][t]
+            if tables == "deep":
+                if kind == 0:
+                    f = [f[s] if s < 12 else 0 for s in range(12)]
+                    specs[kind][t] = _huff_deep([x + 1 for x in f], 1, 12, 5)
+                else:
+                    uni = [0x00, 0xF0] + [(r_ << 4) | s_ for r_ in range(16) for s_ in range(1, 11)]
+                    ff = [f[s] for s in uni]
+                    bits, vi = _huff_deep(ff, 1, 10, 100)
+                    specs[kind][t] = (bits, [uni[i] for i in vi])
+            else:
+                if kind == 0:
+                    f = f[:12]
+                bits, vals = _huff_optimal(f)
+                specs[kind][t] = (bits, vals)
+    codes = [[_huff_codes(*specs[kind][t]) if specs[kind][t] else None for t in range(2)] for kind in range(2)]
+    bw_ = _BitWriter()
+    for e in seq:
+        if e[0] == "rst":
+            bw_.pad()
+            bw_.out += bytes([0xFF, 0xD0 + e[1]])
+            continue
+        ci, kind, sym, v, nb = e
+        code, L = codes[kind][0 if ci == 0 else 1][sym]
+        bw_.put(code, L)
+        if nb:
+            bw_.put(v if v >= 0 else v + (1 << nb) - 1, nb)
+    bw_.pad()
+    # markers
+    out = bytearray(b"\xff\xd8")
+    out += b"\xff\xe0\x00\x10JFIF\x00\x01\x01\x00\x00\x01\x00\x01\x00\x00"
+    for t in range(1 if gray else 2):
+        out += b"\xff\xdb\x00\x43" + bytes([t]) + bytes(qt[t][z] for z in _ZIGZAG)  # zigzag order
+    nc = len(comps)
+    out += b"\xff\xc0" + (8 + 3 * nc).to_bytes(2, "big") + b"\x08" + h.to_bytes(2, "big") + w.to_bytes(2, "big") \
+        + bytes([nc])
+    for ci, (hs, vs) in enumerate(samp):
+        out += bytes([ci + 1, (hs << 4) | vs, 0 if ci == 0 else 1])
+    for kind in range(2):
+        for t in range(1 if gray else 2):
+            bits, vals = specs[kind][t]
+            body = bytes([(kind << 4) | t]) + bytes(bits[1:17]) + bytes(vals)
+            out += b"\xff\xc4" + (len(body) + 2).to_bytes(2, "big") + body
+    if restart_interval:
+        out += b"\xff\xdd\x00\x04" + int(restart_interval).to_bytes(2, "big")
+    out += b"\xff\xda" + (6 + 2 * nc).to_bytes(2, "big") + bytes([nc])
+    for ci in range(nc):
+        out += bytes([ci + 1, 0x00 if ci == 0 else 0x11])
+    out += b"\x00\x3f\x00"
+    out += bw_.out + b"\xff\xd9"
+    return bytes(out)
+
+
 # ---------------------------------------------------------------- PNG
 
 PNG_KINDS = ("L", "LA", "RGB", "RGBA", "P8", "P8T", "P4", "P2", "P1", "L1", "L2", "L4", "LT", "RGBT")
