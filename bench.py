@@ -10,12 +10,22 @@ the whole decode + bucket + crop/resize path.  Coded bytes are resident in HBM
 before timing starts; header parsing and batch planning on the host are
 inside the timed region.
 
-Multi-GPU: one process per GPU (torchrun); each rank decodes its own slice of
-the logical sample list (generator_files.rs:24-42 contiguous slices) with no
-data-path collective ("scaling": "weak"); only the barrier and the max-time
-reduction go over torch.distributed.
+The logical stream: `--samples` file-source samples (100k for configs[1],
+1M for configs[3] = `--workload cfg4`), sample s showing pool image
+s % `--pool` (4,096 unique images for configs[1], 16,384 for configs[3]; the
+pool's coded bytes, ~2.9 GB for 4,096, exceed the 256 MB Infinity Cache).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--pool P]
+Multi-GPU: one process per GPU.  Under torchrun (the driver's N>1 launch)
+RANK/WORLD_SIZE/LOCAL_RANK come from the environment; `python bench.py
+--gpus N` without torchrun starts the N rank processes itself (this parent
+never touches the GPU) with the same variables set.  Each rank decodes its
+own contiguous slice of the logical stream (get_data_slice_multirank,
+generator_files.rs:24-42) on device LOCAL_RANK (mod the device count: on a
+1-GPU box the ranks share the card) with no data-path collective
+("scaling": "weak"); only the barriers and the max-time reduction go over
+torch.distributed (gloo).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--pool P] [--workload jpeg|cfg4|wds|png]
 """
 from __future__ import annotations
 
@@ -23,6 +33,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,7 +53,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0, help="images per step (0: 256, or 1024 for wds's ImageNet-size JPEGs)")
-    ap.add_argument("--pool", type=int, default=256, help="unique images per rank held in HBM")
+    ap.add_argument("--pool", type=int, default=0,
+                    help="unique images in the logical pool (0: 4096 for jpeg, 16384 for cfg4, 256 per rank for png)")
+    ap.add_argument("--samples", type=int, default=0,
+                    help="logical stream length sharded over ranks (0: 100000 for jpeg, 1000000 for cfg4)")
     ap.add_argument("--short-min", type=int, default=256)
     ap.add_argument("--short-max", type=int, default=2048)
     ap.add_argument("--size", type=int, default=0, help="bucket default_image_size (0: 1024, or 512 for wds)")
@@ -66,8 +81,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=3, help="host-memory (PCIe-inclusive) steps")
     ap.add_argument("--shards", type=int, default=8, help="wds workload: shards of 1000 samples")
-    ap.add_argument("--workload", choices=("jpeg", "png", "wds"), default="jpeg",
-                    help="jpeg: configs[1] (the headline); png: configs[4]-style RGB PNG + aligned L8 mask pairs "
+    ap.add_argument("--workload", choices=("jpeg", "cfg4", "png", "wds"), default="jpeg",
+                    help="jpeg: configs[1] (the headline); cfg4: configs[3] (1M samples over a 16,384-image pool, "
+                         "seed 4, sharded over the ranks); png: configs[4]-style RGB PNG + aligned L8 mask pairs "
                          "(decode + bucket-resize; the mask is forced to the image's bucket, worker_http.rs:186-214)")
     ap.add_argument("--encode", action="store_true",
                     help="pre_encode_images with encode_format jpeg, quality 92 (configs[4]: every payload "
@@ -76,6 +92,10 @@ def parse():
                     help="jpeg workload: share of the pool written as progressive JPEGs (not the headline config)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
+    if a.pool <= 0:
+        a.pool = {"jpeg": 4096, "cfg4": 16384, "png": 256, "wds": 0}[a.workload]
+    if a.samples <= 0:
+        a.samples = 1_000_000 if a.workload == "cfg4" else 100_000
     if a.inflight <= 0:
         a.inflight = 4 if a.workload == "png" else 2
     if a.batch <= 0:
@@ -87,11 +107,57 @@ def parse():
     return a
 
 
-def cpu_share() -> int:
+def host_cores() -> tuple[int, str]:
+    """The worker count the reference's runtime would pick: num_cpus::get()
+    (worker_files.rs:86,151), i.e. the CPUs this process may run on, capped by
+    a cgroup CPU quota -- and by the box's CPU share where the harness states
+    one (OMP_NUM_THREADS: 16 per GPU on the MI355X boxes), so the pool never
+    oversubscribes the cores it was given."""
     try:
-        return max(1, min(16, len(os.sched_getaffinity(0))))
+        aff = len(os.sched_getaffinity(0))
     except Exception:
-        return max(1, min(16, os.cpu_count() or 1))
+        aff = os.cpu_count() or 1
+    n, basis = aff, [f"affinity {aff}"]
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+            basis.append(f"cgroup quota {int(q) / int(per):g}")
+    except (OSError, ValueError):
+        pass
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+        basis.append(f"CPU share (OMP_NUM_THREADS) {share}")
+    return max(1, n), ", ".join(basis)
+
+
+def cpu_share() -> int:
+    return host_cores()[0]
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def reference_toolchain() -> str:
+    """Probe for the reference's own toolchain: with cargo and
+    the crates present, the Rust path itself would be the CPU baseline."""
+    try:
+        r = subprocess.run(["cargo", "--version"], capture_output=True, text=True, timeout=20)
+        return (r.stdout or r.stderr).strip() or f"cargo exit {r.returncode}"
+    except FileNotFoundError:
+        return "cargo: not found (no Rust toolchain; the reference's crates are not vendored either)"
+    except (OSError, subprocess.SubprocessError) as e:
+        return f"cargo probe failed: {e}"
 
 
 # --------------------------------------------------------------- CPU baseline
@@ -107,6 +173,55 @@ def _cpu_work(args):
     return dec.shape[0] * dec.shape[1], time.perf_counter() - t
 
 
+def _pil_work(args):
+    """Pillow proxy of the reference's per-sample work: decode, then the two
+    Lanczos calls of crop_and_resize (image_processing.rs:288-323): the
+    full-image resize to the scaled size and the crop box as a second resize."""
+    import io as _io
+
+    from PIL import Image
+
+    from oracle import buckets as B
+    data, tw, th, enc = args
+    im = Image.open(_io.BytesIO(data))
+    im.load()
+    w, h = im.size
+    if (w, h) != (tw, th):
+        nw, nh = B.scaled_size(w, h, tw, th)
+        l, t, bw, bh = B.fit_crop_box(nw, nh, tw, th)
+        im = im.resize((nw, nh), Image.LANCZOS).resize((tw, th), Image.LANCZOS, box=(l, t, l + bw, t + bh))
+    if enc:
+        im.save(_io.BytesIO(), format="JPEG", quality=92)
+    return w * h
+
+
+def pillow_baseline(pool, targets, seconds: float, encode: bool = False):
+    """The same bounded sample through Pillow 12 (libjpeg-turbo decode +
+    Pillow's Lanczos convolution), one image per task on every host core."""
+    import multiprocessing as mp
+    cores, basis = host_cores()
+    t = time.perf_counter()
+    px = _pil_work((pool[0], *targets[0], encode))
+    per_px = (time.perf_counter() - t) / max(px, 1)
+    mean_px = np.mean([w * h for (w, h) in [image_dims(d)[:2] for d in pool[:32]]])
+    n = int(max(cores, min(64 * len(pool), seconds * cores / max(per_px * mean_px, 1e-9))))
+    jobs = [(pool[i % len(pool)], *targets[i % len(pool)], encode) for i in range(n)]
+    p = mp.get_context("fork").Pool(cores)
+    try:
+        p.map(_pil_work, jobs[:cores], chunksize=1)
+        t0 = time.perf_counter()
+        res = p.map(_pil_work, jobs, chunksize=1)
+        wall = time.perf_counter() - t0
+    finally:
+        p.close()
+        p.join()
+    tot = sum(res)
+    return {"value": round(tot / wall / 1e6, 2), "unit": "Mpixel/s", "cores": cores, "kind": "pillow-proxy",
+            "sample": f"{n} images of the same pool ({tot / 1e6:.1f} Mpx): PIL decode + resize(LANCZOS) to the "
+                      f"scaled size + crop box resize(LANCZOS, box=){' + JPEG q92 save' if encode else ''}, "
+                      f"{cores} processes ({basis}), {wall:.1f} s"}
+
+
 def cpu_baseline(pool, targets, seconds: float, encode: bool = False):
     """Oracle (scalar C restatement of the reference path: decode +
     crop_and_resize) on the host cores, one image per task like the
@@ -114,7 +229,7 @@ def cpu_baseline(pool, targets, seconds: float, encode: bool = False):
     import multiprocessing as mp
     from oracle import oracle as O
     O.lib()
-    cores = cpu_share()
+    cores, basis = host_cores()
     # size the sample from a one-image probe so the run takes ~`seconds`
     px, dt = _cpu_work((pool[0], *targets[0], encode))
     per_px = dt / max(px, 1)
@@ -134,7 +249,8 @@ def cpu_baseline(pool, targets, seconds: float, encode: bool = False):
     return {"value": round(tot_px / wall / 1e6, 2), "unit": "Mpixel/s", "cores": cores, "kind": "port",
             "sample": f"{n} images of the same pool ({tot_px / 1e6:.1f} Mpx) through oracle/ (scalar C "
                       f"decode + FIR-mode Lanczos3 crop_and_resize{' + JPEG q92 encode' if encode else ''}), "
-                      f"{cores} processes, {wall:.1f} s"}
+                      f"{cores} processes ({basis}), {wall:.1f} s",
+            "cpu_model": cpu_model(), "reference_toolchain": reference_toolchain()}
 
 
 def image_dims(data: bytes):
@@ -279,13 +395,89 @@ def stage_bytes(L, data: bytes, dim, target) -> dict:
     return b
 
 
+# ------------------------------------------------------------------- ranks
+
+def _free_port() -> int:
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without torchrun: start N rank processes of this script
+    (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set before they start; this parent
+    imports no GPU runtime), stream their output, and return the worst exit
+    code.  If a rank fails, the others are stopped (they would wait forever
+    at the next barrier)."""
+    env = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    rc = 0
+    try:
+        while procs:
+            for p_ in list(procs):
+                code = p_.poll()
+                if code is None:
+                    continue
+                procs.remove(p_)
+                if code != 0:
+                    rc = rc or code
+                    for q in procs:
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for q in procs:
+            q.kill()
+    return rc
+
+
+def jpeg_pool(a, rank: int, world: int, workers: int, dist):
+    """The rank's slice of the logical stream and the pool images it shows.
+
+    Sample s of the `a.samples`-long stream shows pool image s % a.pool (the
+    stream cycles over the pool); rank r owns the contiguous
+    slice get_data_slice_multirank(a.samples, r, world) and step k of the
+    run decodes its samples lo + (k*B + j) mod (hi - lo).  Pool images are
+    generated once per machine into a cache shared by the ranks (each rank
+    makes a 1/world share of what any rank needs, then all load theirs)."""
+    from datago_amd import synth
+    from datago_amd.sharding import get_data_slice_multirank
+    seed = 4 if a.workload == "cfg4" else 2  # SURVEY §8(d): configs[1] seed 2, configs[3] seed 4
+    nb = max(1, a.warmup) + a.steps
+
+    def images_of(r):
+        lo, hi = get_data_slice_multirank(a.samples, r, world)
+        span = max(1, hi - lo)
+        return [(lo + (k * a.batch + j) % span) % a.pool for k in range(nb) for j in range(a.batch)]
+
+    union = sorted({i for r in range(world) for i in images_of(r)})
+    t0 = time.perf_counter()
+    made = synth.generate_pool_images(seed, a.pool, union[rank::world], workers, a.short_min, a.short_max,
+                                      a.progressive_frac,
+                                      progress=lambda m: print(f"[rank {rank}] {m}", file=sys.stderr, flush=True))
+    if world > 1:
+        dist.barrier()
+    mine = images_of(rank)
+    uniq = sorted(set(mine))
+    pos = {img: k for k, img in enumerate(uniq)}
+    pool = synth.load_pool_images(seed, a.pool, uniq, a.short_min, a.short_max, a.progressive_frac)
+    seq = [pos[i] for i in mine]  # batch k = seq[k*B:(k+1)*B]
+    lo, hi = get_data_slice_multirank(a.samples, rank, world)
+    return pool, seq, (lo, hi), made, time.perf_counter() - t0
+
+
 # ------------------------------------------------------------------- main
 
 def main() -> int:
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a.gpus)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and rank == 0:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; measuring {world} ranks", file=sys.stderr)
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -295,15 +487,17 @@ def main() -> int:
     from oracle import buckets as B
 
     from datago_amd.sharding import get_data_slice_multirank, max_over_ranks, sum_over_ranks
-    # ---- this rank's slice of the logical sample stream (generator_files.rs:24-42):
-    # a.pool images per rank, world * a.pool in total, contiguous slices
-    lo, hi = get_data_slice_multirank(a.pool * world, rank, world)
     workers = a.workers or cpu_share()
     t_gen = time.perf_counter()
+    n_made = 0
+    lo, hi = 0, 0
     png = a.workload == "png"
     wds = a.workload == "wds"
     tar_arena = None
-    if wds:  # configs[2]: WebDataset shards held in memory, indexed by dg_wds_index (zero-copy members)
+    seq = None  # jpeg/cfg4: pool positions of the rank's stream, batch after batch
+    if a.workload in ("jpeg", "cfg4"):
+        pool, seq, (lo, hi), n_made, _ = jpeg_pool(a, rank, world, workers, dist)
+    elif wds:  # configs[2]: WebDataset shards held in memory, indexed by dg_wds_index (zero-copy members)
         tars = [synth.make_wds_shard(3 * 1000 + k, 1000, first_key=1000 * k, workers=workers)
                 for k in range(a.shards)]
         t_idx = time.perf_counter()
@@ -319,12 +513,11 @@ def main() -> int:
         npair = max(1, a.pool // 2)
         plo, phi = get_data_slice_multirank(npair * world, rank, world)
         pool = png_corpus(5, npair * world, a.short_min, a.short_max, workers, plo, phi)
-    else:
-        spec_seed = 2  # BASELINE configs[1] seed
-        pool = synth.mixed_corpus(spec_seed, a.pool * world, a.short_min, a.short_max, workers=workers, lo=lo,
-                                  progressive_frac=a.progressive_frac,
-                                  hi=hi)
     t_gen = time.perf_counter() - t_gen
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise RuntimeError("bench.py needs a GPU (HIP device)")
+    local = local % ndev  # more ranks than devices (a 1-GPU rehearsal of --gpus N): ranks share the card
     torch.cuda.set_device(local)
     tr = B.ARAwareTransform(a.size, a.ratio, 0.5, 2.0)
     dims = [image_dims(d) for d in pool]
@@ -384,8 +577,14 @@ def main() -> int:
     out_cap = sum(sorted(out_bytes * reps)[-B_:]) + 16 * B_
     d_out = [ctx.alloc(out_cap) for _ in range(a.inflight)]
 
+    def batch_idx(k: int):
+        if seq is not None:
+            k %= len(seq) // B_  # serial / e2e passes reuse the stream's batches
+            return seq[k * B_:(k + 1) * B_]
+        return [(k * B_ + j) % len(pool) for j in range(B_)]
+
     def submit(k: int):
-        idx = [(k * B_ + j) % len(pool) for j in range(B_)]
+        idx = batch_idx(k)
         hp = [h_base + offs[i] for i in idx]
         dp = [d_arena + offs[i] for i in idx]
         lens = [len(pool[i]) for i in idx]
@@ -454,6 +653,7 @@ def main() -> int:
     ctx.set_option("timing", 0)
     # max over ranks; totals over ranks
     (dt_max,) = max_over_ranks([dt], world)
+    per_rank_s = sum_over_ranks([dt if r == rank else 0.0 for r in range(world)], world)
     px_all, alg_all, outpx_all = sum_over_ranks([float(px_total), alg_bytes, float(out_px)], world)
 
     # ---- isolated per-kernel times: batches one at a time (untimed, reported only)
@@ -476,7 +676,7 @@ def main() -> int:
         t1 = time.perf_counter()
         e2e_px = 0
         for k in range(a.e2e_steps):
-            idx = [(k * B_ + j) % len(pool) for j in range(B_)]
+            idx = batch_idx(k)
             res = ctx.decode_batch([pool[i] for i in idx], [forced_pool[i] for i in idx])
             e2e_px += sum(dims[i][0] * dims[i][1] for i, r in zip(idx, res) if r[0] == 0)
         e2e = e2e_px / (time.perf_counter() - t1) / 1e6
@@ -485,7 +685,7 @@ def main() -> int:
         t1 = time.perf_counter()
         e2e_px = 0
         for k in range(a.e2e_steps):
-            idx = [(k * B_ + j) % len(pool) for j in range(B_)]
+            idx = batch_idx(k)
             res = ctx.decode_batch_torch([pool[i] for i in idx], [forced_pool[i] for i in idx])
             e2e_px += sum(dims[i][0] * dims[i][1] for i, r in zip(idx, res) if r[0] == 0)
             del res
@@ -527,6 +727,7 @@ def main() -> int:
         result = {
             "metric": ("Mpixel/s device-resident PNG decode+bucket-resize (image + aligned mask pairs)" if png else
                        "Mpixel/s device-resident JPEG decode+bucket-resize at 1/2/4/8 MI355X"),
+            "ms_per_step_per_rank": [round(t_ / a.steps * 1e3, 3) for t_ in per_rank_s],
             "value": round(px_all / dt_max / 1e6, 2),
             "unit": "Mpixel/s",
             "n_gpus": world,
@@ -540,17 +741,21 @@ def main() -> int:
             "data": (f"synthetic (seeded PIL PNG pool of {len(pool) // 2} RGB image + L8 mask pairs per rank, cycled)"
                      if png else f"synthetic ({a.shards} seeded WebDataset shards, {len(pool)} .jpg members on this "
                      f"rank, indexed in {wds_index_s * 1e3:.1f} ms by dg_wds_index, cycled)" if wds else
-                     f"synthetic (seeded PIL JPEG pool of {a.pool} unique images per rank, cycled)"),
+                     f"synthetic (seeded PIL JPEG pool of {a.pool} unique images, {len(pool)} of them resident "
+                     f"on rank 0; {a.samples} logical samples, rank 0's slice [{lo}, {hi}))"),
             "config": {"workload": ("configs[2]: WebDataset shards (fake-imagenet-like {key}.jpg + {key}.cls, "
                                     f"W U[300,500] H U[250,500] q90), decode + bucket-resize to {a.size}/{a.ratio}")
-                       if wds else ("configs[1]: file-source JPEGs, mixed aspect ratios, decode + bucket + "
+                       if wds else ("configs[3]: file source sharded by rank/world_size "
+                                    "(get_data_slice_multirank), 1M synthetic JPEGs (16,384-image pool, seed 4), "
+                                    "decode + bucket-resize to 1024/32" if a.workload == "cfg4" else
+                                    "configs[1]: file-source JPEGs, mixed aspect ratios, decode + bucket + "
                                     "crop/resize to 1024/32 buckets") if not png else
                                    (f"configs[4]{'' if a.encode else ' without re-encode'}: RGB PNG (PIL, zlib 6) "
                                     "+ L8 mask PNG pairs, mask aligned to the image's bucket, decode + crop/resize "
                                     f"to 1024/32{' + JPEG q92 re-encode of every payload' if a.encode else ''}"),
                        "pre_encode_images": bool(a.encode),
                        "progressive_frac": a.progressive_frac,
-                       "images_per_step": B_, "pool_per_rank": a.pool,
+                       "images_per_step": B_, "pool": a.pool, "samples": a.samples,
                        "short_side": [a.short_min, a.short_max], "buckets": f"{a.size}/{a.ratio}/0.5/2.0",
                        "parallelism": f"dp{world} (sample shards, no collectives)"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -569,9 +774,12 @@ def main() -> int:
                                    "frac": round(valu[k] / (iso["stages_ms"][k] / 1e3) / 1e12 / VALU_PEAK_T, 4)}
                                for k in valu if iso and iso["stages_ms"].get(k, 0) > 0.05}
                               if valu and iso else None),
-            "roofline_pipeline": {"alg_bytes_per_step": round(per_step_alg), "gpu_ms_per_step": round(gpu_ms, 4),
-                                  "achieved_GBs": round(per_step_alg / (gpu_ms / 1e3) / 1e9, 2),
-                                  "frac": round(per_step_alg / (gpu_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)},
+            # SURVEY §8(d) B_alg of the whole path over the wall-clock step time
+            "roofline_pipeline": {"alg_bytes_per_step": round(per_step_alg),
+                                  "ms_per_step": round(dt_max / a.steps * 1e3, 4),
+                                  "achieved_GBs": round(per_step_alg / (dt_max / a.steps) / 1e9, 2),
+                                  "frac": round(per_step_alg / (dt_max / a.steps) / 1e9 / HBM_PEAK_GBS, 5),
+                                  "sum_of_stage_spans_ms": round(gpu_ms, 4)},
             "stages_ms_per_step": {k: round(v / steps, 4) for k, v in stage_tot.items()},
             "stages_alg_GBs": {k: round(stage_alg[k] / (stage_tot[k] / 1e3) / 1e9, 1)
                                for k in stage_tot if stage_alg.get(k) and stage_tot[k] > 0},
@@ -580,6 +788,7 @@ def main() -> int:
             "e2e_host_mpix_s": round(e2e, 2) if e2e else None,
             "e2e_host_in_hbm_out_mpix_s": round(e2e_dev, 2) if e2e_dev else None,
             "corpus_gen_s": round(t_gen, 1),
+            "corpus_generated_here": n_made if seq is not None else None,
             "stats": {"resync_rounds": ctx.stat("resync_rounds"), "fix_workgroups": ctx.stat("fix_workgroups"),
                       "write_mismatch": ctx.stat("write_mismatch"), "sync_iters_max": ctx.stat("sync_iters_max"),
                       "sub_bits": ctx.stat("sub_bits"), "lead_bits": a.lead_bits},
@@ -588,6 +797,7 @@ def main() -> int:
         }
         if world == 1 and not a.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(pool, targets, a.cpu_seconds, a.encode)
+            result["cpu_baseline_pillow"] = pillow_baseline(pool, targets, a.cpu_seconds, a.encode)
         else:
             result["cpu_baseline"] = None
         if png or wds:  # the PMC file is for the configs[1] workload

@@ -18,7 +18,11 @@ SUBSAMPLING = {"4:4:4": 0, "4:2:2": 1, "4:2:0": 2}
 
 
 def synth_pixels(rng: np.random.Generator, w: int, h: int, gray: bool = False) -> np.ndarray:
-    """Smooth gradient + a few shapes + gaussian noise, uint8 HWC (or HW)."""
+    """Smooth gradient + a few shapes + gaussian noise, uint8 HWC (or HW).
+
+    Worked in 64-row bands so the float temporaries stay in cache; every
+    element sees the same operations in the same order and the RNG is drawn
+    in the same sequence, so the pixels equal the whole-image formulation."""
     c = 1 if gray else 3
     # low-resolution random field upsampled bilinearly -> smooth gradients
     gh, gw = max(2, h // 64 + 2), max(2, w // 64 + 2)
@@ -27,15 +31,19 @@ def synth_pixels(rng: np.random.Generator, w: int, h: int, gray: bool = False) -
     xs = np.linspace(0, gw - 1, w, dtype=np.float32)
     y0 = np.floor(ys).astype(np.int32).clip(0, gh - 2)
     x0 = np.floor(xs).astype(np.int32).clip(0, gw - 2)
-    fy = (ys - y0)[:, None, None]
+    fys = ys - y0
     fx = (xs - x0)[None, :, None]
-    a = grid[y0][:, x0]
-    b = grid[y0][:, x0 + 1]
-    cc = grid[y0 + 1][:, x0]
-    d = grid[y0 + 1][:, x0 + 1]
-    img = (a * (1 - fx) * (1 - fy) + b * fx * (1 - fy) + cc * (1 - fx) * fy + d * fx * fy)
-    im = Image.fromarray(img.clip(0, 255).astype(np.uint8)[:, :, 0] if gray else
-                         img.clip(0, 255).astype(np.uint8))
+    g0, g1 = grid[:, x0], grid[:, x0 + 1]
+    base = np.empty((h, w, c), np.uint8)
+    R = 64
+    for r0 in range(0, h, R):
+        r1 = min(h, r0 + R)
+        fy = fys[r0:r1, None, None]
+        yy = y0[r0:r1]
+        a, b, cc, d = g0[yy], g1[yy], g0[yy + 1], g1[yy + 1]
+        img = (a * (1 - fx) * (1 - fy) + b * fx * (1 - fy) + cc * (1 - fx) * fy + d * fx * fy)
+        base[r0:r1] = img.clip(0, 255).astype(np.uint8)
+    im = Image.fromarray(base[:, :, 0] if gray else base)
     dr = ImageDraw.Draw(im)
     for _ in range(int(rng.integers(2, 8))):
         x1, x2 = sorted(rng.integers(0, w, 2).tolist())
@@ -45,9 +53,13 @@ def synth_pixels(rng: np.random.Generator, w: int, h: int, gray: bool = False) -
             dr.rectangle([x1, y1, x2, y2], fill=col)
         else:
             dr.ellipse([x1, y1, x2, y2], fill=col)
-    arr = np.asarray(im).astype(np.int16)
-    noise = rng.normal(0, 8, size=arr.shape)
-    return (arr + noise).clip(0, 255).astype(np.uint8)
+    arr = np.asarray(im)
+    out = np.empty(arr.shape, np.uint8)
+    for r0 in range(0, h, R):  # N(0, 8) noise, drawn band by band in stream order
+        r1 = min(h, r0 + R)
+        blk = arr[r0:r1].astype(np.int16)
+        out[r0:r1] = (blk + rng.normal(0, 8, size=blk.shape)).clip(0, 255).astype(np.uint8)
+    return out
 
 
 def encode_jpeg(arr: np.ndarray, quality: int = 90, subsampling: str = "4:2:0",
@@ -135,6 +147,85 @@ def mixed_corpus(seed: int, n: int, short_min: int = 256, short_max: int = 2048,
     if workers > 1:
         return _pool_map(jobs, workers)
     return [_make_one(j) for j in jobs]
+
+
+def corpus_cache_dir() -> str:
+    """Where generated pool images are kept between runs on one machine
+    ($DATAGO_CORPUS_CACHE, default <tmp>/datago_amd_corpus): the bench's
+    back-to-back 1/2/4/8-GPU runs, and the ranks of one run, share it."""
+    import os
+    import tempfile
+    return os.environ.get("DATAGO_CORPUS_CACHE") or os.path.join(tempfile.gettempdir(), "datago_amd_corpus")
+
+
+def _pool_job(seed: int, i: int, spec, progressive_frac: float):
+    step = int(round(1.0 / progressive_frac)) if progressive_frac > 0 else 0
+    return (seed * 1_000_003 + i, spec[i], 0, bool(step) and i % step == 0)
+
+
+def _cache_name(job) -> str:
+    s, (w, h, q, ss, gray), rst, prog = job
+    return f"v1_{s}_{w}x{h}_q{q}_{ss.replace(':', '')}_{int(gray)}_{rst}_{int(prog)}.jpg"
+
+
+def _make_cached(args):
+    import os
+    job, path = args
+    data = _make_one(job)
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "wb") as f:
+        f.write(data)
+    os.replace(tmp, path)  # atomic: concurrent ranks never see a partial file
+    return len(data)
+
+
+def generate_pool_images(seed: int, n_pool: int, indices, workers: int = 1, short_min: int = 256,
+                         short_max: int = 2048, progressive_frac: float = 0.0, cache_dir: str | None = None,
+                         progress=None) -> int:
+    """Make sure pool images `indices` of the seed's n_pool-image pool (the
+    mixed_spec distribution; image i is exactly mixed_corpus(seed, n_pool)[i])
+    exist in the cache.  Returns how many were generated."""
+    import os
+    import time
+    cache_dir = cache_dir or corpus_cache_dir()
+    os.makedirs(cache_dir, exist_ok=True)
+    spec = mixed_spec(seed, n_pool, short_min, short_max)
+    todo = []
+    for i in indices:
+        job = _pool_job(seed, i, spec, progressive_frac)
+        path = os.path.join(cache_dir, _cache_name(job))
+        if not os.path.exists(path):
+            todo.append((job, path))
+    if not todo:
+        return 0
+    t0, last = time.time(), time.time()
+    if workers > 1:
+        import multiprocessing as mp
+        pool = mp.get_context("fork").Pool(workers)
+        try:
+            for k, _ in enumerate(pool.imap_unordered(_make_cached, todo, chunksize=2)):
+                if progress and time.time() - last > 20:
+                    last = time.time()
+                    progress(f"corpus: {k + 1}/{len(todo)} images generated in {last - t0:.0f} s")
+        finally:
+            pool.close()
+            pool.join()
+    else:
+        for t in todo:
+            _make_cached(t)
+    return len(todo)
+
+
+def load_pool_images(seed: int, n_pool: int, indices, short_min: int = 256, short_max: int = 2048,
+                     progressive_frac: float = 0.0, cache_dir: str | None = None) -> List[bytes]:
+    import os
+    cache_dir = cache_dir or corpus_cache_dir()
+    spec = mixed_spec(seed, n_pool, short_min, short_max)
+    out = []
+    for i in indices:
+        with open(os.path.join(cache_dir, _cache_name(_pool_job(seed, i, spec, progressive_frac))), "rb") as f:
+            out.append(f.read())
+    return out
 
 
 def uniform_corpus(seed: int, n: int, w: int = 640, h: int = 480, quality: int = 90,

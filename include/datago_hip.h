@@ -66,7 +66,7 @@ typedef struct dg_image_config {
   uint32_t downsampling_ratio;  /* e.g. 32 */
   double min_aspect_ratio;      /* e.g. 0.5 */
   double max_aspect_ratio;      /* e.g. 2.0 */
-  int32_t pre_encode_images;    /* re-encode: JPEG on the GPU; PNG -> DG_ERR_UNSUPPORTED (CPU path) */
+  int32_t pre_encode_images;    /* re-encode on the GPU: JPEG (dg_enc.hip) or PNG (dg_penc.hip) per encode_format */
   int32_t image_to_rgb8;        /* gray -> RGB expansion after resize (:367-372) */
   int32_t encode_format;        /* 0 = PNG, 1 = JPEG (EncodeFormat, :16-22) */
   int32_t jpeg_quality;         /* default 92 (:14) */
@@ -200,7 +200,9 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "wg_timing"   debug: per-workgroup timestamps of the entropy kernels
  *   "timing"      1 = record per-kernel HIP events (dg_last_batch_timings)
  *   "side_stream" 1 = Lanczos tables on a second stream (default 1)
- *   "debug_flags" internal switches for kernel bisection
+ *   "debug_flags" internal switches: bit 0 = direct H-pass kernel only (bisection); bit 16 / 17 =
+ *                 force an entropy write-pass mismatch / a resync that never settles (tests of the
+ *                 per-image DG_ERR_UNSUPPORTED those failures return)
  *   "progressive" 1 = decode progressive JPEGs on the GPU (default 0: DG_ERR_UNSUPPORTED, the
  *                 caller's CPU decoder takes them; refinement scans decode serially)
  *   "slots"       batches in flight, 1..4 (default 2)
@@ -209,8 +211,13 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)
  *   "png_chunked" 0 = inflate every PNG with the serial kernel (test switch; default 1)
  * Stats: "batches", "coalesced_batches", "coalesced_images", "resync_rounds", "fix_workgroups", "write_mismatch",
- * "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool", "png_chunks", "png_serial_fallbacks";
- * -1 if unknown. */
+ * "unsettled_batches", "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool" (tables pooled now),
+ * "pool_flushes" (times the table pools were started over), "png_chunks", "png_serial_fallbacks";
+ * -1 if unknown.
+ *
+ * Entropy-decode self-checks: an image whose write pass disagrees with the sync pass, or every sequential JPEG of
+ * a batch whose boundary repair did not settle, is returned DG_ERR_UNSUPPORTED (the caller's CPU decoder takes
+ * it), never DG_OK with unverified pixels. */
 dg_status dg_ctx_set_option(dg_ctx *ctx, const char *key, int64_t value);
 int64_t dg_ctx_get_stat(dg_ctx *ctx, const char *key);
 
