@@ -34,6 +34,9 @@ void set_error(const std::string &s) { g_last_error = s; }
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// Boundary-repair rounds (finish()) before a batch is declared unsettled.
+static constexpr int kMaxResyncRounds = 64;
+
 static const char *kStageNames[] = {"upload",     "png_inflate", "png_unfilter", "destuff",   "prog_scans",
                                     "huff_sync",  "huff_fix",    "huff_scan",    "huff_write", "coeffs",
                                     "idct",       "color",       "resize_h1",    "resize_v1", "resize_h2",
