@@ -77,7 +77,7 @@ def parse():
     ap.add_argument("--entropy-once", type=int, default=-1, help="decode-once entropy staging (-1 = library default)")
     ap.add_argument("--entropy-lpt", type=int, default=-1, help="slow entropy workgroups first (-1 = library default)")
     ap.add_argument("--hb-bands", type=int, default=0, help="band H kernel: 8-row bands per workgroup (0 = default)")
-    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=3, help="host-memory (PCIe-inclusive) steps")
     ap.add_argument("--shards", type=int, default=8, help="wds workload: shards of 1000 samples")
