@@ -77,6 +77,7 @@ def parse():
     ap.add_argument("--entropy-once", type=int, default=-1, help="decode-once entropy staging (-1 = library default)")
     ap.add_argument("--entropy-lpt", type=int, default=-1, help="slow entropy workgroups first (-1 = library default)")
     ap.add_argument("--hb-bands", type=int, default=0, help="band H kernel: 8-row bands per workgroup (0 = default)")
+    ap.add_argument("--hb-occ", type=int, default=0, help="band H kernels: 4 or 5 waves/SIMD register budget (0 = default)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=3, help="host-memory (PCIe-inclusive) steps")
@@ -539,6 +540,8 @@ def main() -> int:
         ctx.set_option("wg_timing", 1)
     if a.hb_bands:
         ctx.set_option("hb_bands", a.hb_bands)
+    if a.hb_occ:
+        ctx.set_option("hb_occ", a.hb_occ)
     if a.progressive_frac > 0:
         ctx.set_option("progressive", 1)
     if a.entropy_lpt >= 0:

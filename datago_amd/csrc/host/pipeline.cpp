@@ -207,6 +207,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     hb_bands_ = (uint32_t)v;
     return DG_OK;
   }
+  if (k == "hb_occ") {  // band H kernels: register budget for 4 or 5 waves per SIMD
+    if (v != 4 && v != 5) return DG_ERR_INVALID;
+    hb_occ_ = (int)v;
+    return DG_OK;
+  }
   if (k == "png_chunked") {  // 0: every PNG inflates serially (test switch)
     chunked_off_ = v == 0;
     return DG_OK;
@@ -1122,7 +1127,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   // ---- 5. workgroup lists
   for (auto &l : b.lists) l.clear();
-  std::vector<WgItem> hb[2][4];  // band H items per (stage, weight-count class)
+  std::vector<WgItem> hb[2][2][4];  // band H items per (stage, fused fill, weight-count class)
   for (int di = 0; di < (int)b.descs.size(); di++) {
     const ImageDesc &d = b.descs[di];
     const uint32_t I = (uint32_t)di;
@@ -1171,7 +1176,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         // at an odd segment position spans ksize + 1 positions
         const uint32_t kk = ps.ksize + 1;
         const int cls = kk <= 8 ? 0 : kk <= 16 ? 1 : kk <= 32 ? 2 : 3;
-        for (uint32_t it = 0; it < cnt; it++) hb[s / 2][cls].push_back({I, it});
+        const int fused = (ps.mode & kHFused) ? 1 : 0;
+        for (uint32_t it = 0; it < cnt; it++) hb[s / 2][fused][cls].push_back({I, it});
       } else {
         uint32_t cnt = (ps.width * ps.C + 15) / 16 * ps.rows;
         for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_RH0 + s].push_back({I, it});
@@ -1225,11 +1231,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       b.lists[L_PROG][at[b.pscans[j].level]++] = WgItem{b.pscans[j].image, j};
   }
   for (int h = 0; h < 2; h++)
-    for (int c = 0; c < 4; c++) {
-      b.hclass[h][c] = (uint32_t)hb[h][c].size();
-      auto &l = b.lists[h ? L_RH2 : L_RH0];
-      l.insert(l.end(), hb[h][c].begin(), hb[h][c].end());
-    }
+    for (int f = 1; f >= 0; f--)  // launch order: fused classes, then byte-fill classes
+      for (int c = 0; c < 4; c++) {
+        b.hclass[h][f][c] = (uint32_t)hb[h][f][c].size();
+        auto &l = b.lists[h ? L_RH2 : L_RH0];
+        l.insert(l.end(), hb[h][f][c].begin(), hb[h][f][c].end());
+      }
   // ---- 6. meta buffer: [flags][descs][lists...]
   Layout M;
   b.flags_off = M.take(sizeof(BatchFlags));
@@ -1374,13 +1381,13 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (next()) return DG_ERR_DEVICE;
   HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_coef, 0));
   launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
-  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0);
+  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0, hb_occ_);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | (debug_flags_ << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV1), cnt(L_RV1), 1);
   launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
-  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2);
+  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2, hb_occ_);
   launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | (debug_flags_ << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3);

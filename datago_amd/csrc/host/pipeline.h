@@ -71,7 +71,7 @@ struct Batch {
   std::vector<uint32_t> prog_level_n;     // L_PROG holds the scans level by level: counts
   // band H lists (L_RH0, L_RH2) are grouped by weight-count class (<=8, <=16,
   // <=32, more): hclass[stage/2][k] items of class k, in that order
-  uint32_t hclass[2][4] = {{0}};
+  uint32_t hclass[2][2][4] = {{{0}}};  // [stage/2][fused][class]
   size_t desc_off = 0, flags_off = 0;
   size_t meta_bytes = 0;
   size_t total_subs = 0;
@@ -205,6 +205,7 @@ class Context {
   bool wg_timing_ = false;
   bool chunked_off_ = false;  // option "png_chunked" = 0
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
+  int hb_occ_ = 5;                      // option "hb_occ"
   bool progressive_ = false;            // option "progressive"
   bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first
   bool entropy_once_ = false;           // option "entropy_once": decode-once staging + k_huff_scatter

@@ -1149,7 +1149,11 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
     }
 }
 
-template <int KMAX>
+// FUSED: the first pass of a colour JPEG (fill = upsample + colour
+// conversion from the planes, C = 3); otherwise the fill copies interleaved
+// bytes of C = 1..4 channels.  Separate kernels so each allocates registers
+// for its own path only.
+template <int KMAX, bool FUSED>
 __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps, uint32_t item, uint32_t *seg,
                                       uint8_t *ob, uint32_t *ext) {
   // one workgroup: a tile of kHBandCols output columns x ps.bands bands of
@@ -1161,7 +1165,7 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
   const uint32_t x1 = x0 + kHBandCols < ps.width ? x0 + kHBandCols : ps.width;
   // coefficient tables cover all out_size outputs; this pass computes [out0, out0 + width)
   const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds) + 2 * ps.out0;
-  const uint32_t C = ps.C, ksize = ps.ksize;
+  const uint32_t C = FUSED ? 3u : ps.C, ksize = ps.ksize;
   const DG_GLOBAL int16_t *coef = gp<const int16_t>(ps.coef) + (size_t)ps.out0 * ksize;
   const uint32_t t = threadIdx.x, col = t & (kHBandCols - 1), x = x0 + col;
   const bool valid = x < x1;
@@ -1211,7 +1215,7 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
     const uint32_t nrows = ps.rows - y0 < kHBandRows ? ps.rows - y0 : kHBandRows;
     // phase 1: fill
     if (fr < nrows) {
-      if (ps.mode & kHFused) {
+      if (FUSED) {
         const uint32_t noct = (pe - p0 + 7) >> 3;
         for (uint32_t q = fl; q < noct; q += 32)
           hfill_color8(im, ps.row0 + y0 + fr, p0 + 8 * q, seg + fr * kHSegStride + 8 * q);
@@ -1225,7 +1229,7 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
     __syncthreads();
     // phase 2: convolve (thread: column col, rows r0, r0 + 2, ...)
     if (valid) {
-      if (C == 3)
+      if (FUSED || C == 3)
         hconv_rows<KMAX, 3>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
       else if (C == 1)
         hconv_rows<KMAX, 1>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
@@ -1253,15 +1257,17 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
   }
 }
 
-template <int KMAX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_resize_hb(const ImageDesc *__restrict__ imgs,
-                                                   const WgItem *__restrict__ list, int stage) {
+// OCC: waves per SIMD the register allocation targets (5: <= 96 VGPRs, may
+// spill; 4: <= 128 VGPRs, five workgroups' worth of LDS but four resident).
+template <int KMAX, bool FUSED, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void k_resize_hb(
+    const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list, int stage) {
   __shared__ __attribute__((aligned(16))) uint32_t seg[kHBandRows * kHSegStride];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kHBandRows * kHBandCols * 4];
   __shared__ uint32_t ext[2];
   const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
   const ImageDesc &im = imgs[it.image];
-  hband<KMAX>(im, im.pass[stage], it.item0, seg, ob, ext);
+  hband<KMAX, FUSED>(im, im.pass[stage], it.item0, seg, ob, ext);
 }
 
 // Vertical pass: each thread produces 16 consecutive bytes of one output row
@@ -1470,14 +1476,27 @@ void launch_coeffs(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t
 void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
   DG_LAUNCH(k_resize_h, nwg, st, imgs, list, stage);
 }
-void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[4], int stage) {
-  DG_LAUNCH(k_resize_hb<8>, ncls[0], st, imgs, list, stage);
+template <bool FUSED, int OCC>
+static void launch_hb_classes(hipStream_t st, const ImageDesc *imgs, const WgItem *&list, const uint32_t ncls[4],
+                              int stage) {
+  DG_LAUNCH((k_resize_hb<8, FUSED, OCC>), ncls[0], st, imgs, list, stage);
   list += ncls[0];
-  DG_LAUNCH(k_resize_hb<16>, ncls[1], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<16, FUSED, OCC>), ncls[1], st, imgs, list, stage);
   list += ncls[1];
-  DG_LAUNCH(k_resize_hb<32>, ncls[2], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<32, FUSED, OCC>), ncls[2], st, imgs, list, stage);
   list += ncls[2];
-  DG_LAUNCH(k_resize_hb<0>, ncls[3], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<0, FUSED, OCC>), ncls[3], st, imgs, list, stage);
+  list += ncls[3];
+}
+void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][4],
+                      int stage, int occ) {
+  if (occ == 4) {
+    launch_hb_classes<true, 4>(st, imgs, list, ncls[1], stage);
+    launch_hb_classes<false, 4>(st, imgs, list, ncls[0], stage);
+  } else {
+    launch_hb_classes<true, 5>(st, imgs, list, ncls[1], stage);
+    launch_hb_classes<false, 5>(st, imgs, list, ncls[0], stage);
+  }
 }
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
   DG_LAUNCH(k_resize_v, nwg, st, imgs, list, stage);
