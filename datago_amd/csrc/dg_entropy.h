@@ -48,8 +48,13 @@ DG_HD uint32_t ds_word_index(uint32_t w, uint32_t lsw) {
   const uint32_t s = w >> lsw, j = w & ((1u << lsw) - 1u);
   return ((((s >> 6) << lsw) + j) << 6) + (s & 63u);
 }
-// physical words needed for a stream of nsub subsequences (+ one column of margin)
-DG_HD uint64_t ds_words_alloc(uint32_t nsub, uint32_t lsw) { return ((uint64_t)(nsub / 64 + 1) << lsw) * 64; }
+// physical words needed for a stream of nsub subsequences, plus the margin
+// past its end that the zero padding (64 bytes) and a reader's window and
+// lookahead reach: >= 1024 bits, and >= 2 subsequences
+DG_HD uint64_t ds_words_alloc(uint32_t nsub, uint32_t lsw) {
+  const uint32_t margin = ((1024u >> 5) >> lsw) + 2u;
+  return ((uint64_t)((nsub + margin + 63u) / 64u) << lsw) * 64;
+}
 
 struct BitWin {
   const DG_GLOBAL uint32_t *w;  // interleaved stream as little-endian words (byte-swapped on use)
@@ -99,6 +104,32 @@ DG_HD uint32_t huff_lookup(const T &t, uint32_t bits) {
   for (int32_t l = kLutBits + 1; l <= 16; l++)
     if (pk < t.lim[l]) return ((uint32_t)l << 8) | t.vals[(t.valoff[l] + (int32_t)(pk >> (16 - l))) & 255];
   return 16u << 8;  // invalid code: consume 16 bits (only off-sync / past the data)
+}
+
+// First-level lookup, falling back to the sub-tables / lim[] only for codes
+// longer than kLutBits (the one branch left in the per-symbol step).
+template <class T>
+DG_HD uint32_t huff_decode(const T &t, uint32_t bits) {
+  const uint32_t e = t.lut[bits >> (32 - kLutBits)];
+  if (e != 0u && !(e & 0x8000u)) return e;
+  return huff_lookup(t, bits);
+}
+
+// Signed value of the `size` magnitude bits that follow a `len`-bit code at
+// the top of `bits` (T.81 F.2.2.1 EXTEND); 0 when size == 0.  Branch-free:
+// the 64-bit shift by 32 - size yields 0 for size 0.
+DG_HD int32_t huff_value(uint32_t bits, uint32_t len, uint32_t size) {
+  const uint32_t raw = (uint32_t)((uint64_t)(bits << len) >> (32u - size));
+  const uint32_t half = (1u << size) >> 1;
+  return raw < half ? (int32_t)raw - (int32_t)((1u << size) - 1u) : (int32_t)raw;
+}
+
+// Zigzag position after one symbol decoded at position z: a DC symbol moves
+// to 1; an AC symbol to z + run + 1, ZRL (0xF0) to z + 16, EOB to 64.
+DG_HD uint32_t huff_next_z(uint32_t z, uint32_t sym) {
+  const uint32_t size = sym & 15u, run = sym >> 4;
+  const uint32_t zac = (size == 0u && run != 15u) ? 64u : z + run + 1u;
+  return z == 0u ? 1u : zac;
 }
 
 // Accumulators of one subsequence decode.
@@ -354,26 +385,21 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
       bw_seek(b, pos);
     }
     if (pos >= a0) break;
+    // state-only step, straight-line apart from the long-code lookup and the
+    // refill (with 64 lanes in different places of their blocks, a branch per
+    // case would run every case every step)
     const uint32_t bits = bw_peek(b, pos);
-    const bool isdc = (z == 0);
-    const uint32_t e = huff_lookup(*(isdc ? tdc : tac), bits);
-    const uint32_t len = e >> 8, sym = e & 0xFFu;
-    const uint32_t size = sym & 15u;
-    pos += len + size;
+    const uint32_t e = huff_decode(*(z == 0u ? tdc : tac), bits);
+    const uint32_t sym = e & 0xFFu;
+    pos += (e >> 8) + (sym & 15u);
     bw_shift(b, pos);
-    if (isdc) {
-      z = 1;
-    } else {
-      const uint32_t run = sym >> 4;
-      z = (size == 0 && run != 15u) ? 64u : z + run + 1u;
-    }
-    if (z >= 64) {
-      z = 0;
-      r = (r + 1 == bpm) ? 0 : r + 1;
-      comp = (cbits >> (2 * r)) & 3u;
-      tdc = &tabs[(slotmap >> ((comp << 1) << 2)) & 15u];
-      tac = &tabs[(slotmap >> (((comp << 1) | 1u) << 2)) & 15u];
-    }
+    const uint32_t zn = huff_next_z(z, sym);
+    const bool bend = zn >= 64u;
+    z = bend ? 0u : zn;
+    r = bend ? (r + 1u == bpm ? 0u : r + 1u) : r;
+    comp = (cbits >> (2u * r)) & 3u;
+    tdc = &tabs[(slotmap >> ((comp << 1) << 2)) & 15u];
+    tac = &tabs[(slotmap >> (((comp << 1) | 1u) << 2)) & 15u];
   }
   const uint32_t rel = pos - a0;
   return pack_state(rel > 255 ? 255 : rel, r, z);
@@ -500,25 +526,34 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       if (pos >= a1) break;
       ev = next_event();
     }
+    // One symbol.  Straight-line apart from the long-code lookup, the refill
+    // and the write pass's rare partial flush: the 64 lanes of a wave sit at
+    // different places of their blocks, so a branch per case (DC / AC / block
+    // end) would run every case in every step anyway, plus the exec-mask
+    // bookkeeping.
     const uint32_t bits = bw_peek(b, pos);
     const bool isdc = (z == 0);
-    const uint32_t e = huff_lookup(*(isdc ? tdc : tac), bits);
+    const uint32_t e = huff_decode(*(isdc ? tdc : tac), bits);
     const uint32_t len = e >> 8, sym = e & 0xFFu;
     const uint32_t size = sym & 15u;
     const uint32_t run = isdc ? 0u : (sym >> 4);
-    int32_t v = 0;
-    if (size) v = huff_extend((int32_t)((bits << len) >> (32 - size)), (int32_t)size);
+    const int32_t v = huff_value(bits, len, size);
     pos += len + size;
     bw_shift(b, pos);
-    if (isdc) {
-      acc.n++;
-      add3(acc.dc, comp, v);
-      if (stage) {
+    const int32_t vdc = isdc ? v : 0;
+    acc.n += isdc ? 1u : 0u;
+    add3(acc.dc, comp, vdc);
+    if (stage) {
+      if (isdc) {
         stg->started++;
         if (v) stage_push(*stg, stage_coef(0, stg->started, v));
+      } else if (size && z + run < 64) {
+        stage_push(*stg, stage_coef(z + run, stg->started, v));
       }
-      if (WRITE) {
-        add3(w->pred, comp, v);
+    }
+    if (WRITE) {
+      add3(w->pred, comp, vdc);
+      if (isdc) {
         if (COOP) {
           w->cur = wc_index(*w, w->nin);
           w->zs = 0;
@@ -526,25 +561,17 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
           wc_begin(*w, wc_index(*w, w->nin), 0);
         }
         w->nin++;
-        w->blk[0] = (int16_t)sel3(w->pred, comp);
       }
-      z = 1;
-    } else {
-      const bool eob = (size == 0) && (run != 15u);
-      if (WRITE && size) {
-        uint32_t zz = z + run;
-        if (zz < 64) w->blk[zz] = (int16_t)v;
-      }
-      if (stage && size && z + run < 64) stage_push(*stg, stage_coef(z + run, stg->started, v));
-      z = eob ? 64u : z + run + 1u;
+      const uint32_t zz = z + run;
+      if (isdc || (size && zz < 64u)) w->blk[zz] = (int16_t)(isdc ? sel3(w->pred, comp) : v);
     }
-    if (z >= 64) {
-      if (WRITE) wc_end_block<COOP>(*w, pending);
-      z = 0;
-      r = (r + 1 == bpm) ? 0 : r + 1;
-      comp = (cbits >> (2 * r)) & 3u;
-      block_tables(tdc, tac);
-    }
+    const uint32_t zn = huff_next_z(z, sym);
+    const bool bend = zn >= 64u;
+    if (WRITE && bend) wc_end_block<COOP>(*w, pending);
+    z = bend ? 0u : zn;
+    r = bend ? (r + 1u == bpm ? 0u : r + 1u) : r;
+    comp = (cbits >> (2u * r)) & 3u;
+    block_tables(tdc, tac);
   }
   if (WRITE && z > 0) wc_partial<COOP>(*w, z);
   if (stage) stage_finish(*stg);

@@ -27,10 +27,36 @@
  * decoded pixel values of the reference are UNPINNED; this oracle is instead
  * pinned bit-exactly against PIL/libjpeg-turbo 3.1 (tests/test_oracle_jpeg.py
  * and the committed fixtures in tests/golden/).
+ *
+ * Decode semantics switch (oj_set_semantics, SURVEY Appendix B: "encode each
+ * behind a single switch"): OJ_SEM_LIBJPEG (default, above, pinned) or
+ * OJ_SEM_ZUNE, a restatement of zune-jpeg 0.5.12's pixel stages as published
+ * in its source (recalled; the crate is not vendored, so this mode is
+ * PARITY UNPINNED):
+ *   - IDCT `idct_int` (zune-jpeg src/idct/scalar.rs; its AVX2 twin is
+ *     lane-for-lane the same): stb_image's integer IDCT, 12-bit constants,
+ *     pass 1 (x + 512) >> 10, pass 2 (x + 65536 + (128 << 17)) >> 17, clamped
+ *     to 0..255,
+ *   - upsampling (src/upsampler/scalar.rs) over the MCU-padded component
+ *     rows: horizontal (3*a + b + 2) >> 2 on both output phases, first output
+ *     = in[0], last pair from in[n-2], in[n-1]; vertical (h2v2) first
+ *     (3*cur + near + 2) >> 2 then horizontal on each output row; the row
+ *     above the first / below the last padded row is the row itself,
+ *   - YCbCr->RGB (src/color_convert/scalar.rs): r = y + (45*cr' >> 5),
+ *     g = y - ((11*cb' + 23*cr') >> 5), b = y + (113*cb' >> 6) with
+ *     cb' = cb - 128, cr' = cr - 128, clamped.
+ * Entropy decoding and dequantisation are format-defined and identical in
+ * both modes.
  */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+#define OJ_SEM_LIBJPEG 0
+#define OJ_SEM_ZUNE 1
+static int g_sem = OJ_SEM_LIBJPEG;
+void oj_set_semantics(int s) { g_sem = s == OJ_SEM_ZUNE ? OJ_SEM_ZUNE : OJ_SEM_LIBJPEG; }
+int oj_get_semantics(void) { return g_sem; }
 
 #define OJ_OK 0
 #define OJ_UNSUPPORTED 1
@@ -647,6 +673,87 @@ static void idct_islow(const int16_t *in, const uint16_t *q, uint8_t *out, int s
   }
 }
 
+/* zune-jpeg idct_int (stb_image lineage): dequantise, columns then rows */
+static void idct_zune(const int16_t *in, const uint16_t *q, uint8_t *out, int stride) {
+  int32_t v[64], ws[64];
+  for (int i = 0; i < 64; i++) v[i] = (int32_t)in[i] * (int32_t)q[i];
+  for (int pass = 0; pass < 2; pass++) {
+    const int32_t *s = pass ? ws : v;
+    for (int u = 0; u < 8; u++) {
+      /* pass 0: column u (stride 8); pass 1: row u (stride 1) */
+      const int o = pass ? u * 8 : u, st = pass ? 1 : 8;
+      int32_t p2 = s[o + 2 * st], p3 = s[o + 6 * st];
+      int32_t p1 = (p2 + p3) * 2217;
+      int32_t t2 = p1 + p3 * -7567, t3 = p1 + p2 * 3135;
+      p2 = s[o]; p3 = s[o + 4 * st];
+      int32_t t0 = (int32_t)((uint32_t)(p2 + p3) << 12), t1 = (int32_t)((uint32_t)(p2 - p3) << 12);
+      int32_t x0 = t0 + t3, x3 = t0 - t3, x1 = t1 + t2, x2 = t1 - t2;
+      t0 = s[o + 7 * st]; t1 = s[o + 5 * st]; t2 = s[o + 3 * st]; t3 = s[o + st];
+      p3 = t0 + t2; int32_t p4 = t1 + t3; p1 = t0 + t3; p2 = t1 + t2;
+      int32_t p5 = (p3 + p4) * 4816;
+      t0 *= 1223; t1 *= 8410; t2 *= 12586; t3 *= 6149;
+      p1 = p5 + p1 * -3685; p2 = p5 + p2 * -10497; p3 = p3 * -8034; p4 = p4 * -1597;
+      t3 += p1 + p4; t2 += p2 + p3; t1 += p2 + p4; t0 += p1 + p3;
+      const int32_t bias = pass ? 65536 + (128 << 17) : 512, sh = pass ? 17 : 10;
+      x0 += bias; x1 += bias; x2 += bias; x3 += bias;
+      const int32_t r[8] = {(x0 + t3) >> sh, (x1 + t2) >> sh, (x2 + t1) >> sh, (x3 + t0) >> sh,
+                            (x3 - t0) >> sh, (x2 - t1) >> sh, (x1 - t2) >> sh, (x0 - t3) >> sh};
+      for (int k = 0; k < 8; k++) {
+        if (pass) {
+          const int32_t y = r[k];
+          out[u * stride + k] = (uint8_t)(y < 0 ? 0 : y > 255 ? 255 : y);
+        } else {
+          ws[k * 8 + u] = r[k];
+        }
+      }
+    }
+  }
+}
+
+/* zune-jpeg upsample_horizontal over a whole padded row of n >= 2 samples */
+static void zune_up_h(const int32_t *in, int n, int32_t *out) {
+  out[0] = in[0];
+  out[1] = (in[0] * 3 + in[1] + 2) >> 2;
+  for (int i = 1; i + 1 < n; i++) {
+    const int32_t s = 3 * in[i] + 2;
+    out[2 * i] = (s + in[i - 1]) >> 2;
+    out[2 * i + 1] = (s + in[i + 1]) >> 2;
+  }
+  out[2 * n - 2] = (3 * in[n - 2] + in[n - 1] + 2) >> 2;
+  out[2 * n - 1] = in[n - 1];
+}
+
+/* Upsample component k to full resolution row y, columns [0, W), zune-jpeg style */
+static void upsample_row_zune(const oj_jpeg *j, const oj_comp *k, int y, uint8_t *dst) {
+  const int hr = j->hmax / k->h, vr = j->vmax / k->v;
+  const int pw = k->bw * 8, ph = k->bh * 8;
+  const uint8_t *pl = k->plane;
+  if (hr == 1 && vr == 1) {
+    memcpy(dst, pl + (size_t)y * pw, (size_t)j->W);
+    return;
+  }
+  if (pw < 2) return; /* padded rows are >= 8 samples */
+  int32_t *row = (int32_t *)malloc(sizeof(int32_t) * (size_t)pw * 3);
+  int32_t *up = row + pw;
+  if (vr == 1) {
+    for (int x = 0; x < pw; x++) row[x] = pl[(size_t)y * pw + x];
+  } else { /* h2v2: vertical first */
+    const int r = y >> 1;
+    const int rn = (y & 1) ? (r + 1 < ph ? r + 1 : r) : (r > 0 ? r - 1 : 0);
+    for (int x = 0; x < pw; x++)
+      row[x] = (3 * pl[(size_t)r * pw + x] + 2 + pl[(size_t)rn * pw + x]) >> 2;
+  }
+  if (pw >= 2) {
+    zune_up_h(row, pw, up);
+  } else {
+    up[0] = up[1] = row[0];
+  }
+  for (int x = 0; x < j->W; x++) dst[x] = (uint8_t)up[x];
+  free(row);
+}
+
+static inline uint8_t clamp_i(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
 /* -------------------------------------------------- upsample + colour */
 
 static int32_t Crr[256], Cbb[256], Crg[256], Cbg[256];
@@ -810,8 +917,8 @@ int oj_decode(const uint8_t *d, size_t n, uint8_t *out, size_t cap, int *w, int 
     oj_comp *k = &j.comp[c];
     for (int by = 0; by < k->bh; by++)
       for (int bx = 0; bx < k->bw; bx++)
-        idct_islow(k->coef + ((size_t)by * k->bw + bx) * 64, j.q[k->tq],
-                   k->plane + (size_t)by * 8 * k->bw * 8 + bx * 8, k->bw * 8);
+        (g_sem == OJ_SEM_ZUNE ? idct_zune : idct_islow)(k->coef + ((size_t)by * k->bw + bx) * 64, j.q[k->tq],
+                                                         k->plane + (size_t)by * 8 * k->bw * 8 + bx * 8, k->bw * 8);
   }
   if (j.ncomp == 1) {
     for (int y = 0; y < j.H; y++) memcpy(out + (size_t)y * j.W, j.comp[0].plane + (size_t)y * j.comp[0].bw * 8, (size_t)j.W);
@@ -825,14 +932,21 @@ int oj_decode(const uint8_t *d, size_t n, uint8_t *out, size_t cap, int *w, int 
   else if (j.comp[0].id == 82 && j.comp[1].id == 71 && j.comp[2].id == 66) rgb = 1;
   uint8_t *r0 = (uint8_t *)malloc((size_t)j.W * 3);
   for (int y = 0; y < j.H; y++) {
-    upsample_row(&j, &j.comp[0], y, r0);
-    upsample_row(&j, &j.comp[1], y, r0 + j.W);
-    upsample_row(&j, &j.comp[2], y, r0 + 2 * j.W);
+    void (*up)(const oj_jpeg *, const oj_comp *, int, uint8_t *) =
+        g_sem == OJ_SEM_ZUNE ? upsample_row_zune : upsample_row;
+    up(&j, &j.comp[0], y, r0);
+    up(&j, &j.comp[1], y, r0 + j.W);
+    up(&j, &j.comp[2], y, r0 + 2 * j.W);
     uint8_t *o = out + (size_t)y * j.W * 3;
     for (int x = 0; x < j.W; x++) {
       int Y = r0[x], cb = r0[j.W + x], cr = r0[2 * j.W + x];
       if (rgb) {
         o[3 * x] = (uint8_t)Y; o[3 * x + 1] = (uint8_t)cb; o[3 * x + 2] = (uint8_t)cr;
+      } else if (g_sem == OJ_SEM_ZUNE) {
+        const int cbp = cb - 128, crp = cr - 128;
+        o[3 * x] = clamp_i(Y + ((45 * crp) >> 5));
+        o[3 * x + 1] = clamp_i(Y - ((11 * cbp + 23 * crp) >> 5));
+        o[3 * x + 2] = clamp_i(Y + ((113 * cbp) >> 6));
       } else {
         o[3 * x] = clamp255(Y + Crr[cr]);
         o[3 * x + 1] = clamp255(Y + ((Cbg[cb] + Crg[cr]) >> 16));

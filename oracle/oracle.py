@@ -17,6 +17,9 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 OJ_OK, OJ_UNSUPPORTED, OJ_CORRUPT, OJ_SMALLBUF = 0, 1, 2, 3
 MODE_FIR, MODE_PILLOW = 0, 1
+# JPEG decode semantics (jpeg_oracle.c oj_set_semantics): libjpeg-turbo (pinned
+# against PIL) or zune-jpeg 0.5.12 restated (the reference's decoder; unpinned)
+SEM_LIBJPEG, SEM_ZUNE = 0, 1
 
 _lib = None
 
@@ -35,6 +38,7 @@ def lib() -> ctypes.CDLL:
         u8p = ctypes.POINTER(ctypes.c_uint8)
         ip = ctypes.POINTER(ctypes.c_int)
         L.oj_info.argtypes = [u8p, ctypes.c_size_t, ip, ip, ip]
+        L.oj_set_semantics.argtypes = [ctypes.c_int]
         L.oj_decode.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, ip, ip, ip]
         L.oj_decode_coefs.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int16),
                                       ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
@@ -48,6 +52,26 @@ def lib() -> ctypes.CDLL:
         L.or_fit_crop.argtypes = [ctypes.c_int] * 4 + [dp] * 4
         _lib = L
     return _lib
+
+
+def set_semantics(mode: int) -> None:
+    """JPEG decode semantics of every later jpeg_decode call (process-wide)."""
+    lib().oj_set_semantics(mode)
+
+
+class semantics:
+    """with semantics(SEM_ZUNE): ... -- restores libjpeg-turbo mode on exit."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        set_semantics(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        set_semantics(SEM_LIBJPEG)
+        return False
 
 
 def _u8(buf) -> ctypes.POINTER(ctypes.c_uint8):
