@@ -30,12 +30,17 @@ DG_HD uint32_t bswap32(uint32_t x) {
 // 64-bit window over a big-endian bit stream stored as bytes (the stream base
 // is 4-byte aligned and zero-padded by >= 16 bytes past its end).
 //
-// Refills are software-pipelined: the window keeps the next word raw (not
-// yet byte-swapped) and a shift loads the one after it without using it, so
-// the load's latency is covered by at least one symbol's worth of work
-// instead of stalling the whole wave in the lanes' divergent refills.  One
-// symbol consumes at most 31 bits, so with pos - base < 32 before a symbol at
-// most one 32-bit shift follows it.
+// Refills are batched per wave.  Behind the window each lane keeps a buffer
+// of kBwBuf raw (not yet byte-swapped) words; a shift takes the next one from
+// it.  When any lane of a wave has emptied its buffer, every active lane
+// reloads its whole buffer at once (bw_refill): one load latency per wave
+// every ~kBwBuf words of its fastest lane.  Per-lane refills -- one word
+// ahead, issued whenever a lane crossed a word -- stalled the wave on nearly
+// every symbol: a wave has one in-order load counter, so the wait for the
+// word a lane loaded symbols ago also waited for the loads other lanes had
+// issued since.  One symbol consumes at most 31 bits, so with pos - base < 32
+// before a symbol at most one 32-bit shift follows it, and a lane with a
+// non-empty buffer at the start of a step never runs dry within it.
 // Destuffed streams are stored word-interleaved across groups of 64
 // subsequences: logical 32-bit word w of subsequence s = w >> lsw (2^lsw
 // words per subsequence) sits in row (s / 64) * 2^lsw + (w mod 2^lsw),
@@ -56,15 +61,26 @@ DG_HD uint64_t ds_words_alloc(uint32_t nsub, uint32_t lsw) {
   return ((uint64_t)((nsub + margin + 63u) / 64u) << lsw) * 64;
 }
 
+constexpr uint32_t kBwBuf = 6;
+
 struct BitWin {
   const DG_GLOBAL uint32_t *w;  // interleaved stream as little-endian words (byte-swapped on use)
   uint64_t win;       // bits [base, base + 64)
   uint32_t base;      // bit position of win's MSB (multiple of 32)
-  uint32_t nraw;      // raw word base/32 + 2
   uint32_t lsw;       // log2(words per subsequence)
+  uint32_t nbuf;      // valid words in buf
+  uint32_t buf[kBwBuf];  // raw words base/32 + 2 ..
 };
 
 DG_HD uint32_t bw_word(const BitWin &b, uint32_t i) { return b.w[ds_word_index(i, b.lsw)]; }
+
+// buf = the kBwBuf words after the window
+DG_HD void bw_fill(BitWin &b) {
+  const uint32_t nw = (b.base >> 5) + 2u;
+#pragma unroll
+  for (uint32_t k = 0; k < kBwBuf; k++) b.buf[k] = bw_word(b, nw + k);
+  b.nbuf = kBwBuf;
+}
 
 DG_HD void bw_init(BitWin &b, const DG_GLOBAL uint8_t *stream, uint32_t lsw, uint32_t pos) {
   b.w = (const DG_GLOBAL uint32_t *)stream;
@@ -72,19 +88,30 @@ DG_HD void bw_init(BitWin &b, const DG_GLOBAL uint8_t *stream, uint32_t lsw, uin
   uint32_t i = pos >> 5;
   b.base = i << 5;
   b.win = ((uint64_t)bswap32(bw_word(b, i)) << 32) | bswap32(bw_word(b, i + 1));
-  b.nraw = bw_word(b, i + 2);
+  bw_fill(b);
+}
+
+// start of a symbol step: no lane may enter it with an empty buffer
+DG_HD void bw_refill(BitWin &b) {
+#if defined(DG_DEVICE)
+  if (__ballot(b.nbuf == 0u)) bw_fill(b);  // wave-uniform: every active lane reloads together
+#else
+  if (b.nbuf == 0u) bw_fill(b);
+#endif
 }
 
 // 32 bits starting at pos (requires base <= pos < base + 32).
 DG_HD uint32_t bw_peek(const BitWin &b, uint32_t pos) { return (uint32_t)((b.win << (pos - b.base)) >> 32); }
 
 // after a symbol: base <= pos < base + 64 -> base <= pos < base + 32
+// (straight-line: the shift is a select, the buffer moves down one word)
 DG_HD void bw_shift(BitWin &b, uint32_t pos) {
-  if (pos - b.base >= 32) {
-    b.win = (b.win << 32) | bswap32(b.nraw);
-    b.base += 32;
-    b.nraw = bw_word(b, (b.base >> 5) + 2);
-  }
+  const bool adv = pos - b.base >= 32u;
+  b.win = adv ? (b.win << 32) | bswap32(b.buf[0]) : b.win;
+  b.base += adv ? 32u : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k + 1 < kBwBuf; k++) b.buf[k] = adv ? b.buf[k + 1] : b.buf[k];
+  b.nbuf -= adv ? 1u : 0u;
 }
 
 DG_HD void bw_seek(BitWin &b, uint32_t pos) {
@@ -385,6 +412,7 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
       bw_seek(b, pos);
     }
     if (pos >= a0) break;
+    bw_refill(b);
     // state-only step, straight-line apart from the long-code lookup and the
     // refill (with 64 lanes in different places of their blocks, a branch per
     // case would run every case every step)
@@ -531,6 +559,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
     // different places of their blocks, so a branch per case (DC / AC / block
     // end) would run every case in every step anyway, plus the exec-mask
     // bookkeeping.
+    bw_refill(b);
     const uint32_t bits = bw_peek(b, pos);
     const bool isdc = (z == 0);
     const uint32_t e = huff_decode(*(isdc ? tdc : tac), bits);

@@ -72,6 +72,53 @@ DG_HD uint8_t idct_out(int32_t x) {
   return (uint8_t)(x + 128);
 }
 
+// ------------------------------------------- zune-jpeg decode semantics
+// Option "decode_semantics" = 1 (ImageDesc::sem): the pixel stages of the
+// reference's own decoder, zune-jpeg 0.5.12, as oracle/jpeg_oracle.c
+// restates them (OJ_SEM_ZUNE; unpinned -- the crate is not vendored).
+// IDCT `idct_int`: stb_image's factorisation with 12-bit constants; o[k] are
+// the pre-bias sums, pass 1 takes (o + 512) >> 10, pass 2
+// (o + 65536 + (128 << 17)) >> 17 clamped to 0..255.
+DG_HD void idct_1d_stb(const int32_t s0, const int32_t s1, const int32_t s2, const int32_t s3,
+                       const int32_t s4, const int32_t s5, const int32_t s6, const int32_t s7, int32_t o[8]) {
+  int32_t p2 = s2, p3 = s6;
+  int32_t p1 = (p2 + p3) * 2217;
+  const int32_t u2 = p1 + p3 * -7567, u3 = p1 + p2 * 3135;
+  const int32_t t0e = (int32_t)((uint32_t)(s0 + s4) << 12), t1e = (int32_t)((uint32_t)(s0 - s4) << 12);
+  const int32_t x0 = t0e + u3, x3 = t0e - u3, x1 = t1e + u2, x2 = t1e - u2;
+  int32_t t0 = s7, t1 = s5, t2 = s3, t3 = s1;
+  p3 = t0 + t2;
+  int32_t p4 = t1 + t3;
+  p1 = t0 + t3;
+  p2 = t1 + t2;
+  const int32_t p5 = (p3 + p4) * 4816;
+  t0 *= 1223;
+  t1 *= 8410;
+  t2 *= 12586;
+  t3 *= 6149;
+  p1 = p5 + p1 * -3685;
+  p2 = p5 + p2 * -10497;
+  p3 = p3 * -8034;
+  p4 = p4 * -1597;
+  t3 += p1 + p4;
+  t2 += p2 + p3;
+  t1 += p2 + p4;
+  t0 += p1 + p3;
+  o[0] = x0 + t3;
+  o[7] = x0 - t3;
+  o[1] = x1 + t2;
+  o[6] = x1 - t2;
+  o[2] = x2 + t1;
+  o[5] = x2 - t1;
+  o[3] = x3 + t0;
+  o[4] = x3 - t0;
+}
+DG_HD int32_t idct_stb_pass1(int32_t o) { return (o + 512) >> 10; }
+DG_HD uint8_t idct_stb_out(int32_t o) {
+  const int32_t v = (o + 65536 + (128 << 17)) >> 17;
+  return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
 // zigzag index -> natural index
 #if defined(DG_DEVICE)
 __constant__
@@ -105,6 +152,14 @@ DG_HD void ycc_to_rgb(int32_t y, int32_t cb, int32_t cr, uint8_t &r, uint8_t &g,
   r = clamp255(y + crr);
   g = clamp255(y + g_);
   b = clamp255(y + cbb);
+}
+
+// zune-jpeg ycbcr_to_rgb (color_convert/scalar.rs): 5- and 6-bit constants
+DG_HD void ycc_to_rgb_zune(int32_t y, int32_t cb, int32_t cr, uint8_t &r, uint8_t &g, uint8_t &b) {
+  const int32_t xcb = cb - 128, xcr = cr - 128;
+  r = clamp255(y + ((45 * xcr) >> 5));
+  g = clamp255(y - ((11 * xcb + 23 * xcr) >> 5));
+  b = clamp255(y + ((113 * xcb) >> 6));
 }
 
 // ----------------------------------------------------------- upsampling

@@ -274,7 +274,7 @@ struct ImageDesc {
   uint16_t hslot[kMaxSlots];  // pool index of Huffman slot s
   uint8_t ncomp, colorspace, dec_c, nslots;  // dec_c: channels of the decoded image
   uint16_t qpool[3];
-  uint16_t pad1;
+  uint16_t sem;             // decode semantics: 0 libjpeg-turbo, 1 zune-jpeg (option "decode_semantics")
   uint64_t coef;            // device address of block 0 (int16 zigzag[64] per block, decode order)
   uint64_t stage;           // decode-once staging (dg_entropy.h StageCtx), 0 = off
   // ---- geometry

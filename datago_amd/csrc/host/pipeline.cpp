@@ -207,6 +207,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     hb_bands_ = (uint32_t)v;
     return DG_OK;
   }
+  if (k == "decode_semantics") {  // 0: libjpeg-turbo (pinned), 1: zune-jpeg 0.5.12 restated (unpinned)
+    if (v != 0 && v != 1) return DG_ERR_INVALID;
+    decode_sem_ = (int)v;
+    return DG_OK;
+  }
   if (k == "hb_occ") {  // band H kernels: register budget for 4 or 5 waves per SIMD
     if (v != 4 && v != 5) return DG_ERR_INVALID;
     hb_occ_ = (int)v;
@@ -693,6 +698,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     d.height = H;
     d.ncomp = (uint8_t)h.ncomp;
     d.colorspace = (uint8_t)h.colorspace;
+    d.sem = (uint16_t)decode_sem_;
     d.dec_c = h.ncomp == 1 ? 1 : 3;
     d.hmax = (uint32_t)h.hmax;
     d.vmax = (uint32_t)h.vmax;

@@ -598,6 +598,18 @@ __global__ __launch_bounds__(256) void k_huff_scatter(const ImageDesc *__restric
 
 // ------------------------------------------------------------ IDCT
 
+// Pack the low bytes of four values into one dword with explicit v_perm byte
+// selects.  Plain shift/or packing of clamped values lets hipcc (ROCm 7.2,
+// gfx950) fuse pairs into v_ashr_pk_u8_i32 and then OR the next byte into
+// bits 16..23 of that register, whose upper half still holds the old
+// accumulator bits: byte 2 of every 4 came out corrupted.  v_perm only takes
+// the selected bytes.
+__device__ __forceinline__ uint32_t pack4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+  const uint32_t lo = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u);  // [b0, b1, 0, 0]
+  const uint32_t hi = __builtin_amdgcn_perm(b3, b2, 0x0c0c0400u);  // [b2, b3, 0, 0]
+  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);               // [b0, b1, b2, b3]
+}
+
 // One workgroup = kIdctBlocks consecutive blocks of one block row of one
 // component; 8 lanes per block, each lane owning two blocks (slot, slot + 32)
 // so two independent 16-byte coefficient loads are in flight per lane and
@@ -660,18 +672,28 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
   }
   __syncthreads();
   int32_t o0[8], o1[8];
+  const bool zune = im.sem != 0;  // decode semantics (uniform per workgroup)
   // pass 1: column `lane`, dequantised on the way in
-  idct_1d(bv0[0 * RS + lane] * qc[0], bv0[1 * RS + lane] * qc[1], bv0[2 * RS + lane] * qc[2],
-          bv0[3 * RS + lane] * qc[3], bv0[4 * RS + lane] * qc[4], bv0[5 * RS + lane] * qc[5],
-          bv0[6 * RS + lane] * qc[6], bv0[7 * RS + lane] * qc[7], o0);
-  idct_1d(bv1[0 * RS + lane] * qc[0], bv1[1 * RS + lane] * qc[1], bv1[2 * RS + lane] * qc[2],
-          bv1[3 * RS + lane] * qc[3], bv1[4 * RS + lane] * qc[4], bv1[5 * RS + lane] * qc[5],
-          bv1[6 * RS + lane] * qc[6], bv1[7 * RS + lane] * qc[7], o1);
+  if (zune) {
+    idct_1d_stb(bv0[0 * RS + lane] * qc[0], bv0[1 * RS + lane] * qc[1], bv0[2 * RS + lane] * qc[2],
+                bv0[3 * RS + lane] * qc[3], bv0[4 * RS + lane] * qc[4], bv0[5 * RS + lane] * qc[5],
+                bv0[6 * RS + lane] * qc[6], bv0[7 * RS + lane] * qc[7], o0);
+    idct_1d_stb(bv1[0 * RS + lane] * qc[0], bv1[1 * RS + lane] * qc[1], bv1[2 * RS + lane] * qc[2],
+                bv1[3 * RS + lane] * qc[3], bv1[4 * RS + lane] * qc[4], bv1[5 * RS + lane] * qc[5],
+                bv1[6 * RS + lane] * qc[6], bv1[7 * RS + lane] * qc[7], o1);
+  } else {
+    idct_1d(bv0[0 * RS + lane] * qc[0], bv0[1 * RS + lane] * qc[1], bv0[2 * RS + lane] * qc[2],
+            bv0[3 * RS + lane] * qc[3], bv0[4 * RS + lane] * qc[4], bv0[5 * RS + lane] * qc[5],
+            bv0[6 * RS + lane] * qc[6], bv0[7 * RS + lane] * qc[7], o0);
+    idct_1d(bv1[0 * RS + lane] * qc[0], bv1[1 * RS + lane] * qc[1], bv1[2 * RS + lane] * qc[2],
+            bv1[3 * RS + lane] * qc[3], bv1[4 * RS + lane] * qc[4], bv1[5 * RS + lane] * qc[5],
+            bv1[6 * RS + lane] * qc[6], bv1[7 * RS + lane] * qc[7], o1);
+  }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 8; r++) {
-    bv0[r * RS + lane] = descale(o0[r], kConstBits - kPass1Bits);
-    bv1[r * RS + lane] = descale(o1[r], kConstBits - kPass1Bits);
+    bv0[r * RS + lane] = zune ? idct_stb_pass1(o0[r]) : descale(o0[r], kConstBits - kPass1Bits);
+    bv1[r * RS + lane] = zune ? idct_stb_pass1(o1[r]) : descale(o1[r], kConstBits - kPass1Bits);
   }
   __syncthreads();
   // pass 2: row `lane`
@@ -682,12 +704,20 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
     const int32_t *w = (h ? bv1 : bv0) + lane * RS;
     const bool v = h ? v1 : v0;
     int32_t o[8];
-    idct_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
     uint32_t lo = 0, hi = 0;
+    if (zune) {
+      idct_1d_stb(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+      // pack4, not shifts: shift/or packing of clamped values lets hipcc form
+      // v_ashr_pk_u8_i32 and OR the next byte into its stale upper half (pack4)
+      lo = pack4(idct_stb_out(o[0]), idct_stb_out(o[1]), idct_stb_out(o[2]), idct_stb_out(o[3]));
+      hi = pack4(idct_stb_out(o[4]), idct_stb_out(o[5]), idct_stb_out(o[6]), idct_stb_out(o[7]));
+    } else {
+      idct_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      lo |= (uint32_t)idct_out(o[i]) << (8 * i);
-      hi |= (uint32_t)idct_out(o[i + 4]) << (8 * i);
+      for (int i = 0; i < 4; i++) {
+        lo |= (uint32_t)idct_out(o[i]) << (8 * i);
+        hi |= (uint32_t)idct_out(o[i + 4]) << (8 * i);
+      }
     }
     if (v) *(DG_GLOBAL u32x2 *)(plane + (size_t)(h ? bx1 : bx0) * 8) = u32x2{lo, hi};
   }
@@ -793,6 +823,93 @@ __device__ __forceinline__ void upsample8(P pl, uint32_t stride, uint32_t hr, ui
   }
 }
 
+// zune-jpeg upsampling (option "decode_semantics" = 1; oracle upsample_row_zune):
+// over the MCU-padded rows (n = stride samples, ph padded rows), h2v2 first
+// vertically (3 * near + far + 2) >> 2 with the row itself past either end,
+// then horizontally (3 * a + b + 2) >> 2 on both phases; out[0] = in[0],
+// the last pair is ((3 * in[n-2] + in[n-1] + 2) >> 2, in[n-1]).
+template <class P>
+__device__ __forceinline__ void upsample8_zune(P pl, uint32_t stride, uint32_t hr, uint32_t vr, uint32_t ph,
+                                               uint32_t x0, uint32_t y, int32_t o[8]) {
+  if (hr == 1) {
+    u32x2 v = *(const DG_GLOBAL u32x2 *)(pl + (size_t)__umul24(y, stride) + x0);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      o[k] = (v.x >> (8 * k)) & 0xFF;
+      o[k + 4] = (v.y >> (8 * k)) & 0xFF;
+    }
+    return;
+  }
+  const uint32_t n = stride, c0 = x0 >> 1;  // c0 + 3 <= n - 1 (x0 + 8 <= 2n)
+  const uint32_t cl = c0 > 0 ? c0 - 1 : 0, cr = c0 + 4 < n ? c0 + 4 : n - 1;
+  int32_t cs[6];  // (vertically upsampled) samples at columns c0-1 .. c0+4, clamped
+  if (vr == 1) {
+    P in = pl + (size_t)__umul24(y, stride);
+    const uint32_t v = *(const DG_GLOBAL uint32_t *)(in + c0);
+    cs[0] = in[cl];
+#pragma unroll
+    for (int k = 0; k < 4; k++) cs[k + 1] = (v >> (8 * k)) & 0xFF;
+    cs[5] = in[cr];
+  } else {
+    const uint32_t r = y >> 1;
+    const uint32_t rn = (y & 1) ? (r + 1 < ph ? r + 1 : r) : (r > 0 ? r - 1 : 0);
+    P i0 = pl + (size_t)__umul24(r, stride);
+    P i1 = pl + (size_t)__umul24(rn, stride);
+    const uint32_t v0 = *(const DG_GLOBAL uint32_t *)(i0 + c0), v1 = *(const DG_GLOBAL uint32_t *)(i1 + c0);
+    cs[0] = (3 * (int32_t)i0[cl] + 2 + (int32_t)i1[cl]) >> 2;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      cs[k + 1] = (3 * (int32_t)((v0 >> (8 * k)) & 0xFF) + 2 + (int32_t)((v1 >> (8 * k)) & 0xFF)) >> 2;
+    cs[5] = (3 * (int32_t)i0[cr] + 2 + (int32_t)i1[cr]) >> 2;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t i = c0 + (uint32_t)k;
+    const int32_t a = 3 * cs[k + 1] + 2;
+    int32_t ev = (a + cs[k]) >> 2, od = (a + cs[k + 2]) >> 2;
+    if (i == 0) ev = cs[1];
+    if (i + 1 == n) {
+      ev = (3 * cs[k] + cs[k + 1] + 2) >> 2;
+      od = cs[k + 1];
+    }
+    o[2 * k] = ev;
+    o[2 * k + 1] = od;
+  }
+}
+
+// the three components of 8 pixels at (x0.., y), upsampled per the image's decode semantics
+__device__ __forceinline__ void upsample_ycc8(const ImageDesc &im, uint32_t x0, uint32_t y, int32_t Y[8],
+                                             int32_t Cb[8], int32_t Cr[8]) {
+  if (im.sem) {
+    upsample8_zune(gp<const uint8_t>(im.plane[0]), im.cbw[0] * 8, im.hmax / im.ch[0], im.vmax / im.cv[0],
+                   im.cbh[0] * 8, x0, y, Y);
+    upsample8_zune(gp<const uint8_t>(im.plane[1]), im.cbw[1] * 8, im.hmax / im.ch[1], im.vmax / im.cv[1],
+                   im.cbh[1] * 8, x0, y, Cb);
+    upsample8_zune(gp<const uint8_t>(im.plane[2]), im.cbw[2] * 8, im.hmax / im.ch[2], im.vmax / im.cv[2],
+                   im.cbh[2] * 8, x0, y, Cr);
+    return;
+  }
+  upsample8(gp<const uint8_t>(im.plane[0]), im.cbw[0] * 8, im.hmax / im.ch[0], im.vmax / im.cv[0], im.cdsw[0],
+            im.cdsh[0], x0, y, Y);
+  upsample8(gp<const uint8_t>(im.plane[1]), im.cbw[1] * 8, im.hmax / im.ch[1], im.vmax / im.cv[1], im.cdsw[1],
+            im.cdsh[1], x0, y, Cb);
+  upsample8(gp<const uint8_t>(im.plane[2]), im.cbw[2] * 8, im.hmax / im.ch[2], im.vmax / im.cv[2], im.cdsw[2],
+            im.cdsh[2], x0, y, Cr);
+}
+
+__device__ __forceinline__ void ycc_px(const ImageDesc &im, int32_t y, int32_t cb, int32_t cr, uint8_t &r,
+                                       uint8_t &g, uint8_t &b) {
+  if (im.colorspace == CS_RGB) {
+    r = (uint8_t)y;
+    g = (uint8_t)cb;
+    b = (uint8_t)cr;
+  } else if (im.sem) {
+    ycc_to_rgb_zune(y, cb, cr, r, g, b);
+  } else {
+    ycc_to_rgb(y, cb, cr, r, g, b);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_color(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
@@ -801,23 +918,12 @@ __global__ __launch_bounds__(256) void k_color(const ImageDesc *__restrict__ img
   if (q >= ow * im.height) return;
   const uint32_t y = q / ow, x0 = (q - y * ow) * 8;
   int32_t Y[8], Cb[8], Cr[8];
-  upsample8(gp<const uint8_t>(im.plane[0]), im.cbw[0] * 8, im.hmax / im.ch[0], im.vmax / im.cv[0], im.cdsw[0],
-            im.cdsh[0], x0, y, Y);
-  upsample8(gp<const uint8_t>(im.plane[1]), im.cbw[1] * 8, im.hmax / im.ch[1], im.vmax / im.cv[1], im.cdsw[1],
-            im.cdsh[1], x0, y, Cb);
-  upsample8(gp<const uint8_t>(im.plane[2]), im.cbw[2] * 8, im.hmax / im.ch[2], im.vmax / im.cv[2], im.cdsw[2],
-            im.cdsh[2], x0, y, Cr);
+  upsample_ycc8(im, x0, y, Y, Cb, Cr);
   uint32_t w[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     uint8_t r, g, b;
-    if (im.colorspace == CS_RGB) {
-      r = (uint8_t)Y[k];
-      g = (uint8_t)Cb[k];
-      b = (uint8_t)Cr[k];
-    } else {
-      ycc_to_rgb(Y[k], Cb[k], Cr[k], r, g, b);
-    }
+    ycc_px(im, Y[k], Cb[k], Cr[k], r, g, b);
     const int o = 3 * k;
     w[o >> 2] |= (uint32_t)r << (8 * (o & 3));
     w[(o + 1) >> 2] |= (uint32_t)g << (8 * ((o + 1) & 3));
@@ -836,18 +942,6 @@ __global__ __launch_bounds__(256) void k_color(const ImageDesc *__restrict__ img
 }
 
 // ------------------------------------------------------------ resize
-
-// Pack the low bytes of four values into one dword with explicit v_perm byte
-// selects.  Plain shift/or packing of clamped values lets hipcc (ROCm 7.2,
-// gfx950) fuse pairs into v_ashr_pk_u8_i32 and then OR the next byte into
-// bits 16..23 of that register, whose upper half still holds the old
-// accumulator bits: byte 2 of every 4 came out corrupted.  v_perm only takes
-// the selected bytes.
-__device__ __forceinline__ uint32_t pack4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
-  const uint32_t lo = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u);  // [b0, b1, 0, 0]
-  const uint32_t hi = __builtin_amdgcn_perm(b3, b2, 0x0c0c0400u);  // [b2, b3, 0, 0]
-  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);               // [b0, b1, b2, b3]
-}
 
 __device__ __forceinline__ uint8_t clip_shift(int32_t acc, int32_t prec) {
   int32_t v = acc >> prec;
@@ -1027,23 +1121,12 @@ constexpr uint32_t kHSegStride = kHSegPx + 8;
 // job j of the fill: 8 source pixels from the planes, p0 % 8 == 0
 __device__ __forceinline__ void hfill_color8(const ImageDesc &im, uint32_t y, uint32_t x0, uint32_t *d) {
   int32_t Y[8], Cb[8], Cr[8];
-  upsample8(gp<const uint8_t>(im.plane[0]), im.cbw[0] * 8, im.hmax / im.ch[0], im.vmax / im.cv[0], im.cdsw[0],
-            im.cdsh[0], x0, y, Y);
-  upsample8(gp<const uint8_t>(im.plane[1]), im.cbw[1] * 8, im.hmax / im.ch[1], im.vmax / im.cv[1], im.cdsw[1],
-            im.cdsh[1], x0, y, Cb);
-  upsample8(gp<const uint8_t>(im.plane[2]), im.cbw[2] * 8, im.hmax / im.ch[2], im.vmax / im.cv[2], im.cdsw[2],
-            im.cdsh[2], x0, y, Cr);
+  upsample_ycc8(im, x0, y, Y, Cb, Cr);
   uint32_t v[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     uint8_t r, g, b;
-    if (im.colorspace == CS_RGB) {
-      r = (uint8_t)Y[k];
-      g = (uint8_t)Cb[k];
-      b = (uint8_t)Cr[k];
-    } else {
-      ycc_to_rgb(Y[k], Cb[k], Cr[k], r, g, b);
-    }
+    ycc_px(im, Y[k], Cb[k], Cr[k], r, g, b);
     v[k] = (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
   }
   u32x4 *d4 = (u32x4 *)d;

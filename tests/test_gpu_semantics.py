@@ -1,0 +1,87 @@
+"""Decode-semantics switch on the GPU (context option "decode_semantics").
+
+0 (default): libjpeg-turbo semantics, the oracle's pinned mode.
+1: zune-jpeg 0.5.12 -- the reference's own decoder (worker_files.rs:14-16 ->
+image 0.25.9 -> zune-jpeg) -- restated in the oracle's SEM_ZUNE mode from the
+crate's published source.  That restatement is PARITY UNPINNED (the crate is
+not vendored); what is pinned here is that the GPU's zune mode
+is bit-exact to it, so a toolchain that can run the crate can confirm or fix
+one restatement and both paths follow.  Widths/heights around the MCU padding
+exercise zune's edge handling (it reads the padded rows instead of
+replicating the last sample)."""
+import numpy as np
+import pytest
+
+from datago_amd import synth
+from oracle import buckets as B
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(64, 48), (65, 49), (63, 47), (62, 46), (16, 16), (17, 9), (1, 1), (2, 2), (3, 5), (130, 67), (333, 211),
+         (1000, 10), (10, 700)]
+
+
+def _corpus():
+    out = []
+    for i, (w, h) in enumerate(SIZES):
+        for j, ss in enumerate(["4:2:0", "4:2:2", "4:4:4"]):
+            out.append(synth.make_jpeg(7000 + 10 * i + j, w, h, [60, 85, 95][j], ss, gray=(i + j) % 5 == 4,
+                                       restart_marker_rows=1 if (i + j) % 4 == 1 else 0))
+    return out
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    return _corpus()
+
+
+def _ctx(sem, resize):
+    from datago_amd import _lib as L
+    kw = dict(crop_and_resize=True, default_image_size=512, downsampling_ratio=16, min_aspect_ratio=0.5,
+              max_aspect_ratio=2.0) if resize else {}
+    c = L.Context(0, **kw)
+    c.set_option("decode_semantics", sem)
+    return c
+
+
+def _oracle(d, sem):
+    with O.semantics(sem):
+        st, dec = O.jpeg_decode(d)
+    assert st == 0
+    return dec
+
+
+def test_zune_decode_bit_exact_vs_restatement(corpus):
+    res = _ctx(1, False).decode_batch(corpus)
+    for k, (d, (st, arr, meta)) in enumerate(zip(corpus, res)):
+        assert st == 0, k
+        ref = _oracle(d, O.SEM_ZUNE)
+        assert np.array_equal(arr, ref), (k, SIZES[k // 3])
+
+
+def test_zune_crop_resize_bit_exact_vs_restatement(corpus):
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    res = _ctx(1, True).decode_batch(corpus)
+    for k, (d, (st, arr, meta)) in enumerate(zip(corpus, res)):
+        assert st == 0, k
+        dec = _oracle(d, O.SEM_ZUNE)
+        ref = O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR)
+        assert np.array_equal(arr, ref), (k, SIZES[k // 3])
+
+
+def test_default_semantics_unchanged_and_modes_differ(corpus):
+    a = _ctx(0, False).decode_batch(corpus)
+    z = _ctx(1, False).decode_batch(corpus)
+    differ = 0
+    for d, (sa, xa, _), (sz, xz, _) in zip(corpus, a, z):
+        assert np.array_equal(xa, _oracle(d, O.SEM_LIBJPEG))
+        differ += int(not np.array_equal(xa, xz))
+    assert differ > len(corpus) // 2
+
+
+def test_option_validated():
+    from datago_amd import _lib as L
+    c = L.Context(0)
+    with pytest.raises(Exception):
+        c.set_option("decode_semantics", 2)
