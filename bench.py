@@ -79,10 +79,12 @@ def parse():
     ap.add_argument("--hb-bands", type=int, default=0, help="band H kernel: 8-row bands per workgroup (0 = default)")
     ap.add_argument("--decode-semantics", type=int, default=0,
                     help="JPEG pixel semantics: 0 libjpeg-turbo (pinned, default), 1 zune-jpeg 0.5.12 restated")
-    ap.add_argument("--hb-occ", type=int, default=0, help="band H kernels: 4 or 5 waves/SIMD register budget (0 = default)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=3, help="host-memory (PCIe-inclusive) steps")
+    ap.add_argument("--one-threads", type=int, default=32,
+                    help="integration path: host threads calling dg_decode_one (coalesced into GPU batches); 0 = off")
+    ap.add_argument("--one-images", type=int, default=0, help="images through dg_decode_one (0: 2 batches)")
     ap.add_argument("--shards", type=int, default=8, help="wds workload: shards of 1000 samples")
     ap.add_argument("--workload", choices=("jpeg", "cfg4", "png", "wds"), default="jpeg",
                     help="jpeg: configs[1] (the headline); cfg4: configs[3] (1M samples over a 16,384-image pool, "
@@ -542,8 +544,6 @@ def main() -> int:
         ctx.set_option("wg_timing", 1)
     if a.hb_bands:
         ctx.set_option("hb_bands", a.hb_bands)
-    if a.hb_occ:
-        ctx.set_option("hb_occ", a.hb_occ)
     if a.decode_semantics:
         ctx.set_option("decode_semantics", a.decode_semantics)
     if a.progressive_frac > 0:
@@ -698,6 +698,47 @@ def main() -> int:
             del res
         e2e_dev = e2e_px / (time.perf_counter() - t1) / 1e6
 
+    # ---- integration path (INTEGRATION.md GpuImageStage::payload): dg_decode_one from many host threads,
+    # the library coalescing concurrent calls into GPU batches (coalesce_max 64, coalesce_us 500); host in ->
+    # host out like e2e_host_mpix_s, reported only
+    one = None
+    if a.one_threads > 0 and rank == 0 and not a.encode:
+        import itertools
+        import threading
+        n_one = a.one_images or 2 * B_
+        order = [i for k in range(-(-n_one // B_)) for i in batch_idx(k)][:n_one]
+        ctx.decode_one(pool[order[0]], forced_pool[order[0]])  # warm the single-image path
+        b0, i0 = ctx.stat("coalesced_batches"), ctx.stat("coalesced_images")
+        ctr = itertools.count()
+        done_px = [0] * a.one_threads
+        fails = [0] * a.one_threads
+
+        def one_worker(t):
+            while True:
+                j = next(ctr)
+                if j >= n_one:
+                    return
+                i = order[j]
+                st_, _, _ = ctx.decode_one(pool[i], forced_pool[i])
+                if st_ == 0:
+                    done_px[t] += dims[i][0] * dims[i][1]
+                else:
+                    fails[t] += 1
+
+        ths = [threading.Thread(target=one_worker, args=(t,)) for t in range(a.one_threads)]
+        t1 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        dt1 = time.perf_counter() - t1
+        nb_ = ctx.stat("coalesced_batches") - b0
+        one = {"threads": a.one_threads, "images": n_one, "failed": sum(fails),
+               "mpix_s": round(sum(done_px) / dt1 / 1e6, 2), "images_per_s": round(n_one / dt1, 1),
+               "gpu_batches": nb_, "mean_images_per_batch": round((ctx.stat("coalesced_images") - i0) / max(nb_, 1), 1),
+               "coalesce_max": 64, "coalesce_us": 500,
+               "note": "host JPEG bytes in -> host RGB out per call (PCIe both ways), like e2e_host_mpix_s"}
+
     result = None
     if rank == 0:
         steps = a.steps
@@ -794,6 +835,7 @@ def main() -> int:
             "images_per_s": round(B_ * a.steps * world / dt_max, 1),
             "e2e_host_mpix_s": round(e2e, 2) if e2e else None,
             "e2e_host_in_hbm_out_mpix_s": round(e2e_dev, 2) if e2e_dev else None,
+            "e2e_decode_one": one,
             "corpus_gen_s": round(t_gen, 1),
             "corpus_generated_here": n_made if seq is not None else None,
             "stats": {"resync_rounds": ctx.stat("resync_rounds"), "fix_workgroups": ctx.stat("fix_workgroups"),

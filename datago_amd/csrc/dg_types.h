@@ -35,7 +35,7 @@ DG_HD void add3(int32_t v[3], uint32_t c, int32_t d) {
   v[2] += c == 2 ? d : 0;
 }
 
-constexpr int kLutBits = 9;          // Huffman first-level lookup width
+constexpr int kLutBits = 10;          // Huffman first-level lookup width
 constexpr int kMaxSlots = 6;         // Huffman tables per image (DC/AC x 3 components)
 constexpr int kSubPerWg = 256;       // entropy subsequences per workgroup (= threads)
 constexpr int kDefaultSubBits = 2048; // destuffed bits per subsequence
@@ -48,7 +48,7 @@ constexpr uint32_t kInf = 0xFFFFFFFFu;
 //   lut entry: (len << 8) | symbol          for codes of length <= kLutBits
 //              0x8000 | subtable index      when the prefix starts a long code
 //              0                            invalid prefix / fallback below
-constexpr int kSubBits = 16 - kLutBits;   // 7
+constexpr int kSubBits = 16 - kLutBits;   // 6
 constexpr int kMaxSubTables = 8;
 struct HuffTable {
   uint16_t lut[1 << kLutBits];

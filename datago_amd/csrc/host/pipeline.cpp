@@ -212,11 +212,6 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     decode_sem_ = (int)v;
     return DG_OK;
   }
-  if (k == "hb_occ") {  // band H kernels: register budget for 4 or 5 waves per SIMD
-    if (v != 4 && v != 5) return DG_ERR_INVALID;
-    hb_occ_ = (int)v;
-    return DG_OK;
-  }
   if (k == "png_chunked") {  // 0: every PNG inflates serially (test switch)
     chunked_off_ = v == 0;
     return DG_OK;
@@ -1387,13 +1382,13 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (next()) return DG_ERR_DEVICE;
   HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_coef, 0));
   launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
-  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0, hb_occ_);
+  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | (debug_flags_ << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV1), cnt(L_RV1), 1);
   launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
-  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2, hb_occ_);
+  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2);
   launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | (debug_flags_ << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3);
@@ -1498,6 +1493,38 @@ dg_status Context::finish(Slot &sl) {
   }
   const ImageDesc *back = (const ImageDesc *)((char *)sl.out.p + b.desc_off);
   size_t off = align_up(b.desc_off + b.descs.size() * sizeof(ImageDesc), 256);
+  if (b.host_io && b.any_enc) {
+    // Re-encoded payloads are known in length only now: copy all of them
+    // with one async D2H each into pinned staging behind the raw outputs and
+    // wait once, instead of a synchronous hipMemcpy per image.
+    size_t enc_total = 0;
+    for (int i = 0; i < b.n; i++)
+      if (b.desc_of[i] >= 0 && b.plans[i].encode && !back[b.desc_of[i]].status)
+        enc_total += align_up(back[b.desc_of[i]].enc.enc_bytes, 16);
+    if (enc_total) {
+      size_t raw_end = off;
+      for (int i = 0; i < b.n; i++)
+        if (b.desc_of[i] >= 0 && !b.plans[i].encode) raw_end += align_up(b.plans[i].out_bytes, 16);
+      if (sl.out.cap < raw_end + enc_total) {  // grow keeping the read-back descriptors and raw outputs
+        std::vector<char> keep((char *)sl.out.p, (char *)sl.out.p + raw_end);
+        dg_status st = ensure_pinned(sl.out, raw_end + enc_total + 256, sl.st);
+        if (st) return st;
+        memcpy(sl.out.p, keep.data(), keep.size());
+        back = (const ImageDesc *)((char *)sl.out.p + b.desc_off);
+      }
+      size_t eo = raw_end;
+      for (int i = 0; i < b.n; i++) {
+        if (b.desc_of[i] < 0 || !b.plans[i].encode || back[b.desc_of[i]].status) continue;
+        const uint32_t nb = back[b.desc_of[i]].enc.enc_bytes;
+        HIPCHK(hipMemcpyAsync((char *)sl.out.p + eo, (char *)sl.scratch.p + b.out_dev_off[i], nb,
+                              hipMemcpyDeviceToHost, sl.st));
+        b.enc_host_off.resize(b.n, 0);
+        b.enc_host_off[i] = eo;
+        eo += align_up(nb, 16);
+      }
+      HIPCHK(hipStreamSynchronize(sl.st));
+    }
+  }
   for (int i = 0; i < b.n; i++) {
     if (b.desc_of[i] < 0) continue;
     int status = back[b.desc_of[i]].status;
@@ -1511,8 +1538,7 @@ dg_status Context::finish(Slot &sl) {
     if (b.plans[i].encode) {
       const uint32_t nb = back[b.desc_of[i]].enc.enc_bytes;
       b.metas[i].nbytes = nb;
-      if (b.host_io && !status && nb)
-        HIPCHK(hipMemcpy(b.host_outs[i], (char *)sl.scratch.p + b.out_dev_off[i], nb, hipMemcpyDeviceToHost));
+      if (b.host_io && !status && nb) memcpy(b.host_outs[i], (char *)sl.out.p + b.enc_host_off[i], nb);
       continue;
     }
     if (b.host_io) {

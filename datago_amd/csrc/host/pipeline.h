@@ -82,7 +82,8 @@ struct Batch {
   dg_payload_meta *metas = nullptr;
   bool done = false;
   int resync_rounds = 0;
-  bool unsettled = false;  // resync hit kMaxResyncRounds: JPEGs go back as DG_ERR_UNSUPPORTED
+  bool unsettled = false;
+  std::vector<size_t> enc_host_off;  // host_io + encode: offset of image i's payload in the pinned read-back  // resync hit kMaxResyncRounds: JPEGs go back as DG_ERR_UNSUPPORTED
   BatchFlags flags = {0, 0, 0, 0};
   std::vector<float> stage_ms;
 };
@@ -205,7 +206,6 @@ class Context {
   bool wg_timing_ = false;
   bool chunked_off_ = false;  // option "png_chunked" = 0
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
-  int hb_occ_ = 5;                      // option "hb_occ"
   int decode_sem_ = 0;                  // option "decode_semantics"
   bool progressive_ = false;            // option "progressive"
   bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first

@@ -40,9 +40,9 @@ void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
 // band H pass: kHBandCols x kHBandRows outputs per workgroup (see kernels.hip);
 // `list` holds ncls[k] items of weight-count class k (<=8, <=16, <=32, more) in order
 // ncls[fused][class]: the list holds the fused (colour-fill) items first, then the byte-fill ones,
-// each ordered by weight-count class (<= 8, 16, 32 taps, more); occ: 4 or 5 waves per SIMD
+// each ordered by weight-count class (<= 8, 16, 32 taps, more)
 void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][4],
-                      int stage, int occ);
+                      int stage);
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage);
 // final copy / gray->RGB expansion: 256 output pixels per workgroup
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);

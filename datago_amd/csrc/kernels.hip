@@ -1340,10 +1340,11 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
   }
 }
 
-// OCC: waves per SIMD the register allocation targets (5: <= 96 VGPRs, may
-// spill; 4: <= 128 VGPRs, five workgroups' worth of LDS but four resident).
-template <int KMAX, bool FUSED, int OCC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void k_resize_hb(
+// Register budget for 5 waves per SIMD (<= 96 VGPRs; every variant fits
+// without scratch: 66-95 VGPRs).  A 4-wave budget measured slower
+// (resize_h1 2.81-2.90 vs 2.69-2.74 ms) and is no longer built.
+template <int KMAX, bool FUSED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_resize_hb(
     const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list, int stage) {
   __shared__ __attribute__((aligned(16))) uint32_t seg[kHBandRows * kHSegStride];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kHBandRows * kHBandCols * 4];
@@ -1559,27 +1560,22 @@ void launch_coeffs(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t
 void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
   DG_LAUNCH(k_resize_h, nwg, st, imgs, list, stage);
 }
-template <bool FUSED, int OCC>
+template <bool FUSED>
 static void launch_hb_classes(hipStream_t st, const ImageDesc *imgs, const WgItem *&list, const uint32_t ncls[4],
                               int stage) {
-  DG_LAUNCH((k_resize_hb<8, FUSED, OCC>), ncls[0], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<8, FUSED>), ncls[0], st, imgs, list, stage);
   list += ncls[0];
-  DG_LAUNCH((k_resize_hb<16, FUSED, OCC>), ncls[1], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<16, FUSED>), ncls[1], st, imgs, list, stage);
   list += ncls[1];
-  DG_LAUNCH((k_resize_hb<32, FUSED, OCC>), ncls[2], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<32, FUSED>), ncls[2], st, imgs, list, stage);
   list += ncls[2];
-  DG_LAUNCH((k_resize_hb<0, FUSED, OCC>), ncls[3], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<0, FUSED>), ncls[3], st, imgs, list, stage);
   list += ncls[3];
 }
 void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][4],
-                      int stage, int occ) {
-  if (occ == 4) {
-    launch_hb_classes<true, 4>(st, imgs, list, ncls[1], stage);
-    launch_hb_classes<false, 4>(st, imgs, list, ncls[0], stage);
-  } else {
-    launch_hb_classes<true, 5>(st, imgs, list, ncls[1], stage);
-    launch_hb_classes<false, 5>(st, imgs, list, ncls[0], stage);
-  }
+                      int stage) {
+  launch_hb_classes<true>(st, imgs, list, ncls[1], stage);
+  launch_hb_classes<false>(st, imgs, list, ncls[0], stage);
 }
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
   DG_LAUNCH(k_resize_v, nwg, st, imgs, list, stage);
