@@ -1286,9 +1286,18 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
       kw2[j] = lo | (hi << 16);
     }
   }
-  static_assert(kHBandRows * 32 == 256, "fill mapping");
-  const uint32_t fr = t >> 5, fl = t & 31;  // fill: 32 threads per row, no divisions
+  static_assert(kHBandRows * 32 == 256, "store mapping");
+  const uint32_t fr = t >> 5, fl = t & 31;  // store: 32 threads per row
   const uint32_t off = st - p0, r0 = t / kHBandCols;
+  // Fill jobs (an octet, or a 4-pixel unit, of one row) are numbered across
+  // the band's rows, so all 256 threads share them and waves with no job
+  // skip the fill: mapping 32 threads to each row left most lanes of the
+  // last pass idle (a 2x downscale's 35 octets per row ran two full passes
+  // for 3 octets), and every wave ran it.  Row of job j = j / per-row count
+  // n, by a 24-bit multiply with ceil(2^20 / n): exact for every j < 8n and
+  // n <= 160 (kHSegPx / 4 units; checked exhaustively), product < 2^32.
+  const uint32_t njob_row = FUSED ? (pe - p0 + 7) >> 3 : (pe - p0 + 3) >> 2;
+  const uint32_t inv_row = ((1u << 20) - 1u + njob_row) / (njob_row ? njob_row : 1u);
   const int32_t prec = ps.precision;
   const uint32_t rb = (x1 - x0) * C;  // <= kHBandCols * 4 = 512 bytes: 32 chunks of 16
   const uint32_t ybeg = group * kHBandRows * ps.bands;
@@ -1297,16 +1306,14 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
     if (y0 >= ps.rows) break;
     const uint32_t nrows = ps.rows - y0 < kHBandRows ? ps.rows - y0 : kHBandRows;
     // phase 1: fill
-    if (fr < nrows) {
+    const uint32_t njob = nrows * njob_row;
+    for (uint32_t j = t; j < njob; j += 256) {
+      const uint32_t r = __umul24(j, inv_row) >> 20, q = j - r * njob_row;
       if (FUSED) {
-        const uint32_t noct = (pe - p0 + 7) >> 3;
-        for (uint32_t q = fl; q < noct; q += 32)
-          hfill_color8(im, ps.row0 + y0 + fr, p0 + 8 * q, seg + fr * kHSegStride + 8 * q);
+        hfill_color8(im, ps.row0 + y0 + r, p0 + 8 * q, seg + r * kHSegStride + 8 * q);
       } else {
-        const uint32_t nu = (pe - p0 + 3) >> 2;
-        const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0 + fr) * ps.src_stride;
-        for (uint32_t u = fl; u < nu; u += 32)
-          hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * u, seg + fr * kHSegStride + 4 * u);
+        const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0 + r) * ps.src_stride;
+        hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * q, seg + r * kHSegStride + 4 * q);
       }
     }
     __syncthreads();

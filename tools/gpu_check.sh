@@ -26,5 +26,5 @@ rc=$?; ok_or_fail $rc || exit $rc
 step bench 900 python bench.py --steps $STEPS --warmup 2 $BARGS --out $OUT/bench.json
 rc=$?; [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
-step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 5 --warmup 1 $BARGS --no-cpu-baseline --e2e-steps 0
+step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 5 --warmup 1 $BARGS --no-cpu-baseline --e2e-steps 0 --one-threads 0
 exit $?
