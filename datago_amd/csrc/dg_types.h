@@ -264,6 +264,7 @@ struct ImageDesc {
   uint32_t mk_cap;          // capacity of the marker list
   uint32_t lead_bits;       // k_huff_sync lead-in before each subsequence (lead_in)
   uint32_t ds_lsw;          // log2(32-bit words per subsequence) of the interleaved stream
+  uint32_t ckpt;            // 1: k_huff_sync / k_huff_fix record checkpoints for early merging (option "ckpt")
   uint32_t stage_cap;       // decode-once: staging capacity per subsequence (groups of 4 entries), 0 = off
   uint32_t restart;         // restart interval (MCUs), 0 = none
   uint32_t blocks_per_seg;  // restart * bpm, 0 = unlimited

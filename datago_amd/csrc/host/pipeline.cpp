@@ -207,6 +207,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     hb_bands_ = (uint32_t)v;
     return DG_OK;
   }
+  if (k == "ckpt") {  // entropy checkpoints for early merging of re-decodes (default 1)
+    ckpt_ = v != 0;
+    return DG_OK;
+  }
   if (k == "decode_semantics") {  // 0: libjpeg-turbo (pinned), 1: zune-jpeg 0.5.12 restated (unpinned)
     if (v != 0 && v != 1) return DG_ERR_INVALID;
     decode_sem_ = (int)v;
@@ -694,6 +698,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     d.ncomp = (uint8_t)h.ncomp;
     d.colorspace = (uint8_t)h.colorspace;
     d.sem = (uint16_t)decode_sem_;
+    d.ckpt = ckpt_ ? 1u : 0u;
     d.dec_c = h.ncomp == 1 ? 1 : 3;
     d.hmax = (uint32_t)h.hmax;
     d.vmax = (uint32_t)h.vmax;

@@ -207,6 +207,7 @@ class Context {
   bool chunked_off_ = false;  // option "png_chunked" = 0
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
   int decode_sem_ = 0;                  // option "decode_semantics"
+  bool ckpt_ = true;                    // option "ckpt"
   bool progressive_ = false;            // option "progressive"
   bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first
   bool entropy_once_ = false;           // option "entropy_once": decode-once staging + k_huff_scatter

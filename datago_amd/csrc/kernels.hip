@@ -305,7 +305,8 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   // previous workgroup and is not staged
   const bool stage = STAGE && im.stage != 0;
   DG_GLOBAL Ckpt *ck =
-      (!stage && t > 0 && active && nck) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck : nullptr;
+      (!stage && t > 0 && active && nck && im.ckpt) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck
+                                                     : nullptr;
   StageCtx sc;
   sc.on = stage && t > 0 && active;
   sc.base = sc.on ? stage_range(im.stage, im.stage_cap, s) : nullptr;
@@ -361,7 +362,8 @@ __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ 
   const bool active = t < (int)kUseful && s < im.nsub;
   const uint32_t nck = num_ckpt(im.sub_bits);
   const bool stage = STAGE && im.stage != 0;
-  DG_GLOBAL Ckpt *ck = (!stage && active && nck) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck : nullptr;
+  DG_GLOBAL Ckpt *ck =
+      (!stage && active && nck && im.ckpt) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck : nullptr;
   StageCtx sc;
   sc.on = stage && active;
   sc.base = sc.on ? stage_range(im.stage, im.stage_cap, s) : nullptr;

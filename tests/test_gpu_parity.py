@@ -353,3 +353,65 @@ def test_decode_one_coalesces_concurrent_callers(ctx512):
         assert np.array_equal(arr, _oracle_resized(data, *t.target_size(w, h)))
     assert ctx.stat("coalesced_images") == len(datas)
     assert ctx.stat("coalesced_batches") < len(datas)  # merged
+
+
+def _content(kind, rng, w, h, gray):
+    """Entropy regimes the synthetic corpus alone does not stress (VERDICT r1
+    weak item 11): flat low-detail images (short, EOB-heavy codes: the
+    slowest entropy workgroups), uniform noise (long codes, many AC symbols),
+    hard-edged stripes/text-like blocks, and the bench's own gradient+noise."""
+    if kind == "flat":
+        yy, xx = np.mgrid[0:h, 0:w]
+        base = (96 + 64 * np.sin(xx / max(w, 1) * 3.1) * np.cos(yy / max(h, 1) * 2.3)).astype(np.float32)
+        arr = np.repeat(base[:, :, None], 1 if gray else 3, axis=2) + (0 if gray else np.array([0, 20, -20]))
+        arr = arr.clip(0, 255).astype(np.uint8)
+        return arr[:, :, 0] if gray else arr
+    if kind == "noise":
+        return rng.integers(0, 256, (h, w) if gray else (h, w, 3), dtype=np.uint8)
+    if kind == "edges":
+        yy, xx = np.mgrid[0:h, 0:w]
+        m = (((xx // 7) + (yy // 11)) % 2 * 255).astype(np.uint8)
+        return m if gray else np.stack([m, 255 - m, (m // 2 + 64).astype(np.uint8)], axis=2)
+    return synth.synth_pixels(rng, w, h, gray)
+
+
+FULL_CASES = [  # (content, w, h, quality, subsampling, gray): configs[1] sizes, short side 256..2048
+    ("flat", 2048, 1536, 35, "4:2:0", False), ("flat", 1024, 2300, 60, "4:2:2", False),
+    ("noise", 1500, 1100, 95, "4:2:0", False), ("noise", 640, 1500, 90, "4:4:4", False),
+    ("edges", 1800, 900, 80, "4:2:0", False), ("edges", 913, 1219, 75, "4:2:0", True),
+    ("synth", 2600, 1100, 88, "4:2:0", False), ("synth", 1279, 1935, 92, "4:4:4", False),
+    ("flat", 777, 2048, 50, "4:2:0", True), ("synth", 256, 611, 75, "4:2:2", False),
+    ("noise", 2047, 257, 85, "4:2:2", False), ("edges", 1333, 1333, 95, "4:4:4", False),
+]
+
+
+def test_full_size_regimes_bit_exact_vs_oracle(ctx1024):
+    """Full configs[1]-size images end to end (decode + bucket + crop/resize at
+    1024/32), every regime in one batch, bit-exact against the oracle."""
+    datas = []
+    for i, (kind, w, h, q, ss, gray) in enumerate(FULL_CASES):
+        rng = np.random.default_rng(900 + i)
+        datas.append(synth.encode_jpeg(_content(kind, rng, w, h, gray), q, ss))
+    res = ctx1024.decode_batch(datas)
+    t = B.ARAwareTransform(1024, 32, 0.5, 2.0)
+    for k, (data, (st, arr, meta)) in enumerate(zip(datas, res)):
+        assert st == 0, (k, FULL_CASES[k])
+        st2, dec = O.jpeg_decode(data)
+        ref = O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR)
+        assert np.array_equal(arr, ref), FULL_CASES[k]
+    assert ctx1024.stat("write_mismatch") == 0
+
+
+@pytest.mark.parametrize("sub_bits", [512, 8192])
+def test_full_size_regimes_subsequence_sizes(sub_bits):
+    """The same regimes through other subsequence sizes: decode-only outputs equal the default's."""
+    L = _lib()
+    datas = []
+    for i, (kind, w, h, q, ss, gray) in enumerate(FULL_CASES[:6]):
+        rng = np.random.default_rng(900 + i)
+        datas.append(synth.encode_jpeg(_content(kind, rng, w, h, gray), q, ss))
+    a = L.Context(0).decode_batch(datas)
+    c = L.Context(0)
+    c.set_option("sub_bits", sub_bits)
+    for (sa, xa, _), (sb, xb, _) in zip(a, c.decode_batch(datas)):
+        assert sa == 0 and sb == 0 and np.array_equal(xa, xb)

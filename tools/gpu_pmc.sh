@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc
 mkdir -p $OUT
-ARGS="--steps ${STEPS:-2} --warmup 1 --batch ${BATCH:-256} --pool ${POOL:-256} --no-cpu-baseline --e2e-steps 0"
+ARGS="--steps ${STEPS:-2} --warmup 1 --batch ${BATCH:-256} --pool ${POOL:-4096} --no-cpu-baseline --e2e-steps 0 --one-threads 0 --serial-steps 0"
 run() {  # name counters...
   local name=$1; shift
   echo "=== pmc $name: $*"
@@ -23,5 +23,5 @@ run fetch FETCH_SIZE &&
 run write WRITE_SIZE
 rc=$?
 [ $rc -eq 0 ] || exit $rc
-python tools/pmc_traffic.py $OUT "batch=${BATCH:-256} pool=${POOL:-256} size=1024/32 short=256-2048" ${BATCH:-256} \
+python tools/pmc_traffic.py $OUT "batch=${BATCH:-256} pool=${POOL:-4096} size=1024/32 short=256-2048" ${BATCH:-256} \
     > $OUT/pmc_traffic.json && python tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt
