@@ -78,6 +78,7 @@ def parse():
     ap.add_argument("--entropy-lpt", type=int, default=-1, help="slow entropy workgroups first (-1 = library default)")
     ap.add_argument("--hb-bands", type=int, default=0, help="band H kernel: 8-row bands per workgroup (0 = default)")
     ap.add_argument("--ckpt", type=int, default=-1, help="entropy checkpoints (-1 = library default)")
+    ap.add_argument("--idct-fused", type=int, default=-1, help="IDCT inside the entropy write kernel (-1 = default)")
     ap.add_argument("--decode-semantics", type=int, default=0,
                     help="JPEG pixel semantics: 0 libjpeg-turbo (pinned, default), 1 zune-jpeg 0.5.12 restated")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
@@ -549,6 +550,8 @@ def main() -> int:
         ctx.set_option("decode_semantics", a.decode_semantics)
     if a.ckpt >= 0:
         ctx.set_option("ckpt", a.ckpt)
+    if a.idct_fused >= 0:
+        ctx.set_option("idct_fused", a.idct_fused)
     if a.progressive_frac > 0:
         ctx.set_option("progressive", 1)
     if a.entropy_lpt >= 0:

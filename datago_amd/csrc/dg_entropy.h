@@ -17,6 +17,7 @@
 // predictors reset (T.81 F.2.1.3.1); the marker belongs to the subsequence
 // whose range contains its position.
 #pragma once
+#include "dg_pixel.h"
 #include "dg_types.h"
 
 namespace dg {
@@ -182,6 +183,12 @@ struct WriteCtx {
   int16_t *wave_blk;
   uint32_t stride;
   uint32_t *tab;
+  // fused IDCT (ImageDesc::idct_fused): completed blocks become plane pixels
+  const ImageDesc *im;      // nullptr: blocks are written as coefficients
+  const int32_t *qt;        // LDS: the image's quantisation tables, [component][natural index]
+  const uint8_t *n2z;       // LDS: natural index -> zigzag index
+  BatchFlags *flags;        // idct_late / idct_list: blocks left to k_idct_list
+  uint32_t img;             // descriptor index
 #endif
 };
 
@@ -223,6 +230,18 @@ DG_HD void wc_flush(WriteCtx &w, uint32_t ze) {
 }
 
 #if defined(DG_DEVICE)
+// Fused IDCT: a block whose coefficients reach the coefficient buffer (not
+// IDCT-ed in the flush) is listed for k_idct_list.
+__device__ __forceinline__ void wc_list_late(WriteCtx &w, int32_t idx) {
+  if (!w.im || idx < 0) return;
+  const uint32_t e = atomicAdd(&w.flags->idct_late, 1u);
+  if (e < w.flags->idct_cap) {
+    uint32_t *l = (uint32_t *)(uintptr_t)w.flags->idct_list;
+    l[2 * e] = w.img;
+    l[2 * e + 1] = (uint32_t)idx;
+  }
+}
+
 // Full blocks completed by lanes of a wave are written out together: a lane
 // whose block ends only marks it pending, and at the top of the next symbol
 // step the wave's active lanes copy every pending block with one 16-byte
@@ -242,13 +261,72 @@ __device__ __forceinline__ void wc_coop_flush(WriteCtx &w, bool pending) {
   }
   __builtin_amdgcn_wave_barrier();
   const uint32_t wr = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
-  const uint32_t na = (uint32_t)__popcll(am), nc = 8u * (uint32_t)__popcll(pm);
+  const uint32_t na = (uint32_t)__popcll(am), nb = (uint32_t)__popcll(pm), nc = 8u * nb;
   const u32x4 zero = {0u, 0u, 0u, 0u};
+  if (w.im && na >= 8) {
+    // Fused IDCT: groups of 8 active lanes take one pending block each per
+    // round; lane `part` runs column `part` (dequantised from the zigzag
+    // coefficients) of pass 1, the 8 workspace columns go back into the
+    // block's own LDS buffer in natural order, then lane `part` runs row
+    // `part` of pass 2 and stores 8 plane pixels.  All 8 lanes of a block
+    // are in the same round, so every pass-1 read precedes the writes
+    // (one wave: LDS operations in program order).
+    const ImageDesc &im = *w.im;
+    const bool zune = im.sem != 0;
+    const uint32_t groups = na >> 3, g = wr >> 3, part = wr & 7u;
+    for (uint32_t k0 = 0; k0 < nb; k0 += groups) {
+      const uint32_t k = k0 + g;
+      const bool act = g < groups && k < nb;
+      const int32_t idx = act ? (int32_t)w.tab[64 + k] : -1;
+      int16_t *b = w.wave_blk + (act ? w.tab[k] : 0u) * w.stride;
+      const bool live = act && idx >= 0;
+      uint32_t c = 0, by = 0, bx = 0;
+      if (live) block_pos(im, (uint32_t)idx, c, by, bx);
+      int32_t ws[8];
+      if (live) {
+        int32_t v[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) v[r] = (int32_t)b[w.n2z[r * 8 + part]] * w.qt[c * 64 + r * 8 + part];
+        idct_col(zune, v, ws);
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (live) {
+#pragma unroll
+        for (int r = 0; r < 8; r++) b[r * 8 + part] = (int16_t)ws[r];
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (act) {
+        u32x4 *row4 = (u32x4 *)b + part;
+        if (live) {
+          const u32x4 rv = *row4;
+          int16_t h[8];
+          __builtin_memcpy(h, &rv, 16);
+          int32_t row[8];
+          uint32_t px[8];
+#pragma unroll
+          for (int i = 0; i < 8; i++) row[i] = h[i];
+          idct_row(zune, row, px);
+          // byte packing by v_perm (see pack4 in kernels.hip: shift/or packing miscompiles)
+          const uint32_t lo = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[3], px[2], 0x0c0c0400u),
+                                                    __builtin_amdgcn_perm(px[1], px[0], 0x0c0c0400u), 0x05040100u);
+          const uint32_t hi = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[7], px[6], 0x0c0c0400u),
+                                                    __builtin_amdgcn_perm(px[5], px[4], 0x0c0c0400u), 0x05040100u);
+          DG_GLOBAL uint8_t *dst =
+              (DG_GLOBAL uint8_t *)(uintptr_t)im.plane[c] + (size_t)(by * 8 + part) * (im.cbw[c] * 8) + bx * 8;
+          *(DG_GLOBAL u32x2 *)dst = u32x2{lo, hi};
+        }
+        *row4 = zero;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    return;
+  }
   for (uint32_t c = wr; c < nc; c += na) {
     const uint32_t k = c >> 3, part = c & 7u;
     const int32_t idx = (int32_t)w.tab[64 + k];
     u32x4 *src = (u32x4 *)(w.wave_blk + w.tab[k] * w.stride) + part;
     if (idx >= 0) *(DG_GLOBAL u32x4 *)(w.coef + (size_t)idx * 64 + part * 8) = *src;
+    if (part == 0) wc_list_late(w, idx);  // fused IDCT with < 8 active lanes: k_idct_list takes it
     *src = zero;
   }
   __builtin_amdgcn_wave_barrier();
@@ -271,8 +349,13 @@ template <bool COOP>
 DG_HD void wc_end_block(WriteCtx &w, bool &pending) {
 #if defined(DG_DEVICE)
   if (COOP) {
-    if (w.zs == 0) pending = true;
-    else wc_flush_zero(w, 64);
+    if (w.zs == 0) {
+      pending = true;
+    } else {  // carried in from the previous range: its first coefficients are in the buffer already
+      const int32_t idx = w.cur;
+      wc_flush_zero(w, 64);
+      wc_list_late(w, idx);
+    }
     return;
   }
 #endif

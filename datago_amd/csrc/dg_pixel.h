@@ -119,6 +119,54 @@ DG_HD uint8_t idct_stb_out(int32_t o) {
   return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
+// Pass 1 of one column from its 8 dequantised inputs: the workspace values,
+// saturated to 16 bits like libjpeg-turbo's SIMD IDCTs (vpackssdw between the
+// passes; no valid coefficient block comes near the limits).  Pass 2 of one
+// row of workspace values: 8 output samples.  Both decode semantics.
+DG_HD int32_t sat16(int32_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+DG_HD void idct_col(bool zune, const int32_t v[8], int32_t ws[8]) {
+  int32_t o[8];
+  if (zune) {
+    idct_1d_stb(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
+#pragma unroll
+    for (int r = 0; r < 8; r++) ws[r] = sat16(idct_stb_pass1(o[r]));
+  } else {
+    idct_1d(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
+#pragma unroll
+    for (int r = 0; r < 8; r++) ws[r] = sat16(descale(o[r], kConstBits - kPass1Bits));
+  }
+}
+DG_HD void idct_row(bool zune, const int32_t w[8], uint32_t px[8]) {
+  int32_t o[8];
+  if (zune) {
+    idct_1d_stb(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+#pragma unroll
+    for (int i = 0; i < 8; i++) px[i] = idct_stb_out(o[i]);
+  } else {
+    idct_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+#pragma unroll
+    for (int i = 0; i < 8; i++) px[i] = idct_out(o[i]);
+  }
+}
+
+// Component and block coordinates (in that component's plane) of the
+// decode-order block `idx` of a sequential scan: raster order for a single
+// component, MCU-interleaved otherwise.
+DG_HD void block_pos(const ImageDesc &im, uint32_t idx, uint32_t &c, uint32_t &by, uint32_t &bx) {
+  if (im.ncomp == 1) {
+    c = 0;
+    by = idx / im.cbw[0];
+    bx = idx - by * im.cbw[0];
+    return;
+  }
+  const uint32_t mcu = idx / im.bpm, r = idx - mcu * im.bpm;
+  c = (im.comp_bits >> (2 * r)) & 3u;
+  const uint32_t j = r - im.cfirst[c], vy = j / im.ch[c], hx = j - vy * im.ch[c];
+  const uint32_t my = mcu / im.mcux, mx = mcu - my * im.mcux;
+  by = my * im.cv[c] + vy;
+  bx = mx * im.ch[c] + hx;
+}
+
 // zigzag index -> natural index
 #if defined(DG_DEVICE)
 __constant__

@@ -265,6 +265,7 @@ struct ImageDesc {
   uint32_t lead_bits;       // k_huff_sync lead-in before each subsequence (lead_in)
   uint32_t ds_lsw;          // log2(32-bit words per subsequence) of the interleaved stream
   uint32_t ckpt;            // 1: k_huff_sync / k_huff_fix record checkpoints for early merging (option "ckpt")
+  uint32_t idct_fused;      // 1: k_huff_write turns completed blocks into plane pixels (option "idct_fused")
   uint32_t stage_cap;       // decode-once: staging capacity per subsequence (groups of 4 entries), 0 = off
   uint32_t restart;         // restart interval (MCUs), 0 = none
   uint32_t blocks_per_seg;  // restart * bpm, 0 = unlimited
@@ -343,12 +344,17 @@ struct BatchFlags {
   uint32_t fix_count;       // workgroups k_huff_fix had to re-run
   uint32_t write_mismatch;  // k_huff_write exit != next subsequence's input
   uint32_t sync_iters_max;  // longest intra-workgroup sync loop
+  uint32_t idct_late;       // fused IDCT: blocks k_huff_write left to k_idct_list (entries in idct_list)
+  uint32_t pad0;
   uint64_t wgtime;          // debug: device array of {start, end} s_memrealtime per workgroup, 0 = off
   uint32_t wgtime_write;    // first record of k_huff_write's workgroups
   uint32_t debug;           // test switches (kDbg*), kept across resync rounds
+  uint64_t idct_list;       // fused IDCT: uint32 {image, block} pairs, idct_cap of them
+  uint32_t idct_cap;
+  uint32_t pad1;
 };
 // The counters a resync round clears (everything before `wgtime`).
-constexpr size_t kFlagCounters = 16;
+constexpr size_t kFlagCounters = 24;
 // BatchFlags::debug: force the failure paths a valid stream never takes, so
 // tests can check that they surface as a per-image status.
 constexpr uint32_t kDbgForceWriteMismatch = 1u;  // k_huff_write: subsequence 0 of every image disagrees

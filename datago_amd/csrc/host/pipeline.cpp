@@ -207,6 +207,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     hb_bands_ = (uint32_t)v;
     return DG_OK;
   }
+  if (k == "idct_fused") {  // IDCT inside k_huff_write's block flush (default 0: measured slower)
+    idct_fused_ = v != 0;
+    return DG_OK;
+  }
   if (k == "ckpt") {  // entropy checkpoints for early merging of re-decodes (default 1)
     ckpt_ = v != 0;
     return DG_OK;
@@ -756,6 +760,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     // entropy data
     d.scan_len = (uint32_t)(h.scan_end - h.scan_off);
     d.sub_bits = sub_bits;
+    // completed blocks go straight to plane pixels inside k_huff_write (not
+    // with decode-once staging, whose k_huff_scatter writes coefficients)
+    d.idct_fused = (idct_fused_ && !entropy_once_) ? 1u : 0u;
+    if (d.idct_fused) b.any_fused = true;
     // lead-in before each subsequence (lead_in in dg_entropy.h): covers the
     // self-synchronisation distance, which is longest for 6-block MCUs
     // (4:2:0; p99.9 ~7 kbit on the bench corpus, tools/sync_stats.cpp)
@@ -1005,6 +1013,17 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
   const size_t ckpt_off = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits)) * sizeof(Ckpt));
+  // fused IDCT leftovers: at most one carried-in block per subsequence, plus
+  // the blocks of flushes with < 8 active lanes -- the tail of a wave, or
+  // every block of an image with fewer subsequences than that.  Sized for
+  // the worst case (all blocks of the fused images; 8 B each is small next
+  // to their 128 B of coefficients); k_idct_list clamps to it and finish()
+  // checks it.
+  uint64_t fused_blocks = 0;
+  for (const ImageDesc &dd : b.descs)
+    if (dd.idct_fused) fused_blocks += dd.total_blocks;
+  b.idct_cap = b.any_fused ? (uint32_t)std::min<uint64_t>(2 * b.total_subs + fused_blocks + 4096, 0xFFFFFFF0u) : 0u;
+  const size_t idct_list_off = L.take((size_t)b.idct_cap * 8 + 16);
   st = ensure(sl.scratch, L.off + 256, sl.st);
   if (st) return st;
   st = ensure(sl.coef, CO.off + 256, sl.st);
@@ -1162,7 +1181,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     }
     uint32_t items = 0;
     for (uint32_t c = 0; c < d.ncomp; c++) items += d.cbh[c] * ((d.cbw[c] + 63) / 64);  // kIdctBlocks
-    for (uint32_t it = 0; it < items; it++) b.lists[L_IDCT].push_back({I, it});
+    if (!d.idct_fused)  // fused: k_huff_write (+ k_idct_list) produce the planes
+      for (uint32_t it = 0; it < items; it++) b.lists[L_IDCT].push_back({I, it});
     if (d.ncomp == 3 && !d.color_fused) {
       uint32_t q = (d.width + 7) / 8 * d.height;
       for (uint32_t it = 0; it < q; it += 256) b.lists[L_COLOR].push_back({I, it});
@@ -1276,6 +1296,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     bf->wgtime_write = (uint32_t)b.lists[L_SYNC].size();
   }
   ((BatchFlags *)(P + b.flags_off))->debug = (uint32_t)(debug_flags_ >> 16) & 3u;
+  ((BatchFlags *)(P + b.flags_off))->idct_list = (uint64_t)(uintptr_t)((char *)sl.scratch.p + idct_list_off);
+  ((BatchFlags *)(P + b.flags_off))->idct_cap = b.idct_cap;
   memcpy(P + b.desc_off, b.descs.data(), b.descs.size() * sizeof(ImageDesc));
   for (int l = 0; l < L_COUNT; l++)
     if (!b.lists[l].empty()) memcpy(P + b.list_off[l], b.lists[l].data(), b.lists[l].size() * sizeof(WgItem));
@@ -1378,9 +1400,10 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (b.stage_on)
     launch_huff_scatter(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), subs);
   else
-    launch_huff_write(sl.st, dm, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots);
+    launch_huff_write(sl.st, dm, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots, qp);
   if (next()) return DG_ERR_DEVICE;
   if (next()) return DG_ERR_DEVICE;  // coeffs (side stream)
+  if (b.any_fused) launch_idct_list(sl.st, dd, qp, fl, std::min<uint32_t>(2048u, (b.idct_cap + 31) / 32));
   launch_idct(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);
   if (next()) return DG_ERR_DEVICE;
   launch_color(sl.st, dd, lst(L_COLOR), cnt(L_COLOR));
@@ -1446,6 +1469,10 @@ dg_status Context::finish(Slot &sl) {
     stat_fix_ += b.flags.fix_count;
     stat_mismatch_ += b.flags.write_mismatch;
     stat_iters_ = std::max<int64_t>(stat_iters_, b.flags.sync_iters_max);
+    if (b.flags.idct_late > b.idct_cap) {  // never seen; would leave blocks without pixels
+      b.unsettled = true;
+      set_error("fused IDCT list overflow: the batch's JPEGs are returned DG_ERR_UNSUPPORTED");
+    }
     if (b.flags.chain_changed == 0) break;
     if (b.resync_rounds >= kMaxResyncRounds) {
       // The boundary repair did not settle: some entropy chain of this batch

@@ -62,6 +62,8 @@ struct Batch {
   std::vector<uint8_t> blob;
   size_t blob_off = 0;
   bool any_png = false, any_alpha = false, any_enc = false;
+  bool any_fused = false;  // some image's IDCT runs inside k_huff_write
+  uint32_t idct_cap = 0;   // entries of BatchFlags::idct_list
   bool stage_on = false;  // decode-once staging (option "entropy_once")
   uint32_t max_slots = 1; // largest Huffman table count of an image (dynamic LDS of k_huff_sync/fix)
   size_t words_off = 0, words_bytes = 0;  // contiguous encoder bit buffers (zeroed per batch)
@@ -208,6 +210,7 @@ class Context {
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
   int decode_sem_ = 0;                  // option "decode_semantics"
   bool ckpt_ = true;                    // option "ckpt"
+  bool idct_fused_ = false;             // option "idct_fused" (measured 7x slower k_huff_write: off)
   bool progressive_ = false;            // option "progressive"
   bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first
   bool entropy_once_ = false;           // option "entropy_once": decode-once staging + k_huff_scatter

@@ -466,15 +466,27 @@ constexpr int kBlkStride = 72;
 __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs,
                                                     const WgItem *__restrict__ list,
                                                     const HuffTable *__restrict__ pool,
-                                                    const SubState *__restrict__ subs, BatchFlags *flags) {
+                                                    const SubState *__restrict__ subs, BatchFlags *flags,
+                                                    const QuantTable *__restrict__ qpool) {
   extern __shared__ __attribute__((aligned(16))) uint8_t huff_dyn[];  // im.nslots tables (launch: batch max)
   HuffTable *tabs = (HuffTable *)huff_dyn;
   __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][kBlkStride];
   __shared__ uint32_t wtab[kSubPerWg / 64][128];  // wc_coop_flush tables, one per wave
+  __shared__ int32_t qt[3 * 64];                  // fused IDCT: quantisation tables, natural order
+  __shared__ uint8_t n2z[64];                     // fused IDCT: natural -> zigzag index
   const uint64_t t_start = wg_clock();
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
   load_tables(tabs, pool, im);
+  const bool fused = im.idct_fused != 0;
+  if (fused) {
+    const int t = threadIdx.x;
+    if (t < 64) n2z[kZigzagToNatural[t]] = (uint8_t)t;
+    if (t < 3 * 64 && (uint32_t)(t >> 6) < im.ncomp) {
+      const DG_GLOBAL uint16_t *q = gp<const uint16_t>((uint64_t)(uintptr_t)qpool[im.qpool[t >> 6]].q);
+      qt[t] = q[t & 63];
+    }
+  }
   __syncthreads();
   const int t = threadIdx.x;
   const uint32_t s = it.item0 + t;
@@ -495,6 +507,11 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
     w.wave_blk = blk[t & ~63];
     w.stride = kBlkStride;
     w.tab = wtab[t >> 6];
+    w.im = fused ? &im : nullptr;
+    w.qt = qt;
+    w.n2z = n2z;
+    w.flags = flags;
+    w.img = it.image;
     {  // blocks are all-zero whenever none is open (wc_coop_flush)
       u32x4 *p = (u32x4 *)w.blk;
       const u32x4 zero = {0u, 0u, 0u, 0u};
@@ -673,29 +690,23 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
     }
   }
   __syncthreads();
-  int32_t o0[8], o1[8];
   const bool zune = im.sem != 0;  // decode semantics (uniform per workgroup)
   // pass 1: column `lane`, dequantised on the way in
-  if (zune) {
-    idct_1d_stb(bv0[0 * RS + lane] * qc[0], bv0[1 * RS + lane] * qc[1], bv0[2 * RS + lane] * qc[2],
-                bv0[3 * RS + lane] * qc[3], bv0[4 * RS + lane] * qc[4], bv0[5 * RS + lane] * qc[5],
-                bv0[6 * RS + lane] * qc[6], bv0[7 * RS + lane] * qc[7], o0);
-    idct_1d_stb(bv1[0 * RS + lane] * qc[0], bv1[1 * RS + lane] * qc[1], bv1[2 * RS + lane] * qc[2],
-                bv1[3 * RS + lane] * qc[3], bv1[4 * RS + lane] * qc[4], bv1[5 * RS + lane] * qc[5],
-                bv1[6 * RS + lane] * qc[6], bv1[7 * RS + lane] * qc[7], o1);
-  } else {
-    idct_1d(bv0[0 * RS + lane] * qc[0], bv0[1 * RS + lane] * qc[1], bv0[2 * RS + lane] * qc[2],
-            bv0[3 * RS + lane] * qc[3], bv0[4 * RS + lane] * qc[4], bv0[5 * RS + lane] * qc[5],
-            bv0[6 * RS + lane] * qc[6], bv0[7 * RS + lane] * qc[7], o0);
-    idct_1d(bv1[0 * RS + lane] * qc[0], bv1[1 * RS + lane] * qc[1], bv1[2 * RS + lane] * qc[2],
-            bv1[3 * RS + lane] * qc[3], bv1[4 * RS + lane] * qc[4], bv1[5 * RS + lane] * qc[5],
-            bv1[6 * RS + lane] * qc[6], bv1[7 * RS + lane] * qc[7], o1);
-  }
-  __syncthreads();
+  {
+    int32_t v0[8], v1[8], w0[8], w1[8];
 #pragma unroll
-  for (int r = 0; r < 8; r++) {
-    bv0[r * RS + lane] = zune ? idct_stb_pass1(o0[r]) : descale(o0[r], kConstBits - kPass1Bits);
-    bv1[r * RS + lane] = zune ? idct_stb_pass1(o1[r]) : descale(o1[r], kConstBits - kPass1Bits);
+    for (int r = 0; r < 8; r++) {
+      v0[r] = bv0[r * RS + lane] * qc[r];
+      v1[r] = bv1[r * RS + lane] * qc[r];
+    }
+    idct_col(zune, v0, w0);
+    idct_col(zune, v1, w1);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      bv0[r * RS + lane] = w0[r];
+      bv1[r * RS + lane] = w1[r];
+    }
   }
   __syncthreads();
   // pass 2: row `lane`
@@ -705,23 +716,75 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
   for (int h = 0; h < 2; h++) {
     const int32_t *w = (h ? bv1 : bv0) + lane * RS;
     const bool v = h ? v1 : v0;
-    int32_t o[8];
-    uint32_t lo = 0, hi = 0;
-    if (zune) {
-      idct_1d_stb(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
-      // pack4, not shifts: shift/or packing of clamped values lets hipcc form
-      // v_ashr_pk_u8_i32 and OR the next byte into its stale upper half (pack4)
-      lo = pack4(idct_stb_out(o[0]), idct_stb_out(o[1]), idct_stb_out(o[2]), idct_stb_out(o[3]));
-      hi = pack4(idct_stb_out(o[4]), idct_stb_out(o[5]), idct_stb_out(o[6]), idct_stb_out(o[7]));
-    } else {
-      idct_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+    int32_t row[8];
+    uint32_t px[8];
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        lo |= (uint32_t)idct_out(o[i]) << (8 * i);
-        hi |= (uint32_t)idct_out(o[i + 4]) << (8 * i);
+    for (int i = 0; i < 8; i++) row[i] = w[i];
+    idct_row(zune, row, px);
+    // pack4, not shifts: shift/or packing of clamped values lets hipcc form
+    // v_ashr_pk_u8_i32 and OR the next byte into its stale upper half
+    const uint32_t lo = pack4(px[0], px[1], px[2], px[3]), hi = pack4(px[4], px[5], px[6], px[7]);
+    if (v) *(DG_GLOBAL u32x2 *)(plane + (size_t)(h ? bx1 : bx0) * 8) = u32x2{lo, hi};
+  }
+}
+
+// Fused-IDCT leftovers (option "idct_fused"): the blocks k_huff_write could
+// not turn into pixels itself -- a block completed by a range that did not
+// start it (its first coefficients came from the previous range), or
+// flushed when fewer than 8 lanes were active -- were written as
+// coefficients and listed in BatchFlags::idct_list.  8 lanes per block, 32
+// blocks per workgroup round, grid-strided over the device-side count.
+__global__ __launch_bounds__(256) void k_idct_list(const ImageDesc *__restrict__ imgs,
+                                                   const QuantTable *__restrict__ qpool,
+                                                   const BatchFlags *__restrict__ flags) {
+  constexpr int LD = 72, RS = 9;
+  __shared__ int32_t blkv[32 * LD];
+  const uint32_t n = flags->idct_late < flags->idct_cap ? flags->idct_late : flags->idct_cap;
+  const DG_GLOBAL uint32_t *list = gp<const uint32_t>(flags->idct_list);
+  const int t = threadIdx.x, slot = t >> 3, lane = t & 7;
+  int32_t *bv = blkv + slot * LD;
+  for (uint32_t base = blockIdx.x * 32; base < n; base += gridDim.x * 32) {  // uniform per workgroup
+    const uint32_t e = base + (uint32_t)slot;
+    const bool act = e < n;
+    const uint32_t ii = act ? list[2 * e] : 0u, idx = act ? list[2 * e + 1] : 0u;
+    const ImageDesc &im = imgs[ii];
+    uint32_t c = 0, by = 0, bx = 0;
+    if (act) block_pos(im, idx, c, by, bx);
+    if (act) {
+      const u32x4 r0 = *(const DG_GLOBAL u32x4 *)(gp<const int16_t>(im.coef) + (size_t)idx * 64 + lane * 8);
+      int16_t a[8];
+      __builtin_memcpy(a, &r0, 16);
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int nn = kZigzagToNatural[lane * 8 + i];
+        bv[(nn >> 3) * RS + (nn & 7)] = a[i];
       }
     }
-    if (v) *(DG_GLOBAL u32x2 *)(plane + (size_t)(h ? bx1 : bx0) * 8) = u32x2{lo, hi};
+    __syncthreads();
+    int32_t w[8];
+    if (act) {
+      const DG_GLOBAL uint16_t *q = gp<const uint16_t>((uint64_t)(uintptr_t)qpool[im.qpool[c]].q);
+      int32_t v[8];
+#pragma unroll
+      for (int r = 0; r < 8; r++) v[r] = bv[r * RS + lane] * (int32_t)q[r * 8 + lane];
+      idct_col(im.sem != 0, v, w);
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int r = 0; r < 8; r++) bv[r * RS + lane] = w[r];
+    }
+    __syncthreads();
+    if (act) {
+      int32_t row[8];
+      uint32_t px[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) row[i] = bv[lane * RS + i];
+      idct_row(im.sem != 0, row, px);
+      DG_GLOBAL uint8_t *dst = gp<uint8_t>(im.plane[c]) + (size_t)(by * 8 + lane) * (im.cbw[c] * 8) + bx * 8;
+      *(DG_GLOBAL u32x2 *)dst = u32x2{pack4(px[0], px[1], px[2], px[3]), pack4(px[4], px[5], px[6], px[7])};
+    }
+    __syncthreads();
   }
 }
 
@@ -1548,10 +1611,16 @@ void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint3
   DG_LAUNCH(k_huff_scan, nwg, st, imgs, list, subs);
 }
 void launch_huff_write(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg,
-                       const HuffTable *pool, const SubState *subs, BatchFlags *flags, uint32_t max_slots) {
+                       const HuffTable *pool, const SubState *subs, BatchFlags *flags, uint32_t max_slots,
+                       const QuantTable *qpool) {
   if (!nwg) return;
   hipLaunchKernelGGL(k_huff_write, dim3(nwg), dim3(256), (size_t)max_slots * sizeof(HuffTable), st, imgs, list,
-                     pool, subs, flags);
+                     pool, subs, flags, qpool);
+}
+void launch_idct_list(hipStream_t st, const ImageDesc *imgs, const QuantTable *qpool, const BatchFlags *flags,
+                      uint32_t nwg) {
+  if (!nwg) return;
+  DG_LAUNCH(k_idct_list, nwg, st, imgs, qpool, flags);
 }
 void launch_huff_scatter(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                          const SubState *subs) {

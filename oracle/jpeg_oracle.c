@@ -622,6 +622,10 @@ static int decode_progressive(oj_jpeg *j, const uint8_t *d, size_t n) {
 #define FIX_3_072711026 ((int32_t)25172)
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 
+/* pass-1 workspace values saturate to 16 bits, as in libjpeg-turbo's SIMD
+ * IDCTs (vpackssdw between the passes); valid blocks never come near it */
+static inline int32_t sat16(int32_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+
 static inline uint8_t clamp_out(int32_t x) {
   /* libjpeg-turbo SIMD IDCT output: saturate to signed 8 bits, then +128 */
   if (x < -128) x = -128;
@@ -662,7 +666,7 @@ static void idct_islow(const int16_t *in, const uint16_t *q, uint8_t *out, int s
     int32_t o[8];
     IDCT_1D(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o[0], o[1], o[2], o[3], o[4], o[5],
             o[6], o[7]);
-    for (int r = 0; r < 8; r++) ws[r * 8 + c] = DESCALE(o[r], CONST_BITS - PASS1_BITS);
+    for (int r = 0; r < 8; r++) ws[r * 8 + c] = sat16(DESCALE(o[r], CONST_BITS - PASS1_BITS));
   }
   for (int r = 0; r < 8; r++) {
     const int32_t *w = ws + r * 8;
@@ -703,7 +707,7 @@ static void idct_zune(const int16_t *in, const uint16_t *q, uint8_t *out, int st
           const int32_t y = r[k];
           out[u * stride + k] = (uint8_t)(y < 0 ? 0 : y > 255 ? 255 : y);
         } else {
-          ws[k * 8 + u] = r[k];
+          ws[k * 8 + u] = sat16(r[k]);
         }
       }
     }

@@ -415,3 +415,21 @@ def test_full_size_regimes_subsequence_sizes(sub_bits):
     c.set_option("sub_bits", sub_bits)
     for (sa, xa, _), (sb, xb, _) in zip(a, c.decode_batch(datas)):
         assert sa == 0 and sb == 0 and np.array_equal(xa, xb)
+
+
+def test_fused_idct_option_bit_exact():
+    """Option idct_fused (off by default: k_huff_write 1.7 -> 12 ms measured,
+    DESIGN.md §5): completed blocks IDCT-ed inside the entropy write kernel's
+    cooperative flush, carried-in and few-lane blocks through k_idct_list.
+    Same pixels as the separate k_idct, every subsequence size."""
+    L = _lib()
+    datas = _rand_jpegs(12, 9, maxdim=900) + [synth.make_jpeg(77, 3, 2, 90, "4:2:0"),
+                                              synth.make_jpeg(78, 1, 1, 90, "4:4:4", gray=True)]
+    base = [a for _, a, _ in L.Context(0).decode_batch(datas)]
+    for sb in (0, 512, 16384):
+        c = L.Context(0)
+        c.set_option("idct_fused", 1)
+        if sb:
+            c.set_option("sub_bits", sb)
+        for k, ((st, a, _), b) in enumerate(zip(c.decode_batch(datas), base)):
+            assert st == 0 and np.array_equal(a, b), (sb, k)
