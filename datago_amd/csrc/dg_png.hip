@@ -481,126 +481,147 @@ __device__ __forceinline__ uint32_t zbits(const DG_GLOBAL uint32_t *z, uint32_t 
   return n >= 32 ? (uint32_t)v : (uint32_t)v & ((1u << n) - 1u);
 }
 
-// Does a dynamic-Huffman block header with valid, complete codes start at bit
-// `pos`?  (The checks zlib's inflate applies: HLIT <= 29, HDIST <= 29, a
-// complete code-length code, a well-formed run of code lengths, an
-// end-of-block code, complete literal/length and distance codes (a single
-// distance code is allowed).)  Per lane, serial; the cheap tests reject
-// almost every position within a few instructions.
-__device__ bool inf_header_ok(const DG_GLOBAL uint32_t *z, uint32_t zwords, uint32_t pos) {
-  // the 17-bit header and up to 19 x 3 code-length bits (74 bits) from 4 words
-  const uint32_t w = pos >> 5, sh = pos & 31u;
-  uint32_t q[4];
-#pragma unroll
-  for (uint32_t k = 0; k < 4; k++) q[k] = w + k < zwords ? z[w + k] : 0u;
+// Block-start candidates (k_inf_find).  A position qualifies when a
+// dynamic-Huffman block header with valid, complete codes starts there: the
+// checks zlib's inflate applies (HLIT <= 29, HDIST <= 29, a complete
+// code-length code, a well-formed run of code lengths, an end-of-block code,
+// a complete literal/length code, a complete distance code or a single
+// distance code).  Two stages:
+//  * inf_header_fast: header fields and the code-length code's Kraft sum, the
+//    same ~100 instructions in every lane (no divergence); rejects all but
+//    ~0.5% of positions;
+//  * inf_header_full for the survivors: decodes the code lengths with a
+//    register bit buffer and stops as soon as the literal/length or distance
+//    lengths over-subscribe their code (random bits do within a few dozen
+//    symbols), so a false survivor costs little.
+// A false candidate only costs time downstream (the chain skips it), and every
+// real dynamic block header passes, so this is a filter, not a decoder.
+
+// bits [pos, pos + 96) from the 4 words at pos >> 5 (q[]) and pos & 31
+__device__ __forceinline__ void inf_bits96(const uint32_t q[4], uint32_t sh, uint64_t &lo, uint64_t &hi) {
   const uint64_t a = (uint64_t)q[0] | ((uint64_t)q[1] << 32), b = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
-  const uint64_t lo = sh ? (a >> sh) | (b << (64 - sh)) : a, hi = b >> sh;  // bits [pos, pos + 96)
+  lo = sh ? (a >> sh) | (b << (64 - sh)) : a;
+  hi = b >> sh;
+}
+
+// Header fields + complete code-length code.  Returns the 5-bit-per-length
+// histogram of the code-length code (field k = codes of length k) or 0.
+__device__ __forceinline__ uint64_t inf_header_fast(uint64_t lo, uint64_t hi) {
   const uint32_t h = (uint32_t)lo & 0x1FFFFu;
-  if (((h >> 1) & 3u) != 2u) return false;
   const uint32_t nlen = ((h >> 3) & 31u) + 257, ndist = ((h >> 8) & 31u) + 1, ncode = ((h >> 13) & 15u) + 4;
-  if (nlen > 286 || ndist > 30) return false;
-  // code-length code: lengths of up to 19 symbols, 3 bits each, in c_clorder
-  uint32_t clcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t cll = 0;  // 3-bit length of symbol s at bits 3s
   const uint64_t clbits = (lo >> 17) | (hi << 47);  // bits [pos + 17, pos + 81)
-  for (uint32_t i = 0; i < ncode; i++) {
-    const uint32_t l = (uint32_t)(clbits >> (3 * i)) & 7u;
-    cll |= (uint64_t)l << (3 * c_clorder[i]);
-  }
-  pos += 17 + 3 * ncode;
-  for (uint32_t s = 0; s < 19; s++) {
-    const uint32_t l = (uint32_t)(cll >> (3 * s)) & 7u;
+  uint64_t hist = 0;
 #pragma unroll
-    for (uint32_t k = 1; k < 8; k++) clcnt[k] += l == k ? 1u : 0u;
+  for (uint32_t i = 0; i < 19; i++) {
+    const uint32_t l = i < ncode ? (uint32_t)(clbits >> (3 * i)) & 7u : 0u;
+    hist += 1ull << (5 * l);
   }
   int left = 1;
-  uint32_t first[8], offs[8], o = 0, code = 0;
+  bool bad = ((h >> 1) & 3u) != 2u || nlen > 286 || ndist > 30;
 #pragma unroll
   for (uint32_t k = 1; k < 8; k++) {
-    left = 2 * left - (int)clcnt[k];
-    if (left < 0) return false;
-    code = (code + (k > 1 ? clcnt[k - 1] : 0u)) << 1;
+    left = 2 * left - (int)((hist >> (5 * k)) & 31u);
+    bad |= left < 0;
+  }
+  bad |= left != 0;
+  return bad ? 0ull : hist | 1ull;  // bit 0 set: field 0 (length-0 count) is never read
+}
+
+__device__ bool inf_header_full(const DG_GLOBAL uint32_t *z, uint32_t zwords, uint32_t pos, uint64_t lo, uint64_t hi,
+                                uint64_t hist) {
+  const uint32_t h = (uint32_t)lo & 0x1FFFFu;
+  const uint32_t nlen = ((h >> 3) & 31u) + 257, ndist = ((h >> 8) & 31u) + 1, ncode = ((h >> 13) & 15u) + 4;
+  // code-length code: 3-bit lengths in c_clorder; canonical first code and
+  // rank offset per length; symbols sorted by (length, symbol), 5 bits each
+  uint64_t cll = 0;
+  const uint64_t clbits = (lo >> 17) | (hi << 47);
+  for (uint32_t i = 0; i < ncode; i++) cll |= ((clbits >> (3 * i)) & 7ull) << (3 * c_clorder[i]);
+  uint32_t first[8], offs[8], cnt[8], o = 0, code = 0;
+#pragma unroll
+  for (uint32_t k = 1; k < 8; k++) {
+    cnt[k] = (uint32_t)(hist >> (5 * k)) & 31u;
+    code = (code + (k > 1 ? cnt[k - 1] : 0u)) << 1;
     first[k] = k == 1 ? 0u : code;
     offs[k] = o;
-    o += clcnt[k];
+    o += cnt[k];
   }
-  if (left != 0) return false;  // incomplete code-length code
-  // decode the code lengths, counting the litlen / distance codes as we go
-  uint32_t lcnt[16], dcnt[16];
-#pragma unroll
-  for (uint32_t k = 0; k < 16; k++) lcnt[k] = dcnt[k] = 0;
-  uint32_t i = 0, prev = 0, eob = 0;
+  uint64_t sorted_lo = 0, sorted_hi = 0;  // rank r -> symbol at bits 5r (ranks 12.. in sorted_hi)
+  {
+    uint32_t r = 0;
+    for (uint32_t k = 1; k < 8; k++)
+      for (uint32_t s = 0; s < 19; s++)
+        if (((uint32_t)(cll >> (3 * s)) & 7u) == k) {
+          if (r < 12) sorted_lo |= (uint64_t)s << (5 * r);
+          else sorted_hi |= (uint64_t)s << (5 * (r - 12));
+          r++;
+        }
+  }
+  // code lengths through a register bit buffer
+  uint32_t p = pos + 17 + 3 * ncode;
+  uint32_t wp = p >> 5;
+  uint64_t bb = (wp < zwords ? z[wp] : 0u) >> (p & 31u);
+  uint32_t nb = 32 - (p & 31u);
+  wp++;
+  uint32_t i = 0, prev = 0, eob = 0, dn = 0, kl = 0, kd = 0;
   const uint32_t total = nlen + ndist;
   while (i < total) {
-    // bit-serial canonical decode of the code-length code (max 7 bits)
-    const uint32_t bitsv = zbits(z, zwords, pos, 7);
-    uint32_t sym = 99, len = 0, c = 0;
+    if (nb < 32) {
+      bb |= (uint64_t)(wp < zwords ? z[wp] : 0u) << nb;
+      nb += 32;
+      wp++;
+    }
+    const uint32_t bitsv = (uint32_t)bb;
+    uint32_t len = 0, rank = 0, c = 0;
 #pragma unroll
     for (uint32_t k = 1; k < 8; k++) {
       c = (c << 1) | ((bitsv >> (k - 1)) & 1u);
-      if (len == 0 && c - first[k] < clcnt[k]) {
+      if (len == 0 && c - first[k] < cnt[k]) {
         len = k;
-        sym = offs[k] + (c - first[k]);  // rank among codes: resolve to symbol below
+        rank = offs[k] + (c - first[k]);
       }
     }
     if (!len) return false;
-    // rank -> symbol (symbols of equal length in increasing order)
-    uint32_t r = sym, found = 99;
-    for (uint32_t s = 0; s < 19 && found == 99; s++) {
-      if (((uint32_t)(cll >> (3 * s)) & 7u) == len) {
-        if (r == offs[len]) found = s;
-        r--;
-      }
-    }
-    // r counts down from the rank: the symbol is the (rank - offs)th of its length
-    pos += len;
-    uint32_t v = 0, rep = 1;
-    if (found < 16) {
-      v = found;
-    } else if (found == 16) {
+    const uint32_t sym = rank < 12 ? (uint32_t)(sorted_lo >> (5 * rank)) & 31u
+                                   : (uint32_t)(sorted_hi >> (5 * (rank - 12))) & 31u;
+    bb >>= len;
+    nb -= len;
+    uint32_t v = sym, rep = 1;
+    if (sym == 16) {
       if (i == 0) return false;
       v = prev;
-      rep = 3 + zbits(z, zwords, pos, 2);
-      pos += 2;
-    } else if (found == 17) {
-      rep = 3 + zbits(z, zwords, pos, 3);
-      pos += 3;
-    } else if (found == 18) {
-      rep = 11 + zbits(z, zwords, pos, 7);
-      pos += 7;
-    } else {
-      return false;
+      rep = 3 + ((uint32_t)bb & 3u);
+      bb >>= 2;
+      nb -= 2;
+    } else if (sym == 17) {
+      v = 0;
+      rep = 3 + ((uint32_t)bb & 7u);
+      bb >>= 3;
+      nb -= 3;
+    } else if (sym == 18) {
+      v = 0;
+      rep = 11 + ((uint32_t)bb & 127u);
+      bb >>= 7;
+      nb -= 7;
     }
     if (i + rep > total) return false;
-    for (uint32_t k = 0; k < rep; k++, i++) {
-      if (i < nlen) {
-#pragma unroll
-        for (uint32_t q = 1; q < 16; q++) lcnt[q] += v == q ? 1u : 0u;
-        if (i == 256 && v) eob = 1;
-      } else {
-#pragma unroll
-        for (uint32_t q = 1; q < 16; q++) dcnt[q] += v == q ? 1u : 0u;
-      }
+    const uint32_t nl = i >= nlen ? 0u : min(rep, nlen - i), nd = rep - nl;
+    if (v) {
+      const uint32_t wgt = 1u << (15 - v);
+      kl += nl * wgt;
+      kd += nd * wgt;
+      dn += nd;
+      eob |= (i <= 256 && 256 < i + nl) ? 1u : 0u;
+      if (kl > 32768u || kd > 32768u) return false;  // over-subscribed
     }
     prev = v;
+    i += rep;
   }
-  if (!eob) return false;
-  int ll = 1, dl = 1;
-  uint32_t dn = 0;
-#pragma unroll
-  for (uint32_t q = 1; q < 16; q++) {
-    ll = 2 * ll - (int)lcnt[q];
-    dl = 2 * dl - (int)dcnt[q];
-    dn += dcnt[q];
-    if (ll < 0 || dl < 0) return false;
-  }
-  if (ll != 0) return false;
-  if (dl != 0 && !(dn == 1 && dcnt[1] == 1) && dn != 0) return false;
-  return true;
+  return eob && kl == 32768u && (kd == 32768u || dn == 0 || (dn == 1 && kd == 16384u));
 }
 
 // One wave per chunk (but chunk 0): the first candidate block start in the
-// chunk's bit range, 64 consecutive bit positions per step.
+// chunk's bit range, 64 consecutive bit positions per step (the 5 words they
+// span are wave-uniform loads).
 __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
                                                  const WgItem *__restrict__ list) {
   const WgItem it = list[blockIdx.x];
@@ -610,31 +631,48 @@ __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ i
   const uint32_t zlen = im.png.zlen, zwords = (zlen + 3) / 4;
   const uint32_t b0 = c.idx * kInfChunk * 8u;
   const uint32_t b1 = min((c.idx + 1) * kInfChunk * 8u, zlen * 8u);
+  const uint32_t lane = threadIdx.x, hl = lane >> 5, sh = lane & 31u;
   uint32_t found = kInfNone;
-  for (uint32_t p = b0; p < b1; p += 64) {
-    const uint32_t pos = p + threadIdx.x;
-    const bool ok = pos < b1 && inf_header_ok(z, zwords, pos);
+  for (uint32_t p = b0; p < b1; p += 64) {  // b0 and p are multiples of 64
+    const uint32_t W = uni(p >> 5);
+    uint32_t u[5];
+#pragma unroll
+    for (uint32_t k = 0; k < 5; k++) u[k] = uni(W + k < zwords ? z[W + k] : 0u);
+    uint32_t q[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) q[k] = hl ? u[k + 1] : u[k];
+    uint64_t lo, hi;
+    inf_bits96(q, sh, lo, hi);
+    const uint32_t pos = p + lane;
+    const uint64_t hist = pos < b1 ? inf_header_fast(lo, hi) : 0ull;
+    bool ok = false;
+    if (hist) ok = inf_header_full(z, zwords, pos, lo, hi, hist);
     const uint64_t m = __ballot(ok);
     if (m) {
       found = p + (uint32_t)__ffsll((long long)m) - 1u;
       break;
     }
   }
-  if (threadIdx.x == 0) c.start = found;
+  if (lane == 0) c.start = found;
 }
 
-// Per-lane canonical table in global scratch: lut[1 << B] = (sym << 4) | len
-// for codes of <= B bits, 0 for long-code prefixes / unused entries (then the
-// bit-serial walk over cnt/offs/sym); cnt/offs/sym as in puff.c.
+// Per-lane canonical Huffman table.  lut[1 << B] = (sym << 4) | len for codes
+// of <= B bits, 0 for prefixes of longer codes and unused prefixes; the
+// longer codes are walked bit-serially (puff.c's canonical decode) from length
+// B + 1 with that length's first code and symbol index and the per-length
+// counts held in registers, the symbol read from `sym` (sorted by length).
+// k_inf_decode keeps the literal/length and distance lookups in LDS.
+#define DG_LDS __attribute__((address_space(3)))
+template <uint32_t B, typename LutPtr>
 struct LaneTab {
-  DG_GLOBAL uint16_t *lut;
-  DG_GLOBAL uint16_t *cnt;   // [16]
-  DG_GLOBAL uint16_t *offs;  // [16]
-  DG_GLOBAL uint16_t *sym;   // [n]
-  uint32_t B;
+  LutPtr lut;
+  DG_GLOBAL uint16_t *sym;  // [n], by (length, symbol)
+  uint32_t first1, index1;  // canonical walk state at length B + 1
+  uint32_t cpk[3];          // counts of lengths B+1..15, 10 bits each, 3 per word
 };
 
-__device__ bool lane_build(const DG_GLOBAL uint8_t *lens, uint32_t n, LaneTab t) {
+template <uint32_t B, typename LutPtr>
+__device__ bool lane_build(const DG_GLOBAL uint8_t *lens, uint32_t n, LaneTab<B, LutPtr> &t) {
   uint32_t cnt[16];
 #pragma unroll
   for (uint32_t k = 0; k < 16; k++) cnt[k] = 0;
@@ -644,22 +682,27 @@ __device__ bool lane_build(const DG_GLOBAL uint8_t *lens, uint32_t n, LaneTab t)
     for (uint32_t k = 1; k < 16; k++) cnt[k] += l == k ? 1u : 0u;
   }
   int left = 1;
-  uint32_t next[16], o = 0, code = 0;
+  uint32_t next[16], pos[16], o = 0, code = 0, first = 0, index = 0;
 #pragma unroll
   for (uint32_t k = 1; k < 16; k++) {
     left = 2 * left - (int)cnt[k];
     code = (code + (k > 1 ? cnt[k - 1] : 0u)) << 1;
     next[k] = k == 1 ? 0u : code;
-    t.cnt[k] = (uint16_t)cnt[k];
-    t.offs[k] = (uint16_t)o;
+    pos[k] = o;
     o += cnt[k];
+    if (k == B + 1) {
+      t.first1 = first;
+      t.index1 = index;
+    }
+    index += cnt[k];
+    first = (first + cnt[k]) << 1;
   }
+  t.cpk[0] = t.cpk[1] = t.cpk[2] = 0;
+#pragma unroll
+  for (uint32_t k = B + 1; k < 16; k++) t.cpk[(k - B - 1) / 3] |= cnt[k] << (10 * ((k - B - 1) % 3));
   if (left < 0) return false;
   if (left > 0)  // incomplete: unused prefixes must read as invalid
-    for (uint32_t e = 0; e < (1u << t.B); e++) t.lut[e] = 0;
-  uint32_t pos[16];
-#pragma unroll
-  for (uint32_t k = 1; k < 16; k++) pos[k] = t.offs[k];
+    for (uint32_t e = 0; e < (1u << B); e++) t.lut[e] = 0;
   for (uint32_t s = 0; s < n; s++) {
     const uint32_t l = lens[s];
     if (!l) continue;
@@ -672,11 +715,11 @@ __device__ bool lane_build(const DG_GLOBAL uint8_t *lens, uint32_t n, LaneTab t)
       }
     t.sym[ps] = (uint16_t)s;
     const uint32_t rv = __builtin_bitreverse32(cd) >> (32 - l);
-    if (l <= t.B) {
+    if (l <= B) {
       const uint16_t e = (uint16_t)((s << 4) | l);
-      for (uint32_t x = rv; x < (1u << t.B); x += 1u << l) t.lut[x] = e;
+      for (uint32_t x = rv; x < (1u << B); x += 1u << l) t.lut[x] = e;
     } else {
-      t.lut[rv & ((1u << t.B) - 1u)] = 0;  // long code: its B-bit prefix takes the slow path
+      t.lut[rv & ((1u << B) - 1u)] = 0;  // long code: its B-bit prefix takes the slow path
     }
   }
   return true;
@@ -705,9 +748,10 @@ __device__ __forceinline__ uint32_t lb_get(LaneBits &r, uint32_t k) {
 // consumed bit position: wp counts the word held in w1
 __device__ __forceinline__ uint32_t lb_pos(const LaneBits &r) { return r.wp * 32u - r.nb; }
 
-__device__ __forceinline__ uint32_t lane_sym(LaneBits &r, const LaneTab &t) {
+template <uint32_t B, typename LutPtr>
+__device__ __forceinline__ uint32_t lane_sym(LaneBits &r, const LaneTab<B, LutPtr> &t) {
   const uint32_t peek = (uint32_t)r.bb;
-  const uint32_t e = t.lut[peek & ((1u << t.B) - 1u)];
+  const uint32_t e = t.lut[peek & ((1u << B) - 1u)];
   if (e & 15u) {
     const uint32_t l = e & 15u;
     r.bb >>= l;
@@ -715,10 +759,11 @@ __device__ __forceinline__ uint32_t lane_sym(LaneBits &r, const LaneTab &t) {
     return e >> 4;
   }
   const uint32_t rv = __builtin_bitreverse32(peek);
-  uint32_t first = 0, index = 0, code = 0;
-  for (uint32_t L = 1; L < 16; L++) {
-    code = rv >> (32 - L);
-    const uint32_t c = t.cnt[L];
+  uint32_t first = t.first1, index = t.index1;
+#pragma unroll
+  for (uint32_t L = B + 1; L < 16; L++) {
+    const uint32_t code = rv >> (32 - L);
+    const uint32_t c = (t.cpk[(L - B - 1) / 3] >> (10 * ((L - B - 1) % 3))) & 1023u;
     if (code - first < c) {
       r.bb >>= L;
       r.nb -= L;
@@ -729,6 +774,8 @@ __device__ __forceinline__ uint32_t lane_sym(LaneBits &r, const LaneTab &t) {
   }
   return 0xFFFFu;
 }
+
+constexpr uint32_t kInfLdsPerLane = (512 + 128) * 2;  // 80 KiB per 64-lane workgroup: 2 per CU
 
 // One lane per chunk: decode from the chunk's candidate block start until a
 // block ends exactly where a later chunk's candidate starts (or the stream
@@ -751,12 +798,13 @@ __global__ __launch_bounds__(64) void k_inf_decode(const ImageDesc *__restrict__
   DG_GLOBAL uint16_t *out = gp<uint16_t>(c.out);
   DG_GLOBAL uint8_t *tb = gp<uint8_t>(c.tab);
   DG_GLOBAL uint8_t *lens = tb + 3584;
-  LaneTab tl{(DG_GLOBAL uint16_t *)tb, (DG_GLOBAL uint16_t *)(tb + 2560), (DG_GLOBAL uint16_t *)(tb + 2592),
-             (DG_GLOBAL uint16_t *)(tb + 2624), 10};
-  LaneTab td{(DG_GLOBAL uint16_t *)(tb + 2048), (DG_GLOBAL uint16_t *)(tb + 3200), (DG_GLOBAL uint16_t *)(tb + 3232),
-             (DG_GLOBAL uint16_t *)(tb + 3264), 8};
-  LaneTab tc{(DG_GLOBAL uint16_t *)(tb + 3328), (DG_GLOBAL uint16_t *)(tb + 3456), (DG_GLOBAL uint16_t *)(tb + 3488),
-             (DG_GLOBAL uint16_t *)(tb + 3520), 6};
+  // LDS: per lane a 9-bit literal/length and a 7-bit distance lookup
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+  DG_LDS uint16_t *lds = (DG_LDS uint16_t *)(DG_LDS uint8_t *)smem_raw + threadIdx.x * kInfLdsPerLane / 2;
+  LaneTab<9, DG_LDS uint16_t *> tl{lds, (DG_GLOBAL uint16_t *)(tb + 2624), 0, 0, {0, 0, 0}};
+  LaneTab<7, DG_LDS uint16_t *> td{lds + 512, (DG_GLOBAL uint16_t *)(tb + 3264), 0, 0, {0, 0, 0}};
+  LaneTab<6, DG_GLOBAL uint16_t *> tc{(DG_GLOBAL uint16_t *)(tb + 3328), (DG_GLOBAL uint16_t *)(tb + 3520), 0, 0,
+                                      {0, 0, 0}};
   const uint32_t zbits_total = pd.zlen * 8u;
   LaneBits r;
   r.zwords = (pd.zlen + 3) / 4;
@@ -1334,7 +1382,12 @@ void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const 
   if (nwg) hipLaunchKernelGGL(k_inf_find, dim3(nwg), dim3(64), 0, st, imgs, ch, list);
 }
 void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch) {
-  if (nch) hipLaunchKernelGGL(k_inf_decode, dim3((nch + 63) / 64), dim3(64), 0, st, imgs, ch, nch);
+  static bool attr = false;  // > 64 KiB of dynamic LDS
+  if (!attr) {
+    hipFuncSetAttribute((const void *)k_inf_decode, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * kInfLdsPerLane);
+    attr = true;
+  }
+  if (nch) hipLaunchKernelGGL(k_inf_decode, dim3((nch + 63) / 64), dim3(64), 64 * kInfLdsPerLane, st, imgs, ch, nch);
 }
 void launch_inf_resolve(hipStream_t st, ImageDesc *imgs, const InfChunk *ch, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_inf_resolve, dim3(nwg), dim3(1024), 0, st, imgs, ch, list);
