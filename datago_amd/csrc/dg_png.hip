@@ -3,7 +3,7 @@
 //
 //   k_png_gather    IDAT payloads -> one contiguous zlib stream per image
 //   k_png_inflate   zlib/DEFLATE -> filtered scanlines, one wave per image
-//   k_png_unfilter  scanline filters -> samples, one wave per image
+//   k_png_unfilter  scanline filters -> samples, one wave per 64-row band
 //   k_png_expand    palette / sub-byte gray / tRNS -> 8-bit L, LA, RGB, RGBA
 //   k_alpha         premultiply / divide by alpha, in place
 //
@@ -1040,7 +1040,7 @@ __global__ __launch_bounds__(1024) void k_inf_resolve(ImageDesc *__restrict__ im
 
 // ------------------------------------------------------------ unfilter
 
-// One wave per image.  Rows are taken 64 at a time, lane l owning row y0 + l,
+// One wave per band of 64 rows, lane l owning row y0 + l,
 // on a diagonal: at step t lane l unfilters pixel x = t - l, so the pixel
 // above (row y-1, x) and above-left (x-1) were produced by lane l-1 at steps
 // t-1 and t-2 and arrive by a lane shuffle; the left pixel is the lane's own
@@ -1085,11 +1085,40 @@ __device__ __forceinline__ uint32_t unfilter_unit(uint32_t f, uint32_t rawv, uin
   return v;
 }
 
-// One filtered plane (the image, or one Adam7 pass): H rows of 1 + rb bytes
-// at raw_a -> H rows of rb bytes at stride us at unf_a.
+// Progress of a band (one 64-row band of one plane): tiles of its rows stored
+// to HBM, kUfDone when the band is finished or skipped.  The next band of the
+// plane reads this band's last row tile by tile as it becomes available, so
+// consecutive bands run as a pipeline on different CUs, about three tiles
+// apart.
+constexpr uint32_t kUfDone = 0xFFFFFFFFu;
+
+// (every lane stores the same value: no lane-0 branch in the waves' control
+// flow, which the compiler's loop structurizer mishandled here)
+__device__ __forceinline__ void uf_publish(DG_GLOBAL uint32_t *flag, uint32_t v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's tile stores before the flag
+  __hip_atomic_store((uint32_t *)flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until *flag >= need.  False after ~1 s (a producer that never comes:
+// the caller marks the image bad rather than hang the device).
+__device__ __forceinline__ bool uf_wait(const DG_GLOBAL uint32_t *flag, uint32_t need) {
+  for (uint32_t spin = 0;; spin++) {
+    const uint32_t v = uni(__hip_atomic_load((uint32_t *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (v >= need) break;
+    if (spin > (1u << 21)) return false;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return true;
+}
+
+// Rows [y0, y0 + 64) of one filtered plane (the image, or one Adam7 pass) of
+// H rows of 1 + rb bytes at raw_a -> rows of rb bytes at stride us at unf_a.
+// `pred` is the previous band's progress flag (null for the first band).
 template <uint32_t BPP>
-__device__ void unfilter_image(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, uint64_t unf_a, uint32_t rb,
-                               uint32_t us, uint32_t H) {
+__device__ void unfilter_band(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, uint64_t unf_a, uint32_t rb,
+                              uint32_t us, uint32_t H, uint32_t y0, DG_GLOBAL uint32_t *self,
+                              const DG_GLOBAL uint32_t *pred) {
   const uint32_t lane = threadIdx.x;
   const uint32_t units = rb / BPP;  // BPP == 1 covers sub-byte samples (filter unit = 1 byte)
   const uint32_t tb = kUfTile * BPP;
@@ -1097,7 +1126,7 @@ __device__ void unfilter_image(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, 
   const DG_GLOBAL uint8_t *raw = gp<const uint8_t>(raw_a);
   DG_GLOBAL uint8_t *unf = gp<uint8_t>(unf_a);
   int bad = 0;
-  for (uint32_t y0 = 0; y0 < H; y0 += 64) {
+  {
     const uint32_t nrows = H - y0 < 64 ? H - y0 : 64;
     const bool active = lane < nrows;
     uint32_t f = active ? raw[(size_t)(y0 + lane) * (rb + 1)] : 0u;
@@ -1123,6 +1152,7 @@ __device__ void unfilter_image(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, 
                                              (__attribute__((address_space(3))) void *)(T[r] + 4 * w0), 4, 0, 0);
       }
       if (y0) {
+        if (!uf_wait(pred, k + 1)) bad = 1;
         const uint64_t a = unf_a + (uint64_t)(y0 - 1) * us + b0;
         const uint32_t nw = (nb + 3) / 4;
         for (uint32_t w0 = 0; w0 < nw; w0 += 64)
@@ -1160,6 +1190,7 @@ __device__ void unfilter_image(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, 
         if (k >= 2) {
           store_tile(k - 2);
           stored = k - 1;
+          uf_publish(self, stored);
         }
         if (k + 1 < ntiles) load_tile(k + 1);
         __syncthreads();
@@ -1223,39 +1254,57 @@ __device__ void unfilter_image(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, 
     }
     __syncthreads();
     for (uint32_t k = stored; k < ntiles; k++) store_tile(k);
-    // the next band's tiles read this band's last row from HBM
-    __threadfence();
-    __syncthreads();
   }
   if (__ballot(bad) && lane == 0) im.status = 2;
 }
 
-__global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
+// Persistent workers over the batch's bands: a worker takes the next band in
+// ticket order (bands of all planes round-robin, band 0 of every plane first),
+// so a band's predecessor was always taken earlier by a running worker and
+// every wait ends (no dependence on which workgroups are resident).
+__global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ tasks,
+                                                     uint32_t ntasks, uint32_t *__restrict__ flags_,
+                                                     uint32_t *__restrict__ ticket) {
   __shared__ __attribute__((aligned(16))) UnfilterSmem sm;
-  const WgItem it = list[blockIdx.x];
-  ImageDesc &im = imgs[it.image];
-  if (im.status) return;
-  const PngDesc &pd = im.png;
-  const uint32_t np = pd.interlace ? 7u : 1u;
-  const uint32_t spp = pd.ctype == 2 ? 3u : pd.ctype == 4 ? 2u : pd.ctype == 6 ? 4u : 1u;
-  for (uint32_t p = 0; p < np; p++) {
+  __shared__ uint32_t s_ticket;
+  DG_GLOBAL uint32_t *flags = gp<uint32_t>((uint64_t)(uintptr_t)flags_);
+  for (;;) {
+    if (threadIdx.x == 0) s_ticket = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t t = s_ticket;
+    __syncthreads();
+    if (t >= ntasks) break;
+    const WgItem it = tasks[t];
+    ImageDesc &im = imgs[it.image];
+    const PngDesc &pd = im.png;
+    const uint32_t pass = it.item0 >> 24, band = it.item0 & 0xFFFFFFu;
     uint64_t ra = pd.raw, ua = pd.unf;
-    uint32_t rb = pd.rowbytes, us = pd.ustride, H = im.height;
-    if (pd.interlace) {  // Adam7 pass p: a sub-image of its own (PNG spec 8.2)
-      const A7Pass a = png_adam7(im.width, im.height, spp * pd.depth, p);
-      if (!a.pw || !a.ph) continue;
+    uint32_t rb = pd.rowbytes, us = pd.ustride, H = im.height, foff = 0;
+    if (pd.interlace) {  // Adam7 pass: a sub-image of its own (PNG spec 8.2)
+      const uint32_t spp = pd.ctype == 2 ? 3u : pd.ctype == 4 ? 2u : pd.ctype == 6 ? 4u : 1u;
+      const A7Pass a = png_adam7(im.width, im.height, spp * pd.depth, pass);
       ra += a.raw_off;
       ua += a.unf_off;
       rb = a.rb;
       us = a.us;
       H = a.ph;
+      for (uint32_t q = 0; q < pass; q++) {
+        uint32_t pw, ph;
+        png_adam7_pass(im.width, im.height, q, pw, ph);
+        if (pw && ph) foff += (ph + 63) / 64;
+      }
     }
-    switch (pd.bpp) {
-      case 1: unfilter_image<1>(sm, im, ra, ua, rb, us, H); break;
-      case 2: unfilter_image<2>(sm, im, ra, ua, rb, us, H); break;
-      case 3: unfilter_image<3>(sm, im, ra, ua, rb, us, H); break;
-      default: unfilter_image<4>(sm, im, ra, ua, rb, us, H); break;
+    DG_GLOBAL uint32_t *self = flags + pd.uf_flag0 + foff + band;
+    const DG_GLOBAL uint32_t *pred = band ? self - 1 : nullptr;
+    if (!uni(im.status)) {  // (an image whose inflate failed has nothing to unfilter)
+      switch (pd.bpp) {
+        case 1: unfilter_band<1>(sm, im, ra, ua, rb, us, H, band * 64, self, pred); break;
+        case 2: unfilter_band<2>(sm, im, ra, ua, rb, us, H, band * 64, self, pred); break;
+        case 3: unfilter_band<3>(sm, im, ra, ua, rb, us, H, band * 64, self, pred); break;
+        default: unfilter_band<4>(sm, im, ra, ua, rb, us, H, band * 64, self, pred); break;
+      }
     }
+    uf_publish(self, kUfDone);  // the next band's tiles read this band's last row from HBM
   }
 }
 
@@ -1371,8 +1420,8 @@ void launch_png_gather(hipStream_t st, const GatherJob *jobs, const WgItem *list
 void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   static bool attr = false;  // > 64 KiB of dynamic LDS
   if (!attr) {
-    hipFuncSetAttribute((const void *)k_png_inflate, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)sizeof(InflateSmem));
+    (void)hipFuncSetAttribute((const void *)k_png_inflate, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sizeof(InflateSmem));
     attr = true;
   }
   if (nwg)
@@ -1384,7 +1433,8 @@ void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const 
 void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch) {
   static bool attr = false;  // > 64 KiB of dynamic LDS
   if (!attr) {
-    hipFuncSetAttribute((const void *)k_inf_decode, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * kInfLdsPerLane);
+    (void)hipFuncSetAttribute((const void *)k_inf_decode, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              64 * kInfLdsPerLane);
     attr = true;
   }
   if (nch) hipLaunchKernelGGL(k_inf_decode, dim3((nch + 63) / 64), dim3(64), 64 * kInfLdsPerLane, st, imgs, ch, nch);
@@ -1392,8 +1442,11 @@ void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint
 void launch_inf_resolve(hipStream_t st, ImageDesc *imgs, const InfChunk *ch, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_inf_resolve, dim3(nwg), dim3(1024), 0, st, imgs, ch, list);
 }
-void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
-  if (nwg) hipLaunchKernelGGL(k_png_unfilter, dim3(nwg), dim3(64), 0, st, imgs, list);
+void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
+                         uint32_t nworkers) {
+  // flags: ntasks progress words + the ticket counter, zeroed by the caller
+  const uint32_t g = std::min(ntasks, nworkers);
+  if (g) hipLaunchKernelGGL(k_png_unfilter, dim3(g), dim3(64), 0, st, imgs, tasks, ntasks, flags, flags + ntasks);
 }
 void launch_png_expand(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_png_expand, dim3(nwg), dim3(256), 0, st, imgs, list);

@@ -118,7 +118,8 @@ constexpr int kStages = 4;  // R1.H, R1.V, R2.H, R2.V
 constexpr uint32_t kFmtJpeg = 0, kFmtPng = 1;
 // IDAT payloads are gathered into one contiguous zlib stream (k_png_gather),
 // inflated into filtered scanlines (k_png_inflate, one wave per image),
-// unfiltered (k_png_unfilter, one wave per image, 64-row diagonal wavefront)
+// unfiltered (k_png_unfilter, one wave per 64-row band on a diagonal
+// wavefront, consecutive bands pipelined across CUs)
 // and, for palette / sub-byte / tRNS images, expanded to 8-bit L/LA/RGB/RGBA
 // (k_png_expand).
 struct PngDesc {
@@ -137,6 +138,7 @@ struct PngDesc {
   uint32_t serial;    // set by the chunked path when the image must be inflated serially
   uint32_t interlace; // Adam7: raw/unf hold the 7 passes back to back (png_adam7_*)
   uint32_t rawlen;    // inflated bytes expected
+  uint32_t uf_flag0;  // k_png_unfilter: first band progress flag of this image
 };
 
 // Adam7 pass p of a W x H image (PNG spec 8.2): origin (x0, y0), spacing (dx, dy)

@@ -37,6 +37,20 @@ static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; 
 // Boundary-repair rounds (finish()) before a batch is declared unsettled.
 static constexpr int kMaxResyncRounds = 64;
 
+// 64-row unfilter bands of pass p of a PNG (the image itself when not
+// interlaced); k_png_unfilter numbers its progress flags the same way.
+static uint32_t png_pass_bands(const ImageDesc &d, uint32_t p) {
+  if (!d.png.interlace) return p == 0 ? (d.height + 63) / 64 : 0u;
+  uint32_t pw, ph;
+  png_adam7_pass(d.width, d.height, p, pw, ph);
+  return pw && ph ? (ph + 63) / 64 : 0u;
+}
+static uint32_t png_bands(const ImageDesc &d) {
+  uint32_t n = 0;
+  for (uint32_t p = 0; p < 7; p++) n += png_pass_bands(d, p);
+  return n;
+}
+
 static const char *kStageNames[] = {"upload",     "png_inflate", "png_unfilter", "destuff",   "prog_scans",
                                     "huff_sync",  "huff_fix",    "huff_scan",    "huff_write", "coeffs",
                                     "idct",       "color",       "resize_h1",    "resize_v1", "resize_h2",
@@ -100,6 +114,11 @@ dg_status Context::init() {
     return DG_ERR_INVALID;
   }
   HIPCHK(hipSetDevice(device_));
+  {
+    int ncu = 0;
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_));
+    if (ncu > 0) ncu_ = (uint32_t)ncu;
+  }
   HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&ev_meta_, hipEventDisableTiming));
@@ -1011,6 +1030,14 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     b.enctab_off = b.blob.size();
     b.blob.insert(b.blob.end(), (const uint8_t *)&et, (const uint8_t *)&et + sizeof(et));
   }
+  // PNG unfilter: one progress flag per 64-row band of every plane
+  b.uf_n = 0;
+  for (ImageDesc &dd : b.descs)
+    if (dd.fmt == kFmtPng) {
+      dd.png.uf_flag0 = b.uf_n;
+      b.uf_n += png_bands(dd);
+    }
+  b.uf_flags_off = b.uf_n ? L.take((size_t)(b.uf_n + 1) * 4) : 0;
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
   const size_t ckpt_off = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits)) * sizeof(Ckpt));
   // fused IDCT leftovers: at most one carried-in block per subsequence, plus
@@ -1243,6 +1270,29 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   for (uint32_t j = 0; j < (uint32_t)b.gjobs.size(); j++)
     for (uint32_t pc = 0; pc * kGatherPiece < b.gjobs[j].len; pc++) b.lists[L_GATHER].push_back({j, pc});
+  if (b.uf_n) {  // unfilter bands in ticket order: the j-th band of every plane, j = 0, 1, ...
+    std::vector<std::vector<uint32_t>> per;  // per PNG image: pass << 24 | band, pass-major
+    std::vector<uint32_t> who;
+    for (uint32_t di = 0; di < (uint32_t)b.descs.size(); di++) {
+      const ImageDesc &d = b.descs[di];
+      if (d.fmt != kFmtPng) continue;
+      std::vector<uint32_t> v;
+      for (uint32_t p = 0; p < (d.png.interlace ? 7u : 1u); p++) {
+        const uint32_t nb = png_pass_bands(d, p);
+        for (uint32_t k = 0; k < nb; k++) v.push_back(p << 24 | k);
+      }
+      per.push_back(std::move(v));
+      who.push_back(di);
+    }
+    for (size_t j = 0, more = 1; more; j++) {
+      more = 0;
+      for (size_t i = 0; i < per.size(); i++)
+        if (j < per[i].size()) {
+          b.lists[L_UNF].push_back({who[i], per[i][j]});
+          more = 1;
+        }
+    }
+  }
   b.prog_level_n.clear();
   for (uint32_t j = 0; j < (uint32_t)b.pscans.size(); j++) {  // L_PROG: scans grouped by level
     const uint32_t lv = b.pscans[j].level;
@@ -1362,7 +1412,11 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   }
   if (next()) return DG_ERR_DEVICE;
   if (!from_fix && b.any_png) {
-    launch_png_unfilter(sl.st, dm, lst(L_PNG), cnt(L_PNG));
+    if (b.uf_n) {
+      uint32_t *uf = (uint32_t *)((char *)sl.scratch.p + b.uf_flags_off);
+      HIPCHK(hipMemsetAsync(uf, 0, (size_t)(b.uf_n + 1) * 4, sl.st));
+      launch_png_unfilter(sl.st, dm, lst(L_UNF), cnt(L_UNF), uf, ncu_);
+    }
     launch_png_expand(sl.st, dd, lst(L_EXPAND), cnt(L_EXPAND));
   }
   if (next()) return DG_ERR_DEVICE;

@@ -59,6 +59,8 @@ struct Batch {
   size_t gjob_off = 0;
   std::vector<InfChunk> ichunks;  // chunk-parallel inflate records (kernels fill start/len/stop/status)
   size_t ichunk_off = 0;
+  uint32_t uf_n = 0;        // PNG unfilter bands (progress flags, L_UNF tasks)
+  size_t uf_flags_off = 0;  // their flags + ticket in the scratch arena (zeroed per batch)
   std::vector<uint8_t> blob;
   size_t blob_off = 0;
   bool any_png = false, any_alpha = false, any_enc = false;
@@ -84,8 +86,8 @@ struct Batch {
   dg_payload_meta *metas = nullptr;
   bool done = false;
   int resync_rounds = 0;
-  bool unsettled = false;
-  std::vector<size_t> enc_host_off;  // host_io + encode: offset of image i's payload in the pinned read-back  // resync hit kMaxResyncRounds: JPEGs go back as DG_ERR_UNSUPPORTED
+  bool unsettled = false;             // resync hit kMaxResyncRounds: JPEGs go back as DG_ERR_UNSUPPORTED
+  std::vector<size_t> enc_host_off;  // host_io + encode: offset of image i's payload in the pinned read-back
   BatchFlags flags = {0, 0, 0, 0};
   std::vector<float> stage_ms;
 };
@@ -119,6 +121,7 @@ enum ListId {
   L_ENC_MCU, L_ENC_BLK, L_ENC_IMG,                          // JPEG re-encode
   L_PROG_ZERO, L_PROG,                                      // progressive JPEG
   L_PENC_ROW, L_PENC_PIECE, L_PENC_IMG,                     // PNG re-encode
+  L_UNF,                                                    // PNG unfilter bands (ticket order)
   L_COUNT
 };
 static_assert((int)L_COUNT <= 32, "Batch::lists");
@@ -195,6 +198,7 @@ class Context {
   DevBuf d_hpool_, d_qpool_;
 
   Slot slots_[kMaxInflight];
+  uint32_t ncu_ = 256;  // compute units: persistent-worker grids
   int nslots_ = 2;  // option "slots": batches in flight (each slot: own streams + scratch)
   int next_slot_ = 0;
   uint64_t next_ticket_ = 1;
