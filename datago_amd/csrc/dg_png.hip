@@ -619,11 +619,26 @@ __device__ bool inf_header_full(const DG_GLOBAL uint32_t *z, uint32_t zwords, ui
   return eob && kl == 32768u && (kd == 32768u || dn == 0 || (dn == 1 && kd == 16384u));
 }
 
+// Both stages at one position (the full one only if the fast one passes).
+__device__ __forceinline__ bool inf_candidate(const DG_GLOBAL uint32_t *z, uint32_t zwords, uint32_t pos) {
+  const uint32_t w = pos >> 5;
+  uint32_t q[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) q[k] = w + k < zwords ? z[w + k] : 0u;
+  uint64_t lo, hi;
+  inf_bits96(q, pos & 31u, lo, hi);
+  const uint64_t hist = inf_header_fast(lo, hi);
+  return hist && inf_header_full(z, zwords, pos, lo, hi, hist);
+}
+
 // One wave per chunk (but chunk 0): the first candidate block start in the
-// chunk's bit range, 64 consecutive bit positions per step (the 5 words they
-// span are wave-uniform loads).
+// chunk's bit range.  64 consecutive bit positions per step through the fast
+// stage (the 5 words they span are wave-uniform loads); the survivors queue
+// up in LDS in position order and go through the full stage 64 at a time, one
+// per lane, so the wave does not serialise on one lane's check per step.
 __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
                                                  const WgItem *__restrict__ list) {
+  __shared__ uint32_t qpos[128];
   const WgItem it = list[blockIdx.x];
   InfChunk &c = ch[it.image];
   const ImageDesc &im = imgs[c.image];
@@ -632,26 +647,58 @@ __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ i
   const uint32_t b0 = c.idx * kInfChunk * 8u;
   const uint32_t b1 = min((c.idx + 1) * kInfChunk * 8u, zlen * 8u);
   const uint32_t lane = threadIdx.x, hl = lane >> 5, sh = lane & 31u;
-  uint32_t found = kInfNone;
-  for (uint32_t p = b0; p < b1; p += 64) {  // b0 and p are multiples of 64
-    const uint32_t W = uni(p >> 5);
-    uint32_t u[5];
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t found = kInfNone, qn = 0;
+  // words W..W+4 of the current step (W = p / 32) and W+5, W+6 (the next
+  // step's new ones), loaded a step ahead
+  auto word = [&](uint32_t w) { return uni(w < zwords ? z[w] : 0u); };
+  uint32_t u[5], n5 = 0, n6 = 0;
+  {
+    const uint32_t W = b0 >> 5;
 #pragma unroll
-    for (uint32_t k = 0; k < 5; k++) u[k] = uni(W + k < zwords ? z[W + k] : 0u);
-    uint32_t q[4];
+    for (uint32_t k = 0; k < 5; k++) u[k] = word(W + k);
+    n5 = word(W + 5);
+    n6 = word(W + 6);
+  }
+  for (uint32_t p = b0;; p += 64) {  // b0 and p are multiples of 64
+    const bool more = p < b1;
+    if (more) {
+      uint32_t q[4];
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) q[k] = hl ? u[k + 1] : u[k];
-    uint64_t lo, hi;
-    inf_bits96(q, sh, lo, hi);
-    const uint32_t pos = p + lane;
-    const uint64_t hist = pos < b1 ? inf_header_fast(lo, hi) : 0ull;
-    bool ok = false;
-    if (hist) ok = inf_header_full(z, zwords, pos, lo, hi, hist);
-    const uint64_t m = __ballot(ok);
-    if (m) {
-      found = p + (uint32_t)__ffsll((long long)m) - 1u;
-      break;
+      for (uint32_t k = 0; k < 4; k++) q[k] = hl ? u[k + 1] : u[k];
+      uint64_t lo, hi;
+      inf_bits96(q, sh, lo, hi);
+      const bool pass = p + lane < b1 && inf_header_fast(lo, hi) != 0;
+      const uint64_t m = __ballot(pass);
+      if (pass) qpos[qn + (uint32_t)__popcll(m & below)] = p + lane;
+      qn += (uint32_t)__popcll(m);
+      u[0] = u[2];
+      u[1] = u[3];
+      u[2] = u[4];
+      u[3] = n5;
+      u[4] = n6;
+      n5 = word((p >> 5) + 7);
+      n6 = word((p >> 5) + 8);
     }
+    // full checks, oldest 64 survivors first (all remaining ones at the end)
+    while (qn >= 64 || (!more && qn > 0)) {
+      __syncthreads();
+      const uint32_t nb = qn < 64 ? qn : 64u;
+      const uint32_t pos = qpos[lane < nb ? lane : 0];
+      const bool ok = lane < nb && inf_candidate(z, zwords, pos);
+      const uint64_t mo = __ballot(ok);
+      if (mo) {
+        found = uni(qpos[__ffsll((long long)mo) - 1]);
+        break;
+      }
+      const uint32_t rest = qn - nb;  // < 64
+      const uint32_t keep = lane < rest ? qpos[64 + lane] : 0u;
+      __syncthreads();
+      if (lane < rest) qpos[lane] = keep;
+      qn = rest;
+    }
+    if (found != kInfNone || !more) break;
+    __syncthreads();
   }
   if (lane == 0) c.start = found;
 }
