@@ -436,18 +436,27 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
         break;
       }
       stash_flush();
-      // every source byte lies before `op`: one read + one write per lane and 64 bytes
+      // every source byte lies before `op` (an overlapping copy repeats the
+      // first `dist` bytes), so all <= 5 reads per lane go out before the
+      // writes: one LDS round trip per match
       const uint32_t q = op, src0 = op - dist;
       const float rcp = 1.0f / (float)dist;
-      for (uint32_t j = lane; j < len; j += 64) {
+      uint32_t v[5];
+#pragma unroll
+      for (uint32_t i = 0; i < 5; i++) {  // len <= 258
+        const uint32_t j = lane + 64 * i;
         uint32_t k = j;
         if (dist < len) {
           uint32_t qt = (uint32_t)((float)j * rcp);
           k = j - qt * dist;
           if (k >= dist) k -= dist;
         }
-        const uint8_t v = sm.ring[(src0 + k) & kRingMask];
-        sm.ring[(q + j) & kRingMask] = v;
+        v[i] = j < len ? sm.ring[(src0 + k) & kRingMask] : 0u;
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < 5; i++) {
+        const uint32_t j = lane + 64 * i;
+        if (j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)v[i];
       }
       op += len;
       if (op >= want) break;
