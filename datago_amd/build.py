@@ -36,7 +36,7 @@ SOURCES = [
 ]
 
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
-          f"-I{CSRC}", f"-I{os.path.join(ROOT, 'include')}"]
+          f"-I{CSRC}", f"-I{os.path.join(ROOT, 'include')}"] + os.environ.get("DG_HIPCC_FLAGS", "").split()
 
 
 def _obj(src: str) -> str:
