@@ -308,7 +308,14 @@ static inline int getbits(oj_bits *b, int k) {
   return v;
 }
 
+/* Huffman symbols decoded since the last reset (tools/entropy_per_symbol.py:
+ * instructions per symbol of the GPU entropy kernels). */
+static unsigned long long g_symbols = 0;
+unsigned long long oj_symbol_count(void) { return g_symbols; }
+void oj_reset_symbol_count(void) { g_symbols = 0; }
+
 static inline int decode_sym(oj_bits *b, const oj_huff *t) {
+  g_symbols++;
   if (b->nbits < 16) fill(b);
   int code = 0;
   for (int l = 1; l <= 16; l++) {

@@ -39,6 +39,7 @@ def lib() -> ctypes.CDLL:
         ip = ctypes.POINTER(ctypes.c_int)
         L.oj_info.argtypes = [u8p, ctypes.c_size_t, ip, ip, ip]
         L.oj_set_semantics.argtypes = [ctypes.c_int]
+        L.oj_symbol_count.restype = ctypes.c_ulonglong
         L.oj_decode.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, ip, ip, ip]
         L.oj_decode_coefs.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int16),
                                       ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
