@@ -23,8 +23,11 @@ def emu():
     srcs = [os.path.join(NATIVE, "emu.cpp"), os.path.join(ROOT, "datago_amd", "csrc", "host", "jpeg_header.cpp")]
     deps = srcs + [os.path.join(ROOT, "datago_amd", "csrc", f) for f in ("dg_entropy.h", "dg_types.h")]
     if not os.path.exists(SO) or any(os.path.getmtime(p) > os.path.getmtime(SO) for p in deps):
+        # build beside it and rename: parallel test workers never load a half-written library
+        tmp = f"{SO}.{os.getpid()}.tmp"
         subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-                        "-I" + os.path.join(ROOT, "datago_amd", "csrc"), "-o", SO] + srcs, check=True)
+                        "-I" + os.path.join(ROOT, "datago_amd", "csrc"), "-o", tmp] + srcs, check=True)
+        os.replace(tmp, SO)
     E = ctypes.CDLL(SO)
     E.emu_set_lead.argtypes = [ctypes.c_uint32]
     E.emu_decode_coefs.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32,
