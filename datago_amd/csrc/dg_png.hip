@@ -223,13 +223,17 @@ __device__ __forceinline__ void flush_ring(InflateSmem &sm, DG_GLOBAL uint8_t *o
   }
 }
 
-__global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
+// mode 0: streams too small to chunk (launched beside the chunked kernels);
+// 1: images the chunked path gave up on (pd.serial, after k_inf_resolve);
+// 2: both (one launch after the chunked kernels)
+__global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
+                                                    int mode) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   InflateSmem &sm = *reinterpret_cast<InflateSmem *>(smem_raw);
   const WgItem it = list[blockIdx.x];
   ImageDesc &im = imgs[it.image];
   const PngDesc &pd = im.png;
-  if (pd.nchunks && !pd.serial) return;  // the chunk-parallel path produced this image
+  if (mode == 0 ? pd.nchunks != 0 : mode == 1 ? !(pd.nchunks && pd.serial) : (pd.nchunks && !pd.serial)) return;
   const uint32_t lane = threadIdx.x;
   const DG_GLOBAL uint32_t *z = gp<const uint32_t>(pd.zs);
   DG_GLOBAL uint8_t *out = gp<uint8_t>(pd.raw);
@@ -1473,7 +1477,7 @@ __global__ __launch_bounds__(256) void k_alpha(const ImageDesc *__restrict__ img
 void launch_png_gather(hipStream_t st, const GatherJob *jobs, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_png_gather, dim3(nwg), dim3(256), 0, st, jobs, list);
 }
-void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
+void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, int mode) {
   static bool attr = false;  // > 64 KiB of dynamic LDS
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)k_png_inflate, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1481,7 +1485,7 @@ void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
     attr = true;
   }
   if (nwg)
-    hipLaunchKernelGGL(k_png_inflate, dim3(nwg), dim3(64), sizeof(InflateSmem), st, imgs, list);
+    hipLaunchKernelGGL(k_png_inflate, dim3(nwg), dim3(64), sizeof(InflateSmem), st, imgs, list, mode);
 }
 void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_inf_find, dim3(nwg), dim3(64), 0, st, imgs, ch, list);

@@ -74,7 +74,7 @@ Context::~Context() {
   for (Slot &sl : slots_) {
     for (auto e : sl.ev) hipEventDestroy(e);
     if (sl.done) hipEventDestroy(sl.done);
-    for (hipEvent_t e : {sl.ev_meta, sl.ev_coef, sl.ev_zero})
+    for (hipEvent_t e : {sl.ev_meta, sl.ev_coef, sl.ev_zero, sl.ev_png0, sl.ev_png1})
       if (e) hipEventDestroy(e);
     if (sl.coef.p) hipFree(sl.coef.p);
     for (hipStream_t q : {sl.st, sl.side})
@@ -132,6 +132,8 @@ dg_status Context::init() {
     HIPCHK(hipEventCreateWithFlags(&sl.ev_meta, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_coef, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_zero, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_png0, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_png1, hipEventDisableTiming));
   }
   return DG_OK;
 }
@@ -1403,12 +1405,25 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (!from_fix && b.any_png) {
     launch_png_gather(sl.st, (const GatherJob *)(M + b.gjob_off), lst(L_GATHER), cnt(L_GATHER));
     if (!b.ichunks.empty()) {
+      // streams too small to chunk (masks) inflate serially on the side stream,
+      // beside the chunked kernels (which leave most CUs idle); chunked images
+      // the resolve gives up on follow on the main stream
+      const bool beside = side_stream_;
+      if (beside) {
+        HIPCHK(hipEventRecord(sl.ev_png0, sl.st));
+        HIPCHK(hipStreamWaitEvent(sl.side, sl.ev_png0, 0));
+        launch_png_inflate(sl.side, dm, lst(L_PNG), cnt(L_PNG), 0);
+        HIPCHK(hipEventRecord(sl.ev_png1, sl.side));
+      }
       InfChunk *ich = (InfChunk *)(M + b.ichunk_off);
       launch_inf_find(sl.st, dd, ich, lst(L_INF_FIND), cnt(L_INF_FIND));
       launch_inf_decode(sl.st, dd, ich, (uint32_t)b.ichunks.size());
       launch_inf_resolve(sl.st, dm, ich, lst(L_INF_RES), cnt(L_INF_RES));
+      launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG), beside ? 1 : 2);
+      if (beside) HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_png1, 0));
+    } else {
+      launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG), 2);  // serial: every stream
     }
-    launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG));  // serial: small streams + fallbacks
   }
   if (next()) return DG_ERR_DEVICE;
   if (!from_fix && b.any_png) {

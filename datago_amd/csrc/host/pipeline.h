@@ -109,6 +109,7 @@ struct Slot {
   // in their tails).
   hipStream_t st = nullptr, side = nullptr;
   hipEvent_t ev_meta = nullptr, ev_coef = nullptr, ev_zero = nullptr;
+  hipEvent_t ev_png0 = nullptr, ev_png1 = nullptr;  // PNG: serial inflate on the side stream
   std::unique_ptr<Batch> batch;
   size_t subs_off = 0, ckpt_off = 0;
 };

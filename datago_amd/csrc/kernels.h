@@ -62,7 +62,8 @@ void launch_prog_scan(hipStream_t st, const ImageDesc *imgs, const ProgScan *sca
 namespace dg {
 void launch_png_gather(hipStream_t st, const GatherJob *jobs, const WgItem *list, uint32_t nwg);
 // one 64-thread workgroup (one wave) per image
-void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+// mode: 0 unchunked streams only, 1 chunked-path fallbacks only, 2 both
+void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, int mode);
 // tasks: (image, pass << 24 | band) in ticket order; flags: ntasks + 1 zeroed words
 void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
                          uint32_t nworkers);
