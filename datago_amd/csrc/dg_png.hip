@@ -1065,27 +1065,39 @@ __global__ __launch_bounds__(1024) void k_inf_resolve(ImageDesc *__restrict__ im
     const DG_GLOBAL uint16_t *e = gp<const uint16_t>(c.out);
     const uint32_t n = min(c.len, want - P);
     uint32_t oob = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += 1024) {
-      const uint32_t v = e[i];
-      uint8_t b;
-      if (v < 256) {
-        b = (uint8_t)v;
-      } else {
-        const int64_t sp = (int64_t)P - 32768 + (int64_t)(v - 256);
-        if (sp < 0) {
-          oob = 1;
-          b = 0;
-        } else {
-          b = raw[sp];
+    // 8 entries per thread per round, every load issued before any store: a
+    // marker reads bytes before P (earlier chunks, already fenced), never this
+    // chunk's, so nothing orders the loads after the stores
+    constexpr uint32_t U = 8;
+    for (uint32_t i0 = threadIdx.x; i0 < n; i0 += 1024 * U) {
+      uint32_t v[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+        const uint32_t i = i0 + 1024 * u;
+        v[u] = i < n ? e[i] : 0u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+        if (v[u] >= 256) {
+          const int64_t sp = (int64_t)P - 32768 + (int64_t)(v[u] - 256);
+          oob |= sp < 0 ? 1u : 0u;
+          v[u] = sp < 0 ? 0u : (uint32_t)raw[sp];
         }
       }
-      raw[P + i] = b;
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+        const uint32_t i = i0 + 1024 * u;
+        if (i < n) raw[P + i] = (uint8_t)v[u];
+      }
     }
     if (__syncthreads_or(oob)) {
       bad = true;
       break;
     }
-    __threadfence();
+    // a workgroup-scope fence + barrier makes this chunk's bytes visible to
+    // the next chunk's marker loads (every thread is on this CU); the
+    // device-scope __threadfence used before wrote the L2 back on every chunk
+    // (k_inf_resolve 18 -> 5 ms per batch without it)
     __syncthreads();
     P += n;
     if (c.stop <= k) {  // cannot go backwards
