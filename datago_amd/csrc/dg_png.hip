@@ -1137,11 +1137,17 @@ __device__ __forceinline__ uint32_t shfl_up1(uint32_t v) {
 // kUfU*(t-l) ..), so one shuffle round trip serves kUfU units.
 constexpr uint32_t kUfU = 2;
 constexpr uint32_t kUfTile = 64 * kUfU;
-constexpr uint32_t kUfPitch = kUfTile * 4 + 4;  // bytes per tile row (bpp <= 4) + dword misalignment; 129 words: lane rows on distinct banks
-
+// LDS of one worker: 3 tiles of 64 rows plus 3 previous-band rows, each
+// kUfTile * bpp + 4 bytes (dword misalignment; an odd number of words, so
+// lane rows fall on distinct banks).  Sized for the batch's widest filter
+// unit (dynamic LDS), so batches of 1-3-byte units run more workers per CU.
+__host__ __device__ constexpr uint32_t uf_pitch(uint32_t bpp) { return kUfTile * bpp + 4; }
+__host__ __device__ constexpr uint32_t uf_smem_bytes(uint32_t bpp) { return (3 * 64 + 3) * uf_pitch(bpp); }
 struct UnfilterSmem {
-  uint8_t tile[3][64][kUfPitch];
-  uint8_t prow[3][kUfPitch];  // row y0 - 1 (the previous band's last), per tile
+  uint8_t *base;
+  uint32_t pitch;
+  __device__ __forceinline__ uint8_t *tile(uint32_t k, uint32_t r) const { return base + ((k % 3) * 64 + r) * pitch; }
+  __device__ __forceinline__ uint8_t *prow(uint32_t k) const { return base + (192 + k % 3) * pitch; }
 };
 
 template <uint32_t BPP>
@@ -1188,7 +1194,7 @@ __device__ __forceinline__ bool uf_wait(const DG_GLOBAL uint32_t *flag, uint32_t
 // H rows of 1 + rb bytes at raw_a -> rows of rb bytes at stride us at unf_a.
 // `pred` is the previous band's progress flag (null for the first band).
 template <uint32_t BPP>
-__device__ void unfilter_band(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, uint64_t unf_a, uint32_t rb,
+__device__ void unfilter_band(const UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, uint64_t unf_a, uint32_t rb,
                               uint32_t us, uint32_t H, uint32_t y0, DG_GLOBAL uint32_t *self,
                               const DG_GLOBAL uint32_t *pred) {
   const uint32_t lane = threadIdx.x;
@@ -1214,14 +1220,13 @@ __device__ void unfilter_band(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, u
     auto roff = [&](uint32_t r) { return (uint32_t)((rbase + (uint64_t)r * (rb + 1)) & 3u); };
     auto load_tile = [&](uint32_t k) {
       const uint32_t b0 = k * tb, nb = rb - b0 < tb ? rb - b0 : tb;
-      uint8_t(*T)[kUfPitch] = sm.tile[k % 3];
       for (uint32_t r = 0; r < nrows; r++) {
         const uint64_t a = rbase + (uint64_t)r * (rb + 1) + b0, a4 = a & ~(uint64_t)3;
         const uint32_t nw = (uint32_t)((a - a4 + nb + 3) / 4);
         for (uint32_t w0 = 0; w0 < nw; w0 += 64)
           if (w0 + lane < nw)
             __builtin_amdgcn_global_load_lds((const DG_GLOBAL void *)(uintptr_t)(a4 + 4ull * (w0 + lane)),
-                                             (__attribute__((address_space(3))) void *)(T[r] + 4 * w0), 4, 0, 0);
+                                             (__attribute__((address_space(3))) void *)(sm.tile(k, r) + 4 * w0), 4, 0, 0);
       }
       if (y0) {
         if (!uf_wait(pred, k + 1)) bad = 1;
@@ -1230,20 +1235,19 @@ __device__ void unfilter_band(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, u
         for (uint32_t w0 = 0; w0 < nw; w0 += 64)
           if (w0 + lane < nw)
             __builtin_amdgcn_global_load_lds((const DG_GLOBAL void *)(uintptr_t)(a + 4ull * (w0 + lane)),
-                                             (__attribute__((address_space(3))) void *)(sm.prow[k % 3] + 4 * w0), 4,
+                                             (__attribute__((address_space(3))) void *)(sm.prow(k) + 4 * w0), 4,
                                              0, 0);
       } else {
-        for (uint32_t c = lane; c < nb; c += 64) sm.prow[k % 3][c] = 0;
+        for (uint32_t c = lane; c < nb; c += 64) sm.prow(k)[c] = 0;
       }
     };
     auto store_tile = [&](uint32_t k) {
       const uint32_t b0 = k * tb, nb = rb - b0 < tb ? rb - b0 : tb;
       const uint32_t nw = (nb + 3) / 4;  // whole words: the tail lands in the row's stride padding
-      uint8_t(*T)[kUfPitch] = sm.tile[k % 3];
       for (uint32_t r = 0; r < nrows; r++) {
         DG_GLOBAL uint32_t *dst = (DG_GLOBAL uint32_t *)(unf + (size_t)(y0 + r) * us + b0);
         const uint32_t o = roff(r);
-        const uint32_t *src = (const uint32_t *)T[r];
+        const uint32_t *src = (const uint32_t *)sm.tile(k, r);
         for (uint32_t c = lane; c < nw; c += 64) dst[c] = __builtin_amdgcn_alignbyte(src[c + 1], src[c], o);
       }
     };
@@ -1276,7 +1280,7 @@ __device__ void unfilter_band(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, u
         const int32_t x = x0 + (int32_t)j;
         const bool ok = active && x >= 0 && (uint32_t)x < units;
         const uint32_t xx = ok ? (uint32_t)x : 0u;
-        Tp[j] = sm.tile[(xx / kUfTile) % 3][lane] + myoff + (xx % kUfTile) * BPP;
+        Tp[j] = sm.tile(xx / kUfTile, lane) + myoff + (xx % kUfTile) * BPP;
         uint32_t v = 0;
 #pragma unroll
         for (uint32_t k = 0; k < BPP; k++) v |= (uint32_t)Tp[j][k] << (8 * k);
@@ -1291,7 +1295,7 @@ __device__ void unfilter_band(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, u
 #pragma unroll
         for (uint32_t j = 0; j < kUfU; j++) {
           const uint32_t x = (uint32_t)x0 + j < units ? (uint32_t)x0 + j : (uint32_t)x0;
-          const uint8_t *pr = sm.prow[(x / kUfTile) % 3] + (x % kUfTile) * BPP;
+          const uint8_t *pr = sm.prow(x / kUfTile) + (x % kUfTile) * BPP;
           uint32_t v = 0;
 #pragma unroll
           for (uint32_t k = 0; k < BPP; k++) v |= (uint32_t)pr[k] << (8 * k);
@@ -1300,7 +1304,7 @@ __device__ void unfilter_band(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, u
         ul0 = 0;
         if (x0 > 0) {
           const uint32_t x = (uint32_t)x0 - 1;
-          const uint8_t *pr = sm.prow[(x / kUfTile) % 3] + (x % kUfTile) * BPP;
+          const uint8_t *pr = sm.prow(x / kUfTile) + (x % kUfTile) * BPP;
 #pragma unroll
           for (uint32_t k = 0; k < BPP; k++) ul0 |= (uint32_t)pr[k] << (8 * k);
         }
@@ -1337,7 +1341,7 @@ __device__ void unfilter_band(UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, u
 __global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ tasks,
                                                      uint32_t ntasks, uint32_t *__restrict__ flags_,
                                                      uint32_t *__restrict__ ticket) {
-  __shared__ __attribute__((aligned(16))) UnfilterSmem sm;
+  extern __shared__ __attribute__((aligned(16))) uint8_t uf_smem[];  // uf_smem_bytes(batch's widest unit)
   __shared__ uint32_t s_ticket;
   DG_GLOBAL uint32_t *flags = gp<uint32_t>((uint64_t)(uintptr_t)flags_);
   for (;;) {
@@ -1369,6 +1373,7 @@ __global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ img
     DG_GLOBAL uint32_t *self = flags + pd.uf_flag0 + foff + band;
     const DG_GLOBAL uint32_t *pred = band ? self - 1 : nullptr;
     if (!uni(im.status)) {  // (an image whose inflate failed has nothing to unfilter)
+      const UnfilterSmem sm{uf_smem, uf_pitch(pd.bpp <= 4 ? pd.bpp : 4)};
       switch (pd.bpp) {
         case 1: unfilter_band<1>(sm, im, ra, ua, rb, us, H, band * 64, self, pred); break;
         case 2: unfilter_band<2>(sm, im, ra, ua, rb, us, H, band * 64, self, pred); break;
@@ -1515,10 +1520,18 @@ void launch_inf_resolve(hipStream_t st, ImageDesc *imgs, const InfChunk *ch, con
   if (nwg) hipLaunchKernelGGL(k_inf_resolve, dim3(nwg), dim3(1024), 0, st, imgs, ch, list);
 }
 void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
-                         uint32_t nworkers) {
+                         uint32_t ncu, uint32_t maxbpp) {
   // flags: ntasks progress words + the ticket counter, zeroed by the caller
-  const uint32_t g = std::min(ntasks, nworkers);
-  if (g) hipLaunchKernelGGL(k_png_unfilter, dim3(g), dim3(64), 0, st, imgs, tasks, ntasks, flags, flags + ntasks);
+  static bool attr = false;  // > 64 KiB of dynamic LDS
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)k_png_unfilter, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)uf_smem_bytes(4));
+    attr = true;
+  }
+  const uint32_t bpp = maxbpp < 1 ? 1u : maxbpp > 4 ? 4u : maxbpp, lds = uf_smem_bytes(bpp);
+  const uint32_t per_cu = std::max<uint32_t>(1u, (160u * 1024u - 64u) / (lds + 64u));  // workers resident per CU
+  const uint32_t g = std::min(ntasks, ncu * per_cu);
+  if (g) hipLaunchKernelGGL(k_png_unfilter, dim3(g), dim3(64), lds, st, imgs, tasks, ntasks, flags, flags + ntasks);
 }
 void launch_png_expand(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_png_expand, dim3(nwg), dim3(256), 0, st, imgs, list);

@@ -1034,10 +1034,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   // PNG unfilter: one progress flag per 64-row band of every plane
   b.uf_n = 0;
+  b.uf_maxbpp = 1;
   for (ImageDesc &dd : b.descs)
     if (dd.fmt == kFmtPng) {
       dd.png.uf_flag0 = b.uf_n;
       b.uf_n += png_bands(dd);
+      b.uf_maxbpp = std::max(b.uf_maxbpp, dd.png.bpp);
     }
   b.uf_flags_off = b.uf_n ? L.take((size_t)(b.uf_n + 1) * 4) : 0;
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
@@ -1430,7 +1432,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     if (b.uf_n) {
       uint32_t *uf = (uint32_t *)((char *)sl.scratch.p + b.uf_flags_off);
       HIPCHK(hipMemsetAsync(uf, 0, (size_t)(b.uf_n + 1) * 4, sl.st));
-      launch_png_unfilter(sl.st, dm, lst(L_UNF), cnt(L_UNF), uf, ncu_);
+      launch_png_unfilter(sl.st, dm, lst(L_UNF), cnt(L_UNF), uf, ncu_, b.uf_maxbpp);
     }
     launch_png_expand(sl.st, dd, lst(L_EXPAND), cnt(L_EXPAND));
   }

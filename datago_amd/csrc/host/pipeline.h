@@ -60,6 +60,7 @@ struct Batch {
   std::vector<InfChunk> ichunks;  // chunk-parallel inflate records (kernels fill start/len/stop/status)
   size_t ichunk_off = 0;
   uint32_t uf_n = 0;        // PNG unfilter bands (progress flags, L_UNF tasks)
+  uint32_t uf_maxbpp = 1;   // widest filter unit of the batch's PNGs (k_png_unfilter's LDS)
   size_t uf_flags_off = 0;  // their flags + ticket in the scratch arena (zeroed per batch)
   std::vector<uint8_t> blob;
   size_t blob_off = 0;

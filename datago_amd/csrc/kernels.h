@@ -66,7 +66,7 @@ void launch_png_gather(hipStream_t st, const GatherJob *jobs, const WgItem *list
 void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, int mode);
 // tasks: (image, pass << 24 | band) in ticket order; flags: ntasks + 1 zeroed words
 void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
-                         uint32_t nworkers);
+                         uint32_t ncu, uint32_t maxbpp);
 // 256 pixels per workgroup
 void launch_png_expand(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 // alpha program at `point` (0 before call 1, 1 between the calls, 2 after call 2): 256 pixels per workgroup
