@@ -11,8 +11,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <thread>
 
 #include "../dg_entropy.h"
 #include "../dg_pixel.h"
@@ -49,6 +51,39 @@ static uint32_t png_bands(const ImageDesc &d) {
   uint32_t n = 0;
   for (uint32_t p = 0; p < 7; p++) n += png_pass_bands(d, p);
   return n;
+}
+
+// Host-side copies of a finished batch's outputs (pinned staging -> the
+// caller's buffers, ~3 MB per 1024-bucket image): split into 1 MiB pieces
+// and spread over up to `nthreads` threads -- one thread's memcpy (~6-8 GB/s)
+// was the limit of the host-in/host-out path, not PCIe.
+struct CopyJob {
+  void *dst;
+  const void *src;
+  size_t n;
+};
+static void parallel_copy(const std::vector<CopyJob> &jobs, int nthreads) {
+  constexpr size_t kPiece = 1 << 20;
+  std::vector<CopyJob> pieces;
+  size_t total = 0;
+  for (const CopyJob &j : jobs) {
+    for (size_t o = 0; o < j.n; o += kPiece)
+      pieces.push_back({(char *)j.dst + o, (const char *)j.src + o, std::min(kPiece, j.n - o)});
+    total += j.n;
+  }
+  const int nt = (int)std::min<size_t>((size_t)std::max(1, nthreads), std::max<size_t>(1, total / (4 * kPiece)));
+  if (nt <= 1) {
+    for (const CopyJob &p : pieces) memcpy(p.dst, p.src, p.n);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t k; (k = next.fetch_add(1)) < pieces.size();) memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
+  };
+  std::vector<std::thread> ts;
+  for (int t = 1; t < nt; t++) ts.emplace_back(work);
+  work();
+  for (std::thread &t : ts) t.join();
 }
 
 static const char *kStageNames[] = {"upload",     "png_inflate", "png_unfilter", "destuff",   "prog_scans",
@@ -230,6 +265,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
   }
   if (k == "idct_fused") {  // IDCT inside k_huff_write's block flush (default 0: measured slower)
     idct_fused_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "copy_threads") {  // host threads for the output copies of a host-out batch (default 8)
+    if (v < 1 || v > 64) return DG_ERR_INVALID;
+    copy_threads_ = (int)v;
     return DG_OK;
   }
   if (k == "ckpt") {  // entropy checkpoints for early merging of re-decodes (default 1)
@@ -1628,6 +1668,7 @@ dg_status Context::finish(Slot &sl) {
       HIPCHK(hipStreamSynchronize(sl.st));
     }
   }
+  std::vector<CopyJob> copies;
   for (int i = 0; i < b.n; i++) {
     if (b.desc_of[i] < 0) continue;
     int status = back[b.desc_of[i]].status;
@@ -1641,14 +1682,15 @@ dg_status Context::finish(Slot &sl) {
     if (b.plans[i].encode) {
       const uint32_t nb = back[b.desc_of[i]].enc.enc_bytes;
       b.metas[i].nbytes = nb;
-      if (b.host_io && !status && nb) memcpy(b.host_outs[i], (char *)sl.out.p + b.enc_host_off[i], nb);
+      if (b.host_io && !status && nb) copies.push_back({b.host_outs[i], (char *)sl.out.p + b.enc_host_off[i], nb});
       continue;
     }
     if (b.host_io) {
-      if (!status) memcpy(b.host_outs[i], (char *)sl.out.p + off, b.plans[i].out_bytes);
+      if (!status) copies.push_back({b.host_outs[i], (char *)sl.out.p + off, b.plans[i].out_bytes});
       off += align_up(b.plans[i].out_bytes, 16);
     }
   }
+  parallel_copy(copies, copy_threads_);
   b.done = true;
   return DG_OK;
 }
