@@ -1400,8 +1400,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   if (!b.pscans.empty()) memcpy(P + b.pscan_off, b.pscans.data(), b.pscans.size() * sizeof(ProgScan));
   if (!b.blob.empty()) memcpy(P + b.blob_off, b.blob.data(), b.blob.size());
   if (host_io) {
+    std::vector<CopyJob> ins;
     for (int i = 0; i < n; i++)
-      if (b.desc_of[i] >= 0) memcpy(P + b.meta_bytes + in_off[i], h_srcs[i], lens[i]);
+      if (b.desc_of[i] >= 0) ins.push_back({P + b.meta_bytes + in_off[i], h_srcs[i], lens[i]});
+    parallel_copy(ins, copy_threads_);
   }
   if (timing_) HIPCHK(hipEventRecord(sl.ev[0], sl.st));
   HIPCHK(hipMemcpyAsync(sl.meta.p, P, b.meta_bytes, hipMemcpyHostToDevice, sl.st));
