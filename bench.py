@@ -618,10 +618,14 @@ def main() -> int:
                 raise RuntimeError(f"image {i} status {metas[j].status}: {L.last_error()}")
         return idx
 
+    host_s = {"submit": 0.0}
+
     def run(k0: int, n: int, on_done=None):
         pend = []  # batch k + inflight - 1 is submitted before batch k is waited on
         for k in range(k0, k0 + n):
+            ts = time.perf_counter()
             pend.append(submit(k))
+            host_s["submit"] += time.perf_counter() - ts
             if len(pend) >= a.inflight:
                 idx = complete(pend.pop(0))
                 if on_done:
@@ -632,6 +636,8 @@ def main() -> int:
                 on_done(idx)
 
     run(0, max(1, a.warmup))
+    host_s["submit"] = 0.0
+    ctx.set_option("reset_host_us", 1)
     # ---- timed region
     ctx.set_option("timing", 1)
     stage_tot = {}
@@ -839,6 +845,9 @@ def main() -> int:
                                for k in stage_tot if stage_alg.get(k) and stage_tot[k] > 0},
             "output_mpix_s": round(outpx_all / dt_max / 1e6, 2),
             "images_per_s": round(B_ * a.steps * world / dt_max, 1),
+            "host_submit_ms_per_step": round(1e3 * host_s["submit"] / a.steps, 3),  # Python + dg_submit_device planning
+            "host_submit_phases_ms_per_step": {q: round(ctx.stat("host_us_" + q) / 1e3 / a.steps, 3)
+                                               for q in ("plan", "pools", "layout", "lists", "upload", "launch")},
             "e2e_host_mpix_s": round(e2e, 2) if e2e else None,
             "e2e_host_in_hbm_out_mpix_s": round(e2e_dev, 2) if e2e_dev else None,
             "e2e_decode_one": one,

@@ -267,6 +267,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     idct_fused_ = v != 0;
     return DG_OK;
   }
+  if (k == "reset_host_us") {  // zero the host_us_* stats
+    for (double &x : host_us_) x = 0;
+    return DG_OK;
+  }
   if (k == "copy_threads") {  // host threads for the output copies of a host-out batch (default 8)
     if (v < 1 || v > 64) return DG_ERR_INVALID;
     copy_threads_ = (int)v;
@@ -311,6 +315,11 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "sub_bits") return last_sub_bits_;
   if (k == "png_serial_fallbacks") return stat_png_serial_;
   if (k == "png_chunks") return stat_png_chunks_;
+  {  // host microseconds spent in dg_submit* since the last reset, per phase
+    static const char *pn[6] = {"plan", "pools", "layout", "lists", "upload", "launch"};
+    for (int q = 0; q < 6; q++)
+      if (k == std::string("host_us_") + pn[q]) return (int64_t)host_us_[q];
+  }
   if (k == "hpool") return (int64_t)hpool_.size();
   if (k == "qpool") return (int64_t)qpool_.size();
   return -1;
@@ -588,9 +597,15 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.metas = metas;
   b.plans.resize(n);
   b.desc_of.assign(n, -1);
+  auto phase_t0 = std::chrono::steady_clock::now();
+  auto phase = [&](int k) {  // host time per submit phase (stats "host_us_<phase>")
+    const auto now = std::chrono::steady_clock::now();
+    host_us_[k] += std::chrono::duration<double, std::micro>(now - phase_t0).count();
+    phase_t0 = now;
+  };
   // ---- 1. plan every image (host, header only)
+  for (int i = 0; i < n; i++) plan_image(h_srcs[i], lens[i], forced ? forced[i] : -1, b.plans[i]);
   for (int i = 0; i < n; i++) {
-    plan_image(h_srcs[i], lens[i], forced ? forced[i] : -1, b.plans[i]);
     ImagePlan &p = b.plans[i];
     dg_payload_meta &m = metas[i];
     memset(&m, 0, sizeof(m));
@@ -618,6 +633,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       m.status = DG_ERR_INVALID;
     }
   }
+  phase(0);
   // ---- 2. table pools
   if (hpool_.size() > kPoolKeep || qpool_.size() > kPoolKeep) {
     dg_status st = flush_pools();
@@ -649,6 +665,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   dg_status st = upload_pools();
   if (st) return st;
 
+  phase(1);
   // ---- 3. layout
   // Subsequence size: the entropy kernels are latency-bound, so they want as
   // many lanes as the chip can keep resident, but every subsequence costs a
@@ -1221,6 +1238,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     }
     (void)subs_off;
   }
+  phase(2);
   // ---- 5. workgroup lists
   for (auto &l : b.lists) l.clear();
   std::vector<WgItem> hb[2][2][4];  // band H items per (stage, fused fill, weight-count class)
@@ -1357,6 +1375,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         auto &l = b.lists[h ? L_RH2 : L_RH0];
         l.insert(l.end(), hb[h][f][c].begin(), hb[h][f][c].end());
       }
+  phase(3);
   // ---- 6. meta buffer: [flags][descs][lists...]
   Layout M;
   b.flags_off = M.take(sizeof(BatchFlags));
@@ -1416,8 +1435,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     b.host_caps.assign(caps, caps + n);
   }
   sl.batch = std::move(bp);
+  phase(4);
   st = launch_all(sl, false);
   if (st) return st;
+  phase(5);
   stat_batches_++;
   *ticket = sl.batch->ticket;
   next_slot_ = (next_slot_ + 1) % nslots_;

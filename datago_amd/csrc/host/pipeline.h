@@ -216,6 +216,7 @@ class Context {
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
   int decode_sem_ = 0;                  // option "decode_semantics"
   bool ckpt_ = true;                    // option "ckpt"
+  double host_us_[6] = {0, 0, 0, 0, 0, 0};  // submit phases (stats "host_us_*"; option "reset_host_us")
   int copy_threads_ = 8;                // option "copy_threads": host threads for a host-out batch's output copies
   bool idct_fused_ = false;             // option "idct_fused" (measured 7x slower k_huff_write: off)
   bool progressive_ = false;            // option "progressive"
