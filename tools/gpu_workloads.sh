@@ -16,7 +16,7 @@ run() {  # name timeout args...
   return $rc
 }
 run wds 300 --workload wds --steps 8 --warmup 2 &&
-run png 400 --workload png --steps 5 --warmup 1 &&
-run png_encode 400 --workload png --encode --steps 5 --warmup 1 &&
+run png 400 --workload png --steps 10 --warmup 2 &&
+run png_encode 400 --workload png --encode --steps 10 --warmup 2 &&
 run cfg4_gpus2 500 --workload cfg4 --gpus 2 --steps 5 --warmup 1 --e2e-steps 0 --one-threads 0 &&
 run jpeg_gpus2 400 --gpus 2 --steps 10 --warmup 2 --e2e-steps 0 --one-threads 0
