@@ -433,3 +433,24 @@ def test_fused_idct_option_bit_exact():
             c.set_option("sub_bits", sb)
         for k, ((st, a, _), b) in enumerate(zip(c.decode_batch(datas), base)):
             assert st == 0 and np.array_equal(a, b), (sb, k)
+
+
+def test_host_output_copies_threaded_equal():
+    """Host-out batches copy outputs to the caller's buffers on up to
+    `copy_threads` threads in 1 MiB pieces; 1 and 8 threads give identical
+    bytes and both equal the oracle (large 1024-bucket outputs, so the
+    threaded path really splits)."""
+    from datago_amd import _lib as L
+    datas = [synth.make_jpeg(700 + i, 1900 - 97 * i, 1200 + 133 * i, 90, ["4:2:0", "4:4:4", "4:2:2"][i % 3])
+             for i in range(6)]
+    t = B.ARAwareTransform(1024, 32, 0.5, 2.0)
+    outs = {}
+    for nt in (1, 8):
+        ctx = L.Context(0, crop_and_resize=True, default_image_size=1024, downsampling_ratio=32,
+                        min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+        ctx.set_option("copy_threads", nt)
+        outs[nt] = ctx.decode_batch(datas)
+    for d, (s1, a1, _), (s8, a8, _) in zip(datas, outs[1], outs[8]):
+        assert s1 == 0 and s8 == 0 and np.array_equal(a1, a8)
+        _, dec = O.jpeg_decode(d)
+        assert np.array_equal(a8, O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR))

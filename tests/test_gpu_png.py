@@ -243,3 +243,27 @@ def test_png_adam7_bit_exact(ctx_dec, ctx512):
         _, ref = O.png_decode(d)
         tw, th = t.target_size(ref.shape[1], ref.shape[0])
         assert np.array_equal(arr, O.crop_and_resize(ref, tw, th, O.MODE_FIR))
+
+
+def test_serial_inflate_beside_chunked_and_unfilter_unit_widths():
+    """Round-2 scheduling paths: small streams (masks) inflate on the side
+    stream beside the chunk-parallel kernels (option side_stream 1, mode 0 +
+    fallbacks mode 1) or after them on the main stream (side_stream 0, mode
+    2); and the pipelined unfilter sizes its LDS for the batch's widest filter
+    unit (L-only batches: 6 workers per CU, RGBA: 1).  Every variant equals
+    the oracle byte for byte; tall images give many pipelined bands."""
+    L = _lib()
+    rng = np.random.default_rng(47)
+    big = [synth.pil_png(synth.synth_pixels(rng, 1300, 1700), compress_level=6),  # chunked
+           synth.make_png(90, 900, 2300, "RGBA", level=6)]
+    small = [synth.make_png(91 + i, 300 + 50 * i, 900 + 31 * i, "L", level=9) for i in range(3)]  # serial
+    batches = {"mixed": big + small, "L_only": small + [synth.make_png(95, 640, 2600, "L", level=6)],
+               "RGBA_only": [big[1], synth.make_png(96, 333, 1111, "RGBA", level=1)]}
+    for side in (1, 0):
+        ctx = L.Context(0)
+        ctx.set_option("side_stream", side)
+        for name, datas in batches.items():
+            for k, (d, (st, arr, _)) in enumerate(zip(datas, ctx.decode_batch(datas))):
+                ost, ref = O.png_decode(d)
+                assert ost == 0 and st == 0, (side, name, k, st, L.last_error())
+                assert arr.shape == ref.shape and np.array_equal(arr, ref), (side, name, k)
