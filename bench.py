@@ -95,6 +95,9 @@ def parse():
     ap.add_argument("--encode", action="store_true",
                     help="pre_encode_images with encode_format jpeg, quality 92 (configs[4]: every payload "
                          "re-encoded on the GPU, WebDataset semantics worker_wds.rs:47-52)")
+    ap.add_argument("--rst-rows", type=int, default=0,
+                    help="jpeg workload: the twin pool with a restart marker every N MCU rows (SURVEY §8(d); "
+                         "not the headline config)")
     ap.add_argument("--progressive-frac", type=float, default=0.0,
                     help="jpeg workload: share of the pool written as progressive JPEGs (not the headline config)")
     ap.add_argument("--out", default="")
@@ -462,13 +465,15 @@ def jpeg_pool(a, rank: int, world: int, workers: int, dist):
     t0 = time.perf_counter()
     made = synth.generate_pool_images(seed, a.pool, union[rank::world], workers, a.short_min, a.short_max,
                                       a.progressive_frac,
-                                      progress=lambda m: print(f"[rank {rank}] {m}", file=sys.stderr, flush=True))
+                                      progress=lambda m: print(f"[rank {rank}] {m}", file=sys.stderr, flush=True),
+                                      restart_marker_rows=a.rst_rows)
     if world > 1:
         dist.barrier()
     mine = images_of(rank)
     uniq = sorted(set(mine))
     pos = {img: k for k, img in enumerate(uniq)}
-    pool = synth.load_pool_images(seed, a.pool, uniq, a.short_min, a.short_max, a.progressive_frac)
+    pool = synth.load_pool_images(seed, a.pool, uniq, a.short_min, a.short_max, a.progressive_frac,
+                                  restart_marker_rows=a.rst_rows)
     seq = [pos[i] for i in mine]  # batch k = seq[k*B:(k+1)*B]
     lo, hi = get_data_slice_multirank(a.samples, rank, world)
     return pool, seq, (lo, hi), made, time.perf_counter() - t0
@@ -815,6 +820,7 @@ def main() -> int:
                                     f"to 1024/32{' + JPEG q92 re-encode of every payload' if a.encode else ''}"),
                        "pre_encode_images": bool(a.encode),
                        "progressive_frac": a.progressive_frac,
+                       "restart_marker_rows": a.rst_rows,
                        "images_per_step": B_, "pool": a.pool, "samples": a.samples,
                        "short_side": [a.short_min, a.short_max], "buckets": f"{a.size}/{a.ratio}/0.5/2.0",
                        "parallelism": f"dp{world} (sample shards, no collectives)"},

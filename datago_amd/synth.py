@@ -158,9 +158,9 @@ def corpus_cache_dir() -> str:
     return os.environ.get("DATAGO_CORPUS_CACHE") or os.path.join(tempfile.gettempdir(), "datago_amd_corpus")
 
 
-def _pool_job(seed: int, i: int, spec, progressive_frac: float):
+def _pool_job(seed: int, i: int, spec, progressive_frac: float, restart_marker_rows: int = 0):
     step = int(round(1.0 / progressive_frac)) if progressive_frac > 0 else 0
-    return (seed * 1_000_003 + i, spec[i], 0, bool(step) and i % step == 0)
+    return (seed * 1_000_003 + i, spec[i], int(restart_marker_rows), bool(step) and i % step == 0)
 
 
 def _cache_name(job) -> str:
@@ -181,7 +181,7 @@ def _make_cached(args):
 
 def generate_pool_images(seed: int, n_pool: int, indices, workers: int = 1, short_min: int = 256,
                          short_max: int = 2048, progressive_frac: float = 0.0, cache_dir: str | None = None,
-                         progress=None) -> int:
+                         progress=None, restart_marker_rows: int = 0) -> int:
     """Make sure pool images `indices` of the seed's n_pool-image pool (the
     mixed_spec distribution; image i is exactly mixed_corpus(seed, n_pool)[i])
     exist in the cache.  Returns how many were generated."""
@@ -192,7 +192,7 @@ def generate_pool_images(seed: int, n_pool: int, indices, workers: int = 1, shor
     spec = mixed_spec(seed, n_pool, short_min, short_max)
     todo = []
     for i in indices:
-        job = _pool_job(seed, i, spec, progressive_frac)
+        job = _pool_job(seed, i, spec, progressive_frac, restart_marker_rows)
         path = os.path.join(cache_dir, _cache_name(job))
         if not os.path.exists(path):
             todo.append((job, path))
@@ -217,13 +217,15 @@ def generate_pool_images(seed: int, n_pool: int, indices, workers: int = 1, shor
 
 
 def load_pool_images(seed: int, n_pool: int, indices, short_min: int = 256, short_max: int = 2048,
-                     progressive_frac: float = 0.0, cache_dir: str | None = None) -> List[bytes]:
+                     progressive_frac: float = 0.0, cache_dir: str | None = None,
+                     restart_marker_rows: int = 0) -> List[bytes]:
     import os
     cache_dir = cache_dir or corpus_cache_dir()
     spec = mixed_spec(seed, n_pool, short_min, short_max)
     out = []
     for i in indices:
-        with open(os.path.join(cache_dir, _cache_name(_pool_job(seed, i, spec, progressive_frac))), "rb") as f:
+        with open(os.path.join(cache_dir, _cache_name(_pool_job(seed, i, spec, progressive_frac,
+                                                               restart_marker_rows))), "rb") as f:
             out.append(f.read())
     return out
 
