@@ -779,6 +779,27 @@ def main() -> int:
                         for k, v in pmc.get("valu_wave_insts_per_batch", {}).items()}
         except (OSError, ValueError):
             pass
+        # measured device-to-device copy bandwidth (report the
+        # roofline against it too): best of 3 copies of a 1 GiB buffer, bytes
+        # read + written over the event time
+        copy_gbs = None
+        try:
+            nbytes = 1 << 30
+            xs = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+            ys = torch.empty_like(xs)
+            best = None
+            for _ in range(4):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ys.copy_(xs)
+                e1.record()
+                e1.synchronize()
+                t_ = e0.elapsed_time(e1) / 1e3
+                best = t_ if best is None else min(best, t_)
+            copy_gbs = round(2 * nbytes / best / 1e9, 1)
+            del xs, ys
+        except RuntimeError:
+            pass
         iso = None
         if ser_n:
             skern = {k: v / ser_n for k, v in ser_tot.items() if k not in ("upload", "download")}
@@ -828,6 +849,8 @@ def main() -> int:
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": round(dom_alg), "kernel_ms_per_launch": round(dom_ms, 4),
+                         "peak_measured_copy": copy_gbs,
+                         "frac_of_measured_copy": round(achieved / copy_gbs, 5) if copy_gbs else None,
                          "note": "per step (one batch); kernel times from HIP events on the slot stream over the "
                                  "timed region, where consecutive batches overlap"},
             "roofline_isolated": iso,
@@ -845,6 +868,8 @@ def main() -> int:
                                   "ms_per_step": round(dt_max / a.steps * 1e3, 4),
                                   "achieved_GBs": round(per_step_alg / (dt_max / a.steps) / 1e9, 2),
                                   "frac": round(per_step_alg / (dt_max / a.steps) / 1e9 / HBM_PEAK_GBS, 5),
+                                  "frac_of_measured_copy": (round(per_step_alg / (dt_max / a.steps) / 1e9 / copy_gbs, 5)
+                                                            if copy_gbs else None),
                                   "sum_of_stage_spans_ms": round(gpu_ms, 4)},
             "stages_ms_per_step": {k: round(v / steps, 4) for k, v in stage_tot.items()},
             "stages_alg_GBs": {k: round(stage_alg[k] / (stage_tot[k] / 1e3) / 1e9, 1)
