@@ -95,6 +95,7 @@ def parse():
     ap.add_argument("--encode", action="store_true",
                     help="pre_encode_images with encode_format jpeg, quality 92 (configs[4]: every payload "
                          "re-encoded on the GPU, WebDataset semantics worker_wds.rs:47-52)")
+    ap.add_argument("--hv-fused", type=int, default=-1, help="fused first H + V pass (-1 = library default)")
     ap.add_argument("--rst-rows", type=int, default=0,
                     help="jpeg workload: the twin pool with a restart marker every N MCU rows (SURVEY §8(d); "
                          "not the headline config)")
@@ -555,6 +556,8 @@ def main() -> int:
         ctx.set_option("decode_semantics", a.decode_semantics)
     if a.ckpt >= 0:
         ctx.set_option("ckpt", a.ckpt)
+    if a.hv_fused >= 0:
+        ctx.set_option("hv_fused", a.hv_fused)
     if a.idct_fused >= 0:
         ctx.set_option("idct_fused", a.idct_fused)
     if a.progressive_frac > 0:

@@ -107,6 +107,10 @@ struct ResizePass {
                             // in the fill), kHDirect = segment too wide for LDS (legacy kernel)
 };
 constexpr uint32_t kHFused = 1, kHDirect = 2;
+constexpr uint32_t kHVFused = 4;      // pass[0] runs fused with pass[1] in k_resize_hv (its H rows stay in LDS)
+constexpr uint32_t kHVSegPx = 320;    // k_resize_hv: LDS source segment per row (downscales up to ~2.3x)
+constexpr uint32_t kHVTapsMax = 24;   // k_resize_hv: V taps (its LDS ring holds 32 rows)
+constexpr uint32_t kHVRows = 64;      // k_resize_hv: V output rows per workgroup
 constexpr uint32_t kHBandRows = 8;    // rows per workgroup of the band H kernel
 constexpr uint32_t kHBandCols = 128;  // output columns per workgroup
 constexpr uint32_t kHSegPx = 640;     // LDS source segment (pixels) per row

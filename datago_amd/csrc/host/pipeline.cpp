@@ -193,12 +193,21 @@ dg_status Context::sync_all() {
 // fit kHSegPx.  Wider segments (extreme downscales) use the direct kernel;
 // the first pass of a colour JPEG in the band kernel upsamples and converts
 // colour in its fill.
-static uint32_t h_pass_mode(const ResizePass &ps, bool colour_source) {
+static double h_pass_span(const ResizePass &ps) {
   const double scale = (ps.in1 - ps.in0) / (double)ps.out_size;
   const double fs = scale > 1.0 ? scale : 1.0;
-  const double span = std::ceil((kHBandCols - 1) * scale + 6.0 * fs) + 2.0 + 8.0 + (double)ps.ksize + 8.0;
-  if (span > (double)kHSegPx) return kHDirect;
+  return std::ceil((kHBandCols - 1) * scale + 6.0 * fs) + 2.0 + 8.0 + (double)ps.ksize + 8.0;
+}
+static uint32_t h_pass_mode(const ResizePass &ps, bool colour_source) {
+  if (h_pass_span(ps) > (double)kHSegPx) return kHDirect;
   return colour_source ? kHFused : 0u;
+}
+// k_resize_hv takes the first H and V passes of a colour JPEG together when
+// its smaller segment and ring fit them and the H taps are in the <= 16 class
+static bool hv_fusable(const ResizePass &h, const ResizePass &v) {
+  return h.kind == 1 && (h.mode & kHFused) && !(h.mode & kHDirect) && v.kind == 2 && h.C == 3 && h.row0 == 0 &&
+         v.row0 == 0 &&
+         h.ksize + 1 <= 16 && v.ksize <= kHVTapsMax && h_pass_span(h) <= (double)kHVSegPx;
 }
 
 dg_status Context::set_option(const std::string &k, int64_t v) {
@@ -269,6 +278,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
   }
   if (k == "reset_host_us") {  // zero the host_us_* stats
     for (double &x : host_us_) x = 0;
+    return DG_OK;
+  }
+  if (k == "hv_fused") {  // fused first H + V pass of colour JPEGs where it fits (default 0: slower)
+    hv_fused_ = v != 0;
     return DG_OK;
   }
   if (k == "copy_threads") {  // host threads for the output copies of a host-out batch (default 8)
@@ -993,6 +1006,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     }
     // colour images whose first pass is not a fused H pass need the RGB image
     d.color_fused = colour && d.pass[0].kind == 1 && (d.pass[0].mode & kHFused);
+    if (hv_fused_ && hv_fusable(d.pass[0], d.pass[1])) d.pass[0].mode |= kHVFused;
     if (colour && !d.color_fused) o.pix = L.take((size_t)d.pix_stride * H);
     // final write: the last pass writes straight into the output when the
     // channel count is unchanged; otherwise (or with no pass) k_copy runs.
@@ -1242,6 +1256,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   // ---- 5. workgroup lists
   for (auto &l : b.lists) l.clear();
   std::vector<WgItem> hb[2][2][4];  // band H items per (stage, fused fill, weight-count class)
+  std::vector<WgItem> hvl[2];       // k_resize_hv items per H weight class
   for (int di = 0; di < (int)b.descs.size(); di++) {
     const ImageDesc &d = b.descs[di];
     const uint32_t I = (uint32_t)di;
@@ -1277,10 +1292,18 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       for (uint32_t it = 0; it < q; it += 256) b.lists[L_COLOR].push_back({I, it});
     }
     }  // JPEG
+    const bool hv = (d.pass[0].mode & kHVFused) != 0;
+    if (hv) {  // one workgroup per (V segment of kHVRows rows, column tile)
+      const uint32_t tiles = (d.pass[0].width + kHBandCols - 1) / kHBandCols;
+      const uint32_t cnt = tiles * ((d.pass[1].rows + kHVRows - 1) / kHVRows);
+      const int cls = d.pass[0].ksize + 1 <= 8 ? 0 : 1;
+      for (uint32_t it = 0; it < cnt; it++) hvl[cls].push_back({I, it});
+    }
     for (int s = 0; s < kStages; s++) {
       const ResizePass &ps = d.pass[s];
       if (!ps.kind) continue;
       b.lists[L_COEF].push_back({I, (uint32_t)s});
+      if (hv && s < 2) continue;  // k_resize_hv runs both
       if (ps.kind == 1 && (ps.mode & kHDirect)) {  // one workgroup per (row, 512-column tile)
         uint32_t cnt = ps.rows * ((ps.width + 511) / 512);
         for (uint32_t it = 0; it < cnt; it++) b.lists[s == 0 ? L_RHX0 : L_RHX2].push_back({I, it});
@@ -1367,6 +1390,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     b.lists[L_PROG].resize(b.pscans.size());
     for (uint32_t j = 0; j < (uint32_t)b.pscans.size(); j++)
       b.lists[L_PROG][at[b.pscans[j].level]++] = WgItem{b.pscans[j].image, j};
+  }
+  for (int c = 0; c < 2; c++) {
+    b.hvclass[c] = (uint32_t)hvl[c].size();
+    b.lists[L_RHV].insert(b.lists[L_RHV].end(), hvl[c].begin(), hvl[c].end());
   }
   for (int h = 0; h < 2; h++)
     for (int f = 1; f >= 0; f--)  // launch order: fused classes, then byte-fill classes
@@ -1545,6 +1572,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_coef, 0));
   launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
   launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0);
+  launch_resize_hv(sl.st, dd, lst(L_RHV), b.hvclass);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | (debug_flags_ << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV1), cnt(L_RV1), 1);

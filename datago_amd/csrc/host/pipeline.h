@@ -77,6 +77,7 @@ struct Batch {
   // band H lists (L_RH0, L_RH2) are grouped by weight-count class (<=8, <=16,
   // <=32, more): hclass[stage/2][k] items of class k, in that order
   uint32_t hclass[2][2][4] = {{{0}}};  // [stage/2][fused][class]
+  uint32_t hvclass[2] = {0, 0};        // L_RHV items of H weight class <= 8, <= 16 (k_resize_hv)
   size_t desc_off = 0, flags_off = 0;
   size_t meta_bytes = 0;
   size_t total_subs = 0;
@@ -124,6 +125,7 @@ enum ListId {
   L_PROG_ZERO, L_PROG,                                      // progressive JPEG
   L_PENC_ROW, L_PENC_PIECE, L_PENC_IMG,                     // PNG re-encode
   L_UNF,                                                    // PNG unfilter bands (ticket order)
+  L_RHV,                                                    // fused first H + V pass (k_resize_hv)
   L_COUNT
 };
 static_assert((int)L_COUNT <= 32, "Batch::lists");
@@ -218,6 +220,7 @@ class Context {
   bool ckpt_ = true;                    // option "ckpt"
   double host_us_[6] = {0, 0, 0, 0, 0, 0};  // submit phases (stats "host_us_*"; option "reset_host_us")
   int copy_threads_ = 8;                // option "copy_threads": host threads for a host-out batch's output copies
+  bool hv_fused_ = false;               // option "hv_fused": first H + V pass fused (k_resize_hv) when it fits
   bool idct_fused_ = false;             // option "idct_fused" (measured 7x slower k_huff_write: off)
   bool progressive_ = false;            // option "progressive"
   bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first

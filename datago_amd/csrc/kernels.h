@@ -47,6 +47,8 @@ void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
 // each ordered by weight-count class (<= 8, 16, 32 taps, more)
 void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][4],
                       int stage);
+// fused first H + V pass (pass[0].mode & kHVFused): lists of H weight classes <= 8, <= 16 taps
+void launch_resize_hv(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2]);
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage);
 // final copy / gray->RGB expansion: 256 output pixels per workgroup
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);

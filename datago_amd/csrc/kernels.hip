@@ -1182,6 +1182,11 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
 // colour-converts straight from the Y/Cb/Cr planes, so the full-size RGB
 // image never exists in HBM.
 constexpr uint32_t kHSegStride = kHSegPx + 8;
+// Fused first H + V pass (k_resize_hv): the H rows a workgroup's V outputs
+// need stay in an LDS ring of kHVRing rows instead of going through HBM.
+constexpr uint32_t kHVRing = 32;                  // >= V taps + one band of 8 rows
+constexpr uint32_t kHVSegStride = kHVSegPx + 8;  // (kHVSegPx, kHVTapsMax, kHVRows: dg_types.h)
+constexpr uint32_t kHVOut = 8;                    // k_resize_hv: V rows produced per round
 
 // job j of the fill: 8 source pixels from the planes, p0 % 8 == 0
 __device__ __forceinline__ void hfill_color8(const ImageDesc &im, uint32_t y, uint32_t x0, uint32_t *d) {
@@ -1240,10 +1245,11 @@ __device__ __forceinline__ void hfill_bytes4(const DG_GLOBAL uint8_t *row, uint3
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-template <int KMAX, int C>
+template <int KMAX, int C, uint32_t SEGSTRIDE = kHSegStride, bool RING = false>
 __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, const uint32_t *kw2,
                                            const DG_GLOBAL int16_t *kp, uint32_t ksize, uint32_t n, uint32_t r0,
-                                           uint32_t nrows, int32_t prec, uint8_t *ob, uint32_t col) {
+                                           uint32_t nrows, int32_t prec, uint8_t *ob, uint32_t col,
+                                           uint32_t *ring = nullptr, uint32_t ring_row0 = 0) {
   constexpr uint32_t R = kHBandRows / 2;  // rows r0, r0 + 2, ...
   const int32_t bias = 1 << (prec - 1);
   int32_t a[R][C];
@@ -1267,7 +1273,7 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
       const s16x2 w = __builtin_bit_cast(s16x2, kw2[j]);
 #pragma unroll
       for (uint32_t r = 0; r < R; r++) {
-        const u32x2 vv = *(const u32x2 *)(seg + (r0 + 2 * r) * kHSegStride + offe + 2 * j);
+        const u32x2 vv = *(const u32x2 *)(seg + (r0 + 2 * r) * SEGSTRIDE + offe + 2 * j);
         const uint32_t v0 = vv.x, v1 = vv.y;
 #pragma unroll
         for (int c = 0; c < C; c++) {
@@ -1282,7 +1288,7 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
       const int32_t w = kp[i];
 #pragma unroll
       for (uint32_t r = 0; r < R; r++) {
-        const uint32_t v = seg[(r0 + 2 * r) * kHSegStride + off + i];
+        const uint32_t v = seg[(r0 + 2 * r) * SEGSTRIDE + off + i];
 #pragma unroll
         for (int c = 0; c < C; c++) a[r][c] += (int32_t)((v >> (8 * c)) & 0xFF) * w;
       }
@@ -1291,9 +1297,16 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
 #pragma unroll
   for (uint32_t r = 0; r < R; r++)
     if (r0 + 2 * r < nrows) {
-      uint8_t *o = ob + (r0 + 2 * r) * (kHBandCols * 4) + col * C;
+      if (RING) {  // one dword per pixel into row (ring_row0 + r0 + 2r) of the H+V kernel's ring
+        uint32_t v = 0;
 #pragma unroll
-      for (int c = 0; c < C; c++) o[c] = clip_shift(a[r][c], prec);
+        for (int c = 0; c < C; c++) v |= (uint32_t)clip_shift(a[r][c], prec) << (8 * c);
+        ring[((ring_row0 + r0 + 2 * r) % kHVRing) * kHBandCols + col] = v;
+      } else {
+        uint8_t *o = ob + (r0 + 2 * r) * (kHBandCols * 4) + col * C;
+#pragma unroll
+        for (int c = 0; c < C; c++) o[c] = clip_shift(a[r][c], prec);
+      }
     }
 }
 
@@ -1424,6 +1437,154 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
   const ImageDesc &im = imgs[it.image];
   hband<KMAX, FUSED>(im, im.pass[stage], it.item0, seg, ob, ext);
+}
+
+// Fused first H + V pass of a colour JPEG (ImageDesc pass[0] mode kHVFused):
+// one workgroup = kHBandCols columns x kHVRows V output rows.  It computes
+// the H rows those outputs' windows span, band by band exactly as
+// k_resize_hb does (fill from the Y/Cb/Cr planes, same weights and sums),
+// keeps them in an LDS ring, and after each band produces every V row whose
+// window is complete (two rows at a time: thread = column x row parity; tap
+// pairs by v_dot2 as k_resize_v).  The H intermediate (about 1.1 GB per
+// configs[1] batch) never reaches HBM; rows at segment borders are computed
+// by both neighbours.  Integer sums: bit-exact with the two-pass path.
+template <int KMAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_resize_hv(
+    const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list) {
+  __shared__ __attribute__((aligned(16))) uint32_t seg[kHBandRows * kHVSegStride];
+  __shared__ __attribute__((aligned(16))) uint32_t ring[kHVRing * kHBandCols];
+  __shared__ __attribute__((aligned(16))) uint8_t ob[kHVOut * kHBandCols * 3];
+  __shared__ uint32_t ext[4];
+  const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
+  const ImageDesc &im = imgs[it.image];
+  const ResizePass &ps = im.pass[0], &pv = im.pass[1];
+  const uint32_t tiles = (ps.width + kHBandCols - 1) / kHBandCols;
+  const uint32_t sg = it.item0 / tiles, tile = it.item0 - sg * tiles;
+  const uint32_t x0 = tile * kHBandCols;
+  const uint32_t x1 = x0 + kHBandCols < ps.width ? x0 + kHBandCols : ps.width;
+  const uint32_t oy0 = sg * kHVRows, oy1 = oy0 + kHVRows < pv.rows ? oy0 + kHVRows : pv.rows;
+  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds) + 2 * ps.out0;
+  const DG_GLOBAL int32_t *vb = gp<const int32_t>(pv.bounds) + 2 * pv.out0;
+  const uint32_t ksize = ps.ksize;
+  const DG_GLOBAL int16_t *coef = gp<const int16_t>(ps.coef) + (size_t)ps.out0 * ksize;
+  const uint32_t t = threadIdx.x, col = t & (kHBandCols - 1), x = x0 + col;
+  const bool valid = x < x1;
+  uint32_t st = 0, n = 0;
+  if (valid) {
+    st = (uint32_t)bounds[2 * x];
+    n = (uint32_t)bounds[2 * x + 1];
+  }
+  if (t == 0) {
+    ext[0] = 0xFFFFFFFFu;
+    ext[1] = 0;
+    ext[2] = 0xFFFFFFFFu;
+    ext[3] = 0;
+  }
+  __syncthreads();
+  if (valid && t < kHBandCols) {
+    atomicMin(&ext[0], st);
+    atomicMax(&ext[1], st + ksize);
+  }
+  if (t < oy1 - oy0) {  // the H rows the segment's V windows span (starts are not strictly monotone)
+    const int32_t vs = vb[2 * (oy0 + t)], vn = vb[2 * (oy0 + t) + 1];
+    atomicMin(&ext[2], (uint32_t)vs);
+    atomicMax(&ext[3], (uint32_t)(vs + vn));
+  }
+  __syncthreads();
+  const uint32_t p0 = __builtin_amdgcn_readfirstlane(ext[0]) & ~7u;
+  uint32_t p1 = __builtin_amdgcn_readfirstlane(ext[1]);
+  if (p1 - p0 > kHVSegPx) p1 = p0 + kHVSegPx;  // host sizing guarantees this never triggers
+  const uint32_t pe = p1 < ps.in_size ? p1 : ps.in_size;
+  const uint32_t hy0 = __builtin_amdgcn_readfirstlane(ext[2]), hy1 = __builtin_amdgcn_readfirstlane(ext[3]);
+  uint32_t kw2[KMAX > 0 ? (KMAX + 1) / 2 : 1];
+  const DG_GLOBAL int16_t *kp = coef + (size_t)(valid ? x : x0) * ksize;
+  {
+    const uint32_t sh = (st - p0) & 1u;
+#pragma unroll
+    for (int j = 0; j < (KMAX + 1) / 2; j++) {
+      const int32_t tl = 2 * j - (int32_t)sh, th = tl + 1;
+      const uint32_t lo = (valid && tl >= 0 && (uint32_t)tl < n) ? (uint16_t)kp[tl] : 0u;
+      const uint32_t hi = (valid && (uint32_t)th < n) ? (uint16_t)kp[th] : 0u;
+      kw2[j] = lo | (hi << 16);
+    }
+  }
+  const uint32_t off = st - p0, r0 = t / kHBandCols;
+  const uint32_t njob_row = (pe - p0 + 7) >> 3;
+  const uint32_t inv_row = ((1u << 20) - 1u + njob_row) / (njob_row ? njob_row : 1u);
+  const int32_t prec = ps.precision, vprec = pv.precision, vbias = 1 << (vprec - 1);
+  const uint32_t vk = pv.ksize;
+  const DG_GLOBAL int16_t *vcoef = gp<const int16_t>(pv.coef) + (size_t)pv.out0 * vk;
+  const uint32_t rb = (x1 - x0) * 3;  // V output bytes per row of the tile (<= 384)
+  uint32_t oy = oy0;
+  for (uint32_t y0 = hy0; y0 < hy1; y0 += kHBandRows) {
+    const uint32_t nrows = hy1 - y0 < kHBandRows ? hy1 - y0 : kHBandRows;
+    // H: fill, convolve into the ring (rows y0 .. y0 + nrows - 1)
+    const uint32_t njob = nrows * njob_row;
+    for (uint32_t j = t; j < njob; j += 256) {
+      const uint32_t r = __umul24(j, inv_row) >> 20, q = j - r * njob_row;
+      hfill_color8(im, ps.row0 + y0 + r, p0 + 8 * q, seg + r * kHVSegStride + 8 * q);
+    }
+    __syncthreads();
+    if (valid) hconv_rows<KMAX, 3, kHVSegStride, true>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, nullptr, col,
+                                                      ring, y0);
+    __syncthreads();
+    // V: every output row whose window is now complete, up to kHVOut per round
+    // (thread = column x row parity, rows h, h + 2, ...)
+    const uint32_t done = y0 + nrows;
+    for (;;) {
+      uint32_t nr = 0;
+      while (nr < kHVOut && oy + nr < oy1 && (uint32_t)(vb[2 * (oy + nr)] + vb[2 * (oy + nr) + 1]) <= done) nr++;
+      if (!nr) break;
+      if (valid) {
+        // h is wave-uniform (two waves per row parity): bounds and weights by scalar loads
+        for (uint32_t h = __builtin_amdgcn_readfirstlane(t >> 7); h < nr; h += 2) {
+          const uint32_t y = oy + h;
+          const int32_t vs = vb[2 * y], vn = vb[2 * y + 1];
+          const DG_GLOBAL int16_t *kv = vcoef + (size_t)y * vk;
+          int32_t acc[3] = {vbias, vbias, vbias};
+          int32_t i = 0;
+          for (; i + 1 < vn; i += 2) {
+            const uint32_t w2 = (uint32_t)(uint16_t)kv[i] | ((uint32_t)(uint16_t)kv[i + 1] << 16);
+            const s16x2 w = __builtin_bit_cast(s16x2, w2);
+            const uint32_t a0 = ring[((uint32_t)(vs + i) % kHVRing) * kHBandCols + col];
+            const uint32_t a1 = ring[((uint32_t)(vs + i + 1) % kHVRing) * kHBandCols + col];
+#pragma unroll
+            for (int b = 0; b < 3; b++) {
+              const uint32_t sel = 0x0C000C00u | ((4u + (uint32_t)b) << 16) | (uint32_t)b;  // [a0.b, 0, a1.b, 0]
+              acc[b] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, __builtin_amdgcn_perm(a1, a0, sel)), w,
+                                              acc[b], false);
+            }
+          }
+          if (i < vn) {
+            const int32_t w = kv[i];
+            const uint32_t a0 = ring[((uint32_t)(vs + i) % kHVRing) * kHBandCols + col];
+#pragma unroll
+            for (int b = 0; b < 3; b++) acc[b] += (int32_t)((a0 >> (8 * b)) & 0xFF) * w;
+          }
+          uint8_t *o = ob + h * (kHBandCols * 3) + col * 3;
+#pragma unroll
+          for (int b = 0; b < 3; b++) o[b] = clip_shift(acc[b], vprec);
+        }
+      }
+      __syncthreads();
+      {  // store the rows: 16 bytes per thread, 24 threads per row (rb <= 384)
+        for (uint32_t j = t; j < nr * 24; j += 256) {
+          const uint32_t fr = j / 24, fl = j - fr * 24;
+          if (fl * 16 >= rb) continue;
+          DG_GLOBAL uint8_t *d = gp<uint8_t>(pv.dst) + (size_t)(oy + fr) * pv.dst_stride + (size_t)x0 * 3 + fl * 16;
+          const uint8_t *src = ob + fr * (kHBandCols * 3) + fl * 16;
+          if (fl * 16 + 16 <= rb && (((uintptr_t)d) & 15) == 0) {
+            *(DG_GLOBAL u32x4 *)d = *(const u32x4 *)src;
+          } else {
+            const uint32_t e = fl * 16 + 16 <= rb ? 16 : rb - fl * 16;
+            for (uint32_t i = 0; i < e; i++) d[i] = src[i];
+          }
+        }
+      }
+      __syncthreads();
+      oy += nr;
+    }
+  }
 }
 
 // Vertical pass: each thread produces 16 consecutive bytes of one output row
@@ -1654,6 +1815,10 @@ void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
                       int stage) {
   launch_hb_classes<true>(st, imgs, list, ncls[1], stage);
   launch_hb_classes<false>(st, imgs, list, ncls[0], stage);
+}
+void launch_resize_hv(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2]) {
+  DG_LAUNCH(k_resize_hv<8>, ncls[0], st, imgs, list);
+  DG_LAUNCH(k_resize_hv<16>, ncls[1], st, imgs, list + ncls[0]);
 }
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
   DG_LAUNCH(k_resize_v, nwg, st, imgs, list, stage);

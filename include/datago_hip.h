@@ -211,6 +211,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)
  *   "png_chunked" 0 = inflate every PNG with the serial kernel (test switch; default 1)
  *   "copy_threads" host threads copying a host-out batch's outputs to the caller's buffers (default 8)
+ *   "hv_fused"     1 = fuse the first H and V passes of colour JPEGs where they fit (default 0; slower)
+ *   "reset_host_us" clears the host submit phase timers (stats "host_us_*")
  * Stats: "batches", "coalesced_batches", "coalesced_images", "resync_rounds", "fix_workgroups", "write_mismatch",
  * "unsettled_batches", "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool" (tables pooled now),
  * "pool_flushes" (times the table pools were started over), "png_chunks", "png_serial_fallbacks";

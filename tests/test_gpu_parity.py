@@ -454,3 +454,25 @@ def test_host_output_copies_threaded_equal():
         assert s1 == 0 and s8 == 0 and np.array_equal(a1, a8)
         _, dec = O.jpeg_decode(d)
         assert np.array_equal(a8, O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR))
+
+
+def test_fused_hv_resize_equal():
+    """Option hv_fused routes colour JPEGs whose first H and V passes fit
+    k_resize_hv (H taps <= 15, V taps <= 24, source span <= 320 px per 128
+    output columns) through the fused kernel: outputs equal the two-pass
+    path and the oracle byte for byte (downscales 1.0-2.3x, tall and wide
+    crops, every subsampling)."""
+    from datago_amd import _lib as L
+    dims = [(1100, 1500), (2048, 1536), (1536, 2048), (1300, 700), (900, 1800), (2300, 2300), (1030, 1030)]
+    datas = [synth.make_jpeg(900 + i, w, h, 88, ["4:2:0", "4:4:4", "4:2:2"][i % 3]) for i, (w, h) in enumerate(dims)]
+    t = B.ARAwareTransform(1024, 32, 0.5, 2.0)
+    outs = {}
+    for hv in (0, 1):
+        ctx = L.Context(0, crop_and_resize=True, default_image_size=1024, downsampling_ratio=32,
+                        min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+        ctx.set_option("hv_fused", hv)
+        outs[hv] = ctx.decode_batch(datas)
+    for d, (s0, a0, _), (s1, a1, _) in zip(datas, outs[0], outs[1]):
+        assert s0 == 0 and s1 == 0 and np.array_equal(a0, a1)
+        _, dec = O.jpeg_decode(d)
+        assert np.array_equal(a1, O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR))
