@@ -58,6 +58,8 @@ __global__ __launch_bounds__(256) void k_prog_zero(const ImageDesc *__restrict__
 constexpr uint32_t kPWin = 4096;  // stuffed-stream window (bytes)
 constexpr uint32_t kPBlk = 64;    // coefficient blocks per chunk
 
+constexpr uint32_t kDWin = 4096;  // destuffed window (bytes), speculative-table decoder
+
 struct ProgSmem {
   HuffTable tabs[4];
   int16_t blk[kPBlk][64];
@@ -66,7 +68,10 @@ struct ProgSmem {
   uint32_t ncor[kPBlk]; //   how many
   uint64_t nwp[kPBlk];  //   new coefficients +1 << Al
   uint64_t nwn[kPBlk];  //   new coefficients -1 << Al
-  uint8_t win[kPWin + 16];
+  union {
+    uint8_t win[kPWin + 16];                // serial decoder: stuffed bytes
+    alignas(16) uint8_t dwin[kDWin + 64];   // speculative decoder: destuffed bytes + zero pad
+  };
 };
 
 // Every lane runs the same decode: make that explicit, so the state lives in
@@ -329,13 +334,452 @@ __device__ __forceinline__ uint32_t prog_unit_block(const ImageDesc &im, const P
   return m * im.bpm + im.cfirst[c] + j;  // blocks of c within an MCU are in (v, h) raster order
 }
 
+// ------------------------------------------------------------ scan pipeline
+//
+// A scan's chunk may read blocks only after the scans it depends on (its
+// deps: earlier scans of the image sharing a component and an overlapping
+// band) have written them.  Progress is counted in MCU rows: a
+// non-interleaved scan of component c has finished MCU row m once it has
+// written block row (m + 1) * v_c - 1 of c.  Waits are bounded (~10 s of
+// s_memrealtime): a scan whose producer never comes marks its image
+// unsupported instead of hanging the device.
+struct ProgDeps {
+  DG_GLOBAL uint32_t *flags;  // null: level-by-level launches, nothing to wait for
+  uint64_t deps;
+  uint32_t first, self;
+  uint32_t last;              // last value published
+  uint32_t bad;
+};
+
+// MCU row of unit u of the scan
+__device__ __forceinline__ uint32_t prog_unit_mrow(const ImageDesc &im, const ProgScan &sc, uint32_t u) {
+  if (sc.ns > 1) return u / im.mcux;
+  const uint32_t c = sc.comp[0];
+  const uint32_t nbx = (im.cdsw[c] + 7) / 8;
+  return (u / nbx) / (im.ncomp == 1 ? 1u : im.cv[c]);
+}
+
+// MCU rows complete once units [0, u_end) are written
+__device__ __forceinline__ uint32_t prog_rows_done(const ImageDesc &im, const ProgScan &sc, uint32_t u_end) {
+  if (sc.ns > 1) return u_end / im.mcux;
+  const uint32_t c = sc.comp[0];
+  const uint32_t nbx = (im.cdsw[c] + 7) / 8;
+  return (u_end / nbx) / (im.ncomp == 1 ? 1u : im.cv[c]);
+}
+
+__device__ __forceinline__ void prog_wait(ProgDeps &pd, uint32_t need) {
+  if (!pd.flags || !pd.deps) return;
+  for (uint64_t m = pd.deps; m; m &= m - 1ull) {
+    const DG_GLOBAL uint32_t *f = pd.flags + 1 + pd.first + (uint32_t)__builtin_ctzll(m);
+    uint64_t t0 = 0;
+    for (;;) {
+      const uint32_t v = uni(__hip_atomic_load((uint32_t *)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (v >= need) break;
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+      if (!t0) t0 = now;
+      if (now - t0 > 1000000000ull) {
+        pd.bad = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+__device__ __forceinline__ void prog_publish(ProgDeps &pd, uint32_t v);
+
+// end of a scan: everything written; a timed-out wait sends the image to the CPU
+__device__ __forceinline__ void prog_finish(ProgDeps &pd, const ImageDesc *imgs, const ProgScan &sc, uint32_t lane) {
+  prog_publish(pd, kProgDone);
+  if (pd.bad && lane == 0) ((ImageDesc *)imgs)[sc.image].status = 1;  // DG_ERR_UNSUPPORTED
+}
+
+__device__ __forceinline__ void prog_publish(ProgDeps &pd, uint32_t v) {
+  if (!pd.flags || v == pd.last) return;
+  pd.last = v;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's coefficient stores before the word
+  __hip_atomic_store((uint32_t *)(pd.flags + 1 + pd.self), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------ speculative-table decoder
+//
+// For scans without restart intervals (nearly all progressive files).  The
+// serial decoder above spends a shared-memory round trip on every symbol
+// (table lookup) and every 4 bytes (bit buffer refill), each followed by a
+// readfirstlane, so a wave decodes ~100 ns per bit.  Here the 64 lanes do
+// the lookups for the next 64 bit positions at once: lane l peeks the 32
+// bits that start at bit bp + l of the destuffed window and decodes the
+// Huffman code found there.  The uniform walk then follows the real chain
+// of symbols through that table with v_readlane (register reads, no memory
+// latency): symbol at offset o = lane o's entry, its extra / sign /
+// correction bits = the top bits of lane o's peek.  A new round (two LDS
+// round trips) starts whenever the walk reaches offset 48, so a round
+// decodes at least 48 bits.  The stream is destuffed (FF00 -> FF, fill FFs
+// dropped, end at the first marker) into the window 1 KiB at a time by the
+// 64 lanes together (per-lane 16-byte lines, wave prefix sum of kept
+// bytes).  Bits past the scan's end read as zeros, as the serial reader
+// feeds them (libjpeg jpeg_fill_bit_buffer).
+struct DStream {
+  uint64_t src;   // absolute address of the scan's first stuffed byte
+  uint32_t len;   // stuffed bytes
+  uint32_t q;     // next stuffed byte to destuff
+  uint32_t prev;  // the stuffed byte before q (0 at the start)
+  uint32_t dend;  // valid destuffed bytes in dwin
+  uint32_t done;  // source exhausted (end of scan or a marker): zeros follow dend
+  uint32_t bp;    // bit position (in dwin) of the current round's offset 0
+};
+
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uint32_t &total) {
+  uint32_t s = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)s, d, 64);
+    if (lane >= (uint32_t)d) s += t;
+  }
+  total = uni((uint32_t)__shfl((int)s, 63, 64));
+  return s - v;
+}
+
+// Move the unread tail of the window to its front, then destuff 64 aligned
+// 16-byte lines of the scan at a time until the window is nearly full or
+// the scan's data ends.
+__device__ __forceinline__ void ds_refill(DStream &s, ProgSmem &sm, uint32_t lane) {
+  const uint32_t sb = uni((s.bp >> 3) & ~15u);
+  const uint32_t tail = s.dend > sb ? s.dend - sb : 0u;  // < 40 bytes (refill runs with < 24 unread)
+  __syncthreads();
+  const uint32_t t = lane < tail ? sm.dwin[sb + lane] : 0u;
+  __syncthreads();
+  if (lane < tail) sm.dwin[lane] = (uint8_t)t;
+  uint32_t bp = s.bp - sb * 8, dend = tail, q = s.q, prev = s.prev, done = s.done;
+  const uint64_t end = s.src + s.len;
+  while (!done && dend + 1024 + 16 <= kDWin) {
+    const uint64_t a0 = (s.src + q) & ~(uint64_t)15;  // line of lane 0
+    const uint64_t la = a0 + (uint64_t)lane * 16;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (la < end) v = *(const DG_GLOBAL u32x4 *)(uintptr_t)la;
+    uint32_t nx = 0;  // lane 63: first byte of the next line
+    if (lane == 63 && la + 16 < end) nx = *(const DG_GLOBAL uint8_t *)(uintptr_t)(la + 16);
+    const uint32_t nfirst = (uint32_t)__shfl_down((int)(v.x & 0xFFu), 1, 64);
+    const uint32_t plast = (uint32_t)__shfl_up((int)(v.w >> 24), 1, 64);
+    if (lane != 63) nx = nfirst;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    // relative offset of this line's byte 0 (may be < q for lane 0's line)
+    const int64_t r0 = (int64_t)(la - s.src);
+    uint32_t keep = 0, mk = 16;  // kept-byte mask, first marker byte index in the line
+    uint32_t pb = lane == 0 ? prev : plast;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++) {
+      const int64_t r = r0 + j;
+      const uint32_t c = (w[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
+      const uint32_t n = j < 15 ? (w[(j + 1) >> 2] >> (((j + 1) & 3) * 8)) & 0xFFu : nx;
+      const bool valid = r >= (int64_t)q && r < (int64_t)s.len;
+      const bool nvalid = r + 1 < (int64_t)s.len;
+      const uint32_t nn = nvalid ? n : 0xD9u;  // past the scan: a marker follows
+      if (valid) {
+        if (c == 0xFFu) {
+          if (nn == 0x00u) keep |= 1u << j;
+          else if (nn != 0xFFu && mk == 16) mk = j;
+        } else if (!(c == 0x00u && pb == 0xFFu && r > 0)) {
+          keep |= 1u << j;
+        }
+      }
+      pb = c;
+    }
+    // the scan's data ends at the first marker of the chunk
+    const uint64_t has = __ballot(mk < 16);
+    uint32_t cut_lane = 64;
+    if (has) {
+      cut_lane = (uint32_t)__builtin_ctzll(has);
+      done = 1;
+    }
+    if (lane > cut_lane) keep = 0;
+    if (lane == cut_lane) keep &= (1u << mk) - 1u;
+    uint32_t total;
+    const uint32_t pre = wave_excl_sum((uint32_t)__builtin_popcount(keep), lane, total);
+    uint32_t at = dend + pre;
+    for (uint32_t m = keep; m; m &= m - 1u) {
+      const uint32_t j = (uint32_t)__builtin_ctz(m);
+      const uint32_t wd = j < 8 ? (j < 4 ? v.x : v.y) : (j < 12 ? v.z : v.w);  // no dynamic register indexing
+      sm.dwin[at++] = (uint8_t)(wd >> ((j & 3) * 8));
+    }
+    dend += total;
+    const uint64_t next = a0 + 64 * 16 - s.src;  // relative offset after the last line
+    prev = uni((uint32_t)__shfl((int)(v.w >> 24), 63, 64));
+    q = next < s.len ? (uint32_t)next : s.len;
+    if (q >= s.len) done = 1;
+  }
+  __syncthreads();
+  if (done)
+    for (uint32_t i = lane; i < 64; i += 64) sm.dwin[dend + i] = 0;
+  __syncthreads();
+  s.bp = bp;
+  s.dend = dend;
+  s.q = q;
+  s.prev = prev;
+  s.done = done;
+}
+
+// lane's 32-bit peek at bit bp + lane of the window
+__device__ __forceinline__ uint32_t ds_peek(const ProgSmem &sm, uint32_t bp, uint32_t lane) {
+  const uint32_t o = bp + lane, bi = o >> 3;
+  const uint32_t *w = (const uint32_t *)sm.dwin;
+  const uint32_t a = bi >> 2;
+  const uint32_t w0 = w[a], w1 = w[a + 1], w2 = w[a + 2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, bi & 3u), hi = __builtin_amdgcn_alignbyte(w2, w1, bi & 3u);
+  const uint64_t v = ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
+  return (uint32_t)((v << (o & 7u)) >> 32);
+}
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+// v with lane `at` replaced by the uniform val
+__device__ __forceinline__ uint32_t wrl(uint32_t v, uint32_t val, uint32_t at) {
+  return threadIdx.x == at ? val : v;
+}
+
+__device__ __forceinline__ void prog_scan_spec(const ProgScan &sc, const ImageDesc &im, ProgSmem &sm, uint32_t lane,
+                               DG_GLOBAL int16_t *coef, uint32_t bpmu, uint32_t nunits, ProgDeps &pd) {
+  const uint32_t upc = kPBlk / bpmu;
+  const bool refine = sc.ah != 0;
+  const uint32_t ss = sc.ss, se = sc.se, al = sc.al;
+  const uint32_t nt = (ss == 0) ? (sc.ah == 0 ? sc.ns : 0) : 1;
+  // component of block j of an MCU (DC scans), 2 bits each
+  uint32_t cmap = 0;
+  {
+    uint32_t j = 0;
+    for (uint32_t i = 0; i < sc.ns && i < 4; i++) {
+      const uint32_t nb = sc.ns == 1 ? 1 : im.ch[sc.comp[i]] * im.cv[sc.comp[i]];
+      for (uint32_t b = 0; b < nb && j < 16; b++, j++) cmap |= i << (2 * j);
+    }
+    cmap = uni(cmap);
+  }
+  DStream s;
+  s.src = sc.data;
+  s.len = sc.len;
+  s.q = 0;
+  s.prev = 0;
+  s.dend = 0;
+  s.done = sc.len == 0;
+  s.bp = 0;
+  if (s.done) {
+    __syncthreads();
+    sm.dwin[lane] = 0;
+    __syncthreads();
+  }
+  uint32_t o = 0, peek = 0, sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
+  auto round = [&]() {
+    s.bp += o;
+    o = 0;
+    if (!s.done && (s.bp >> 3) + 24 > s.dend) ds_refill(s, sm, lane);
+    if (s.done && (s.bp >> 3) > s.dend + 8) s.bp = (s.dend + 8) * 8;  // past the data: zeros forever
+    peek = ds_peek(sm, s.bp, lane);
+    sp0 = huff_lookup(sm.tabs[0], peek);
+    if (nt > 1) sp1 = huff_lookup(sm.tabs[1], peek);
+    if (nt > 2) sp2 = huff_lookup(sm.tabs[2], peek);
+    if (nt > 3) sp3 = huff_lookup(sm.tabs[3], peek);
+  };
+  // n (<= 32) bits at offset off (<= 63) of the round
+  auto rd = [&](uint32_t off, uint32_t n) -> uint32_t { return n ? rdl(peek, off) >> (32u - n) : 0u; };
+  round();
+  int32_t pred0 = 0, pred1 = 0, pred2 = 0, pred3 = 0;
+  uint32_t eobrun = 0;
+  const uint64_t band = (se < 63 ? (2ull << se) - 1ull : ~0ull) & ~((1ull << ss) - 1ull);
+  for (uint32_t u0 = 0; u0 < nunits; u0 += upc) {
+    const uint32_t nu = nunits - u0 < upc ? nunits - u0 : upc;
+    const uint32_t nb = nu * bpmu;
+    prog_wait(pd, prog_unit_mrow(im, sc, u0 + nu - 1) + 1);
+    // stage this chunk's blocks (lane = block slot); history masks stay in registers
+    uint32_t g = 0, lci, nzlo = 0, nzhi = 0;
+    if (lane < nb) {
+      g = prog_unit_block(im, sc, u0 + lane / bpmu, lane % bpmu, lci);
+      u32x4 *dst = (u32x4 *)sm.blk[lane];
+      const DG_GLOBAL u32x4 *src = (const DG_GLOBAL u32x4 *)(coef + (size_t)g * 64);
+#pragma unroll
+      for (int qq = 0; qq < 8; qq++) {
+        const u32x4 x = refine ? src[qq] : u32x4{0u, 0u, 0u, 0u};
+        dst[qq] = x;
+        const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {  // coefficients 8qq + 2e, 8qq + 2e + 1
+          const uint32_t bits = ((ws[e] & 0xFFFFu) ? 1u : 0u) | ((ws[e] >> 16) ? 2u : 0u);
+          const int kk = qq * 8 + e * 2;
+          if (kk < 32) nzlo |= bits << kk;
+          else nzhi |= bits << (kk - 32);
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t corlo = 0, corhi = 0, ncor = 0, nplo = 0, nphi = 0, nnlo = 0, nnhi = 0;
+    uint64_t dcb = 0;
+    if (ss == 0 && !refine) {  // DC first
+      uint32_t j = 0;
+      for (uint32_t slot = 0; slot < nb; slot++) {
+        const uint32_t ci = (cmap >> (2 * j)) & 3u;
+        if (++j == bpmu) j = 0;
+        if (o > 47) round();
+        const uint32_t spv = ci == 0 ? sp0 : ci == 1 ? sp1 : ci == 2 ? sp2 : sp3;
+        const uint32_t e = rdl(spv, o);
+        o += e >> 8;
+        const uint32_t sz = e & 15u;
+        const int32_t diff = sz ? huff_extend((int32_t)rd(o, sz), (int32_t)sz) : 0;
+        o += sz;
+        int32_t p;
+        if (ci == 0) p = pred0 += diff;
+        else if (ci == 1) p = pred1 += diff;
+        else if (ci == 2) p = pred2 += diff;
+        else p = pred3 += diff;
+        sm.blk[slot][0] = (int16_t)((uint32_t)p << al);
+      }
+    } else if (ss == 0) {  // DC refine: one bit per block
+      for (uint32_t left = nb; left;) {
+        if (o > 63) round();
+        const uint32_t n = left < 32 ? left : 32;
+        dcb = (dcb << n) | rd(o, n);
+        o += n;
+        left -= n;
+      }
+    } else if (!refine) {  // AC first
+      for (uint32_t slot = 0; slot < nb;) {
+        if (eobrun) {
+          const uint32_t skip = eobrun < nb - slot ? eobrun : nb - slot;
+          eobrun -= skip;
+          slot += skip;
+          continue;
+        }
+        for (uint32_t k = ss; k <= se; k++) {
+          if (o > 47) round();
+          const uint32_t e = rdl(sp0, o);
+          o += e >> 8;
+          const uint32_t rr = (e >> 4) & 15u, sz = e & 15u;
+          if (sz) {
+            k += rr;
+            const int32_t v = huff_extend((int32_t)rd(o, sz), (int32_t)sz);
+            o += sz;
+            sm.blk[slot][zz(k)] = (int16_t)((uint32_t)v << al);
+          } else if (rr == 15) {
+            k += 15;
+          } else {
+            eobrun = (1u << rr) - 1u + rd(o, rr);
+            o += rr;
+            break;
+          }
+        }
+        slot++;
+      }
+    } else {  // AC refine
+      for (uint32_t slot = 0; slot < nb; slot++) {
+        const uint64_t nz = ((uint64_t)rdl(nzhi, slot) << 32) | rdl(nzlo, slot);
+        const uint64_t nzb = nz & band;
+        uint64_t cb = 0, np = 0, nn = 0;
+        uint32_t cc = 0;
+        auto take = [&](uint32_t c) {
+          while (c) {
+            if (o > 63) round();
+            const uint32_t n = c < 32 ? c : 32;
+            cb = (cb << n) | rd(o, n);
+            o += n;
+            cc += n;
+            c -= n;
+          }
+        };
+        uint32_t k = ss;
+        if (eobrun == 0) {
+          for (; k <= se; k++) {
+            if (o > 47) round();
+            const uint32_t e = rdl(sp0, o);
+            o += e >> 8;
+            const uint32_t rr = (e >> 4) & 15u, sz = e & 15u;
+            int32_t sg = 0;
+            if (sz) {
+              sg = rd(o, 1) ? 1 : -1;
+              o += 1;
+            } else if (rr != 15) {
+              eobrun = (1u << rr) + rd(o, rr);
+              o += rr;
+              break;
+            }
+            const uint64_t from = ~0ull << k;
+            uint64_t z = ~nz & band & from;
+            for (uint32_t i = 0; i < rr && z; i++) z &= z - 1ull;
+            if (z) {
+              const uint32_t pos = (uint32_t)__builtin_ctzll(z);
+              take((uint32_t)__builtin_popcountll(nzb & from & ((1ull << pos) - 1ull)));
+              k = pos;
+            } else {
+              take((uint32_t)__builtin_popcountll(nzb & from));
+              k = se + 1;
+            }
+            if (sg > 0) np |= 1ull << zz(k);
+            if (sg < 0) nn |= 1ull << zz(k);
+          }
+        }
+        if (eobrun > 0) {
+          if (k <= se) take((uint32_t)__builtin_popcountll(nzb & (~0ull << k)));
+          eobrun--;
+        }
+        corlo = wrl(corlo, (uint32_t)cb, slot);
+        corhi = wrl(corhi, (uint32_t)(cb >> 32), slot);
+        ncor = wrl(ncor, cc, slot);
+        nplo = wrl(nplo, (uint32_t)np, slot);
+        nphi = wrl(nphi, (uint32_t)(np >> 32), slot);
+        nnlo = wrl(nnlo, (uint32_t)nn, slot);
+        nnhi = wrl(nnhi, (uint32_t)(nn >> 32), slot);
+      }
+    }
+    __syncthreads();
+    if (lane < nb && refine) {
+      int16_t *bk = sm.blk[lane];
+      if (ss == 0) {
+        if ((dcb >> (nb - 1 - lane)) & 1u) bk[0] = (int16_t)(bk[0] | (int16_t)(1u << al));
+      } else {
+        const int32_t p1 = 1 << al, m1 = -(1 << al);
+        const uint64_t bits = ((uint64_t)corhi << 32) | corlo;
+        int32_t i = (int32_t)ncor - 1;  // bit of the lowest history-nonzero position
+        for (uint64_t m = (((uint64_t)nzhi << 32) | nzlo) & band; m && i >= 0; m &= m - 1ull, i--) {
+          if (!((bits >> i) & 1u)) continue;
+          const uint32_t pos = (uint32_t)__builtin_ctzll(m);
+          const int32_t v = bk[pos];
+          if ((v & p1) == 0) bk[pos] = (int16_t)(v >= 0 ? v + p1 : v + m1);
+        }
+        for (uint64_t m = ((uint64_t)nphi << 32) | nplo; m; m &= m - 1ull) bk[__builtin_ctzll(m)] = (int16_t)p1;
+        for (uint64_t m = ((uint64_t)nnhi << 32) | nnlo; m; m &= m - 1ull) bk[__builtin_ctzll(m)] = (int16_t)m1;
+      }
+    }
+    if (lane < nb) {
+      DG_GLOBAL int16_t *dst = coef + (size_t)g * 64;
+      for (uint32_t k = ss; k <= se; k++) dst[k] = sm.blk[lane][k];
+    }
+    prog_publish(pd, prog_rows_done(im, sc, u0 + nu));
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ imgs,
                                                   const ProgScan *__restrict__ scans,
-                                                  const WgItem *__restrict__ list, const HuffTable *__restrict__ pool) {
+                                                  const WgItem *__restrict__ list, const HuffTable *__restrict__ pool,
+                                                  uint32_t serial, DG_GLOBAL uint32_t *pflags) {
   __shared__ ProgSmem sm;
-  const ProgScan &sc = scans[list[blockIdx.x].item0];
-  const ImageDesc &im = imgs[sc.image];
   const uint32_t lane = threadIdx.x;
+  // pipelined launch: scans are taken in list (level) order, so every scan a
+  // worker waits for was taken earlier by a worker that is running
+  uint32_t t = blockIdx.x;
+  if (pflags) {
+    uint32_t v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add((uint32_t *)pflags, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = uni(v);
+  }
+  const uint32_t self = list[t].item0;
+  const ProgScan &sc = scans[self];
+  const ImageDesc &im = imgs[sc.image];
+  ProgDeps pd;
+  pd.flags = pflags;
+  pd.deps = sc.deps;
+  pd.first = sc.first;
+  pd.self = self;
+  pd.last = 0;
+  pd.bad = 0;
   // tables: one per scan component (DC first) or the AC table
   {
     const uint32_t words = (uint32_t)(sizeof(HuffTable) / 4);
@@ -355,6 +799,12 @@ __global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ 
     for (uint32_t i = 0; i < sc.ns; i++) bpmu += im.ch[sc.comp[i]] * im.cv[sc.comp[i]];
     nunits = im.mcux * im.mcuy;
   }
+  if (sc.restart == 0 && !serial) {
+    __syncthreads();
+    prog_scan_spec(sc, im, sm, lane, coef, bpmu, nunits, pd);
+    prog_finish(pd, imgs, sc, lane);
+    return;
+  }
   const uint32_t upc = kPBlk / bpmu;  // units per chunk
   const bool refine = sc.ah != 0;
   WReader r;
@@ -371,6 +821,7 @@ __global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ 
   for (uint32_t u0 = 0; u0 < nunits; u0 += upc) {
     const uint32_t nu = nunits - u0 < upc ? nunits - u0 : upc;
     const uint32_t nb = nu * bpmu;
+    prog_wait(pd, prog_unit_mrow(im, sc, u0 + nu - 1) + 1);
     // stage this chunk's blocks (lane = block slot)
     uint32_t g = 0, lci;
     if (lane < nb) {
@@ -430,7 +881,9 @@ __global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ 
       DG_GLOBAL int16_t *dst = coef + (size_t)g * 64;
       for (uint32_t k = sc.ss; k <= sc.se; k++) dst[k] = sm.blk[lane][k];
     }
+    prog_publish(pd, prog_rows_done(im, sc, u0 + nu));
   }
+  prog_finish(pd, imgs, sc, lane);
 }
 
 // ------------------------------------------------------------ launchers
@@ -440,8 +893,8 @@ void launch_prog_zero(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
 }
 
 void launch_prog_scan(hipStream_t st, const ImageDesc *imgs, const ProgScan *scans, const WgItem *list, uint32_t n,
-                      const HuffTable *pool) {
-  if (n) hipLaunchKernelGGL(k_prog_scan, dim3(n), dim3(64), 0, st, imgs, scans, list, pool);
+                      const HuffTable *pool, uint32_t serial, uint32_t *pflags) {
+  if (n) hipLaunchKernelGGL(k_prog_scan, dim3(n), dim3(64), 0, st, imgs, scans, list, pool, serial, (DG_GLOBAL uint32_t *)pflags);
 }
 
 }  // namespace dg

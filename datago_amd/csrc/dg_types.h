@@ -318,11 +318,14 @@ struct ImageDesc {
 };
 
 // ---- progressive JPEG (ImageDesc::prog > 0).  The coefficient blocks are
-// zeroed (k_prog_zero), then every scan is decoded by one lane of k_prog_scan
+// zeroed (k_prog_zero), then every scan is decoded by one wave of k_prog_scan
 // straight from the stuffed bytes.  Scans that touch disjoint (component,
-// coefficient band) sets are independent; the host groups them into levels
-// (a scan's level = 1 + the highest level of an earlier overlapping scan),
-// one launch per level.
+// coefficient band) sets are independent; the host gives each scan a level
+// (1 + the highest level of an earlier overlapping scan) and the list of
+// those earlier scans (deps).  All scans of a batch run in one launch,
+// taken in level order; a scan waits, chunk by chunk, only until its deps
+// have written the MCU rows it is about to read (a pipeline over the
+// image's rows instead of a barrier per level).
 struct ProgScan {
   uint64_t data;        // device address of the scan's first entropy-coded byte
   uint32_t len;         // entropy-coded bytes (up to the next non-RST marker)
@@ -335,7 +338,15 @@ struct ProgScan {
   uint32_t ss, se, ah, al;
   uint32_t restart;     // restart interval (MCUs; blocks when ns == 1), 0 = none
   uint32_t level;
+  uint32_t first;       // batch index of the image's first scan
+  uint32_t pad1;
+  uint64_t deps;        // earlier scans of the image this one reads (bit e = scan first + e)
 };
+// Pipelined scans (one launch per batch): progress word of scan j =
+// flags[1 + j], in MCU rows whose blocks the scan has written (kProgDone
+// when finished); flags[0] hands out scans to workgroups in list order.
+constexpr uint32_t kProgDone = 0xFFFFFFFFu;
+constexpr uint32_t kProgMaxScans = 64;  // per image (deps is a 64-bit mask)
 constexpr uint32_t kProgZeroBytes = 65536;  // coefficient bytes zeroed per k_prog_zero workgroup
 
 // One workgroup's work: an image and the first item it handles.

@@ -259,6 +259,14 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     progressive_ = v != 0;
     return DG_OK;
   }
+  if (k == "prog_pipe") {  // 0: one k_prog_scan launch per level (A/B)
+    prog_pipe_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "prog_serial") {  // every progressive scan on the serial reader (A/B; restart scans always are)
+    prog_serial_ = v != 0;
+    return DG_OK;
+  }
   if (k == "entropy_once") {  // decode-once: k_huff_sync stages coefficients, k_huff_scatter writes them
     entropy_once_ = v != 0;
     return DG_OK;
@@ -1113,6 +1121,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       b.uf_maxbpp = std::max(b.uf_maxbpp, dd.png.bpp);
     }
   b.uf_flags_off = b.uf_n ? L.take((size_t)(b.uf_n + 1) * 4) : 0;
+  b.pf_n = 0;
+  for (const ImageDesc &dd : b.descs)
+    if (dd.fmt == kFmtJpeg) b.pf_n += dd.prog;
+  b.pf_off = b.pf_n ? L.take((size_t)(b.pf_n + 1) * 4) : 0;
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
   const size_t ckpt_off = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits)) * sizeof(Ckpt));
   // fused IDCT leftovers: at most one carried-in block per subsequence, plus
@@ -1204,6 +1216,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         r.ah = (uint32_t)sc.ah;
         r.al = (uint32_t)sc.al;
         r.restart = (uint32_t)sc.restart;
+        r.first = (uint32_t)first;
         uint32_t lvl = 0;
         for (size_t e = 0; e < j; e++) {
           const JpegScan &pr = h.scans[e];
@@ -1211,7 +1224,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
           bool share = false;
           for (int x = 0; x < pr.ns; x++)
             for (int y = 0; y < sc.ns; y++) share |= pr.comp[x] == sc.comp[y];
-          if (share) lvl = std::max(lvl, b.pscans[first + e].level + 1);
+          if (share) {
+            lvl = std::max(lvl, b.pscans[first + e].level + 1);
+            r.deps |= 1ull << e;
+          }
         }
         r.level = lvl;
         b.pscans.push_back(r);
@@ -1544,10 +1560,16 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (!from_fix && !b.pscans.empty()) {  // progressive JPEG: zero, then the scans level by level
     launch_prog_zero(sl.st, dd, lst(L_PROG_ZERO), cnt(L_PROG_ZERO));
     const ProgScan *ps = (const ProgScan *)(M + b.pscan_off);
-    uint32_t at = 0;
-    for (uint32_t nl : b.prog_level_n) {
-      launch_prog_scan(sl.st, dd, ps, lst(L_PROG) + at, nl, hp);
-      at += nl;
+    if (prog_pipe_) {
+      uint32_t *pf = (uint32_t *)((char *)sl.scratch.p + b.pf_off);
+      HIPCHK(hipMemsetAsync(pf, 0, (size_t)(b.pf_n + 1) * 4, sl.st));
+      launch_prog_scan(sl.st, dd, ps, lst(L_PROG), cnt(L_PROG), hp, prog_serial_ ? 1u : 0u, pf);
+    } else {
+      uint32_t at = 0;
+      for (uint32_t nl : b.prog_level_n) {
+        launch_prog_scan(sl.st, dd, ps, lst(L_PROG) + at, nl, hp, prog_serial_ ? 1u : 0u, nullptr);
+        at += nl;
+      }
     }
   }
   if (next()) return DG_ERR_DEVICE;

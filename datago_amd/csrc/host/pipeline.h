@@ -62,6 +62,8 @@ struct Batch {
   uint32_t uf_n = 0;        // PNG unfilter bands (progress flags, L_UNF tasks)
   uint32_t uf_maxbpp = 1;   // widest filter unit of the batch's PNGs (k_png_unfilter's LDS)
   size_t uf_flags_off = 0;  // their flags + ticket in the scratch arena (zeroed per batch)
+  uint32_t pf_n = 0;        // progressive scans (progress words, one pipelined k_prog_scan launch)
+  size_t pf_off = 0;        // ticket + progress words in the scratch arena (zeroed per batch)
   std::vector<uint8_t> blob;
   size_t blob_off = 0;
   bool any_png = false, any_alpha = false, any_enc = false;
@@ -223,6 +225,8 @@ class Context {
   bool hv_fused_ = false;               // option "hv_fused": first H + V pass fused (k_resize_hv) when it fits
   bool idct_fused_ = false;             // option "idct_fused" (measured 7x slower k_huff_write: off)
   bool progressive_ = false;            // option "progressive"
+  bool prog_serial_ = false;            // option "prog_serial": serial reader for every scan (A/B)
+  bool prog_pipe_ = true;               // option "prog_pipe": all scans in one pipelined launch (0: one launch per level)
   bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first
   bool entropy_once_ = false;           // option "entropy_once": decode-once staging + k_huff_scatter
   int64_t stat_png_serial_ = 0, stat_png_chunks_ = 0;

@@ -53,10 +53,12 @@ void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
 // final copy / gray->RGB expansion: 256 output pixels per workgroup
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 // progressive JPEG (dg_prog.hip): zero coefficients (kProgZeroBytes per
-// workgroup), then one lane per scan of one dependency level
+// workgroup), then one wave per scan: all scans in one launch with pflags
+// (zeroed, 1 + scans words; dg_types.h ProgScan), or one level per launch
+// with pflags null
 void launch_prog_zero(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 void launch_prog_scan(hipStream_t st, const ImageDesc *imgs, const ProgScan *scans, const WgItem *list, uint32_t n,
-                      const HuffTable *pool);
+                      const HuffTable *pool, uint32_t serial, uint32_t *pflags);
 
 }  // namespace dg
 

@@ -95,3 +95,30 @@ def test_progressive_off_by_default_is_unsupported():
     ctx = L.Context(0)
     res = ctx.decode_batch([_prog(45, 64, 48), synth.make_jpeg(46, 64, 48)])
     assert res[0][0] == L.DG_ERR_UNSUPPORTED and res[1][0] == L.DG_OK
+
+
+def test_progressive_speculative_equals_serial_reader():
+    """The speculative-table decoder (scans without restarts) in the
+    pipelined single launch against the serial reader launched level by level
+    (options prog_serial, prog_pipe) and the oracle, over qualities 1-100
+    (long EOB runs at low quality, dense refinements at high quality), all
+    samplings and gray, sizes from 1 px to > 64 blocks per chunk row."""
+    L = _lib()
+    spec_ctx, ser_ctx = L.Context(0), L.Context(0)
+    for c in (spec_ctx, ser_ctx):
+        c.set_option("progressive", 1)
+    ser_ctx.set_option("prog_serial", 1)
+    ser_ctx.set_option("prog_pipe", 0)  # serial reader, one launch per level: the round-1 schedule
+    datas = []
+    for i, q in enumerate([1, 5, 12, 30, 50, 70, 85, 95, 100, 100, 97, 3]):
+        rng = np.random.default_rng(900 + i)
+        w, h = [(1, 1), (7, 9), (640, 480), (1031, 77), (64, 1500), (333, 333)][i % 6]
+        datas.append(_prog(900 + i, w, h, q, ["4:2:0", "4:2:2", "4:4:4"][i % 3], i % 5 == 4))
+        datas.append(synth.make_jpeg(950 + i, int(rng.integers(100, 900)), int(rng.integers(100, 900)), q,
+                                     progressive=True))
+    a, b = spec_ctx.decode_batch(datas), ser_ctx.decode_batch(datas)
+    for i, (data, (st, arr, _), (st2, arr2, _)) in enumerate(zip(datas, a, b)):
+        assert st == 0 and st2 == 0, (i, L.last_error())
+        ost, ref = O.jpeg_decode(data)
+        assert np.array_equal(arr.reshape(ref.shape), ref), i
+        assert np.array_equal(arr, arr2), i

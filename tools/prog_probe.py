@@ -18,16 +18,23 @@ def main():
         cases.append(("pool-largest", synth.make_jpeg(2 * 1_000_003 + i, w, h, q, ss, g, 0, progressive=True)))
     cases.append(("1024x1024 q90", synth.make_jpeg(5, 1024, 1024, 90, progressive=True)))
     cases.append(("1024x1024 q90 baseline", synth.make_jpeg(5, 1024, 1024, 90)))
-    ctx = L.Context(0)
-    ctx.set_option("timing", 1)
-    ctx.set_option("progressive", 1)
+    for serial, pipe in ((1, 0), (0, 0), (0, 1)):
+        ctx = L.Context(0)
+        ctx.set_option("timing", 1)
+        ctx.set_option("progressive", 1)
+        ctx.set_option("prog_serial", serial)
+        ctx.set_option("prog_pipe", pipe)
+        run(ctx, cases, ("serial" if serial else "speculative") + ("+pipelined" if pipe else "+levels"))
+
+
+def run(ctx, cases, mode):
     for name, d in cases:
         for rep in range(3):
             t = time.perf_counter()
             res = ctx.decode_batch([d])
             dt = time.perf_counter() - t
         tm = ctx.timings()
-        print(name, len(d), "status", res[0][0], f"wall {dt*1e3:.1f} ms",
+        print(mode, name, len(d), "status", res[0][0], f"wall {dt*1e3:.1f} ms",
               {k: round(v, 3) for k, v in tm.items() if v > 0.01}, flush=True)
 
 
