@@ -87,6 +87,11 @@ def parse():
     ap.add_argument("--one-threads", type=int, default=32,
                     help="integration path: host threads calling dg_decode_one (coalesced into GPU batches); 0 = off")
     ap.add_argument("--one-images", type=int, default=0, help="images through dg_decode_one (0: 2 batches)")
+    ap.add_argument("--ctx-opt", action="append", default=[],
+                    help="extra context option key=value (experiments; repeatable)")
+    ap.add_argument("--prog-lanes", type=int, default=-1,
+                    help="context option prog_lanes: progressive batches in flight beside the baseline ones "
+                         "(dg_decode_one coalescing; -1 = library default)")
     ap.add_argument("--shards", type=int, default=8, help="wds workload: shards of 1000 samples")
     ap.add_argument("--workload", choices=("jpeg", "cfg4", "png", "wds"), default="jpeg",
                     help="jpeg: configs[1] (the headline); cfg4: configs[3] (1M samples over a 16,384-image pool, "
@@ -562,6 +567,11 @@ def main() -> int:
         ctx.set_option("idct_fused", a.idct_fused)
     if a.progressive_frac > 0:
         ctx.set_option("progressive", 1)
+    if a.prog_lanes >= 0:
+        ctx.set_option("prog_lanes", a.prog_lanes)
+    for kv in a.ctx_opt:
+        k_, v_ = kv.split("=", 1)
+        ctx.set_option(k_, int(v_))
     if a.entropy_lpt >= 0:
         ctx.set_option("entropy_lpt", a.entropy_lpt)
     if a.entropy_once >= 0:
@@ -756,7 +766,7 @@ def main() -> int:
         one = {"threads": a.one_threads, "images": n_one, "failed": sum(fails),
                "mpix_s": round(sum(done_px) / dt1 / 1e6, 2), "images_per_s": round(n_one / dt1, 1),
                "gpu_batches": nb_, "mean_images_per_batch": round((ctx.stat("coalesced_images") - i0) / max(nb_, 1), 1),
-               "coalesce_max": 64, "coalesce_us": 500,
+               "coalesce_max": 64, "coalesce_us": 500, "prog_lanes": a.prog_lanes,
                "note": "host JPEG bytes in -> host RGB out per call (PCIe both ways), like e2e_host_mpix_s"}
 
     result = None
@@ -843,7 +853,7 @@ def main() -> int:
                                     "+ L8 mask PNG pairs, mask aligned to the image's bucket, decode + crop/resize "
                                     f"to 1024/32{' + JPEG q92 re-encode of every payload' if a.encode else ''}"),
                        "pre_encode_images": bool(a.encode),
-                       "progressive_frac": a.progressive_frac,
+                       "progressive_frac": a.progressive_frac, **({"ctx_opt": a.ctx_opt} if a.ctx_opt else {}),
                        "restart_marker_rows": a.rst_rows,
                        "images_per_step": B_, "pool": a.pool, "samples": a.samples,
                        "short_side": [a.short_min, a.short_max], "buckets": f"{a.size}/{a.ratio}/0.5/2.0",

@@ -675,6 +675,14 @@ __device__ __forceinline__ void prog_scan_spec(const ProgScan &sc, const ImageDe
         uint64_t cb = 0, np = 0, nn = 0;
         uint32_t cc = 0;
         auto take = [&](uint32_t c) {
+          if (c == 0) return;
+          if (o > 63) round();
+          if (c <= 32) {  // the common case: one register read
+            cb = (cb << c) | rd(o, c);
+            o += c;
+            cc += c;
+            return;
+          }
           while (c) {
             if (o > 63) round();
             const uint32_t n = c < 32 ? c : 32;
@@ -684,35 +692,30 @@ __device__ __forceinline__ void prog_scan_spec(const ProgScan &sc, const ImageDe
             c -= n;
           }
         };
+        const uint64_t hz = ~nz & band;  // history-zero positions of the band
         uint32_t k = ss;
         if (eobrun == 0) {
           for (; k <= se; k++) {
             if (o > 47) round();
             const uint32_t e = rdl(sp0, o);
-            o += e >> 8;
-            const uint32_t rr = (e >> 4) & 15u, sz = e & 15u;
-            int32_t sg = 0;
-            if (sz) {
-              sg = rd(o, 1) ? 1 : -1;
-              o += 1;
-            } else if (rr != 15) {
-              eobrun = (1u << rr) + rd(o, rr);
-              o += rr;
+            const uint32_t l = e >> 8, rr = (e >> 4) & 15u, sz = e & 15u;
+            const uint32_t after = rdl(peek, o + l);  // the bits after the code (o + l <= 63)
+            if (!sz && rr != 15) {                    // EOBn
+              eobrun = (1u << rr) + (rr ? after >> (32u - rr) : 0u);
+              o += l + rr;
               break;
             }
+            o += l + (sz ? 1u : 0u);  // sign bit
+            // land on the (rr+1)-th history-zero position from k (ZRL: the 16th)
             const uint64_t from = ~0ull << k;
-            uint64_t z = ~nz & band & from;
+            uint64_t z = hz & from;
             for (uint32_t i = 0; i < rr && z; i++) z &= z - 1ull;
-            if (z) {
-              const uint32_t pos = (uint32_t)__builtin_ctzll(z);
-              take((uint32_t)__builtin_popcountll(nzb & from & ((1ull << pos) - 1ull)));
-              k = pos;
-            } else {
-              take((uint32_t)__builtin_popcountll(nzb & from));
-              k = se + 1;
-            }
-            if (sg > 0) np |= 1ull << zz(k);
-            if (sg < 0) nn |= 1ull << zz(k);
+            const uint32_t pos = z ? (uint32_t)__builtin_ctzll(z) : se + 1;
+            take((uint32_t)__builtin_popcountll(nzb & from & (z ? (1ull << pos) - 1ull : ~0ull)));
+            k = pos;
+            const uint64_t bit = sz ? 1ull << zz(k) : 0ull;
+            np |= (after >> 31) ? bit : 0ull;
+            nn |= (after >> 31) ? 0ull : bit;
           }
         }
         if (eobrun > 0) {

@@ -13,6 +13,23 @@ static const int kNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
 static inline int rd16(const uint8_t *p) { return (p[0] << 8) | p[1]; }
 
 bool is_jpeg(const uint8_t *d, size_t n) { return n >= 3 && d[0] == 0xFF && d[1] == 0xD8 && d[2] == 0xFF; }
+bool jpeg_sniff_progressive(const uint8_t *d, size_t n) {
+  if (!is_jpeg(d, n)) return false;
+  size_t p = 2;
+  while (p + 4 <= n) {
+    if (d[p] != 0xFF) return false;
+    const uint8_t m = d[p + 1];
+    if (m == 0xFF) {  // fill byte
+      p++;
+      continue;
+    }
+    if (m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) return m == 0xC2;
+    if (m == 0xD9 || m == 0xDA) return false;
+    p += 2 + (((size_t)d[p + 2] << 8) | d[p + 3]);
+  }
+  return false;
+}
+
 bool is_png(const uint8_t *d, size_t n) {
   static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
   return n >= 8 && memcmp(d, sig, 8) == 0;

@@ -77,6 +77,8 @@ void parse_jpeg_header(const uint8_t *d, size_t n, JpegHeader &h);
 bool build_huff_table(const HuffSpec &spec, HuffTable &out);
 
 bool is_jpeg(const uint8_t *d, size_t n);
+// Marker walk up to the first SOFn: true for SOF2 (progressive, Huffman).
+bool jpeg_sniff_progressive(const uint8_t *d, size_t n);
 bool is_png(const uint8_t *d, size_t n);
 
 }  // namespace dg

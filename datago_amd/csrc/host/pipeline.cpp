@@ -109,7 +109,7 @@ Context::~Context() {
   for (Slot &sl : slots_) {
     for (auto e : sl.ev) hipEventDestroy(e);
     if (sl.done) hipEventDestroy(sl.done);
-    for (hipEvent_t e : {sl.ev_meta, sl.ev_coef, sl.ev_zero, sl.ev_png0, sl.ev_png1})
+    for (hipEvent_t e : {sl.ev_meta, sl.ev_coef, sl.ev_zero, sl.ev_prog, sl.ev_png0, sl.ev_png1})
       if (e) hipEventDestroy(e);
     if (sl.coef.p) hipFree(sl.coef.p);
     for (hipStream_t q : {sl.st, sl.side})
@@ -167,6 +167,7 @@ dg_status Context::init() {
     HIPCHK(hipEventCreateWithFlags(&sl.ev_meta, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_coef, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_zero, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&sl.ev_prog, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_png0, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_png1, hipEventDisableTiming));
   }
@@ -257,6 +258,15 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     // image holds its whole batch for ~0.1-2 s; the default
     // returns DG_ERR_UNSUPPORTED and the caller's CPU decoder takes them.
     progressive_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "prog_lanes") {  // progressive batches in flight beside the baseline ones (dg_decode_one); 0: mixed in
+    if (v < 0 || v > kMaxInflight - 1) return DG_ERR_INVALID;
+    prog_lanes_ = (int)v;
+    return DG_OK;
+  }
+  if (k == "prog_side") {  // progressive scans on the side stream, beside the baseline entropy decode
+    prog_side_ = v != 0;
     return DG_OK;
   }
   if (k == "prog_pipe") {  // 0: one k_prog_scan launch per level (A/B)
@@ -415,7 +425,7 @@ static constexpr size_t kPoolKeep = 4096;
 static constexpr size_t kPoolMax = 65535;
 
 dg_status Context::flush_pools() {
-  for (int s = 0; s < nslots_; s++) {  // batches in flight still read (and may resync with) the pools
+  for (int s = 0; s < kMaxInflight; s++) {  // batches in flight still read (and may resync with) the pools
     Slot &o = slots_[s];
     if (o.batch && !o.batch->done) {
       dg_status st = finish(o);
@@ -605,7 +615,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     return DG_ERR_INVALID;
   }
   HIPCHK(hipSetDevice(device_));
-  Slot &sl = slots_[next_slot_];
+  Slot &sl = slots_[pick_slot()];
   if (sl.batch && !sl.batch->done) {  // this slot's previous batch must complete first
     dg_status st = finish(sl);
     if (st) return st;
@@ -613,6 +623,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   std::unique_ptr<Batch> bp(new Batch());
   Batch &b = *bp;
   b.ticket = next_ticket_++;
+  b.fin = std::make_shared<BatchEvent>();
+  HIPCHK(hipEventCreateWithFlags(&b.fin->e, hipEventDisableTiming));
   b.n = n;
   b.host_io = host_io;
   b.metas = metas;
@@ -1484,8 +1496,22 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   phase(5);
   stat_batches_++;
   *ticket = sl.batch->ticket;
-  next_slot_ = (next_slot_ + 1) % nslots_;
   return DG_OK;
+}
+
+// A slot for the next batch: an idle one (never used, or its batch finished
+// or complete on the device), else the next in turn, whose batch the caller
+// then finishes first.  With progressive lanes a long progressive batch
+// holds its slot while baseline batches keep cycling through the others.
+int Context::pick_slot() {
+  const int total = std::min(kMaxInflight, nslots_ + (progressive_ ? prog_lanes_ : 0));
+  for (int i = 0; i < total; i++)
+    if (!slots_[i].batch || slots_[i].batch->done) return i;
+  for (int i = 0; i < total; i++)
+    if (hipEventQuery(slots_[i].done) == hipSuccess) return i;
+  const int i = next_slot_ % total;
+  next_slot_ = (i + 1) % total;
+  return i;
 }
 
 dg_status Context::launch_all(Slot &sl, bool from_fix) {
@@ -1557,20 +1583,27 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     launch_destuff_write(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
   }
   if (next()) return DG_ERR_DEVICE;
-  if (!from_fix && !b.pscans.empty()) {  // progressive JPEG: zero, then the scans level by level
-    launch_prog_zero(sl.st, dd, lst(L_PROG_ZERO), cnt(L_PROG_ZERO));
+  // progressive JPEG: zero, then the scans (one pipelined launch, or level by
+  // level).  On the side stream, beside the baseline images' entropy decode
+  // (the main stream waits for it before the IDCT), except with stage timing
+  // on, where every stage runs on the main stream so its events bracket it.
+  const bool pside = side_stream_ && prog_side_ && !timing_ && !b.pscans.empty();
+  if (!from_fix && !b.pscans.empty()) {
+    hipStream_t pst = pside ? sl.side : sl.st;
+    launch_prog_zero(pst, dd, lst(L_PROG_ZERO), cnt(L_PROG_ZERO));
     const ProgScan *ps = (const ProgScan *)(M + b.pscan_off);
     if (prog_pipe_) {
       uint32_t *pf = (uint32_t *)((char *)sl.scratch.p + b.pf_off);
-      HIPCHK(hipMemsetAsync(pf, 0, (size_t)(b.pf_n + 1) * 4, sl.st));
-      launch_prog_scan(sl.st, dd, ps, lst(L_PROG), cnt(L_PROG), hp, prog_serial_ ? 1u : 0u, pf);
+      HIPCHK(hipMemsetAsync(pf, 0, (size_t)(b.pf_n + 1) * 4, pst));
+      launch_prog_scan(pst, dd, ps, lst(L_PROG), cnt(L_PROG), hp, prog_serial_ ? 1u : 0u, pf);
     } else {
       uint32_t at = 0;
       for (uint32_t nl : b.prog_level_n) {
-        launch_prog_scan(sl.st, dd, ps, lst(L_PROG) + at, nl, hp, prog_serial_ ? 1u : 0u, nullptr);
+        launch_prog_scan(pst, dd, ps, lst(L_PROG) + at, nl, hp, prog_serial_ ? 1u : 0u, nullptr);
         at += nl;
       }
     }
+    if (pside) HIPCHK(hipEventRecord(sl.ev_prog, sl.side));
   }
   if (next()) return DG_ERR_DEVICE;
   Ckpt *ck = (Ckpt *)((char *)sl.scratch.p + sl.ckpt_off);
@@ -1586,6 +1619,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     launch_huff_write(sl.st, dm, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots, qp);
   if (next()) return DG_ERR_DEVICE;
   if (next()) return DG_ERR_DEVICE;  // coeffs (side stream)
+  if (pside) HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_prog, 0));  // progressive coefficients
   if (b.any_fused) launch_idct_list(sl.st, dd, qp, fl, std::min<uint32_t>(2048u, (b.idct_cap + 31) / 32));
   launch_idct(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);
   if (next()) return DG_ERR_DEVICE;
@@ -1642,6 +1676,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   }
   if (next()) return DG_ERR_DEVICE;  // download
   HIPCHK(hipEventRecord(sl.done, sl.st));
+  HIPCHK(hipEventRecord(b.fin->e, sl.st));
   return DG_OK;
 }
 
@@ -1775,19 +1810,19 @@ Slot *Context::find(uint64_t ticket) {
 }
 
 dg_status Context::wait(uint64_t ticket) {
-  hipEvent_t ev;
+  std::shared_ptr<BatchEvent> fin;
   {
     std::lock_guard<std::mutex> lk(mu_);
     HIPCHK(hipSetDevice(device_));
     Slot *sl = find(ticket);
     if (!sl) return ticket < next_ticket_ ? DG_OK : DG_ERR_INVALID;  // already recycled => completed
     if (sl->batch->done) return DG_OK;
-    ev = sl->done;
+    fin = sl->batch->fin;
   }
   // block on the GPU without holding the context lock, so other threads can
-  // plan and submit meanwhile (if the slot is recycled first, the wait below
-  // only takes longer; the ticket then reads as completed)
-  HIPCHK(hipEventSynchronize(ev));
+  // plan and submit meanwhile (the batch's own event: if the slot is
+  // recycled first, the ticket then reads as completed)
+  HIPCHK(hipEventSynchronize(fin->e));
   std::lock_guard<std::mutex> lk(mu_);
   Slot *sl = find(ticket);
   if (!sl) return ticket < next_ticket_ ? DG_OK : DG_ERR_INVALID;
@@ -1823,38 +1858,46 @@ dg_status Context::flush_batch(std::vector<OneReq *> &batch) {
 
 dg_status Context::decode_one(const uint8_t *src, size_t len, int32_t forced, uint8_t *out, uint64_t cap,
                               dg_payload_meta *meta) {
-  OneReq r{src, len, forced, out, cap, meta, false, DG_OK};
+  OneReq r{src, len, forced, out, cap, meta, false, DG_OK, false};
   if (coalesce_max_ <= 1) {
     std::vector<OneReq *> one{&r};
     flush_batch(one);
     return r.st;
   }
+  // Progressive JPEGs decode their scans serially (one wave per scan, ~0.1-1 s
+  // for a large file), so they coalesce into batches of their own: a
+  // baseline caller never waits behind a progressive chain, and up to
+  // prog_lanes progressive batches run beside the baseline ones.
+  r.prog = progressive_ && prog_lanes_ > 0 && jpeg_sniff_progressive(src, len);
   std::unique_lock<std::mutex> lk(cmu_);
   callers_++;
-  pending_.push_back(&r);
+  std::vector<OneReq *> &q = r.prog ? ppending_ : pending_;
+  q.push_back(&r);
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(coalesce_us_);
   for (;;) {
     if (r.done) break;
     // flush when the batch is full, when every caller in here is already
-    // waiting (nobody else can add), or at the deadline; two batches in
-    // flight at most (the context's two slots)
-    const bool ready = !pending_.empty() &&
-                       ((int)pending_.size() >= coalesce_max_ || (int)pending_.size() >= callers_ - inflight_reqs_ ||
-                        std::chrono::steady_clock::now() >= deadline);
-    if (ready && inflight_ < nslots_ && std::find(pending_.begin(), pending_.end(), &r) != pending_.end()) {
+    // waiting (nobody else can add), or at the deadline; nslots baseline
+    // batches (+ prog_lanes progressive ones) in flight at most
+    const int waiting = callers_ - inflight_reqs_;
+    const bool ready = !q.empty() && ((int)q.size() >= coalesce_max_ ||
+                                      (int)(pending_.size() + ppending_.size()) >= waiting ||
+                                      std::chrono::steady_clock::now() >= deadline);
+    const bool room = r.prog ? pinflight_ < prog_lanes_ : inflight_ < nslots_;
+    if (ready && room && std::find(q.begin(), q.end(), &r) != q.end()) {
       std::vector<OneReq *> batch;
-      const size_t take = std::min(pending_.size(), (size_t)coalesce_max_);
-      batch.assign(pending_.begin(), pending_.begin() + take);
-      pending_.erase(pending_.begin(), pending_.begin() + take);
-      inflight_++;
+      const size_t take = std::min(q.size(), (size_t)coalesce_max_);
+      batch.assign(q.begin(), q.begin() + take);
+      q.erase(q.begin(), q.begin() + take);
+      (r.prog ? pinflight_ : inflight_)++;
       inflight_reqs_ += (int)batch.size();
       stat_coalesced_batches_++;
       stat_coalesced_images_ += (int64_t)batch.size();
       lk.unlock();
       flush_batch(batch);
       lk.lock();
-      for (OneReq *q : batch) q->done = true;
-      inflight_--;
+      for (OneReq *x : batch) x->done = true;
+      (r.prog ? pinflight_ : inflight_)--;
       inflight_reqs_ -= (int)batch.size();
       ccv_.notify_all();
       continue;

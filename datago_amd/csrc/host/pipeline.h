@@ -44,8 +44,18 @@ struct ImagePlan {
   uint64_t img_bytes = 0;  // transformed image bytes (out_w * out_h * out_c)
 };
 
+// The completion event of one batch (shared with waiters, so a slot recycled
+// for a later batch never makes a waiter sync on that batch's work).
+struct BatchEvent {
+  hipEvent_t e = nullptr;
+  ~BatchEvent() {
+    if (e) hipEventDestroy(e);
+  }
+};
+
 struct Batch {
   uint64_t ticket = 0;
+  std::shared_ptr<BatchEvent> fin;
   int n = 0;
   bool host_io = false;
   std::vector<ImagePlan> plans;
@@ -112,7 +122,7 @@ struct Slot {
   // beside batch k's pixel kernels (the entropy kernels leave most CUs idle
   // in their tails).
   hipStream_t st = nullptr, side = nullptr;
-  hipEvent_t ev_meta = nullptr, ev_coef = nullptr, ev_zero = nullptr;
+  hipEvent_t ev_meta = nullptr, ev_coef = nullptr, ev_zero = nullptr, ev_prog = nullptr;
   hipEvent_t ev_png0 = nullptr, ev_png1 = nullptr;  // PNG: serial inflate on the side stream
   std::unique_ptr<Batch> batch;
   size_t subs_off = 0, ckpt_off = 0;
@@ -168,6 +178,7 @@ class Context {
   dg_status launch_all(Slot &sl, bool from_fix);
   dg_status finish(Slot &sl);
   Slot *find(uint64_t ticket);
+  int pick_slot();
 
   int device_;
   bool has_cfg_ = false;
@@ -187,11 +198,14 @@ class Context {
     dg_payload_meta *meta;
     bool done;
     dg_status st;
+    bool prog;  // progressive JPEG: coalesced apart (option "prog_lanes")
   };
   std::mutex cmu_;
   std::condition_variable ccv_;
-  std::vector<OneReq *> pending_;
-  int callers_ = 0, inflight_ = 0, inflight_reqs_ = 0;
+  std::vector<OneReq *> pending_, ppending_;  // baseline / progressive callers waiting for a batch
+  int callers_ = 0, inflight_ = 0, inflight_reqs_ = 0, pinflight_ = 0;
+  int prog_lanes_ = 1;  // option "prog_lanes": progressive batches in flight beside the baseline ones
+  bool prog_side_ = false;  // option "prog_side": progressive scans on the side stream (measured slower: off)
   int coalesce_max_ = 64, coalesce_us_ = 500;
   int64_t stat_coalesced_batches_ = 0, stat_coalesced_images_ = 0;
   dg_status flush_batch(std::vector<OneReq *> &batch);

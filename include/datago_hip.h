@@ -204,7 +204,13 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *                 force an entropy write-pass mismatch / a resync that never settles (tests of the
  *                 per-image DG_ERR_UNSUPPORTED those failures return)
  *   "progressive" 1 = decode progressive JPEGs on the GPU (default 0: DG_ERR_UNSUPPORTED, the
- *                 caller's CPU decoder takes them; refinement scans decode serially)
+ *                 caller's CPU decoder takes them; a refinement scan is one serial chain, so a large
+ *                 file holds its batch for ~0.1-1 s: worth it for progressive-heavy corpora)
+ *   "prog_lanes"  dg_decode_one: progressive files coalesce into batches of their own, this many in
+ *                 flight beside the baseline batches (default 1; 0 = mixed into the baseline batches)
+ *   "prog_pipe"   1 = all scans of a batch in one pipelined launch (default); 0 = one launch per level
+ *   "prog_serial" 1 = serial bit reader for every scan (A/B; scans with restart intervals always use it)
+ *   "prog_side"   1 = progressive scans on the slot's side stream (default 0: measured slower)
  *   "slots"       batches in flight, 1..4 (default 2)
  *   "hb_bands"    band H kernel: 8-row bands per workgroup, 1..64 (default 8)
  *   "entropy_lpt" 1 = dispatch the slowest entropy workgroups first (default 1)

@@ -122,3 +122,43 @@ def test_progressive_speculative_equals_serial_reader():
         ost, ref = O.jpeg_decode(data)
         assert np.array_equal(arr.reshape(ref.shape), ref), i
         assert np.array_equal(arr, arr2), i
+
+
+@pytest.mark.parametrize("lanes", [1, 0])
+def test_decode_one_progressive_lane(lanes):
+    """dg_decode_one with progressive files among baseline ones: progressive
+    callers coalesce into batches of their own (option prog_lanes, default 1)
+    that run beside the baseline batches in a slot of their own; every result
+    equals the oracle's, and the two kinds never share a batch."""
+    import threading
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+    ctx.set_option("progressive", 1)
+    ctx.set_option("prog_lanes", lanes)
+    ctx.set_option("coalesce_us", 5000)
+    datas = []
+    for i in range(48):
+        rng = np.random.default_rng(3100 + i)
+        datas.append(synth.make_jpeg(3100 + i, int(rng.integers(64, 900)), int(rng.integers(64, 900)),
+                                     int(rng.integers(40, 98)), ["4:2:0", "4:2:2", "4:4:4"][i % 3],
+                                     progressive=i % 4 == 1))
+    res = [None] * len(datas)
+
+    def work(k):
+        for i in range(k, len(datas), 12):
+            res[i] = ctx.decode_one(datas[i])
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(12)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    for i, (data, (st, arr, meta)) in enumerate(zip(datas, res)):
+        assert st == 0, (i, L.last_error())
+        w, h = O.jpeg_info(data)[1:3]
+        tw, th_ = t.target_size(w, h)
+        ost, dec = O.jpeg_decode(data)
+        assert np.array_equal(arr, O.crop_and_resize(dec, tw, th_, O.MODE_FIR)), i
+    assert ctx.stat("coalesced_images") == len(datas)
