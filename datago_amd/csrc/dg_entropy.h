@@ -160,6 +160,49 @@ DG_HD uint32_t huff_next_z(uint32_t z, uint32_t sym) {
   return z == 0u ? 1u : zac;
 }
 
+// ---- multi-symbol AC steps for the state-only decodes (lead-in, sync)
+//
+// The state-only decodes need no AC values, only where the symbols end.  A
+// per-AC-table lookup on the next kMultiBits stream bits gives how many of
+// them the AC symbols (code + magnitude bits) that fit entirely inside take,
+// their zigzag advance, and whether the last one was EOB:
+//   entry = bits (0 = none fits) | advance << 4 | eob << 11
+// A step takes the entry instead of one symbol when the whole run stays in
+// the block and ends at or before the next event, so it passes exactly the
+// symbol boundaries single steps would: the same states, fewer steps.
+constexpr uint32_t kMultiBits = 10;
+constexpr uint32_t kMultiLuts = 3;  // distinct AC tables per image
+
+template <class TAB>
+DG_HD uint32_t multi_entry(const TAB &t, uint32_t pfx) {
+  const uint32_t bits = pfx << (32u - kMultiBits);
+  uint32_t o = 0, adv = 0, eob = 0;
+  while (o < kMultiBits) {
+    const uint32_t e = huff_lookup(t, bits << o);
+    const uint32_t len = e >> 8, sym = e & 0xFFu, size = sym & 15u, run = sym >> 4;
+    if (len == 0u || len >= 16u || o + len + size > kMultiBits) break;  // invalid, or not inside the window
+    if (size == 0u && run != 15u) {  // EOB
+      o += len;
+      eob = 1;
+      break;
+    }
+    const uint32_t nadv = adv + (size == 0u ? 16u : run + 1u);
+    if (nadv > 64u) break;
+    adv = nadv;
+    o += len + size;
+    if (adv == 64u) break;  // the block ends with this coefficient
+  }
+  return o | (adv << 4) | (eob << 11);
+}
+
+// z after a multi entry m taken at z, or 0xFFFFFFFF if it cannot be taken
+// there (no symbol fits, or the run would leave the block)
+DG_HD uint32_t multi_next_z(uint32_t m, uint32_t z) {
+  const uint32_t c = m & 15u, adv = (m >> 4) & 127u, eob = (m >> 11) & 1u;
+  const bool ok = c != 0u && z != 0u && (eob ? z + adv < 64u : z + adv <= 64u);
+  return ok ? (eob ? 64u : z + adv) : 0xFFFFFFFFu;
+}
+
 // Accumulators of one subsequence decode.
 struct RangeAcc {
   uint32_t out;
@@ -469,7 +512,8 @@ DG_HD uint32_t first_marker(const DG_GLOBAL uint32_t *mk, uint32_t nmk, uint32_t
 // re-decode.
 template <class TAB>
 DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uint8_t *stream,
-                       const DG_GLOBAL uint32_t *mk, uint32_t s, uint32_t lead) {
+                       const DG_GLOBAL uint32_t *mk, uint32_t s, uint32_t lead,
+                       const uint16_t *mt = nullptr, uint32_t acm = 0xFFu) {
   const uint32_t a0 = s * im.sub_bits;
   if (s == 0 || lead == 0 || a0 >= im.ds_bits) return pack_state(0, 0, 0);
   uint32_t pos = a0 > lead ? a0 - lead : 0u;
@@ -480,6 +524,8 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
   // the current block's DC/AC tables, resolved when the block changes
   const TAB *tdc = &tabs[(slotmap >> ((comp << 1) << 2)) & 15u];
   const TAB *tac = &tabs[(slotmap >> (((comp << 1) | 1u) << 2)) & 15u];
+  // multi-symbol table of the block's AC table (acm: 2 bits per component, 3 = none)
+  uint32_t mi = mt ? (acm >> (2u * comp)) & 3u : 3u;
   BitWin b;
   bw_init(b, stream, im.ds_lsw, pos);
   for (;;) {
@@ -490,6 +536,7 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
       comp = cbits & 3u;
       tdc = &tabs[(slotmap >> ((comp << 1) << 2)) & 15u];
       tac = &tabs[(slotmap >> (((comp << 1) | 1u) << 2)) & 15u];
+      mi = mt ? (acm >> (2u * comp)) & 3u : 3u;
       midx++;
       mpos = midx < im.nmk ? mk[midx] : kInf;
       bw_seek(b, pos);
@@ -498,19 +545,25 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
     bw_refill(b);
     // state-only step, straight-line apart from the long-code lookup and the
     // refill (with 64 lanes in different places of their blocks, a branch per
-    // case would run every case every step)
+    // case would run every case every step): one symbol, or a multi-symbol
+    // AC run that ends at or before the next event (start or marker)
     const uint32_t bits = bw_peek(b, pos);
     const uint32_t e = huff_decode(*(z == 0u ? tdc : tac), bits);
+    const uint32_t m = (mi != 3u && z != 0u) ? (uint32_t)mt[(mi << kMultiBits) | (bits >> (32u - kMultiBits))] : 0u;
     const uint32_t sym = e & 0xFFu;
-    pos += (e >> 8) + (sym & 15u);
+    const uint32_t zm = multi_next_z(m, z);
+    const uint32_t lim = a0 < mpos ? a0 : mpos;
+    const bool take_m = zm != 0xFFFFFFFFu && pos + (m & 15u) <= lim;
+    pos += take_m ? (m & 15u) : (e >> 8) + (sym & 15u);
     bw_shift(b, pos);
-    const uint32_t zn = huff_next_z(z, sym);
+    const uint32_t zn = take_m ? zm : huff_next_z(z, sym);
     const bool bend = zn >= 64u;
     z = bend ? 0u : zn;
     r = bend ? (r + 1u == bpm ? 0u : r + 1u) : r;
     comp = (cbits >> (2u * r)) & 3u;
     tdc = &tabs[(slotmap >> ((comp << 1) << 2)) & 15u];
     tac = &tabs[(slotmap >> (((comp << 1) | 1u) << 2)) & 15u];
+    mi = mt ? (acm >> (2u * comp)) & 3u : 3u;
   }
   const uint32_t rel = pos - a0;
   return pack_state(rel > 255 ? 255 : rel, r, z);
@@ -525,7 +578,8 @@ template <bool WRITE, class TAB, bool COOP = false>
 DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uint8_t *stream,
                         const DG_GLOBAL uint32_t *mk,
                         uint32_t s, uint32_t in, RangeAcc &acc, WriteCtx *w, DG_GLOBAL Ckpt *ck = nullptr,
-                        bool merge = false, uint32_t old_out = 0, StageCtx *stg = nullptr) {
+                        bool merge = false, uint32_t old_out = 0, StageCtx *stg = nullptr,
+                        const uint16_t *mt = nullptr, uint32_t acm = 0xFFu) {
   const uint32_t S = im.sub_bits, total = im.ds_bits;
   const uint32_t a0 = s * S;
   const uint32_t a1 = (a0 + S < total) ? a0 + S : total;
@@ -566,9 +620,13 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
     uint32_t e = a1 < mpos ? a1 : mpos;
     return (k < nck && cpos < e) ? cpos : e;
   };
+  // multi-symbol AC steps (state-only passes: no AC values written or staged)
+  const bool multi = !WRITE && !stage && mt != nullptr;
+  uint32_t mi = 3u;
   auto block_tables = [&](const TAB *&tdc, const TAB *&tac) {
     tdc = &tabs[(slotmap >> ((comp << 1) << 2)) & 15u];
     tac = &tabs[(slotmap >> (((comp << 1) | 1u) << 2)) & 15u];
+    mi = multi ? (acm >> (2u * comp)) & 3u : 3u;
   };
   const TAB *tdc, *tac;
   block_tables(tdc, tac);
@@ -650,7 +708,14 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
     const uint32_t size = sym & 15u;
     const uint32_t run = isdc ? 0u : (sym >> 4);
     const int32_t v = huff_value(bits, len, size);
-    pos += len + size;
+    uint32_t zm = 0xFFFFFFFFu, mc = 0;
+    if (!WRITE) {  // an AC run ending at or before the next event: same boundaries as single steps
+      const uint32_t m = (mi != 3u && !isdc) ? (uint32_t)mt[(mi << kMultiBits) | (bits >> (32u - kMultiBits))] : 0u;
+      mc = m & 15u;
+      zm = pos + mc <= ev ? multi_next_z(m, z) : 0xFFFFFFFFu;
+    }
+    const bool take_m = zm != 0xFFFFFFFFu;
+    pos += take_m ? mc : len + size;
     bw_shift(b, pos);
     const int32_t vdc = isdc ? v : 0;
     acc.n += isdc ? 1u : 0u;
@@ -677,7 +742,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       const uint32_t zz = z + run;
       if (isdc || (size && zz < 64u)) w->blk[zz] = (int16_t)(isdc ? sel3(w->pred, comp) : v);
     }
-    const uint32_t zn = huff_next_z(z, sym);
+    const uint32_t zn = take_m ? zm : huff_next_z(z, sym);
     const bool bend = zn >= 64u;
     if (WRITE && bend) wc_end_block<COOP>(*w, pending);
     z = bend ? 0u : zn;

@@ -265,6 +265,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     prog_lanes_ = (int)v;
     return DG_OK;
   }
+  if (k == "multi_lead") {  // multi-symbol AC steps in k_huff_sync's lead-in (A/B)
+    multi_lead_ = v != 0;
+    return DG_OK;
+  }
   if (k == "prog_side") {  // progressive scans on the side stream, beside the baseline entropy decode
     prog_side_ = v != 0;
     return DG_OK;
@@ -864,6 +868,11 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     }
     d.nslots = (uint8_t)nslots;
     b.max_slots = std::max<uint32_t>(b.max_slots, (uint32_t)nslots);
+    if (!h.progressive) {  // distinct AC slots (k_huff_sync builds a multi-symbol lookup for each, up to 3)
+      uint32_t acs = 0;
+      for (int c = 0; c < h.ncomp; c++) acs |= 1u << ((d.slotmap >> ((2 * c + 1) * 4)) & 15u);
+      b.max_ac = std::max<uint32_t>(b.max_ac, std::min<uint32_t>((uint32_t)__builtin_popcount(acs), kMultiLuts));
+    }
     if (h.progressive) {  // scans decoded by k_prog_scan (records built once the source address is known)
       d.prog = (uint32_t)h.scans.size();
       if (host_io) in_off[i] = IN.take(lens[i] + 16, 16);
@@ -1607,7 +1616,9 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   }
   if (next()) return DG_ERR_DEVICE;
   Ckpt *ck = (Ckpt *)((char *)sl.scratch.p + sl.ckpt_off);
-  if (!from_fix) launch_huff_sync(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on, b.max_slots);
+  if (!from_fix)
+    launch_huff_sync(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on, b.max_slots,
+                     multi_lead_ ? b.max_ac : 0u);
   if (next()) return DG_ERR_DEVICE;
   launch_huff_fix(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on, b.max_slots);
   if (next()) return DG_ERR_DEVICE;

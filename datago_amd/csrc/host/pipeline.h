@@ -81,6 +81,7 @@ struct Batch {
   uint32_t idct_cap = 0;   // entries of BatchFlags::idct_list
   bool stage_on = false;  // decode-once staging (option "entropy_once")
   uint32_t max_slots = 1; // largest Huffman table count of an image (dynamic LDS of k_huff_sync/fix)
+  uint32_t max_ac = 0;    // most distinct AC tables of a baseline JPEG (k_huff_sync multi-symbol lookups)
   size_t words_off = 0, words_bytes = 0;  // contiguous encoder bit buffers (zeroed per batch)
   size_t enctab_off = 0;                  // EncTables in the blob
   std::vector<ProgScan> pscans;           // progressive JPEG scans of the batch
@@ -205,6 +206,7 @@ class Context {
   std::vector<OneReq *> pending_, ppending_;  // baseline / progressive callers waiting for a batch
   int callers_ = 0, inflight_ = 0, inflight_reqs_ = 0, pinflight_ = 0;
   int prog_lanes_ = 1;  // option "prog_lanes": progressive batches in flight beside the baseline ones
+  bool multi_lead_ = true;  // option "multi_lead": multi-symbol AC steps in k_huff_sync's lead-in
   bool prog_side_ = false;  // option "prog_side": progressive scans on the side stream (measured slower: off)
   int coalesce_max_ = 64, coalesce_us_ = 500;
   int64_t stat_coalesced_batches_ = 0, stat_coalesced_images_ = 0;

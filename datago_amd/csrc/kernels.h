@@ -14,10 +14,11 @@ void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *l
 // (sync/fix: 255 useful subsequences per workgroup, see kernels.hip)
 struct Ckpt;
 // stage: decode-once staging (ImageDesc::stage), see k_huff_scatter
-// max_slots: the largest ImageDesc::nslots in the batch (dynamic LDS for the tables)
+// max_slots: the largest ImageDesc::nslots in the batch (dynamic LDS for the tables);
+// max_ac: the most distinct AC tables of an image (multi-symbol lead-in lookups, 0 = off)
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                       const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
-                      uint32_t max_slots);
+                      uint32_t max_slots, uint32_t max_ac);
 void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
                      uint32_t max_slots);

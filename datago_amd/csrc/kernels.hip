@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
                                                    const WgItem *__restrict__ list,
                                                    const HuffTable *__restrict__ pool,
                                                    SubState *__restrict__ subs, Ckpt *__restrict__ ckpt,
-                                                   BatchFlags *flags) {
+                                                   BatchFlags *flags, uint32_t multi) {
   extern __shared__ __attribute__((aligned(16))) uint8_t huff_dyn[];  // im.nslots tables (launch: batch max)
   HuffTable *tabs = (HuffTable *)huff_dyn;
   __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
@@ -292,6 +292,29 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
   load_tables(tabs, pool, im);
+  // multi-symbol lookups of the image's distinct AC tables (after its tables;
+  // the launch sizes the area for the batch's most), built from the LDS tables
+  uint16_t *mt = (uint16_t *)(huff_dyn + (size_t)im.nslots * sizeof(HuffTable));
+  uint32_t acm = 0xFFu, nac = 0, acs[kMultiLuts] = {0, 0, 0};
+  for (uint32_t c = 0; c < im.ncomp && c < 4; c++) {
+    const uint32_t sl = (im.slotmap >> ((2 * c + 1) * 4)) & 15u;
+    uint32_t a = 3;
+    for (uint32_t q = 0; q < nac; q++)
+      if (acs[q] == sl) a = q;
+    if (a == 3 && nac < kMultiLuts) {
+      acs[nac] = sl;
+      a = nac++;
+    }
+    acm = (acm & ~(3u << (2 * c))) | (a << (2 * c));
+  }
+  __syncthreads();
+  if (multi) {
+    for (uint32_t i = threadIdx.x; i < (nac << kMultiBits); i += blockDim.x) {
+      const uint32_t q = i >> kMultiBits;
+      const uint32_t sl = q == 0 ? acs[0] : q == 1 ? acs[1] : acs[2];
+      mt[i] = (uint16_t)multi_entry(tabs[sl], i & ((1u << kMultiBits) - 1u));
+    }
+  }
   __syncthreads();
   const int t = threadIdx.x;
   const uint32_t s0 = it.item0;                  // first useful subsequence
@@ -315,8 +338,9 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   const DG_GLOBAL uint32_t *mkp = gp<const uint32_t>(im.mk);
   RangeAcc acc = {0, 0, 0, {0, 0, 0}};
   // entry state: exact for s == 0, otherwise the lead-in decode's guess
-  uint32_t in = active ? lead_in(im, tabs, scan, mkp, s, im.lead_bits) : pack_state(0, 0, 0);
-  if (active) decode_range<false>(im, tabs, scan, mkp, s, in, acc, nullptr, ck, false, 0, stg);
+  uint32_t in = active ? lead_in(im, tabs, scan, mkp, s, im.lead_bits, multi ? mt : nullptr, acm)
+                       : pack_state(0, 0, 0);
+  if (active) decode_range<false>(im, tabs, scan, mkp, s, in, acc, nullptr, ck, false, 0, stg, multi ? mt : nullptr, acm);
   ex[t] = active ? acc.out : 0u;
   ins[t] = in;
   __syncthreads();
@@ -326,7 +350,7 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
     uint32_t pin = redo ? ex[t - 1] : 0u;
     __syncthreads();
     if (redo) {
-      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr, ck, true, ex[t], stg);
+      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr, ck, true, ex[t], stg, multi ? mt : nullptr, acm);
       ex[t] = acc.out;
       ins[t] = pin;
     }
@@ -1750,13 +1774,14 @@ void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *l
 // per workgroup, 8 resident workgroups per CU instead of 6
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                       const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
-                      uint32_t max_slots) {
+                      uint32_t max_slots, uint32_t max_ac) {
   if (!nwg) return;
-  const size_t lds = (size_t)max_slots * sizeof(HuffTable);
+  const size_t lds = (size_t)max_slots * sizeof(HuffTable) + ((size_t)max_ac << kMultiBits) * 2;
+  const uint32_t multi = max_ac ? 1u : 0u;
   if (stage)
-    hipLaunchKernelGGL(k_huff_sync<true>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags);
+    hipLaunchKernelGGL(k_huff_sync<true>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags, multi);
   else
-    hipLaunchKernelGGL(k_huff_sync<false>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags);
+    hipLaunchKernelGGL(k_huff_sync<false>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags, multi);
 }
 void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,

@@ -16,6 +16,10 @@ using namespace dg;
 
 static uint32_t g_lead = 0;
 extern "C" void emu_set_lead(uint32_t lead) { g_lead = lead; }
+// lead-ins whose multi-symbol result (k_huff_sync's) differs from the single-step one
+static int64_t g_multi_mismatch = 0, g_multi_checked = 0;
+extern "C" int64_t emu_multi_mismatch() { return g_multi_mismatch; }
+extern "C" int64_t emu_multi_checked() { return g_multi_checked; }
 
 extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bits, int16_t *out,
                                 size_t cap_blocks, size_t *nblocks, int64_t *stats) {
@@ -58,6 +62,13 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
     build_huff_table(h.ac[h.comp[c].ta], t);
     d.slotmap |= (uint32_t)tabs.size() << ((2 * c + 1) * 4);
     tabs.push_back(t);
+  }
+  // k_huff_sync's multi-symbol lookups: one per component's AC table here (slots 2c + 1)
+  std::vector<uint16_t> mt;
+  uint32_t acm = 0xFFu;
+  for (int c = 0; c < h.ncomp && c < (int)kMultiLuts; c++) {
+    for (uint32_t p = 0; p < (1u << kMultiBits); p++) mt.push_back((uint16_t)multi_entry(tabs[2 * c + 1], p));
+    acm = (acm & ~(3u << (2 * c))) | ((uint32_t)c << (2 * c));
   }
   d.scan_len = (uint32_t)(h.scan_end - h.scan_off);
   const uint8_t *raw = data + h.scan_off;
@@ -106,8 +117,13 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
       active[t] = si >= 0 && si < (int64_t)d.nsub;
       head[t] = (t == 0) || (s0 == 0 && t == 1);
       if (!active[t]) continue;
-      ins[t] = lead_in(d, tabs.data(), scan, mkp, (uint32_t)si, d.lead_bits);
-      decode_range<false>(d, tabs.data(), scan, mkp, (uint32_t)si, ins[t], acc[t], nullptr, t ? ckp((uint32_t)si) : nullptr);
+      ins[t] = lead_in(d, tabs.data(), scan, mkp, (uint32_t)si, d.lead_bits, mt.data(), acm);
+      if (d.lead_bits) {
+        g_multi_checked++;
+        g_multi_mismatch += ins[t] != lead_in(d, tabs.data(), scan, mkp, (uint32_t)si, d.lead_bits);
+      }
+      decode_range<false>(d, tabs.data(), scan, mkp, (uint32_t)si, ins[t], acc[t], nullptr, t ? ckp((uint32_t)si) : nullptr,
+                          false, 0, nullptr, mt.data(), acm);
       ex[t] = acc[t].out;
     }
     int64_t it = 0;
@@ -120,7 +136,8 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
       for (uint32_t t = 1; t < (uint32_t)kSubPerWg; t++)
         if (redo[t]) {
           uint32_t si = s0 + t - 1;
-          decode_range<false>(d, tabs.data(), scan, mkp, si, pin[t], acc[t], nullptr, ckp(si), true, ex[t]);
+          decode_range<false>(d, tabs.data(), scan, mkp, si, pin[t], acc[t], nullptr, ckp(si), true, ex[t], nullptr,
+                              mt.data(), acm);
           ex[t] = acc[t].out;
           ins[t] = pin[t];
           redo_total++;
