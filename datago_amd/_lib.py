@@ -22,7 +22,7 @@ except Exception:  # pragma: no cover - torch is part of the image
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdatago_hip.so")
+LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(HERE, "libdatago_hip.so")  # override: experiment builds
 
 DG_OK, DG_ERR_UNSUPPORTED, DG_ERR_CORRUPT, DG_ERR_OOM, DG_ERR_BAD_BUCKET = 0, 1, 2, 3, 4
 DG_ERR_INVALID, DG_ERR_SMALL_BUFFER, DG_ERR_DEVICE, DG_ERR_NOT_READY = 5, 6, 7, 8

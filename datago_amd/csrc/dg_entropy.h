@@ -170,7 +170,10 @@ DG_HD uint32_t huff_next_z(uint32_t z, uint32_t sym) {
 // A step takes the entry instead of one symbol when the whole run stays in
 // the block and ends at or before the next event, so it passes exactly the
 // symbol boundaries single steps would: the same states, fewer steps.
-constexpr uint32_t kMultiBits = 10;
+#ifndef DG_MULTI_BITS
+#define DG_MULTI_BITS 11  // 10 / 11 / 12 measured: huff_sync 1.77 / 1.63 / 1.75 ms (experiment builds: DG_HIPCC_FLAGS=-DDG_MULTI_BITS=n, n <= 15)
+#endif
+constexpr uint32_t kMultiBits = DG_MULTI_BITS;
 constexpr uint32_t kMultiLuts = 3;  // distinct AC tables per image
 
 template <class TAB>
