@@ -107,9 +107,9 @@ struct Batch {
   std::vector<float> stage_ms;
 };
 
-// One in-flight batch's device/pinned buffers.  Two (or, option "slots", up
-// to kMaxInflight) slots let the host plan and upload batch k+1 while the GPU
-// still runs batch k.
+// One in-flight batch's device/pinned buffers.  Three (option "slots", 1 to
+// kMaxInflight) slots let the host plan and upload batch k+1 while the GPU
+// still runs batches k and k-1.
 constexpr int kMaxInflight = 4;
 struct Slot {
   DevBuf scratch, meta, input;
@@ -221,7 +221,7 @@ class Context {
 
   Slot slots_[kMaxInflight];
   uint32_t ncu_ = 256;  // compute units: persistent-worker grids
-  int nslots_ = 2;  // option "slots": batches in flight (each slot: own streams + scratch)
+  int nslots_ = 3;  // option "slots": batches in flight (each slot: own streams + scratch; 3 measured +3-4% over 2)
   int next_slot_ = 0;
   uint64_t next_ticket_ = 1;
 

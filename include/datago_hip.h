@@ -211,7 +211,7 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "prog_pipe"   1 = all scans of a batch in one pipelined launch (default); 0 = one launch per level
  *   "prog_serial" 1 = serial bit reader for every scan (A/B; scans with restart intervals always use it)
  *   "prog_side"   1 = progressive scans on the slot's side stream (default 0: measured slower)
- *   "slots"       batches in flight, 1..4 (default 2)
+ *   "slots"       batches in flight, 1..4 (default 3)
  *   "hb_bands"    band H kernel: 8-row bands per workgroup, 1..64 (default 8)
  *   "entropy_lpt" 1 = dispatch the slowest entropy workgroups first (default 1)
  *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)
