@@ -582,7 +582,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
                         const DG_GLOBAL uint32_t *mk,
                         uint32_t s, uint32_t in, RangeAcc &acc, WriteCtx *w, DG_GLOBAL Ckpt *ck = nullptr,
                         bool merge = false, uint32_t old_out = 0, StageCtx *stg = nullptr,
-                        const uint16_t *mt = nullptr, uint32_t acm = 0xFFu) {
+                        const uint16_t *mt = nullptr, uint32_t acm = 0xFFu, bool pair = false) {
   const uint32_t S = im.sub_bits, total = im.ds_bits;
   const uint32_t a0 = s * S;
   const uint32_t a1 = (a0 + S < total) ? a0 + S : total;
@@ -719,7 +719,6 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
     }
     const bool take_m = zm != 0xFFFFFFFFu;
     pos += take_m ? mc : len + size;
-    bw_shift(b, pos);
     const int32_t vdc = isdc ? v : 0;
     acc.n += isdc ? 1u : 0u;
     add3(acc.dc, comp, vdc);
@@ -745,7 +744,25 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       const uint32_t zz = z + run;
       if (isdc || (size && zz < 64u)) w->blk[zz] = (int16_t)(isdc ? sel3(w->pred, comp) : v);
     }
-    const uint32_t zn = take_m ? zm : huff_next_z(z, sym);
+    uint32_t zn = take_m ? zm : huff_next_z(z, sym);
+    if (WRITE && pair) {
+      // A second AC symbol of the same block out of the same 32-bit peek, when
+      // the first leaves the block open, ends before the next event and both
+      // fit in the peek: exactly the symbol the next single step would decode.
+      const uint32_t c1 = len + size;
+      const bool eob1 = !isdc && size == 0u && run != 15u;
+      const uint32_t bits2 = c1 < 32u ? bits << c1 : 0u;
+      const uint32_t e2 = huff_decode(*tac, bits2);
+      const uint32_t len2 = e2 >> 8, sym2 = e2 & 0xFFu, size2 = sym2 & 15u;
+      const bool take2 = !eob1 && zn < 64u && pos < ev && c1 + len2 + size2 <= 32u;
+      if (take2) {
+        const uint32_t zz2 = zn + (sym2 >> 4);
+        if (size2 && zz2 < 64u) w->blk[zz2] = (int16_t)huff_value(bits2, len2, size2);
+        pos += len2 + size2;
+        zn = huff_next_z(zn, sym2);
+      }
+    }
+    bw_shift(b, pos);  // one shift: both symbols came out of one peek (< 32 bits past it)
     const bool bend = zn >= 64u;
     if (WRITE && bend) wc_end_block<COOP>(*w, pending);
     z = bend ? 0u : zn;

@@ -491,7 +491,7 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
                                                     const WgItem *__restrict__ list,
                                                     const HuffTable *__restrict__ pool,
                                                     const SubState *__restrict__ subs, BatchFlags *flags,
-                                                    const QuantTable *__restrict__ qpool) {
+                                                    const QuantTable *__restrict__ qpool, uint32_t pair) {
   extern __shared__ __attribute__((aligned(16))) uint8_t huff_dyn[];  // im.nslots tables (launch: batch max)
   HuffTable *tabs = (HuffTable *)huff_dyn;
   __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][kBlkStride];
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
     }
     RangeAcc acc;
     decode_range<true, HuffTable, true>(im, tabs, gp<const uint8_t>(im.ds), gp<const uint32_t>(im.mk), s, ss.in,
-                                        acc, &w);
+                                        acc, &w, nullptr, false, 0, nullptr, nullptr, 0xFFu, pair != 0);
     if (acc.out != ss.out || (s == 0 && (flags->debug & kDbgForceWriteMismatch))) {
       // the write pass left this range in another state than the sync pass
       // proved: the blocks after it are not trustworthy.  The image goes back
@@ -1798,10 +1798,10 @@ void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint3
 }
 void launch_huff_write(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                        const HuffTable *pool, const SubState *subs, BatchFlags *flags, uint32_t max_slots,
-                       const QuantTable *qpool) {
+                       const QuantTable *qpool, uint32_t pair) {
   if (!nwg) return;
   hipLaunchKernelGGL(k_huff_write, dim3(nwg), dim3(256), (size_t)max_slots * sizeof(HuffTable), st, imgs, list,
-                     pool, subs, flags, qpool);
+                     pool, subs, flags, qpool, pair);
 }
 void launch_idct_list(hipStream_t st, const ImageDesc *imgs, const QuantTable *qpool, const BatchFlags *flags,
                       uint32_t nwg) {
