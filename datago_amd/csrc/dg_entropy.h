@@ -516,7 +516,7 @@ DG_HD uint32_t first_marker(const DG_GLOBAL uint32_t *mk, uint32_t nmk, uint32_t
 template <class TAB>
 DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uint8_t *stream,
                        const DG_GLOBAL uint32_t *mk, uint32_t s, uint32_t lead,
-                       const uint16_t *mt = nullptr, uint32_t acm = 0xFFu) {
+                       const uint16_t *mt = nullptr, uint32_t acm = 0xFFu, bool pair = false) {
   const uint32_t a0 = s * im.sub_bits;
   if (s == 0 || lead == 0 || a0 >= im.ds_bits) return pack_state(0, 0, 0);
   uint32_t pos = a0 > lead ? a0 - lead : 0u;
@@ -558,8 +558,19 @@ DG_HD uint32_t lead_in(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uin
     const uint32_t lim = a0 < mpos ? a0 : mpos;
     const bool take_m = zm != 0xFFFFFFFFu && pos + (m & 15u) <= lim;
     pos += take_m ? (m & 15u) : (e >> 8) + (sym & 15u);
+    uint32_t zn = take_m ? zm : huff_next_z(z, sym);
+    if (pair && !take_m) {  // a second AC symbol from the same peek (see decode_range)
+      const uint32_t c1 = (e >> 8) + (sym & 15u);
+      const bool eob1 = z != 0u && (sym & 15u) == 0u && (sym >> 4) != 15u;
+      const uint32_t bits2 = c1 < 32u ? bits << c1 : 0u;
+      const uint32_t e2 = huff_decode(*tac, bits2);
+      const uint32_t sym2 = e2 & 0xFFu, c2 = (e2 >> 8) + (sym2 & 15u);
+      if (!eob1 && zn < 64u && pos < lim && c1 + c2 <= 32u) {
+        pos += c2;
+        zn = huff_next_z(zn, sym2);
+      }
+    }
     bw_shift(b, pos);
-    const uint32_t zn = take_m ? zm : huff_next_z(z, sym);
     const bool bend = zn >= 64u;
     z = bend ? 0u : zn;
     r = bend ? (r + 1u == bpm ? 0u : r + 1u) : r;
@@ -745,10 +756,11 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       if (isdc || (size && zz < 64u)) w->blk[zz] = (int16_t)(isdc ? sel3(w->pred, comp) : v);
     }
     uint32_t zn = take_m ? zm : huff_next_z(z, sym);
-    if (WRITE && pair) {
+    if (pair && !stage && (WRITE || !take_m)) {
       // A second AC symbol of the same block out of the same 32-bit peek, when
       // the first leaves the block open, ends before the next event and both
       // fit in the peek: exactly the symbol the next single step would decode.
+      // (The state-only sync decode takes it only after a single symbol.)
       const uint32_t c1 = len + size;
       const bool eob1 = !isdc && size == 0u && run != 15u;
       const uint32_t bits2 = c1 < 32u ? bits << c1 : 0u;
@@ -756,8 +768,10 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
       const uint32_t len2 = e2 >> 8, sym2 = e2 & 0xFFu, size2 = sym2 & 15u;
       const bool take2 = !eob1 && zn < 64u && pos < ev && c1 + len2 + size2 <= 32u;
       if (take2) {
-        const uint32_t zz2 = zn + (sym2 >> 4);
-        if (size2 && zz2 < 64u) w->blk[zz2] = (int16_t)huff_value(bits2, len2, size2);
+        if (WRITE) {
+          const uint32_t zz2 = zn + (sym2 >> 4);
+          if (size2 && zz2 < 64u) w->blk[zz2] = (int16_t)huff_value(bits2, len2, size2);
+        }
         pos += len2 + size2;
         zn = huff_next_z(zn, sym2);
       }

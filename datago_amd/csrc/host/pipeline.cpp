@@ -265,6 +265,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     prog_lanes_ = (int)v;
     return DG_OK;
   }
+  if (k == "sync_pair") {  // k_huff_sync: a second AC symbol per single step from the same peek (A/B)
+    sync_pair_ = v != 0;
+    return DG_OK;
+  }
   if (k == "write_pair") {  // k_huff_write: a second AC symbol per step from the same peek (A/B)
     write_pair_ = v != 0;
     return DG_OK;
@@ -1622,7 +1626,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   Ckpt *ck = (Ckpt *)((char *)sl.scratch.p + sl.ckpt_off);
   if (!from_fix)
     launch_huff_sync(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on, b.max_slots,
-                     multi_lead_ ? b.max_ac : 0u);
+                     multi_lead_ ? b.max_ac : 0u, sync_pair_);
   if (next()) return DG_ERR_DEVICE;
   launch_huff_fix(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on, b.max_slots);
   if (next()) return DG_ERR_DEVICE;

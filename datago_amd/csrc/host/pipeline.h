@@ -207,7 +207,8 @@ class Context {
   int callers_ = 0, inflight_ = 0, inflight_reqs_ = 0, pinflight_ = 0;
   int prog_lanes_ = 1;  // option "prog_lanes": progressive batches in flight beside the baseline ones
   bool multi_lead_ = true;
-  bool write_pair_ = true;  // option "write_pair": two AC symbols per k_huff_write step when they fit one peek  // option "multi_lead": multi-symbol AC steps in k_huff_sync's lead-in
+  bool write_pair_ = true;
+  bool sync_pair_ = false;  // option "sync_pair": the same in k_huff_sync (measured slower beside the multi-symbol steps: off)  // option "write_pair": two AC symbols per k_huff_write step when they fit one peek  // option "multi_lead": multi-symbol AC steps in k_huff_sync's lead-in
   bool prog_side_ = false;  // option "prog_side": progressive scans on the side stream (measured slower: off)
   int coalesce_max_ = 64, coalesce_us_ = 500;
   int64_t stat_coalesced_batches_ = 0, stat_coalesced_images_ = 0;

@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
     acm = (acm & ~(3u << (2 * c))) | (a << (2 * c));
   }
   __syncthreads();
-  if (multi) {
+  if (multi & 1u) {
     for (uint32_t i = threadIdx.x; i < (nac << kMultiBits); i += blockDim.x) {
       const uint32_t q = i >> kMultiBits;
       const uint32_t sl = q == 0 ? acs[0] : q == 1 ? acs[1] : acs[2];
@@ -338,9 +338,12 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   const DG_GLOBAL uint32_t *mkp = gp<const uint32_t>(im.mk);
   RangeAcc acc = {0, 0, 0, {0, 0, 0}};
   // entry state: exact for s == 0, otherwise the lead-in decode's guess
-  uint32_t in = active ? lead_in(im, tabs, scan, mkp, s, im.lead_bits, multi ? mt : nullptr, acm)
+  const bool pair = (multi & 2u) != 0;
+  uint32_t in = active ? lead_in(im, tabs, scan, mkp, s, im.lead_bits, (multi & 1u) ? mt : nullptr, acm, pair)
                        : pack_state(0, 0, 0);
-  if (active) decode_range<false>(im, tabs, scan, mkp, s, in, acc, nullptr, ck, false, 0, stg, multi ? mt : nullptr, acm);
+  if (active)
+    decode_range<false>(im, tabs, scan, mkp, s, in, acc, nullptr, ck, false, 0, stg, (multi & 1u) ? mt : nullptr, acm,
+                        pair);
   ex[t] = active ? acc.out : 0u;
   ins[t] = in;
   __syncthreads();
@@ -350,7 +353,8 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
     uint32_t pin = redo ? ex[t - 1] : 0u;
     __syncthreads();
     if (redo) {
-      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr, ck, true, ex[t], stg, multi ? mt : nullptr, acm);
+      decode_range<false>(im, tabs, scan, mkp, s, pin, acc, nullptr, ck, true, ex[t], stg, (multi & 1u) ? mt : nullptr,
+                          acm, pair);
       ex[t] = acc.out;
       ins[t] = pin;
     }
@@ -1774,10 +1778,10 @@ void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *l
 // per workgroup, 8 resident workgroups per CU instead of 6
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                       const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
-                      uint32_t max_slots, uint32_t max_ac) {
+                      uint32_t max_slots, uint32_t max_ac, bool pair) {
   if (!nwg) return;
   const size_t lds = (size_t)max_slots * sizeof(HuffTable) + ((size_t)max_ac << kMultiBits) * 2;
-  const uint32_t multi = max_ac ? 1u : 0u;
+  const uint32_t multi = (max_ac ? 1u : 0u) | (pair ? 2u : 0u);  // bit 0: multi-symbol lookups, bit 1: pair steps
   if (stage)
     hipLaunchKernelGGL(k_huff_sync<true>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags, multi);
   else

@@ -117,13 +117,13 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
       active[t] = si >= 0 && si < (int64_t)d.nsub;
       head[t] = (t == 0) || (s0 == 0 && t == 1);
       if (!active[t]) continue;
-      ins[t] = lead_in(d, tabs.data(), scan, mkp, (uint32_t)si, d.lead_bits, mt.data(), acm);
+      ins[t] = lead_in(d, tabs.data(), scan, mkp, (uint32_t)si, d.lead_bits, mt.data(), acm, true);
       if (d.lead_bits) {
         g_multi_checked++;
         g_multi_mismatch += ins[t] != lead_in(d, tabs.data(), scan, mkp, (uint32_t)si, d.lead_bits);
       }
       decode_range<false>(d, tabs.data(), scan, mkp, (uint32_t)si, ins[t], acc[t], nullptr, t ? ckp((uint32_t)si) : nullptr,
-                          false, 0, nullptr, mt.data(), acm);
+                          false, 0, nullptr, mt.data(), acm, true);
       ex[t] = acc[t].out;
     }
     int64_t it = 0;
@@ -137,7 +137,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
         if (redo[t]) {
           uint32_t si = s0 + t - 1;
           decode_range<false>(d, tabs.data(), scan, mkp, si, pin[t], acc[t], nullptr, ckp(si), true, ex[t], nullptr,
-                              mt.data(), acm);
+                              mt.data(), acm, true);
           ex[t] = acc[t].out;
           ins[t] = pin[t];
           redo_total++;
