@@ -593,7 +593,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
                         const DG_GLOBAL uint32_t *mk,
                         uint32_t s, uint32_t in, RangeAcc &acc, WriteCtx *w, DG_GLOBAL Ckpt *ck = nullptr,
                         bool merge = false, uint32_t old_out = 0, StageCtx *stg = nullptr,
-                        const uint16_t *mt = nullptr, uint32_t acm = 0xFFu, bool pair = false) {
+                        const uint16_t *mt = nullptr, uint32_t acm = 0xFFu, uint32_t pair = 0) {
   const uint32_t S = im.sub_bits, total = im.ds_bits;
   const uint32_t a0 = s * S;
   const uint32_t a1 = (a0 + S < total) ? a0 + S : total;
@@ -757,23 +757,30 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
     }
     uint32_t zn = take_m ? zm : huff_next_z(z, sym);
     if (pair && !stage && (WRITE || !take_m)) {
-      // A second AC symbol of the same block out of the same 32-bit peek, when
-      // the first leaves the block open, ends before the next event and both
-      // fit in the peek: exactly the symbol the next single step would decode.
-      // (The state-only sync decode takes it only after a single symbol.)
-      const uint32_t c1 = len + size;
-      const bool eob1 = !isdc && size == 0u && run != 15u;
-      const uint32_t bits2 = c1 < 32u ? bits << c1 : 0u;
-      const uint32_t e2 = huff_decode(*tac, bits2);
-      const uint32_t len2 = e2 >> 8, sym2 = e2 & 0xFFu, size2 = sym2 & 15u;
-      const bool take2 = !eob1 && zn < 64u && pos < ev && c1 + len2 + size2 <= 32u;
-      if (take2) {
-        if (WRITE) {
-          const uint32_t zz2 = zn + (sym2 >> 4);
-          if (size2 && zz2 < 64u) w->blk[zz2] = (int16_t)huff_value(bits2, len2, size2);
+      // Further AC symbols of the same block out of the same 32-bit peek
+      // (up to `pair` more), each when the block is still open, it starts
+      // before the next event and it fits in the peek: exactly the symbols
+      // the next single steps would decode.  (The state-only sync decode
+      // takes them only after a single symbol.)
+      uint32_t used = len + size;
+      bool open = isdc || !(size == 0u && run != 15u);  // not EOB
+#pragma unroll
+      for (uint32_t x = 0; x < 3u; x++) {
+        if (x >= pair) break;
+        const uint32_t bx = used < 32u ? bits << used : 0u;
+        const uint32_t ex = huff_decode(*tac, bx);
+        const uint32_t lx = ex >> 8, sx = ex & 0xFFu, zx = sx & 15u;
+        const bool tk = open && zn < 64u && pos < ev && used + lx + zx <= 32u;
+        if (tk) {
+          if (WRITE) {
+            const uint32_t zz2 = zn + (sx >> 4);
+            if (zx && zz2 < 64u) w->blk[zz2] = (int16_t)huff_value(bx, lx, zx);
+          }
+          pos += lx + zx;
+          used += lx + zx;
+          zn = huff_next_z(zn, sx);
         }
-        pos += len2 + size2;
-        zn = huff_next_z(zn, sym2);
+        open = tk && !(zx == 0u && (sx >> 4) != 15u);
       }
     }
     bw_shift(b, pos);  // one shift: both symbols came out of one peek (< 32 bits past it)

@@ -269,8 +269,9 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     sync_pair_ = v != 0;
     return DG_OK;
   }
-  if (k == "write_pair") {  // k_huff_write: a second AC symbol per step from the same peek (A/B)
-    write_pair_ = v != 0;
+  if (k == "write_pair") {  // k_huff_write: up to v more AC symbols per step from the same peek (0..3)
+    if (v < 0 || v > 3) return DG_ERR_INVALID;
+    write_pair_ = (int)v;
     return DG_OK;
   }
   if (k == "multi_lead") {  // multi-symbol AC steps in k_huff_sync's lead-in (A/B)
@@ -1635,7 +1636,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (b.stage_on)
     launch_huff_scatter(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), subs);
   else
-    launch_huff_write(sl.st, dm, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots, qp, write_pair_ ? 1u : 0u);
+    launch_huff_write(sl.st, dm, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots, qp, (uint32_t)write_pair_);
   if (next()) return DG_ERR_DEVICE;
   if (next()) return DG_ERR_DEVICE;  // coeffs (side stream)
   if (pside) HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_prog, 0));  // progressive coefficients

@@ -207,7 +207,7 @@ class Context {
   int callers_ = 0, inflight_ = 0, inflight_reqs_ = 0, pinflight_ = 0;
   int prog_lanes_ = 1;  // option "prog_lanes": progressive batches in flight beside the baseline ones
   bool multi_lead_ = true;   // option "multi_lead": multi-symbol AC steps in k_huff_sync's state-only decodes
-  bool write_pair_ = true;   // option "write_pair": two AC symbols per k_huff_write step when they fit one peek
+  int write_pair_ = 3;       // option "write_pair": up to this many more AC symbols per k_huff_write step from one peek
   bool sync_pair_ = false;   // option "sync_pair": the same in k_huff_sync (measured slower beside multi_lead: off)
   bool prog_side_ = false;  // option "prog_side": progressive scans on the side stream (measured slower: off)
   int coalesce_max_ = 64, coalesce_us_ = 500;

@@ -548,7 +548,7 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
     }
     RangeAcc acc;
     decode_range<true, HuffTable, true>(im, tabs, gp<const uint8_t>(im.ds), gp<const uint32_t>(im.mk), s, ss.in,
-                                        acc, &w, nullptr, false, 0, nullptr, nullptr, 0xFFu, pair != 0);
+                                        acc, &w, nullptr, false, 0, nullptr, nullptr, 0xFFu, pair);
     if (acc.out != ss.out || (s == 0 && (flags->debug & kDbgForceWriteMismatch))) {
       // the write pass left this range in another state than the sync pass
       // proved: the blocks after it are not trustworthy.  The image goes back

@@ -211,6 +211,10 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "prog_pipe"   1 = all scans of a batch in one pipelined launch (default); 0 = one launch per level
  *   "prog_serial" 1 = serial bit reader for every scan (A/B; scans with restart intervals always use it)
  *   "prog_side"   1 = progressive scans on the slot's side stream (default 0: measured slower)
+ *   "multi_lead"  1 = multi-symbol AC steps in k_huff_sync's state-only decodes (default 1)
+ *   "write_pair"  k_huff_write: up to this many more AC symbols per step out of one 32-bit peek (0..3,
+ *                 default 3)
+ *   "sync_pair"   1 = the same in k_huff_sync after a single-symbol step (default 0: measured slower)
  *   "slots"       batches in flight, 1..4 (default 3)
  *   "hb_bands"    band H kernel: 8-row bands per workgroup, 1..64 (default 8)
  *   "entropy_lpt" 1 = dispatch the slowest entropy workgroups first (default 1)

@@ -219,7 +219,7 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
     w.blocks_per_seg = d.blocks_per_seg; w.total_blocks = d.total_blocks; w.cur = -1; w.zs = 0;
     RangeAcc acc;
     decode_range<true>(d, tabs.data(), scan, mkp, s, subs[s].in, acc, &w, nullptr, false, 0, nullptr, nullptr, 0xFFu,
-                       true);  // k_huff_write's two-symbol steps
+                       3u);  // k_huff_write's multi-symbol steps (up to 3 more symbols per peek)
     if (acc.out != subs[s].out) mismatch++;
   }
   // zigzag -> natural
