@@ -1517,17 +1517,19 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   return DG_OK;
 }
 
-// A slot for the next batch: an idle one (never used, or its batch finished
-// or complete on the device), else the next in turn, whose batch the caller
-// then finishes first.  With progressive lanes a long progressive batch
-// holds its slot while baseline batches keep cycling through the others.
+// A slot for the next batch: the next in turn, whose batch the caller then
+// finishes first.  With progressive lanes (dg_decode_one), a slot still busy
+// with its batch -- possibly a long progressive one -- is passed over for an
+// idle slot, so baseline batches keep cycling while it runs.  (Idle-first for
+// every batch measured 4% slower on the PNG workload: out-of-turn reuse.)
 int Context::pick_slot() {
   const int total = std::min(kMaxInflight, nslots_ + (progressive_ ? prog_lanes_ : 0));
-  for (int i = 0; i < total; i++)
-    if (!slots_[i].batch || slots_[i].batch->done) return i;
-  for (int i = 0; i < total; i++)
-    if (hipEventQuery(slots_[i].done) == hipSuccess) return i;
-  const int i = next_slot_ % total;
+  int i = next_slot_ % total;
+  const Slot &s = slots_[i];
+  if (progressive_ && prog_lanes_ > 0 && s.batch && !s.batch->done && hipEventQuery(s.done) != hipSuccess) {
+    for (int j = 0; j < total; j++)
+      if (!slots_[j].batch || slots_[j].batch->done) return j;
+  }
   next_slot_ = (i + 1) % total;
   return i;
 }
