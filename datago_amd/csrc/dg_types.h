@@ -114,7 +114,7 @@ constexpr uint32_t kHVRows = 64;      // k_resize_hv: V output rows per workgrou
 constexpr uint32_t kHBandRows = 8;    // rows per workgroup of the band H kernel
 constexpr uint32_t kHBandCols = 128;  // output columns per workgroup
 constexpr uint32_t kHSegPx = 640;     // LDS source segment (pixels) per row
-constexpr uint32_t kHBandsDefault = 8;  // default ResizePass::bands
+constexpr uint32_t kHBandsDefault = 16;  // default ResizePass::bands (8 -> 16: +1.5% overlapped, profiles/r02/bands)
 
 constexpr int kStages = 4;  // R1.H, R1.V, R2.H, R2.V
 

@@ -216,7 +216,7 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *                 default 3)
  *   "sync_pair"   1 = the same in k_huff_sync after a single-symbol step (default 0: measured slower)
  *   "slots"       batches in flight, 1..4 (default 3)
- *   "hb_bands"    band H kernel: 8-row bands per workgroup, 1..64 (default 8)
+ *   "hb_bands"    band H kernel: 8-row bands per workgroup, 1..64 (default 16)
  *   "entropy_lpt" 1 = dispatch the slowest entropy workgroups first (default 1)
  *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)
  *   "png_chunked" 0 = inflate every PNG with the serial kernel (test switch; default 1)

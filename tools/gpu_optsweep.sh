@@ -12,5 +12,5 @@ for cfg in "${CFGS[@]}"; do
   for kv in $cfg; do [ "$kv" = "-" ] || args="$args --ctx-opt $kv"; done
   timeout -k 10 300 python bench.py --steps 20 --warmup 3 --e2e-steps 0 --one-threads 0 --no-cpu-baseline $args --out $OUT/b_$i.json > $OUT/b_$i.log 2>&1
   rc=$?; echo "=== [$cfg] exit $rc"; [ $rc -eq 0 ] || exit $rc
-  python -c "import json;d=json.load(open('$OUT/b_$i.json'));s=d['roofline_isolated']['stages_ms'];print(d['value'],d['ms_per_step'],s['huff_sync'],s['huff_write'])"
+  python -c "import json;d=json.load(open('$OUT/b_$i.json'));s=d['roofline_isolated']['stages_ms'];print(d['value'],d['ms_per_step'],s['huff_sync'],s['huff_write'],s['resize_h1'])"
 done
