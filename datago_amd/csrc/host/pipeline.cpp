@@ -1430,7 +1430,30 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     if (lv >= b.prog_level_n.size()) b.prog_level_n.resize(lv + 1, 0);
     b.prog_level_n[lv]++;
   }
-  {
+  if (prog_pipe_) {
+    // One pipelined launch takes scans in list order.  A scan waits only on
+    // earlier scans of its own image, so images may follow one another:
+    // largest coded size first (its slowest scan is the batch's long pole,
+    // and the launch has more scans than resident waves), each image's scans
+    // in level order.
+    std::vector<std::pair<uint64_t, uint32_t>> imgs;  // (coded bytes, first scan)
+    for (uint32_t j = 0; j < (uint32_t)b.pscans.size(); j++) {
+      if (j == 0 || b.pscans[j].image != b.pscans[j - 1].image) imgs.push_back({0, j});
+      imgs.back().first += b.pscans[j].len;
+    }
+    std::stable_sort(imgs.begin(), imgs.end(), [](const auto &a, const auto &c) { return a.first > c.first; });
+    b.lists[L_PROG].clear();
+    for (const auto &im : imgs) {
+      const uint32_t j0 = im.second;
+      uint32_t j1 = j0;
+      while (j1 < b.pscans.size() && b.pscans[j1].image == b.pscans[j0].image) j1++;
+      uint32_t maxlv = 0;
+      for (uint32_t j = j0; j < j1; j++) maxlv = std::max(maxlv, b.pscans[j].level);
+      for (uint32_t lv = 0; lv <= maxlv; lv++)
+        for (uint32_t j = j0; j < j1; j++)
+          if (b.pscans[j].level == lv) b.lists[L_PROG].push_back(WgItem{b.pscans[j].image, j});
+    }
+  } else {  // one launch per level: scans grouped by level
     std::vector<uint32_t> at(b.prog_level_n.size(), 0);
     for (size_t lv = 1; lv < at.size(); lv++) at[lv] = at[lv - 1] + b.prog_level_n[lv - 1];
     b.lists[L_PROG].resize(b.pscans.size());
