@@ -368,7 +368,7 @@ __device__ __forceinline__ uint32_t prog_rows_done(const ImageDesc &im, const Pr
 }
 
 __device__ __forceinline__ void prog_wait(ProgDeps &pd, uint32_t need) {
-  if (!pd.flags || !pd.deps) return;
+  if (!pd.flags || !pd.deps || pd.bad) return;  // after one timeout the image is lost: stop waiting
   for (uint64_t m = pd.deps; m; m &= m - 1ull) {
     const DG_GLOBAL uint32_t *f = pd.flags + 1 + pd.first + (uint32_t)__builtin_ctzll(m);
     uint64_t t0 = 0;
