@@ -1177,13 +1177,20 @@ __device__ __forceinline__ void uf_publish(DG_GLOBAL uint32_t *flag, uint32_t v)
   __hip_atomic_store((uint32_t *)flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wait until *flag >= need.  False after ~1 s (a producer that never comes:
-// the caller marks the image bad rather than hang the device).
-__device__ __forceinline__ bool uf_wait(const DG_GLOBAL uint32_t *flag, uint32_t need) {
-  for (uint32_t spin = 0;; spin++) {
+// Wait until *flag >= need.  False after ~1 s of s_memrealtime (100 MHz) --
+// a producer that never comes, or one starved by other work on the device
+// (ranks sharing a GPU): the caller then returns the image
+// DG_ERR_UNSUPPORTED, so the CPU decodes it, rather than hang the device.
+// `force` (test switch kDbgForceUfTimeout) times out at once.
+__device__ __forceinline__ bool uf_wait(const DG_GLOBAL uint32_t *flag, uint32_t need, bool force) {
+  if (force) return false;
+  uint64_t t0 = 0;
+  for (;;) {
     const uint32_t v = uni(__hip_atomic_load((uint32_t *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (v >= need) break;
-    if (spin > (1u << 21)) return false;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (!t0) t0 = now;
+    if (now - t0 > 100000000ull) return false;
     __builtin_amdgcn_s_sleep(8);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1196,14 +1203,15 @@ __device__ __forceinline__ bool uf_wait(const DG_GLOBAL uint32_t *flag, uint32_t
 template <uint32_t BPP>
 __device__ void unfilter_band(const UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, uint64_t unf_a, uint32_t rb,
                               uint32_t us, uint32_t H, uint32_t y0, DG_GLOBAL uint32_t *self,
-                              const DG_GLOBAL uint32_t *pred) {
+                              const DG_GLOBAL uint32_t *pred, bool force_timeout) {
   const uint32_t lane = threadIdx.x;
   const uint32_t units = rb / BPP;  // BPP == 1 covers sub-byte samples (filter unit = 1 byte)
   const uint32_t tb = kUfTile * BPP;
   const uint32_t ntiles = (units + kUfTile - 1) / kUfTile;
   const DG_GLOBAL uint8_t *raw = gp<const uint8_t>(raw_a);
   DG_GLOBAL uint8_t *unf = gp<uint8_t>(unf_a);
-  int bad = 0;
+  int bad = 0;    // a filter type byte > 4: the stream is corrupt
+  int stall = 0;  // the previous band's wait timed out: valid data, not decoded here
   {
     const uint32_t nrows = H - y0 < 64 ? H - y0 : 64;
     const bool active = lane < nrows;
@@ -1229,7 +1237,7 @@ __device__ void unfilter_band(const UnfilterSmem &sm, ImageDesc &im, uint64_t ra
                                              (__attribute__((address_space(3))) void *)(sm.tile(k, r) + 4 * w0), 4, 0, 0);
       }
       if (y0) {
-        if (!uf_wait(pred, k + 1)) bad = 1;
+        if (!stall && !uf_wait(pred, k + 1, force_timeout)) stall = 1;
         const uint64_t a = unf_a + (uint64_t)(y0 - 1) * us + b0;
         const uint32_t nw = (nb + 3) / 4;
         for (uint32_t w0 = 0; w0 < nw; w0 += 64)
@@ -1331,7 +1339,13 @@ __device__ void unfilter_band(const UnfilterSmem &sm, ImageDesc &im, uint64_t ra
     __syncthreads();
     for (uint32_t k = stored; k < ntiles; k++) store_tile(k);
   }
-  if (__ballot(bad) && lane == 0) im.status = 2;
+  const bool any_bad = __ballot(bad) != 0, any_stall = __ballot(stall) != 0;
+  if (lane == 0) {
+    if (any_bad)
+      im.status = 2;  // DG_ERR_CORRUPT: drop the sample, as image::ImageError does
+    else if (any_stall)
+      atomicCAS((int *)&im.status, 0, 1);  // DG_ERR_UNSUPPORTED (CORRUPT from another band wins)
+  }
 }
 
 // Persistent workers over the batch's bands: a worker takes the next band in
@@ -1340,7 +1354,7 @@ __device__ void unfilter_band(const UnfilterSmem &sm, ImageDesc &im, uint64_t ra
 // every wait ends (no dependence on which workgroups are resident).
 __global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ tasks,
                                                      uint32_t ntasks, uint32_t *__restrict__ flags_,
-                                                     uint32_t *__restrict__ ticket) {
+                                                     uint32_t *__restrict__ ticket, uint32_t dbg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t uf_smem[];  // uf_smem_bytes(batch's widest unit)
   __shared__ uint32_t s_ticket;
   DG_GLOBAL uint32_t *flags = gp<uint32_t>((uint64_t)(uintptr_t)flags_);
@@ -1372,13 +1386,15 @@ __global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ img
     }
     DG_GLOBAL uint32_t *self = flags + pd.uf_flag0 + foff + band;
     const DG_GLOBAL uint32_t *pred = band ? self - 1 : nullptr;
+    // test switch (debug_flags bit 18): band 1 of every plane times out on its first wait
+    const bool force = (dbg & 1u) && band == 1;
     if (!uni(im.status)) {  // (an image whose inflate failed has nothing to unfilter)
       const UnfilterSmem sm{uf_smem, uf_pitch(pd.bpp <= 4 ? pd.bpp : 4)};
       switch (pd.bpp) {
-        case 1: unfilter_band<1>(sm, im, ra, ua, rb, us, H, band * 64, self, pred); break;
-        case 2: unfilter_band<2>(sm, im, ra, ua, rb, us, H, band * 64, self, pred); break;
-        case 3: unfilter_band<3>(sm, im, ra, ua, rb, us, H, band * 64, self, pred); break;
-        default: unfilter_band<4>(sm, im, ra, ua, rb, us, H, band * 64, self, pred); break;
+        case 1: unfilter_band<1>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
+        case 2: unfilter_band<2>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
+        case 3: unfilter_band<3>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
+        default: unfilter_band<4>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
       }
     }
     uf_publish(self, kUfDone);  // the next band's tiles read this band's last row from HBM
@@ -1520,7 +1536,7 @@ void launch_inf_resolve(hipStream_t st, ImageDesc *imgs, const InfChunk *ch, con
   if (nwg) hipLaunchKernelGGL(k_inf_resolve, dim3(nwg), dim3(1024), 0, st, imgs, ch, list);
 }
 void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
-                         uint32_t ncu, uint32_t maxbpp) {
+                         uint32_t ncu, uint32_t maxbpp, uint32_t dbg) {
   // flags: ntasks progress words + the ticket counter, zeroed by the caller
   static bool attr = false;  // > 64 KiB of dynamic LDS
   if (!attr) {
@@ -1531,7 +1547,7 @@ void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, u
   const uint32_t bpp = maxbpp < 1 ? 1u : maxbpp > 4 ? 4u : maxbpp, lds = uf_smem_bytes(bpp);
   const uint32_t per_cu = std::max<uint32_t>(1u, (160u * 1024u - 64u) / (lds + 64u));  // workers resident per CU
   const uint32_t g = std::min(ntasks, ncu * per_cu);
-  if (g) hipLaunchKernelGGL(k_png_unfilter, dim3(g), dim3(64), lds, st, imgs, tasks, ntasks, flags, flags + ntasks);
+  if (g) hipLaunchKernelGGL(k_png_unfilter, dim3(g), dim3(64), lds, st, imgs, tasks, ntasks, flags, flags + ntasks, dbg);
 }
 void launch_png_expand(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_png_expand, dim3(nwg), dim3(256), 0, st, imgs, list);

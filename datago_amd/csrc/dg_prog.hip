@@ -348,7 +348,8 @@ struct ProgDeps {
   uint64_t deps;
   uint32_t first, self;
   uint32_t last;              // last value published
-  uint32_t bad;
+  uint32_t bad;               // a wait timed out: the image goes back UNSUPPORTED, the scan stops
+  uint32_t force;             // test switch: the first wait times out at once
 };
 
 // MCU row of unit u of the scan
@@ -369,6 +370,10 @@ __device__ __forceinline__ uint32_t prog_rows_done(const ImageDesc &im, const Pr
 
 __device__ __forceinline__ void prog_wait(ProgDeps &pd, uint32_t need) {
   if (!pd.flags || !pd.deps || pd.bad) return;  // after one timeout the image is lost: stop waiting
+  if (pd.force) {
+    pd.bad = 1;
+    return;
+  }
   for (uint64_t m = pd.deps; m; m &= m - 1ull) {
     const DG_GLOBAL uint32_t *f = pd.flags + 1 + pd.first + (uint32_t)__builtin_ctzll(m);
     uint64_t t0 = 0;
@@ -590,6 +595,7 @@ __device__ __forceinline__ void prog_scan_spec(const ProgScan &sc, const ImageDe
     const uint32_t nu = nunits - u0 < upc ? nunits - u0 : upc;
     const uint32_t nb = nu * bpmu;
     prog_wait(pd, prog_unit_mrow(im, sc, u0 + nu - 1) + 1);
+    if (pd.bad) break;  // (wave-uniform) the image is lost: no reads of blocks a producer may still write
     // stage this chunk's blocks (lane = block slot); history masks stay in registers
     uint32_t g = 0, lci, nzlo = 0, nzhi = 0;
     if (lane < nb) {
@@ -783,6 +789,7 @@ __global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ 
   pd.self = self;
   pd.last = 0;
   pd.bad = 0;
+  pd.force = (serial & 2u) && sc.deps ? 1u : 0u;
   // tables: one per scan component (DC first) or the AC table
   {
     const uint32_t words = (uint32_t)(sizeof(HuffTable) / 4);
@@ -802,7 +809,7 @@ __global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ 
     for (uint32_t i = 0; i < sc.ns; i++) bpmu += im.ch[sc.comp[i]] * im.cv[sc.comp[i]];
     nunits = im.mcux * im.mcuy;
   }
-  if (sc.restart == 0 && !serial) {
+  if (sc.restart == 0 && !(serial & 1u)) {
     __syncthreads();
     prog_scan_spec(sc, im, sm, lane, coef, bpmu, nunits, pd);
     prog_finish(pd, imgs, sc, lane);
@@ -825,6 +832,7 @@ __global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ 
     const uint32_t nu = nunits - u0 < upc ? nunits - u0 : upc;
     const uint32_t nb = nu * bpmu;
     prog_wait(pd, prog_unit_mrow(im, sc, u0 + nu - 1) + 1);
+    if (pd.bad) break;  // (wave-uniform) the image is lost: no reads of blocks a producer may still write
     // stage this chunk's blocks (lane = block slot)
     uint32_t g = 0, lci;
     if (lane < nb) {

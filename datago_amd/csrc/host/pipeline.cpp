@@ -1607,7 +1607,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     if (b.uf_n) {
       uint32_t *uf = (uint32_t *)((char *)sl.scratch.p + b.uf_flags_off);
       HIPCHK(hipMemsetAsync(uf, 0, (size_t)(b.uf_n + 1) * 4, sl.st));
-      launch_png_unfilter(sl.st, dm, lst(L_UNF), cnt(L_UNF), uf, ncu_, b.uf_maxbpp);
+      launch_png_unfilter(sl.st, dm, lst(L_UNF), cnt(L_UNF), uf, ncu_, b.uf_maxbpp, (uint32_t)(debug_flags_ >> 18) & 1u);
     }
     launch_png_expand(sl.st, dd, lst(L_EXPAND), cnt(L_EXPAND));
   }
@@ -1635,10 +1635,11 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     hipStream_t pst = pside ? sl.side : sl.st;
     launch_prog_zero(pst, dd, lst(L_PROG_ZERO), cnt(L_PROG_ZERO));
     const ProgScan *ps = (const ProgScan *)(M + b.pscan_off);
+    const uint32_t prog_dbg = ((uint32_t)(debug_flags_ >> 19) & 1u) << 1;  // forced wait timeouts (tests)
     if (prog_pipe_) {
       uint32_t *pf = (uint32_t *)((char *)sl.scratch.p + b.pf_off);
       HIPCHK(hipMemsetAsync(pf, 0, (size_t)(b.pf_n + 1) * 4, pst));
-      launch_prog_scan(pst, dd, ps, lst(L_PROG), cnt(L_PROG), hp, prog_serial_ ? 1u : 0u, pf);
+      launch_prog_scan(pst, dd, ps, lst(L_PROG), cnt(L_PROG), hp, (prog_serial_ ? 1u : 0u) | prog_dbg, pf);
     } else {
       uint32_t at = 0;
       for (uint32_t nl : b.prog_level_n) {
@@ -1674,13 +1675,13 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
   launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0);
   launch_resize_hv(sl.st, dd, lst(L_RHV), b.hvclass);
-  launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | (debug_flags_ << 8));
+  launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV1), cnt(L_RV1), 1);
   launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2);
-  launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | (debug_flags_ << 8));
+  launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3);
   launch_alpha(sl.st, dd, lst(L_ALPHA2), cnt(L_ALPHA2), 2 | (alpha_flags << 8));

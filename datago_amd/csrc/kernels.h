@@ -56,7 +56,8 @@ void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint
 // progressive JPEG (dg_prog.hip): zero coefficients (kProgZeroBytes per
 // workgroup), then one wave per scan: all scans in one launch with pflags
 // (zeroed, 1 + scans words; dg_types.h ProgScan), or one level per launch
-// with pflags null
+// with pflags null.  serial bit 0: serial bit reader for every scan; bit 1 (test
+// switch): every scan with dependencies times out on its first wait
 void launch_prog_zero(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 void launch_prog_scan(hipStream_t st, const ImageDesc *imgs, const ProgScan *scans, const WgItem *list, uint32_t n,
                       const HuffTable *pool, uint32_t serial, uint32_t *pflags);
@@ -69,9 +70,10 @@ void launch_png_gather(hipStream_t st, const GatherJob *jobs, const WgItem *list
 // one 64-thread workgroup (one wave) per image
 // mode: 0 unchunked streams only, 1 chunked-path fallbacks only, 2 both
 void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, int mode);
-// tasks: (image, pass << 24 | band) in ticket order; flags: ntasks + 1 zeroed words
+// tasks: (image, pass << 24 | band) in ticket order; flags: ntasks + 1 zeroed words;
+// dbg bit 0: band 1 of every plane times out on its first wait (test switch)
 void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
-                         uint32_t ncu, uint32_t maxbpp);
+                         uint32_t ncu, uint32_t maxbpp, uint32_t dbg);
 // 256 pixels per workgroup
 void launch_png_expand(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 // alpha program at `point` (0 before call 1, 1 between the calls, 2 after call 2): 256 pixels per workgroup

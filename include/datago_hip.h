@@ -201,8 +201,9 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "timing"      1 = record per-kernel HIP events (dg_last_batch_timings)
  *   "side_stream" 1 = Lanczos tables on a second stream (default 1)
  *   "debug_flags" internal switches: bit 0 = direct H-pass kernel only (bisection); bit 16 / 17 =
- *                 force an entropy write-pass mismatch / a resync that never settles (tests of the
- *                 per-image DG_ERR_UNSUPPORTED those failures return)
+ *                 force an entropy write-pass mismatch / a resync that never settles; bit 18 / 19 = force
+ *                 a PNG unfilter band wait / a progressive scan wait to time out (tests of the per-image
+ *                 DG_ERR_UNSUPPORTED those failures return)
  *   "progressive" 1 = decode progressive JPEGs on the GPU (default 0: DG_ERR_UNSUPPORTED, the
  *                 caller's CPU decoder takes them; a refinement scan is one serial chain, so a large
  *                 file holds its batch for ~0.1-1 s: worth it for progressive-heavy corpora)
@@ -215,7 +216,9 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "write_pair"  k_huff_write: up to this many more AC symbols per step out of one 32-bit peek (0..3,
  *                 default 3)
  *   "sync_pair"   1 = the same in k_huff_sync after a single-symbol step (default 0: measured slower)
- *   "slots"       batches in flight, 1..4 (default 3)
+ *   "slots"       baseline batches in flight, 1..4 (default 3); with "progressive" = 1 and "prog_lanes" > 0
+ *                 the context cycles through slots + prog_lanes slots (at most 4), each with its own scratch
+ *                 arena, pinned staging and streams
  *   "hb_bands"    band H kernel: 8-row bands per workgroup, 1..64 (default 16)
  *   "entropy_lpt" 1 = dispatch the slowest entropy workgroups first (default 1)
  *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)

@@ -4,7 +4,9 @@ starts), as under torchrun.  The rank owns the contiguous slice
 get_data_slice_multirank(N, rank, world) of a seeded N-image stream
 (generator_files.rs:24-42), decodes + bucket-resizes it through its own
 dg_ctx on device LOCAL_RANK mod the device count, and writes the outputs to
-<out>/rank<r>.npz for the parent to check."""
+<out>/rank<r>.npz for the parent to check.
+
+    rank_worker.py OUT_DIR N [SIZE RATIO]   (bucket config, default 512/16)"""
 import os
 import sys
 
@@ -14,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main(out_dir: str, n: int) -> int:
+def main(out_dir: str, n: int, size: int = 512, ratio: int = 16) -> int:
     import torch
     import torch.distributed as dist
 
@@ -27,7 +29,7 @@ def main(out_dir: str, n: int) -> int:
     lo, hi = get_data_slice_multirank(n, rank, world)
     datas = synth.mixed_corpus(11, n, 96, 640, lo=lo, hi=hi)
     dev = local % torch.cuda.device_count()
-    ctx = L.Context(dev, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+    ctx = L.Context(dev, crop_and_resize=True, default_image_size=size, downsampling_ratio=ratio,
                     min_aspect_ratio=0.5, max_aspect_ratio=2.0)
     res = ctx.decode_batch(datas)
     dist.barrier()
@@ -41,4 +43,4 @@ def main(out_dir: str, n: int) -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1], int(sys.argv[2])))
+    sys.exit(main(sys.argv[1], int(sys.argv[2]), *[int(x) for x in sys.argv[3:5]]))

@@ -30,25 +30,51 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_two_ranks_through_the_library(tmp_path):
-    n, world = 21, 2
+def _run_ranks(tmp_path, n, world, size, ratio):
     env = dict(os.environ, WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
-    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "rank_worker.py"), str(tmp_path), str(n)],
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "rank_worker.py"), str(tmp_path), str(n),
+                               str(size), str(ratio)],
                               env=dict(env, RANK=str(r), LOCAL_RANK=str(r))) for r in range(world)]
-    for p in procs:
-        assert p.wait(timeout=240) == 0
-    got = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    try:
+        for p in procs:
+            assert p.wait(timeout=300) == 0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+
+
+def _check_ranks(got, n, world, size, ratio):
     idx = [set(g["indices"].tolist()) for g in got]
-    assert idx[0].isdisjoint(idx[1]) and idx[0] | idx[1] == set(range(n))
-    assert [len(i) for i in idx] == [11, 10]  # the first n % world ranks take one extra
+    for a in range(world):
+        for b in range(a + 1, world):
+            assert idx[a].isdisjoint(idx[b])
+    assert set().union(*idx) == set(range(n))
+    base, extra = divmod(n, world)  # get_data_slice_multirank: the first n % world ranks take one extra
+    assert [len(i) for i in idx] == [base + (r < extra) for r in range(world)]
     datas = synth.mixed_corpus(11, n, 96, 640)
-    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    t = B.ARAwareTransform(size, ratio, 0.5, 2.0)
     for g in got:
         assert (g["status"] == 0).all()
         for i in g["indices"].tolist():
             _, dec = O.jpeg_decode(datas[i])
             ref = O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR)
             assert np.array_equal(g[f"img{i}"], ref), i
+
+
+def test_two_ranks_through_the_library(tmp_path):
+    _check_ranks(_run_ranks(tmp_path, 21, 2, 512, 16), 21, 2, 512, 16)
+
+
+def test_eight_ranks_configs3_through_the_library(tmp_path):
+    """configs[3]'s world_size 8 (rank r takes get_data_slice_multirank(N, r, 8),
+    generator_files.rs:24-42,75-80) with its 1024/32 buckets: eight rank
+    processes, each with its own context (all on device 0 of a one-GPU box),
+    started before any GPU call as torchrun starts them.  The slices are
+    disjoint, cover the stream (43 = 8 x 5 + 3: ranks 0-2 take one extra) and
+    every output is bit-exact against the oracle."""
+    _check_ranks(_run_ranks(tmp_path, 43, 8, 1024, 32), 43, 8, 1024, 32)
 
 
 def test_bench_gpus_flag_launches_ranks(tmp_path):

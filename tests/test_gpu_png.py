@@ -267,3 +267,33 @@ def test_serial_inflate_beside_chunked_and_unfilter_unit_widths():
                 ost, ref = O.png_decode(d)
                 assert ost == 0 and st == 0, (side, name, k, st, L.last_error())
                 assert arr.shape == ref.shape and np.array_equal(arr, ref), (side, name, k)
+
+
+DBG_FORCE_UF_TIMEOUT = 1 << 18
+
+
+def test_unfilter_wait_timeout_is_unsupported_not_corrupt():
+    """A band whose wait for the previous band times out (a starved producer,
+    e.g. ranks sharing the GPU) returns the image DG_ERR_UNSUPPORTED -- valid
+    data the caller's CPU decoder takes -- not DG_ERR_CORRUPT, which would drop
+    the sample.  Test switch: band 1 of every plane times out on its first
+    wait.  Images of one band (<= 64 rows) never wait and stay bit-exact; the
+    kernel returns (no hang)."""
+    L = _lib()
+    ctx = L.Context(0)
+    tall = [synth.make_png(1301, 200, 130, "RGB"), synth.make_png(1302, 90, 700, "L", level=6)]
+    short = [synth.make_png(1303, 300, 64, "RGBA"), synth.make_png(1304, 50, 20, "P8")]
+    ctx.set_option("debug_flags", DBG_FORCE_UF_TIMEOUT)
+    try:
+        res = ctx.decode_batch(tall + short)
+    finally:
+        ctx.set_option("debug_flags", 0)
+    for st, _, _ in res[:2]:
+        assert st == L.DG_ERR_UNSUPPORTED
+    for d, (st, arr, _) in zip(short, res[2:]):
+        assert st == 0
+        ost, ref = O.png_decode(d)
+        assert np.array_equal(arr.reshape(ref.shape), ref)
+    for d, (st, arr, _) in zip(tall, ctx.decode_batch(tall)):  # switch off: decoded again
+        assert st == 0
+        assert np.array_equal(arr.reshape(O.png_decode(d)[1].shape), O.png_decode(d)[1])

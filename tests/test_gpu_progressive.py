@@ -162,3 +162,30 @@ def test_decode_one_progressive_lane(lanes):
         ost, dec = O.jpeg_decode(data)
         assert np.array_equal(arr, O.crop_and_resize(dec, tw, th_, O.MODE_FIR)), i
     assert ctx.stat("coalesced_images") == len(datas)
+
+
+DBG_FORCE_PROG_TIMEOUT = 1 << 19
+
+
+def test_progressive_wait_timeout_is_unsupported_and_isolated():
+    """A scan whose wait for an earlier scan of its image times out stops
+    (no reads of blocks a producer may still be writing) and returns its image
+    DG_ERR_UNSUPPORTED; baseline images of the same batch stay bit-exact and
+    the launch drains.  Test switch: every scan with dependencies times out on
+    its first wait."""
+    L = _lib()
+    ctx = L.Context(0)
+    ctx.set_option("progressive", 1)
+    prog = [_prog(4701, 300, 200), _prog(4702, 640, 480, 90, "4:4:4")]
+    base = [synth.make_jpeg(4703, 320, 240), synth.make_jpeg(4704, 123, 77, 70, "4:2:2")]
+    ctx.set_option("debug_flags", DBG_FORCE_PROG_TIMEOUT)
+    try:
+        res = ctx.decode_batch(prog + base)
+    finally:
+        ctx.set_option("debug_flags", 0)
+    assert [r[0] for r in res[:2]] == [L.DG_ERR_UNSUPPORTED] * 2
+    for d, (st, arr, _) in zip(base, res[2:]):
+        assert st == 0
+        ost, ref = O.jpeg_decode(d)
+        assert np.array_equal(arr.reshape(ref.shape), ref)
+    assert all(r[0] == 0 for r in ctx.decode_batch(prog))
