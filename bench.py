@@ -361,9 +361,22 @@ def pmc_config_key(a) -> str:
     return f"batch={a.batch} pool={a.pool} size={a.size}/{a.ratio} short={a.short_min}-{a.short_max}"
 
 
-def stage_bytes(L, data: bytes, dim, target) -> dict:
+def band_dec_takes(w: int, nw: int) -> bool:
+    """Mirrors band_dec_mode (pipeline.cpp): k_band_dec runs the first H pass
+    W -> nw when the 128-column tile's segment fits 640 pixels and every
+    16-column subtile's window two 64-wide K steps."""
+    scale = w / nw
+    fs = max(scale, 1.0)
+    ksize = math.ceil(3.0 * fs) * 2 + 1
+    span = math.ceil(127 * scale + 6.0 * fs) + 2 + 8 + ksize + 8 + 16
+    return span <= 640 and 15 + math.ceil(15 * scale) + ksize + 2 <= 128
+
+
+def stage_bytes(L, data: bytes, dim, target, band_dec: bool = True) -> dict:
     """Algorithmic bytes each kernel stage must move for one image (DESIGN.md
-    §Roofline): its minimal input + output, intermediates counted once."""
+    §Roofline): its minimal input + output, intermediates counted once.  With
+    k_band_dec the first H pass reads the coefficients (128 B per block) and
+    writes the H intermediate: no planes in between."""
     from oracle import buckets as B
     w, h, nc = dim
     tw, th = target
@@ -388,7 +401,11 @@ def stage_bytes(L, data: bytes, dim, target) -> dict:
         cw, ch = w, h
         if nw != w:
             wx = tw if fold_x else nw
-            if nc == 3:  # fused: upsample + colour from the planes inside the first H pass
+            if band_dec and band_dec_takes(w, nw):  # k_band_dec: coefficients in, H intermediate out
+                b["resize_h1"] = 128 * nblk + nc * wx * h
+                b["idct"] = 0.0
+                b["color"] = 0.0
+            elif nc == 3:  # fused: upsample + colour from the planes inside the first H pass
                 b["resize_h1"] = b["color"] - 3 * w * h + nc * wx * h
                 b["color"] = 0.0
             else:
@@ -599,7 +616,8 @@ def main() -> int:
         out_bytes = [ctx.output_size(d, f)[1] for d, f in zip(pool, forced_pool)]
     else:
         out_bytes = [tw * th * nc for (tw, th), (_, _, nc) in zip(targets, dims)]
-    img_stage_bytes = [(png_stage_bytes if png else stage_bytes)(*((d, dim, tgt) if png else (L, d, dim, tgt)))
+    band_dec = all(kv != "band_dec=0" for kv in a.ctx_opt)
+    img_stage_bytes = [png_stage_bytes(d, dim, tgt) if png else stage_bytes(L, d, dim, tgt, band_dec)
                        for d, dim, tgt in zip(pool, dims, targets)]
     B_ = min(a.batch, 1 << 16)
     # output arena for one step (reused), sized for the largest B_ outputs

@@ -26,6 +26,7 @@ SOURCES = [
     ("dg_enc.hip", True),
     ("dg_prog.hip", True),
     ("dg_penc.hip", True),
+    ("dg_band.hip", True),
     ("host/jpeg_enc.cpp", False),
     ("host/wds.cpp", False),
     ("host/png_header.cpp", False),

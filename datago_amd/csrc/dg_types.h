@@ -108,6 +108,12 @@ struct ResizePass {
 };
 constexpr uint32_t kHFused = 1, kHDirect = 2;
 constexpr uint32_t kHVFused = 4;      // pass[0] runs fused with pass[1] in k_resize_hv (its H rows stay in LDS)
+// pass[0] of a JPEG runs in k_band_dec (dg_band.hip): IDCT + upsampling + colour + this H pass from the
+// coefficients, 16-row strips of kDecCols output columns; kHDecWide: the 640-pixel segment class
+constexpr uint32_t kHDecode = 8, kHDecWide = 16;
+constexpr uint32_t kDecCols = 128;    // k_band_dec: output columns per workgroup (8 MFMA subtiles of 16)
+constexpr uint32_t kDecSeg0 = 320, kDecSeg1 = 640;  // k_band_dec source segment classes (pixels)
+constexpr uint32_t kDecStripsDefault = 8;           // k_band_dec: 16-row strips per workgroup (option "dec_strips")
 constexpr uint32_t kHVSegPx = 320;    // k_resize_hv: LDS source segment per row (downscales up to ~2.3x)
 constexpr uint32_t kHVTapsMax = 24;   // k_resize_hv: V taps (its LDS ring holds 32 rows)
 constexpr uint32_t kHVRows = 64;      // k_resize_hv: V output rows per workgroup

@@ -211,6 +211,30 @@ static bool hv_fusable(const ResizePass &h, const ResizePass &v) {
          h.ksize + 1 <= 16 && v.ksize <= kHVTapsMax && h_pass_span(h) <= (double)kHVSegPx;
 }
 
+// k_band_dec takes pass[0] of a JPEG when its sampling is one the fused fill
+// knows (gray; 4:4:4, 4:2:2, 4:2:0 with luma at the maximum factors) and its
+// segments fit: the 128-column tile's source segment (plus the 16-pixel
+// alignment) in the class's LDS, every 16-column MFMA subtile's window in two
+// 64-wide K steps.  Returns the mode bits (0: not eligible).
+static uint32_t band_dec_mode(const ImageDesc &d, const ResizePass &ps) {
+  if (ps.kind != 1 || (ps.mode & (kHDirect | kHVFused)) || d.idct_fused) return 0;
+  if (d.ncomp == 3) {
+    if (!(ps.mode & kHFused)) return 0;
+    if (d.ch[0] != d.hmax || d.cv[0] != d.vmax || d.ch[1] != d.ch[2] || d.cv[1] != d.cv[2]) return 0;
+    if (d.hmax % d.ch[1] || d.vmax % d.cv[1]) return 0;
+    const uint32_t hr = d.hmax / d.ch[1], vr = d.vmax / d.cv[1];
+    if (hr > 2 || vr > 2 || (hr == 1 && vr == 2)) return 0;
+  } else if (d.ncomp != 1) {
+    return 0;
+  }
+  const double scale = (ps.in1 - ps.in0) / (double)ps.out_size;
+  if (15.0 + std::ceil(15.0 * scale) + (double)ps.ksize + 2.0 > 128.0) return 0;
+  const double span = h_pass_span(ps) + 16.0;
+  if (span <= (double)kDecSeg0) return kHDecode;
+  if (span <= (double)kDecSeg1) return kHDecode | kHDecWide;
+  return 0;
+}
+
 dg_status Context::set_option(const std::string &k, int64_t v) {
   if (k == "sub_bits") {
     if (v != 0 && (v < 64 || v > 65536 || (v & (v - 1)))) return DG_ERR_INVALID;  // power of two
@@ -333,6 +357,19 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     chunked_off_ = v == 0;
     return DG_OK;
   }
+  if (k == "band_dec") {  // 0: IDCT to planes + band H kernel (the split path, A/B)
+    band_dec_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "dec_dbg") {  // timing experiments: skip k_band_dec phases (wrong pixels)
+    dec_dbg_ = (uint32_t)v;
+    return DG_OK;
+  }
+  if (k == "dec_strips") {
+    if (v < 1 || v > 4096) return DG_ERR_INVALID;
+    dec_strips_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "debug_flags") {
     debug_flags_ = (int)v;
     return DG_OK;
@@ -358,6 +395,7 @@ int64_t Context::get_stat(const std::string &k) {
   }
   if (k == "sub_bits") return last_sub_bits_;
   if (k == "png_serial_fallbacks") return stat_png_serial_;
+  if (k == "band_dec_images") return stat_band_dec_;
   if (k == "png_chunks") return stat_png_chunks_;
   {  // host microseconds spent in dg_submit* since the last reset, per phase
     static const char *pn[6] = {"plan", "pools", "layout", "lists", "upload", "launch"};
@@ -917,7 +955,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     }  // sequential
     // buffers
     o.coef = CO.take((size_t)d.total_blocks * 128);
-    for (int c = 0; c < h.ncomp; c++) o.plane[c] = L.take((size_t)d.cbw[c] * 8 * d.cbh[c] * 8);
+    for (int c = 0; c < 3; c++) o.plane[c] = (size_t)-1;  // allocated after the pass plan (not for k_band_dec)
     C = d.dec_c;
     colour = h.ncomp == 3;
     if (h.ncomp == 3) {
@@ -1045,6 +1083,14 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     // colour images whose first pass is not a fused H pass need the RGB image
     d.color_fused = colour && d.pass[0].kind == 1 && (d.pass[0].mode & kHFused);
     if (hv_fused_ && hv_fusable(d.pass[0], d.pass[1])) d.pass[0].mode |= kHVFused;
+    if (p.fmt == kFmtJpeg) {
+      // k_band_dec decodes pass[0]'s source from the coefficients: no planes
+      const uint32_t dm = band_dec_ ? band_dec_mode(d, d.pass[0]) : 0u;
+      d.pass[0].mode |= dm;
+      if (dm) stat_band_dec_++;
+      if (!dm)
+        for (uint32_t c = 0; c < d.ncomp; c++) o.plane[c] = L.take((size_t)d.cbw[c] * 8 * d.cbh[c] * 8);
+    }
     if (colour && !d.color_fused) o.pix = L.take((size_t)d.pix_stride * H);
     // final write: the last pass writes straight into the output when the
     // channel count is unchanged; otherwise (or with no pass) k_copy runs.
@@ -1268,7 +1314,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     d.mk = (uint64_t)(uintptr_t)(S + o.mk);
     d.chunk = (uint64_t)(uintptr_t)(S + o.chunk);
     }
-    for (int c = 0; c < h.ncomp; c++) d.plane[c] = (uint64_t)(uintptr_t)(S + o.plane[c]);
+    for (int c = 0; c < h.ncomp; c++) d.plane[c] = o.plane[c] == (size_t)-1 ? 0 : (uint64_t)(uintptr_t)(S + o.plane[c]);
     d.pix = h.ncomp == 3 && !d.color_fused ? (uint64_t)(uintptr_t)(S + o.pix) : 0;
     }  // JPEG
     uint64_t cur = (d.fmt == kFmtPng || h.ncomp == 3) ? d.pix : d.plane[0];
@@ -1303,6 +1349,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   for (auto &l : b.lists) l.clear();
   std::vector<WgItem> hb[2][2][4];  // band H items per (stage, fused fill, weight-count class)
   std::vector<WgItem> hvl[2];       // k_resize_hv items per H weight class
+  std::vector<WgItem> decl[2];      // k_band_dec items per segment class
   for (int di = 0; di < (int)b.descs.size(); di++) {
     const ImageDesc &d = b.descs[di];
     const uint32_t I = (uint32_t)di;
@@ -1331,7 +1378,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     }
     uint32_t items = 0;
     for (uint32_t c = 0; c < d.ncomp; c++) items += d.cbh[c] * ((d.cbw[c] + 63) / 64);  // kIdctBlocks
-    if (!d.idct_fused)  // fused: k_huff_write (+ k_idct_list) produce the planes
+    if (!d.idct_fused && !(d.pass[0].mode & kHDecode))  // fused: k_huff_write (+ k_idct_list) / k_band_dec
       for (uint32_t it = 0; it < items; it++) b.lists[L_IDCT].push_back({I, it});
     if (d.ncomp == 3 && !d.color_fused) {
       uint32_t q = (d.width + 7) / 8 * d.height;
@@ -1345,11 +1392,19 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       const int cls = d.pass[0].ksize + 1 <= 8 ? 0 : 1;
       for (uint32_t it = 0; it < cnt; it++) hvl[cls].push_back({I, it});
     }
+    if (d.pass[0].mode & kHDecode) {  // one workgroup per (group of dec_strips 16-row strips, 128-column tile)
+      const ResizePass &ps = d.pass[0];
+      const uint32_t tiles = (ps.width + kDecCols - 1) / kDecCols;
+      const uint32_t strips = (ps.row0 + ps.rows + 15) / 16 - ps.row0 / 16;
+      const uint32_t cnt = tiles * ((strips + dec_strips_ - 1) / dec_strips_);
+      for (uint32_t it = 0; it < cnt; it++) decl[(ps.mode & kHDecWide) ? 1 : 0].push_back({I, it});
+    }
     for (int s = 0; s < kStages; s++) {
       const ResizePass &ps = d.pass[s];
       if (!ps.kind) continue;
       b.lists[L_COEF].push_back({I, (uint32_t)s});
       if (hv && s < 2) continue;  // k_resize_hv runs both
+      if (s == 0 && (ps.mode & kHDecode)) continue;  // k_band_dec runs it
       if (ps.kind == 1 && (ps.mode & kHDirect)) {  // one workgroup per (row, 512-column tile)
         uint32_t cnt = ps.rows * ((ps.width + 511) / 512);
         for (uint32_t it = 0; it < cnt; it++) b.lists[s == 0 ? L_RHX0 : L_RHX2].push_back({I, it});
@@ -1459,6 +1514,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     b.lists[L_PROG].resize(b.pscans.size());
     for (uint32_t j = 0; j < (uint32_t)b.pscans.size(); j++)
       b.lists[L_PROG][at[b.pscans[j].level]++] = WgItem{b.pscans[j].image, j};
+  }
+  for (int c = 0; c < 2; c++) {
+    b.decclass[c] = (uint32_t)decl[c].size();
+    b.lists[L_DEC].insert(b.lists[L_DEC].end(), decl[c].begin(), decl[c].end());
   }
   for (int c = 0; c < 2; c++) {
     b.hvclass[c] = (uint32_t)hvl[c].size();
@@ -1673,6 +1732,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (next()) return DG_ERR_DEVICE;
   HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_coef, 0));
   launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
+  launch_band_dec(sl.st, dd, lst(L_DEC), b.decclass, qp, dec_strips_ | (dec_dbg_ << 16));
   launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0);
   launch_resize_hv(sl.st, dd, lst(L_RHV), b.hvclass);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | ((debug_flags_ & 0xFF) << 8));

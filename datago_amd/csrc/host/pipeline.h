@@ -62,8 +62,8 @@ struct Batch {
   std::vector<ImageDesc> descs;
   std::vector<int> desc_of;           // image -> desc index or -1
   // workgroup lists (host copies) and their offsets in the device meta buffer
-  std::vector<WgItem> lists[32];
-  size_t list_off[32] = {0};
+  std::vector<WgItem> lists[40];
+  size_t list_off[40] = {0};
   // PNG: IDAT gather jobs and palettes, uploaded with the descriptors
   std::vector<GatherJob> gjobs;
   size_t gjob_off = 0;
@@ -91,6 +91,7 @@ struct Batch {
   // <=32, more): hclass[stage/2][k] items of class k, in that order
   uint32_t hclass[2][2][4] = {{{0}}};  // [stage/2][fused][class]
   uint32_t hvclass[2] = {0, 0};        // L_RHV items of H weight class <= 8, <= 16 (k_resize_hv)
+  uint32_t decclass[2] = {0, 0};       // L_DEC items of the 320- / 640-pixel segment class (k_band_dec)
   size_t desc_off = 0, flags_off = 0;
   size_t meta_bytes = 0;
   size_t total_subs = 0;
@@ -139,9 +140,10 @@ enum ListId {
   L_PENC_ROW, L_PENC_PIECE, L_PENC_IMG,                     // PNG re-encode
   L_UNF,                                                    // PNG unfilter bands (ticket order)
   L_RHV,                                                    // fused first H + V pass (k_resize_hv)
+  L_DEC,                                                    // IDCT + colour + first H pass (k_band_dec)
   L_COUNT
 };
-static_assert((int)L_COUNT <= 32, "Batch::lists");
+static_assert((int)L_COUNT <= 40, "Batch::lists");
 
 class Context {
  public:
@@ -241,6 +243,9 @@ class Context {
   double host_us_[6] = {0, 0, 0, 0, 0, 0};  // submit phases (stats "host_us_*"; option "reset_host_us")
   int copy_threads_ = 8;                // option "copy_threads": host threads for a host-out batch's output copies
   bool hv_fused_ = false;               // option "hv_fused": first H + V pass fused (k_resize_hv) when it fits
+  bool band_dec_ = false;               // option "band_dec": IDCT + colour + first H pass in k_band_dec
+  uint32_t dec_dbg_ = 0;                // option "dec_dbg": k_band_dec phase switches (timing experiments only)
+  uint32_t dec_strips_ = kDecStripsDefault;  // option "dec_strips"
   bool idct_fused_ = false;             // option "idct_fused" (measured 7x slower k_huff_write: off)
   bool progressive_ = false;            // option "progressive"
   bool prog_serial_ = false;            // option "prog_serial": serial reader for every scan (A/B)
@@ -248,6 +253,7 @@ class Context {
   bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first
   bool entropy_once_ = false;           // option "entropy_once": decode-once staging + k_huff_scatter
   int64_t stat_png_serial_ = 0, stat_png_chunks_ = 0;
+  int64_t stat_band_dec_ = 0;  // images whose first H pass ran in k_band_dec (stat "band_dec_images")
   // "wg_timing" summaries of the last batch (microseconds): per kernel {span, mean, p90, max}
   double wgstat_[2][4] = {{0}};
   // stats

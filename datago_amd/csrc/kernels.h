@@ -51,6 +51,10 @@ void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
 // fused first H + V pass (pass[0].mode & kHVFused): lists of H weight classes <= 8, <= 16 taps
 void launch_resize_hv(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2]);
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage);
+// k_band_dec (dg_band.hip): IDCT + upsampling + colour + the first H pass of images with pass[0].mode &
+// kHDecode; list = ncls[0] items of the 320-pixel class, then ncls[1] of the 640-pixel class
+void launch_band_dec(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2],
+                     const QuantTable *qpool, uint32_t strips_per_wg);
 // final copy / gray->RGB expansion: 256 output pixels per workgroup
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 // progressive JPEG (dg_prog.hip): zero coefficients (kProgZeroBytes per
