@@ -369,7 +369,8 @@ def band_dec_takes(w: int, nw: int) -> bool:
     fs = max(scale, 1.0)
     ksize = math.ceil(3.0 * fs) * 2 + 1
     span = math.ceil(127 * scale + 6.0 * fs) + 2 + 8 + ksize + 8 + 16
-    return span <= 640 and 15 + math.ceil(15 * scale) + ksize + 2 <= 128
+    window = 15 + math.ceil(15 * scale) + ksize + 2
+    return (span <= 320 and window <= 64) or (span <= 640 and window <= 128)
 
 
 def stage_bytes(L, data: bytes, dim, target, band_dec: bool = True) -> dict:

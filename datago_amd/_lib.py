@@ -53,7 +53,7 @@ class ImageConfig(ctypes.Structure):
                 ("downsampling_ratio", ctypes.c_uint32), ("min_aspect_ratio", ctypes.c_double),
                 ("max_aspect_ratio", ctypes.c_double), ("pre_encode_images", ctypes.c_int32),
                 ("image_to_rgb8", ctypes.c_int32), ("encode_format", ctypes.c_int32),
-                ("jpeg_quality", ctypes.c_int32)]
+                ("jpeg_quality", ctypes.c_int32), ("decode_semantics", ctypes.c_int32)]
 
 
 class ProbeInfo(ctypes.Structure):
@@ -253,11 +253,11 @@ class Context:
     def __init__(self, device: int = 0, crop_and_resize: bool = False, default_image_size: int = 0,
                  downsampling_ratio: int = 0, min_aspect_ratio: float = 0.0, max_aspect_ratio: float = 0.0,
                  image_to_rgb8: bool = False, pre_encode_images: bool = False, encode_format: int = 0,
-                 jpeg_quality: int = 92):
+                 jpeg_quality: int = 92, decode_semantics: int = 0):
         L = load()
         cfg = ImageConfig(int(crop_and_resize), default_image_size, downsampling_ratio, min_aspect_ratio,
                           max_aspect_ratio, int(pre_encode_images), int(image_to_rgb8), encode_format,
-                          jpeg_quality)
+                          jpeg_quality, decode_semantics)
         h = ctypes.c_void_p()
         _check(L.dg_ctx_create(device, ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

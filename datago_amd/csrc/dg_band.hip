@@ -55,21 +55,28 @@ __device__ __forceinline__ uint32_t dec_pack4(uint32_t b0, uint32_t b1, uint32_t
 }
 
 // LDS layout of one workgroup (SEG = widest source segment, pixels).
-template <uint32_t SEG>
+// Planar operand rows are read 16 bytes per lane, 16 rows per lane group: a
+// row stride of an odd multiple of 16 bytes (mod 256) puts the 16 rows on
+// distinct 4-bank groups.
+constexpr uint32_t dec_row_stride(uint32_t need) {
+  uint32_t a = (need + 15) / 16 * 16;
+  while (((a / 16) & 1u) == 0) a += 16;
+  return a;
+}
+template <uint32_t SEG, int KS>
 struct DecSmem {
   static constexpr uint32_t YS = SEG;                   // Y plane row stride
   static constexpr uint32_t CS = SEG;                   // chroma row stride (h2: SEG/2 + 32 used)
-  static constexpr uint32_t AS = (SEG + 128 + 255) / 256 * 256 + 16;  // planar operand rows: 16 mod 256 bytes
-  static constexpr uint32_t OBS = kDecCols * 3;         // output staging row
+  static constexpr uint32_t AS = dec_row_stride(SEG + 64 * KS);  // planar operand rows (reads reach 64 * KS past k0)
   int32_t q[3][64];                                     // quant tables (natural order)
   uint32_t ext[4];
+  __attribute__((aligned(16))) int32_t corr[kDecCols];  // per output column: 128 * sum(w) + rounding bias
   __attribute__((aligned(16))) uint8_t yp[kDecRows * YS];
   __attribute__((aligned(16))) uint8_t cp[2][kDecRows * CS];  // 4:4:4 / 4:2:2 rows, or the 4:2:0 ring (24 rows of SEG/2 + 32)
   union {
     __attribute__((aligned(16))) uint8_t ap[3][kDecRows * AS];  // planar operand rows (i8)
     int32_t blk[kDecRound * 72];                                // IDCT transpose scratch
   };
-  __attribute__((aligned(16))) uint8_t ob[kDecRows * OBS];
 };
 
 // 8 libjpeg-turbo fancy-upsampled chroma samples at full-resolution columns
@@ -88,10 +95,11 @@ __device__ __forceinline__ void dec_ups_lj(const uint8_t *r0, const uint8_t *r1,
 #pragma unroll
     for (int k = 0; k < 4; k++) cs[k + 1] = (v >> (8 * k)) & 0xFF;
     cs[5] = r0[cr];
-    if (c0 + 5 > dsw) {
+    if (c0 + 5 > dsw) {  // past the downsampled width: the edge sample (re-read: no dynamic register index)
+      const int32_t edge = r0[dsw - 1];
 #pragma unroll
       for (int k = 0; k < 4; k++)
-        if (c0 + k >= dsw) cs[k + 1] = cs[dsw - c0];
+        if (c0 + k >= dsw) cs[k + 1] = edge;
     }
     if (!fancy) {
 #pragma unroll
@@ -121,9 +129,12 @@ __device__ __forceinline__ void dec_ups_lj(const uint8_t *r0, const uint8_t *r1,
 #pragma unroll
   for (int k = 0; k < 4; k++) cs[k + 1] = (int32_t)((v0 >> (8 * k)) & 0xFF) * 3 + (int32_t)((v1 >> (8 * k)) & 0xFF);
   cs[5] = r0[cr] * 3 + r1[cr];
+  if (c0 + 5 > dsw) {
+    const int32_t edge = r0[dsw - 1] * 3 + r1[dsw - 1];
 #pragma unroll
-  for (int k = 0; k < 4; k++)
-    if (c0 + k >= dsw) cs[k + 1] = cs[dsw - c0];
+    for (int k = 0; k < 4; k++)
+      if (c0 + k >= dsw) cs[k + 1] = edge;
+  }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int32_t nl = (c0 + k + 1 < dsw) ? cs[k + 2] : cs[k + 1];
@@ -175,10 +186,10 @@ struct DecComp {
   uint32_t lim;       // clamp width of the horizontal filter (libjpeg: downsampled width; zune: padded)
 };
 
-template <uint32_t SEG>
-__global__ __launch_bounds__(256) void k_band_dec(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
+template <uint32_t SEG, int KS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_band_dec(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
                                                   const QuantTable *__restrict__ qpool, uint32_t strips_arg) {
-  using SM = DecSmem<SEG>;
+  using SM = DecSmem<SEG, KS>;
   const uint32_t strips_per_wg = strips_arg & 0xFFFFu, dbg = strips_arg >> 16;  // dbg: timing experiments only
   __shared__ SM sm;
   const WgItem it = list[dec_xcd_remap(blockIdx.x, gridDim.x)];
@@ -242,8 +253,7 @@ __global__ __launch_bounds__(256) void k_band_dec(const ImageDesc *__restrict__ 
   // ---- MFMA weights of this wave's two subtiles (set up once)
   // lane: column n = lane & 15 of the subtile, k group g = lane >> 4
   const uint32_t n = lane & 15, g = lane >> 4;
-  i32x4 wlo[2][2], wmid[2][2], whi[2][2];  // weight digits c, b, a of (subtile, K step)
-  int32_t corr[2];
+  i32x4 wlo[2][KS], wmid[2][KS], whi[2][KS];  // weight digits c, b, a of (subtile, K step)
   uint32_t k0[2], steps[2];
 #pragma unroll
   for (int j = 0; j < 2; j++) {
@@ -264,13 +274,13 @@ __global__ __launch_bounds__(256) void k_band_dec(const ImageDesc *__restrict__ 
     }
     k0[j] = mn == 0xFFFFFFFFu ? p0 : (mn & ~15u);
     steps[j] = mx > k0[j] ? (mx - k0[j] + 63) / 64 : 0;
-    if (steps[j] > 2) steps[j] = 2;  // host guarantees windows <= 128 (kHDecode eligibility)
+    if (steps[j] > (uint32_t)KS) steps[j] = KS;  // host guarantees windows <= 64 * KS (band_dec_mode)
     const DG_GLOBAL int16_t *kp = coef + (size_t)(valid ? xs : x0) * ps.ksize;
     int32_t sum = 0;
     for (uint32_t i = 0; i < cnt; i++) sum += kp[i];
-    corr[j] = sum * 128 + (1 << (prec - 1));
+    if (g == 0) sm.corr[sub * kDecSub + n] = sum * 128 + (1 << (prec - 1));
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
+    for (int s = 0; s < KS; s++) {
       uint32_t lo[4] = {0, 0, 0, 0}, md[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
       const int32_t kb = (int32_t)(k0[j] + 64 * s + 16 * g) - (int32_t)st;
 #pragma unroll
@@ -294,59 +304,96 @@ __global__ __launch_bounds__(256) void k_band_dec(const ImageDesc *__restrict__ 
   const uint32_t sb = sa + strips_per_wg < s_end ? sa + strips_per_wg : s_end;
   const DG_GLOBAL int16_t *cf = gp<const int16_t>(im.coef);
 
-  for (uint32_t s = sa; s < sb; s++) {
-    // -- 1. IDCT: Y block rows 2s, 2s+1; chroma rows of this strip (or the ring's new rows)
-    const uint32_t ny_r0 = 2 * s, ny_rows = (2 * s + 2 <= im.cbh[0] ? 2u : (2 * s < im.cbh[0] ? 1u : 0u));
-    uint32_t c_r0 = 0, c_rows = 0;
+  // IDCT jobs of strip s: Y block rows 2s, 2s+1, then the chroma block rows
+  // of the strip (4:4:4 / 4:2:2) or the ring's new rows (4:2:0: rows s-1..s+1
+  // at the group's first strip, s+1 after), block columns of the segment
+  struct Jobs {
+    uint32_t ny_r0, nyj, c_r0, ncj, njobs;
+  };
+  auto jobs_of = [&](uint32_t s, bool first) -> Jobs {
+    Jobs J;
+    J.ny_r0 = 2 * s;
+    const uint32_t ny_rows = (2 * s + 2 <= im.cbh[0] ? 2u : (2 * s < im.cbh[0] ? 1u : 0u));
+    uint32_t c_rows = 0;
+    J.c_r0 = 0;
     if (ncomp == 3) {
       if (ring) {
-        c_r0 = s == sa ? (s > 0 ? s - 1 : 0) : s + 1;
+        J.c_r0 = first ? (s > 0 ? s - 1 : 0) : s + 1;
         const uint32_t c_end = s + 2 < im.cbh[1] ? s + 2 : im.cbh[1];
-        c_rows = c_end > c_r0 ? c_end - c_r0 : 0;
+        c_rows = c_end > J.c_r0 ? c_end - J.c_r0 : 0;
       } else {
-        c_r0 = 2 * s;
+        J.c_r0 = 2 * s;
         c_rows = (2 * s + 2 <= im.cbh[1] ? 2u : (2 * s < im.cbh[1] ? 1u : 0u));
       }
     }
-    const uint32_t nyj = ny_rows * cc[0].nb, ncj = c_rows * cc[1].nb;
-    const uint32_t njobs = (dbg & 1) ? 0u : nyj + 2 * ncj;
-    for (uint32_t r0 = 0; r0 < njobs; r0 += kDecRound) {
-      const uint32_t slot = t >> 3, l8 = t & 7;
-      // two jobs per lane group: r0 + slot, r0 + slot + 32
+    J.nyj = ny_rows * cc[0].nb;
+    J.ncj = c_rows * cc[1].nb;
+    J.njobs = (dbg & 1) ? 0u : J.nyj + 2 * J.ncj;
+    return J;
+  };
+  // job j of J -> (component, block row, block column); false past the end
+  auto job_at = [&](const Jobs &J, uint32_t j, uint32_t &c, uint32_t &r, uint32_t &b) -> bool {
+    c = r = b = 0;
+    if (j >= J.njobs) return false;
+    if (j < J.nyj) {
+      r = J.ny_r0 + j / cc[0].nb;
+      b = cc[0].b0 + j % cc[0].nb;
+      return true;
+    }
+    j -= J.nyj;
+    c = 1 + j / J.ncj;
+    j -= (c - 1) * J.ncj;
+    r = J.c_r0 + j / cc[1].nb;
+    b = cc[1].b0 + j % cc[1].nb;
+    return true;
+  };
+  // Each 8-lane group of a wave owns two blocks of a round (wave w: scratch
+  // blocks 8w..8w+7 and 32+8w..), so a round needs only wave-level ordering,
+  // and the loads of the next round (or the next strip's first round) are in
+  // flight while this one computes.
+  const uint32_t slot = t >> 3, l8 = t & 7;
+  auto load2 = [&](const Jobs &J, uint32_t r0, u32x4 raw[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      uint32_t c, r, b;
+      raw[h] = u32x4{0u, 0u, 0u, 0u};
+      if (job_at(J, r0 + slot + 32 * h, c, r, b)) {
+        uint32_t idx;
+        if (ncomp == 1) {
+          idx = r * im.cbw[0] + b;
+        } else {
+          const uint32_t my = r / im.cv[c], vy = r - my * im.cv[c];
+          const uint32_t mx = b / im.ch[c], hx = b - mx * im.ch[c];
+          idx = (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * im.ch[c] + hx;
+        }
+        raw[h] = *(const DG_GLOBAL u32x4 *)(cf + (size_t)idx * 64 + l8 * 8);
+      }
+    }
+  };
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  Jobs cur = jobs_of(sa, true);
+  u32x4 pre[2];
+  load2(cur, 0, pre);
+  for (uint32_t s = sa; s < sb; s++) {
+    // -- 1. IDCT into the LDS planes
+    Jobs nxt = cur;
+    if (s + 1 < sb) nxt = jobs_of(s + 1, false);
+    if (cur.njobs == 0 && s + 1 < sb) load2(nxt, 0, pre);
+    for (uint32_t r0 = 0; r0 < cur.njobs; r0 += kDecRound) {
+      u32x4 raw[2] = {pre[0], pre[1]};
+      if (r0 + kDecRound < cur.njobs)
+        load2(cur, r0 + kDecRound, pre);
+      else if (s + 1 < sb)
+        load2(nxt, 0, pre);
       uint32_t comp[2], brow[2], bcol[2];
       bool act[2];
-      u32x4 raw[2];
 #pragma unroll
-      for (int h = 0; h < 2; h++) {
-        uint32_t j = r0 + slot + 32 * h;
-        act[h] = j < njobs;
-        uint32_t c = 0, r = 0, b = 0;
-        if (j < nyj) {
-          r = ny_r0 + j / cc[0].nb;
-          b = cc[0].b0 + j % cc[0].nb;
-        } else if (act[h]) {
-          j -= nyj;
-          c = 1 + j / ncj;
-          j -= (c - 1) * ncj;
-          r = c_r0 + j / cc[1].nb;
-          b = cc[1].b0 + j % cc[1].nb;
-        }
-        comp[h] = c;
-        brow[h] = r;
-        bcol[h] = b;
-        raw[h] = u32x4{0u, 0u, 0u, 0u};
-        if (act[h]) {
-          uint32_t idx;
-          if (ncomp == 1) {
-            idx = r * im.cbw[0] + b;
-          } else {
-            const uint32_t my = r / im.cv[c], vy = r - my * im.cv[c];
-            const uint32_t mx = b / im.ch[c], hx = b - mx * im.ch[c];
-            idx = (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * im.ch[c] + hx;
-          }
-          raw[h] = *(const DG_GLOBAL u32x4 *)(cf + (size_t)idx * 64 + l8 * 8);
-        }
-      }
+      for (int h = 0; h < 2; h++) act[h] = job_at(cur, r0 + slot + 32 * h, comp[h], brow[h], bcol[h]);
       constexpr int LD = 72, RS = 9;
 #pragma unroll
       for (int h = 0; h < 2; h++) {
@@ -359,12 +406,12 @@ __global__ __launch_bounds__(256) void k_band_dec(const ImageDesc *__restrict__ 
           bv[(nn >> 3) * RS + (nn & 7)] = a[i];
         }
       }
-      __syncthreads();
-      // pass 1: column l8, dequantised (each lane owns its column: no barrier between read and write)
-#pragma unroll
+      wave_sync();
+      // pass 1: column l8, dequantised (each lane owns its column: no sync between read and write)
+#pragma unroll 1
       for (int h = 0; h < 2; h++) {
         int32_t *bv = sm.blk + (slot + 32 * h) * LD;
-        const int32_t *q = sm.q[comp[h]];
+        const int32_t *q = sm.q[h ? comp[1] : comp[0]];  // (selects: no dynamic register index)
         int32_t v[8], w[8];
 #pragma unroll
         for (int r = 0; r < 8; r++) v[r] = bv[r * RS + l8] * q[r * 8 + l8];
@@ -372,30 +419,31 @@ __global__ __launch_bounds__(256) void k_band_dec(const ImageDesc *__restrict__ 
 #pragma unroll
         for (int r = 0; r < 8; r++) bv[r * RS + l8] = w[r];
       }
-      __syncthreads();
+      wave_sync();
       // pass 2: row l8 -> 8 samples into the component's LDS plane
-#pragma unroll
+#pragma unroll 1
       for (int h = 0; h < 2; h++) {
-        if (!act[h]) continue;
+        if (!(h ? act[1] : act[0])) continue;
         const int32_t *w = sm.blk + (slot + 32 * h) * LD + l8 * RS;
         int32_t row[8];
         uint32_t px[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) row[i] = w[i];
         idct_row(zune, row, px);
-        const uint32_t c = comp[h];
+        const uint32_t c = h ? comp[1] : comp[0], br = h ? brow[1] : brow[0], bc = h ? bcol[1] : bcol[0];
         uint8_t *dst;
         if (c == 0) {
-          dst = sm.yp + ((brow[h] - ny_r0) * 8 + l8) * SM::YS + (bcol[h] - cc[0].b0) * 8;
+          dst = sm.yp + ((br - cur.ny_r0) * 8 + l8) * SM::YS + (bc - cc[0].b0) * 8;
         } else if (ring) {
-          dst = sm.cp[c - 1] + ((brow[h] % 3) * 8 + l8) * cstr + (bcol[h] - cc[1].b0) * 8;
+          dst = sm.cp[c - 1] + ((br % 3) * 8 + l8) * cstr + (bc - cc[1].b0) * 8;
         } else {
-          dst = sm.cp[c - 1] + ((brow[h] - c_r0) * 8 + l8) * cstr + (bcol[h] - cc[1].b0) * 8;
+          dst = sm.cp[c - 1] + ((br - cur.c_r0) * 8 + l8) * cstr + (bc - cc[1].b0) * 8;
         }
         *(u32x2 *)dst = u32x2{dec_pack4(px[0], px[1], px[2], px[3]), dec_pack4(px[4], px[5], px[6], px[7])};
       }
-      __syncthreads();
+      wave_sync();
     }
+    __syncthreads();  // planes complete
 
     // -- 2. fill: planar operand rows (p - 128) for the strip's 16 rows, columns [p0, pe)
     for (uint32_t j = t; j < ((dbg & 2) ? 0u : kDecRows * nu); j += 256) {
@@ -473,67 +521,86 @@ __global__ __launch_bounds__(256) void k_band_dec(const ImageDesc *__restrict__ 
     }
     __syncthreads();
 
-    // -- 3. convolution on the matrix cores: subtile (wave*2 + j) x channel
+    // -- 3. convolution on the matrix cores, D = W . P per subtile (wave*2 + j)
+    // and channel: A = the weight digits (output column n, K group g), B =
+    // the strip's pixels (row n, K group g), so lane (n, g) receives output
+    // columns 4g .. 4g+3 of strip row n -- 4 adjacent pixels, stored
+    // straight to HBM (12 bytes RGB / 4 bytes gray) without an LDS staging.
+    const uint32_t y = s * kDecRows + n;  // this lane's image row
+    const bool row_ok = y >= ps.row0 && y < ps.row0 + ps.rows;
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       const uint32_t sub = wave * 2 + j;
       if (x0 + sub * kDecSub >= x1 || steps[j] == 0 || (dbg & 4)) continue;  // wave-uniform
-      const uint32_t xo = sub * kDecSub + n;                      // column within the tile
+      uint32_t px[3] = {0, 0, 0};  // channel c of columns 4g .. 4g+3, packed
       for (uint32_t c = 0; c < C; c++) {
-        const uint8_t *arow = sm.ap[c] + n * SM::AS + (k0[j] - p0) + 16 * g;  // A: row n, k group g
-        i32x4 alo = {0, 0, 0, 0}, amd = {0, 0, 0, 0}, ahi = {0, 0, 0, 0};
+        const uint8_t *brow = sm.ap[c] + n * SM::AS + (k0[j] - p0) + 16 * g;  // B: strip row n, K group g
+        i32x4 alo = *(const i32x4 *)(sm.corr + sub * kDecSub + 4 * g), amd = {0, 0, 0, 0}, ahi = {0, 0, 0, 0};
         {
-          const i32x4 a = *(const i32x4 *)arow;
-          alo = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wlo[j][0], alo, 0, 0, 0);
-          amd = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wmid[j][0], amd, 0, 0, 0);
-          ahi = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, whi[j][0], ahi, 0, 0, 0);
+          const i32x4 b = *(const i32x4 *)brow;
+          alo = __builtin_amdgcn_mfma_i32_16x16x64_i8(wlo[j][0], b, alo, 0, 0, 0);
+          amd = __builtin_amdgcn_mfma_i32_16x16x64_i8(wmid[j][0], b, amd, 0, 0, 0);
+          ahi = __builtin_amdgcn_mfma_i32_16x16x64_i8(whi[j][0], b, ahi, 0, 0, 0);
         }
-        if (steps[j] > 1) {
-          const i32x4 a = *(const i32x4 *)(arow + 64);
-          alo = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wlo[j][1], alo, 0, 0, 0);
-          amd = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wmid[j][1], amd, 0, 0, 0);
-          ahi = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, whi[j][1], ahi, 0, 0, 0);
+        if (KS > 1 && steps[j] > 1) {
+          const i32x4 b = *(const i32x4 *)(brow + 64);
+          alo = __builtin_amdgcn_mfma_i32_16x16x64_i8(wlo[j][KS - 1], b, alo, 0, 0, 0);
+          amd = __builtin_amdgcn_mfma_i32_16x16x64_i8(wmid[j][KS - 1], b, amd, 0, 0, 0);
+          ahi = __builtin_amdgcn_mfma_i32_16x16x64_i8(whi[j][KS - 1], b, ahi, 0, 0, 0);
         }
-        // D: column n of the subtile, rows 4g .. 4g+3
-        if (x0 + xo < x1) {
+        uint32_t o[4];
 #pragma unroll
-          for (int rr = 0; rr < 4; rr++) {
-            const int32_t v = (ahi[rr] << 14) + (amd[rr] << 7) + alo[rr] + corr[j];
-            int32_t o = v >> prec;
-            o = o < 0 ? 0 : (o > 255 ? 255 : o);
-            sm.ob[(4 * g + rr) * SM::OBS + xo * C + c] = (uint8_t)o;
-          }
+        for (int rr = 0; rr < 4; rr++) {
+          const int32_t v = ((ahi[rr] << 14) + (amd[rr] << 7) + alo[rr]) >> prec;
+          o[rr] = (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
         }
+        const uint32_t w4 = dec_pack4(o[0], o[1], o[2], o[3]);
+        px[0] = c == 0 ? w4 : px[0];
+        px[1] = c == 1 ? w4 : px[1];
+        px[2] = c == 2 ? w4 : px[2];
       }
-    }
-    __syncthreads();
-
-    // -- 4. store the strip's rows of the H intermediate
-    const uint32_t rb = (x1 - x0) * C;
-    for (uint32_t j = t; j < ((dbg & 8) ? 0u : kDecRows * 32); j += 256) {
-      const uint32_t r = j >> 5, b = (j & 31) * 16;
-      const uint32_t y = s * kDecRows + r;
-      if (b >= rb || y < ps.row0 || y >= ps.row0 + ps.rows) continue;
-      DG_GLOBAL uint8_t *d = gp<uint8_t>(ps.dst) + (size_t)(y - ps.row0) * ps.dst_stride + (size_t)x0 * C + b;
-      const uint8_t *o = sm.ob + r * SM::OBS + b;
-      if (b + 16 <= rb && (((uintptr_t)d) & 15) == 0) {
-        *(DG_GLOBAL u32x4 *)d = *(const u32x4 *)o;
+      if (!row_ok || (dbg & 8)) continue;
+      const uint32_t xs = x0 + sub * kDecSub + 4 * g;  // first of the lane's 4 columns
+      if (xs >= x1) continue;
+      DG_GLOBAL uint8_t *d = gp<uint8_t>(ps.dst) + (size_t)(y - ps.row0) * ps.dst_stride + (size_t)xs * C;
+      if (C == 1) {
+        if (xs + 4 <= x1 && (((uintptr_t)d) & 3) == 0) {
+          *(DG_GLOBAL uint32_t *)d = px[0];
+        } else {
+          for (uint32_t k = 0; k < 4 && xs + k < x1; k++) d[k] = (uint8_t)(px[0] >> (8 * k));
+        }
+        continue;
+      }
+      // [R0 G0 B0 R1] [G1 B1 R2 G2] [B2 R3 G3 B3]
+      const uint32_t rg = __builtin_amdgcn_perm(px[1], px[0], 0x05010400u);   // R0 G0 R1 G1
+      const uint32_t rg2 = __builtin_amdgcn_perm(px[1], px[0], 0x07030602u);  // R2 G2 R3 G3
+      const uint32_t d0 = __builtin_amdgcn_perm(px[2], rg, 0x02040100u);      // R0 G0 B0 R1
+      const uint32_t gb = __builtin_amdgcn_perm(px[2], rg, 0x0c0c0503u);      // G1 B1 0 0
+      const uint32_t d1 = __builtin_amdgcn_perm(rg2, gb, 0x05040100u);        // G1 B1 R2 G2
+      const uint32_t d2 = __builtin_amdgcn_perm(rg2, px[2], 0x03070602u);     // B2 R3 G3 B3
+      if (xs + 4 <= x1 && (((uintptr_t)d) & 3) == 0) {
+        DG_GLOBAL uint32_t *d4 = (DG_GLOBAL uint32_t *)d;
+        d4[0] = d0;
+        d4[1] = d1;
+        d4[2] = d2;
       } else {
-        const uint32_t e = b + 16 < rb ? 16 : rb - b;
-        for (uint32_t i = 0; i < e; i++) d[i] = o[i];
+        const uint32_t w[3] = {d0, d1, d2};
+        for (uint32_t k = 0; k < 12 && xs + k / 3 < x1; k++) d[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
       }
     }
+    __syncthreads();  // the next strip's IDCT scratch aliases the operand rows
     // (the next strip's IDCT writes yp / cp / the scratch aliasing ap, all
     // read before the barriers above; ob is next written after two barriers)
+    cur = nxt;
   }
 }
 
 void launch_band_dec(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2],
                      const QuantTable *qpool, uint32_t strips_per_wg) {
   if (ncls[0])
-    hipLaunchKernelGGL(k_band_dec<kDecSeg0>, dim3(ncls[0]), dim3(256), 0, st, imgs, list, qpool, strips_per_wg);
+    hipLaunchKernelGGL((k_band_dec<kDecSeg0, 1>), dim3(ncls[0]), dim3(256), 0, st, imgs, list, qpool, strips_per_wg);
   if (ncls[1])
-    hipLaunchKernelGGL(k_band_dec<kDecSeg1>, dim3(ncls[1]), dim3(256), 0, st, imgs, list + ncls[0], qpool,
+    hipLaunchKernelGGL((k_band_dec<kDecSeg1, 2>), dim3(ncls[1]), dim3(256), 0, st, imgs, list + ncls[0], qpool,
                        strips_per_wg);
 }
 

@@ -129,7 +129,8 @@ dg_status dg_probe(const uint8_t *bytes, size_t len, dg_probe_info *out) {
   out->arithmetic = h.arithmetic;
   out->precision = h.precision;
   out->restart_interval = h.restart;
-  out->gpu_supported = h.status == dg::JH_OK;
+  // (a context with decode_semantics 1 also decodes incompletely refined progressive files)
+  out->gpu_supported = h.status == dg::JH_OK && !h.incomplete_refinement;
   if (h.status == dg::JH_CORRUPT) {
     dg::set_error(h.why);
     return DG_ERR_CORRUPT;

@@ -211,9 +211,12 @@ void parse_jpeg_header(const uint8_t *d, size_t n, JpegHeader &h) {
     for (const JpegScan &sc : h.scans)
       for (int i = 0; i < sc.ns; i++)
         for (int k = sc.ss; k <= sc.se; k++) bits[sc.comp[i]][k] = sc.al;
+    // recorded, not refused here: libjpeg-turbo semantics refuse such files
+    // (plan_image / dg_probe), zune-jpeg applies no smoothing and decodes the
+    // coefficients as they stand
     for (int c = 0; c < h.ncomp; c++)
       for (int k = 0; k < 10; k++)
-        if (bits[c][k] != 0) return fail(h, JH_UNSUPPORTED, "incomplete progressive refinement (block smoothing)");
+        if (bits[c][k] != 0) h.incomplete_refinement = true;
     h.scan_end = h.scans.empty() ? h.scan_off : h.scans.back().end;
   }
   h.hmax = h.vmax = 1;

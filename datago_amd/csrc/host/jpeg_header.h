@@ -51,6 +51,7 @@ struct JpegHeader {
   int ncomp = 0;
   JpegComponent comp[4];
   bool progressive = false, arithmetic = false, lossless = false;
+  bool incomplete_refinement = false;  // progressive: DC or AC 1..9 not fully refined (libjpeg would smooth blocks)
   int restart = 0;
   bool jfif = false, adobe = false;
   int adobe_transform = -1;

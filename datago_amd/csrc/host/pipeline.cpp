@@ -99,6 +99,7 @@ Context::Context(int device, const dg_image_config *cfg) : device_(device) {
   } else if (cfg) {
     cfg_ = *cfg;
   }
+  if (cfg) decode_sem_ = cfg->decode_semantics == 1 ? 1 : 0;
 }
 
 Context::~Context() {
@@ -214,8 +215,9 @@ static bool hv_fusable(const ResizePass &h, const ResizePass &v) {
 // k_band_dec takes pass[0] of a JPEG when its sampling is one the fused fill
 // knows (gray; 4:4:4, 4:2:2, 4:2:0 with luma at the maximum factors) and its
 // segments fit: the 128-column tile's source segment (plus the 16-pixel
-// alignment) in the class's LDS, every 16-column MFMA subtile's window in two
-// 64-wide K steps.  Returns the mode bits (0: not eligible).
+// alignment) in the class's LDS, every 16-column MFMA subtile's window in the
+// class's K steps (320-pixel class: one 64-wide step, downscales up to ~2x;
+// 640-pixel class: two).  Returns the mode bits (0: not eligible).
 static uint32_t band_dec_mode(const ImageDesc &d, const ResizePass &ps) {
   if (ps.kind != 1 || (ps.mode & (kHDirect | kHVFused)) || d.idct_fused) return 0;
   if (d.ncomp == 3) {
@@ -228,10 +230,10 @@ static uint32_t band_dec_mode(const ImageDesc &d, const ResizePass &ps) {
     return 0;
   }
   const double scale = (ps.in1 - ps.in0) / (double)ps.out_size;
-  if (15.0 + std::ceil(15.0 * scale) + (double)ps.ksize + 2.0 > 128.0) return 0;
+  const double window = 15.0 + std::ceil(15.0 * scale) + (double)ps.ksize + 2.0;  // a subtile's K range
   const double span = h_pass_span(ps) + 16.0;
-  if (span <= (double)kDecSeg0) return kHDecode;
-  if (span <= (double)kDecSeg1) return kHDecode | kHDecWide;
+  if (span <= (double)kDecSeg0 && window <= 64.0) return kHDecode;  // one K step
+  if (span <= (double)kDecSeg1 && window <= 128.0) return kHDecode | kHDecWide;
   return 0;
 }
 
@@ -585,6 +587,12 @@ dg_status Context::plan_image(const uint8_t *h, size_t len, int32_t forced, Imag
     }
     if (p.hdr.progressive && !progressive_) {  // see option "progressive"
       p.hdr.why = "progressive JPEG (context option \"progressive\" decodes it on the GPU)";
+      p.status = DG_ERR_UNSUPPORTED;
+      return DG_OK;
+    }
+    if (p.hdr.incomplete_refinement && decode_sem_ == 0) {
+      // libjpeg-turbo would smooth these blocks (jdcoefct.c smoothing_ok); zune-jpeg does not
+      p.hdr.why = "incomplete progressive refinement (libjpeg block smoothing; decodes with decode_semantics 1)";
       p.status = DG_ERR_UNSUPPORTED;
       return DG_OK;
     }

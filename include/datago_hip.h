@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 1
+#define DG_ABI_VERSION 2  /* 2: dg_image_config.decode_semantics */
 
 typedef enum dg_status {
   DG_OK = 0,
@@ -70,6 +70,12 @@ typedef struct dg_image_config {
   int32_t image_to_rgb8;        /* gray -> RGB expansion after resize (:367-372) */
   int32_t encode_format;        /* 0 = PNG, 1 = JPEG (EncodeFormat, :16-22) */
   int32_t jpeg_quality;         /* default 92 (:14) */
+  /* JPEG pixel semantics (IDCT, chroma upsampling, YCbCr->RGB, progressive block smoothing):
+   * 0 = libjpeg-turbo (pinned bit-exact to PIL; refuses progressive files libjpeg would block-smooth),
+   * 1 = zune-jpeg 0.5.12, the reference's own decoder (worker_files.rs:14-16 -> image 0.25.9 ->
+   *     zune-jpeg), restated from the crate's published source (unpinned offline).
+   * The Rust drop-in sets 1; same as the context option "decode_semantics". */
+  int32_t decode_semantics;
 } dg_image_config;
 
 /* ------------------------------------------------------------ buckets */
@@ -200,6 +206,7 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "wg_timing"   debug: per-workgroup timestamps of the entropy kernels
  *   "timing"      1 = record per-kernel HIP events (dg_last_batch_timings)
  *   "side_stream" 1 = Lanczos tables on a second stream (default 1)
+ *   "decode_semantics" 0 / 1: overrides dg_image_config.decode_semantics
  *   "debug_flags" internal switches: bit 0 = direct H-pass kernel only (bisection); bit 16 / 17 =
  *                 force an entropy write-pass mismatch / a resync that never settles; bit 18 / 19 = force
  *                 a PNG unfilter band wait / a progressive scan wait to time out (tests of the per-image

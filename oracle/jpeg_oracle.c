@@ -10,7 +10,8 @@
  *   - progressive scans per T.81 G.1.2 (libjpeg jdphuff.c: DC first/refine,
  *     AC first with EOB runs, AC refine with correction bits); files whose
  *     coefficients 1..9 stay incomplete after the last scan (libjpeg would
- *     apply block smoothing, jdcoefct.c smoothing_ok) are UNSUPPORTED,
+ *     apply block smoothing, jdcoefct.c smoothing_ok) are UNSUPPORTED
+ *     (under OJ_SEM_ZUNE they decode as they stand: zune-jpeg does not smooth),
  *   - ISLOW integer IDCT (libjpeg jidctint.c, CONST_BITS=13, PASS1_BITS=2) with
  *     the SIMD build's saturating output (clamp to [-128,127] + 128),
  *   - "fancy" triangular chroma upsampling h2v1 / h2v2 (libjpeg jdsample.c),
@@ -603,6 +604,7 @@ static int decode_progressive(oj_jpeg *j, const uint8_t *d, size_t n) {
     if (st == OJ_EOI) break;
     if (st) return st;
   }
+  if (g_sem == OJ_SEM_ZUNE) return OJ_OK; /* zune-jpeg has no block smoothing: coefficients as decoded */
   for (int c = 0; c < j->ncomp; c++) {
     if (bits[c][0] != 0) return OJ_UNSUPPORTED; /* DC incomplete */
     for (int k = 1; k < 10; k++)

@@ -85,3 +85,36 @@ def test_option_validated():
     c = L.Context(0)
     with pytest.raises(Exception):
         c.set_option("decode_semantics", 2)
+
+
+def _truncate_scans(data: bytes, keep: int) -> bytes:
+    """The progressive file cut after its first `keep` scans (+ EOI): valid,
+    with coefficients left incompletely refined -- libjpeg would smooth those
+    blocks (jdcoefct.c), zune-jpeg decodes them as they stand."""
+    sos = [i for i in range(len(data) - 1) if data[i] == 0xFF and data[i + 1] == 0xDA]
+    assert len(sos) > keep
+    # the scan after `keep` starts at its SOS (or at a DHT just before it)
+    cut = sos[keep]
+    j = cut - 1
+    while j > sos[keep - 1] and not (data[j] == 0xFF and data[j + 1] == 0xC4):
+        j -= 1
+    if j > sos[keep - 1]:
+        cut = j
+    return data[:cut] + b"\xff\xd9"
+
+
+def test_incomplete_progressive_refinement_decodes_in_zune_mode():
+    from datago_amd import _lib as L
+    datas = [_truncate_scans(synth.make_jpeg(7400 + i, w, h, 88, ss, progressive=True), keep)
+             for i, (w, h, ss, keep) in enumerate([(300, 200, "4:2:0", 3), (257, 131, "4:4:4", 5),
+                                                    (640, 480, "4:2:0", 7), (99, 301, "4:2:2", 2)])]
+    lj = _ctx(0, False)
+    lj.set_option("progressive", 1)
+    zu = L.Context(0, decode_semantics=1)  # through dg_image_config.decode_semantics
+    zu.set_option("progressive", 1)
+    for d, (st, _, _) in zip(datas, lj.decode_batch(datas)):
+        assert st == L.DG_ERR_UNSUPPORTED  # libjpeg semantics would block-smooth
+        assert O.jpeg_decode(d)[0] == O.OJ_UNSUPPORTED
+    for k, (d, (st, arr, _)) in enumerate(zip(datas, zu.decode_batch(datas))):
+        assert st == 0, (k, L.last_error())
+        assert np.array_equal(arr, _oracle(d, O.SEM_ZUNE)), k
