@@ -41,7 +41,8 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t kDecRows = 16;    // strip height: the MFMA M dimension
 constexpr uint32_t kDecSub = 16;     // output columns per MFMA subtile (N)
-constexpr uint32_t kDecRound = 64;   // IDCT blocks per round (two per 8-lane group)
+constexpr uint32_t kDecThreads = 512; // 8 waves: one 16-column MFMA subtile each
+constexpr uint32_t kDecRound = 64;   // IDCT blocks per round (one per 8-lane group)
 
 __device__ __forceinline__ uint32_t dec_xcd_remap(uint32_t b, uint32_t n) {
   const uint32_t per = n >> 3, rem = n & 7, x = b & 7, l = b >> 3;
@@ -68,7 +69,7 @@ struct DecSmem {
   static constexpr uint32_t YS = SEG;                   // Y plane row stride
   static constexpr uint32_t CS = SEG;                   // chroma row stride (h2: SEG/2 + 32 used)
   static constexpr uint32_t AS = dec_row_stride(SEG + 64 * KS);  // planar operand rows (reads reach 64 * KS past k0)
-  int32_t q[3][64];                                     // quant tables (natural order)
+  __attribute__((aligned(16))) int16_t qt[3][64];       // quant tables, transposed: qt[c][col * 8 + row]
   uint32_t ext[4];
   __attribute__((aligned(16))) int32_t corr[kDecCols];  // per output column: 128 * sum(w) + rounding bias
   __attribute__((aligned(16))) uint8_t yp[kDecRows * YS];
@@ -77,6 +78,10 @@ struct DecSmem {
     __attribute__((aligned(16))) uint8_t ap[3][kDecRows * AS];  // planar operand rows (i8)
     int32_t blk[kDecRound * 72];                                // IDCT transpose scratch
   };
+  // the next strip's coefficient blocks (zigzag int16, 128 B each, job order), landed by LDS-DMA
+  // while this strip fills and convolves; jobs past STG load from HBM in their round
+  static constexpr uint32_t STG = KS == 1 ? 128 : 64;
+  __attribute__((aligned(16))) uint8_t stg[STG * 128];
 };
 
 // 8 libjpeg-turbo fancy-upsampled chroma samples at full-resolution columns
@@ -179,6 +184,12 @@ __device__ __forceinline__ void dec_ups_zune(const uint8_t *r0, const uint8_t *r
   }
 }
 
+// n / d for n, d < 2^16 by one multiply-high with m = ceil(2^32 / d) (the
+// error n * (m - 2^32 / d) / 2^32 < 2^-16 < 1 / d never crosses an integer).
+// (m = 0 stands for d = 1; one 32-bit division per divisor, no 64-bit one)
+__device__ __forceinline__ uint32_t dec_magic(uint32_t d) { return d <= 1 ? 0u : 0xFFFFFFFFu / d + 1u; }
+__device__ __forceinline__ uint32_t dec_div(uint32_t n, uint32_t m) { return m ? __umulhi(n, m) : n; }
+
 // Per-component block ranges of the workgroup's segment (uniform).
 struct DecComp {
   uint32_t b0, nb;    // block columns [b0, b0 + nb) held in LDS
@@ -187,7 +198,7 @@ struct DecComp {
 };
 
 template <uint32_t SEG, int KS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_band_dec(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
+__global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_band_dec(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
                                                   const QuantTable *__restrict__ qpool, uint32_t strips_arg) {
   using SM = DecSmem<SEG, KS>;
   const uint32_t strips_per_wg = strips_arg & 0xFFFFu, dbg = strips_arg >> 16;  // dbg: timing experiments only
@@ -214,7 +225,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   if (t < 192) {
     const uint32_t c = t >> 6, k = t & 63;
     const DG_GLOBAL uint16_t *q = gp<const uint16_t>((uint64_t)(uintptr_t)qpool[im.qpool[c < ncomp ? c : 0]].q);
-    sm.q[c][k] = q[k];
+    sm.qt[c][(k & 7) * 8 + (k >> 3)] = (int16_t)q[k];
   }
   __syncthreads();
   if (t < kDecCols && x0 + t < x1) {
@@ -250,14 +261,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool ring = ncomp == 3 && cc[1].vr == 2;  // h2v2 chroma: three-block-row ring
   const uint32_t cstr = (ncomp == 3 && cc[1].hr == 2) ? SEG / 2 + 32 : SEG;
 
-  // ---- MFMA weights of this wave's two subtiles (set up once)
+  // ---- MFMA weights of this wave's subtile (set up once)
   // lane: column n = lane & 15 of the subtile, k group g = lane >> 4
   const uint32_t n = lane & 15, g = lane >> 4;
-  i32x4 wlo[2][KS], wmid[2][KS], whi[2][KS];  // weight digits c, b, a of (subtile, K step)
-  uint32_t k0[2], steps[2];
-#pragma unroll
-  for (int j = 0; j < 2; j++) {
-    const uint32_t sub = wave * 2 + j;
+  i32x4 wlo[KS], wmid[KS], whi[KS];  // weight digits c, b, a per K step
+  uint32_t k0, steps;
+  const uint32_t sub = wave;
+  {
     const uint32_t xs = x0 + sub * kDecSub + n;
     const bool valid = xs < x1;
     uint32_t st = 0, cnt = 0;
@@ -272,29 +282,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       mn = a < mn ? a : mn;
       mx = b > mx ? b : mx;
     }
-    k0[j] = mn == 0xFFFFFFFFu ? p0 : (mn & ~15u);
-    steps[j] = mx > k0[j] ? (mx - k0[j] + 63) / 64 : 0;
-    if (steps[j] > (uint32_t)KS) steps[j] = KS;  // host guarantees windows <= 64 * KS (band_dec_mode)
+    k0 = mn == 0xFFFFFFFFu ? p0 : (mn & ~15u);
+    steps = mx > k0 ? (mx - k0 + 63) / 64 : 0;
+    if (steps > (uint32_t)KS) steps = KS;  // host guarantees windows <= 64 * KS (band_dec_mode)
     const DG_GLOBAL int16_t *kp = coef + (size_t)(valid ? xs : x0) * ps.ksize;
-    int32_t sum = 0;
-    for (uint32_t i = 0; i < cnt; i++) sum += kp[i];
-    if (g == 0) sm.corr[sub * kDecSub + n] = sum * 128 + (1 << (prec - 1));
+    int32_t sum = 0;  // of column n's weights: this lane's K groups, then over the four groups
 #pragma unroll
     for (int s = 0; s < KS; s++) {
       uint32_t lo[4] = {0, 0, 0, 0}, md[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
-      const int32_t kb = (int32_t)(k0[j] + 64 * s + 16 * g) - (int32_t)st;
+      const int32_t kb = (int32_t)(k0 + 64 * s + 16 * g) - (int32_t)st;
 #pragma unroll
       for (int e = 0; e < 16; e++) {
         const int32_t i = kb + e;
         const int32_t w = (valid && i >= 0 && i < (int32_t)cnt) ? (int32_t)kp[i] : 0;
+        sum += w;
         lo[e >> 2] |= (uint32_t)(w & 127) << (8 * (e & 3));
         md[e >> 2] |= (uint32_t)((w >> 7) & 127) << (8 * (e & 3));
         hi[e >> 2] |= (uint32_t)((w >> 14) & 0xFF) << (8 * (e & 3));
       }
-      wlo[j][s] = i32x4{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]};
-      wmid[j][s] = i32x4{(int)md[0], (int)md[1], (int)md[2], (int)md[3]};
-      whi[j][s] = i32x4{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      wlo[s] = i32x4{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]};
+      wmid[s] = i32x4{(int)md[0], (int)md[1], (int)md[2], (int)md[3]};
+      whi[s] = i32x4{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    if (g == 0) sm.corr[sub * kDecSub + n] = sum * 128 + (1 << (prec - 1));
   }
 
   // ---- strips of this workgroup
@@ -308,8 +320,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   // of the strip (4:4:4 / 4:2:2) or the ring's new rows (4:2:0: rows s-1..s+1
   // at the group's first strip, s+1 after), block columns of the segment
   struct Jobs {
-    uint32_t ny_r0, nyj, c_r0, ncj, njobs;
+    uint32_t ny_r0, nyj, c_r0, ncj, njobs, m_ncj;
   };
+  const uint32_t m_nby = dec_magic(cc[0].nb ? cc[0].nb : 1u), m_nbc = dec_magic(cc[1].nb ? cc[1].nb : 1u);
+  const uint32_t m_nu = dec_magic(nu ? nu : 1u);
   auto jobs_of = [&](uint32_t s, bool first) -> Jobs {
     Jobs J;
     J.ny_r0 = 2 * s;
@@ -328,46 +342,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
     J.nyj = ny_rows * cc[0].nb;
     J.ncj = c_rows * cc[1].nb;
+    J.m_ncj = dec_magic(J.ncj ? J.ncj : 1u);
     J.njobs = (dbg & 1) ? 0u : J.nyj + 2 * J.ncj;
     return J;
   };
   // job j of J -> (component, block row, block column); false past the end
+  // (uniform divisors: multiply-high by precomputed magics, no division loops)
   auto job_at = [&](const Jobs &J, uint32_t j, uint32_t &c, uint32_t &r, uint32_t &b) -> bool {
     c = r = b = 0;
     if (j >= J.njobs) return false;
     if (j < J.nyj) {
-      r = J.ny_r0 + j / cc[0].nb;
-      b = cc[0].b0 + j % cc[0].nb;
+      const uint32_t q = dec_div(j, m_nby);
+      r = J.ny_r0 + q;
+      b = cc[0].b0 + (j - q * cc[0].nb);
       return true;
     }
     j -= J.nyj;
-    c = 1 + j / J.ncj;
+    c = 1 + dec_div(j, J.m_ncj);
     j -= (c - 1) * J.ncj;
-    r = J.c_r0 + j / cc[1].nb;
-    b = cc[1].b0 + j % cc[1].nb;
+    const uint32_t q = dec_div(j, m_nbc);
+    r = J.c_r0 + q;
+    b = cc[1].b0 + (j - q * cc[1].nb);
     return true;
   };
-  // Each 8-lane group of a wave owns two blocks of a round (wave w: scratch
-  // blocks 8w..8w+7 and 32+8w..), so a round needs only wave-level ordering,
-  // and the loads of the next round (or the next strip's first round) are in
-  // flight while this one computes.
+  // Each 8-lane group of a wave owns one block of a round (wave w: scratch
+  // blocks 8w..8w+7), so a round needs only wave-level ordering.  The
+  // blocks come from the LDS staging, which LDS-DMA filled during the
+  // previous strip's fill and convolution (~16 KiB per workgroup in flight
+  // without a register), or, past STG jobs, straight from HBM.
   const uint32_t slot = t >> 3, l8 = t & 7;
-  auto load2 = [&](const Jobs &J, uint32_t r0, u32x4 raw[2]) {
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
+  auto block_ptr = [&](uint32_t c, uint32_t r, uint32_t b) -> const DG_GLOBAL int16_t * {
+    uint32_t idx;
+    if (ncomp == 1) {
+      idx = r * im.cbw[0] + b;
+    } else {
+      const uint32_t my = r / im.cv[c], vy = r - my * im.cv[c];
+      const uint32_t mx = b / im.ch[c], hx = b - mx * im.ch[c];
+      idx = (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * im.ch[c] + hx;
+    }
+    return cf + (size_t)idx * 64;
+  };
+  // LDS-DMA of jobs [0, min(njobs, STG)): one wave instruction = 8 blocks (1 KiB), lane l the 16-byte
+  // chunk l % 8 of block l / 8; wave w takes instructions w, w + 8, ...
+  auto stage = [&](const Jobs &J) {
+    const uint32_t nst = J.njobs < SM::STG ? J.njobs : SM::STG;
+    for (uint32_t i = wave; i * 8 < nst; i += kDecThreads / 64) {
+      const uint32_t j = i * 8 + (lane >> 3);
       uint32_t c, r, b;
-      raw[h] = u32x4{0u, 0u, 0u, 0u};
-      if (job_at(J, r0 + slot + 32 * h, c, r, b)) {
-        uint32_t idx;
-        if (ncomp == 1) {
-          idx = r * im.cbw[0] + b;
-        } else {
-          const uint32_t my = r / im.cv[c], vy = r - my * im.cv[c];
-          const uint32_t mx = b / im.ch[c], hx = b - mx * im.ch[c];
-          idx = (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * im.ch[c] + hx;
-        }
-        raw[h] = *(const DG_GLOBAL u32x4 *)(cf + (size_t)idx * 64 + l8 * 8);
-      }
+      if (j < nst && job_at(J, j, c, r, b))
+        __builtin_amdgcn_global_load_lds((const DG_GLOBAL void *)((const DG_GLOBAL uint8_t *)block_ptr(c, r, b) +
+                                                                  (lane & 7) * 16),
+                                         (__attribute__((address_space(3))) void *)(sm.stg + i * 1024), 16, 0, 0);
     }
   };
   auto wave_sync = [] {
@@ -377,29 +402,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   };
 
   Jobs cur = jobs_of(sa, true);
-  u32x4 pre[2];
-  load2(cur, 0, pre);
+  stage(cur);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (uint32_t s = sa; s < sb; s++) {
     // -- 1. IDCT into the LDS planes
     Jobs nxt = cur;
     if (s + 1 < sb) nxt = jobs_of(s + 1, false);
-    if (cur.njobs == 0 && s + 1 < sb) load2(nxt, 0, pre);
     for (uint32_t r0 = 0; r0 < cur.njobs; r0 += kDecRound) {
-      u32x4 raw[2] = {pre[0], pre[1]};
-      if (r0 + kDecRound < cur.njobs)
-        load2(cur, r0 + kDecRound, pre);
-      else if (s + 1 < sb)
-        load2(nxt, 0, pre);
-      uint32_t comp[2], brow[2], bcol[2];
-      bool act[2];
-#pragma unroll
-      for (int h = 0; h < 2; h++) act[h] = job_at(cur, r0 + slot + 32 * h, comp[h], brow[h], bcol[h]);
+      uint32_t comp, brow, bcol;
+      const uint32_t jb = r0 + slot;
+      const bool act = job_at(cur, jb, comp, brow, bcol);
+      u32x4 raw = u32x4{0u, 0u, 0u, 0u};
+      if (jb < SM::STG)
+        raw = *(const u32x4 *)(sm.stg + jb * 128 + l8 * 16);
+      else if (act)
+        raw = *(const DG_GLOBAL u32x4 *)(block_ptr(comp, brow, bcol) + l8 * 8);
       constexpr int LD = 72, RS = 9;
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        int32_t *bv = sm.blk + (slot + 32 * h) * LD;
+      int32_t *bv = sm.blk + slot * LD;
+      {
         int16_t a[8];
-        __builtin_memcpy(a, &raw[h], 16);
+        __builtin_memcpy(a, &raw, 16);
 #pragma unroll
         for (int i = 0; i < 8; i++) {
           const int nn = kZigzagToNatural[l8 * 8 + i];
@@ -408,46 +431,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       }
       wave_sync();
       // pass 1: column l8, dequantised (each lane owns its column: no sync between read and write)
-#pragma unroll 1
-      for (int h = 0; h < 2; h++) {
-        int32_t *bv = sm.blk + (slot + 32 * h) * LD;
-        const int32_t *q = sm.q[h ? comp[1] : comp[0]];  // (selects: no dynamic register index)
+      {
+        // column l8 of the component's quant table: one 16-byte read
+        const u32x4 qv = *(const u32x4 *)(sm.qt[comp] + l8 * 8);
+        int16_t qc[8];
+        __builtin_memcpy(qc, &qv, 16);
         int32_t v[8], w[8];
 #pragma unroll
-        for (int r = 0; r < 8; r++) v[r] = bv[r * RS + l8] * q[r * 8 + l8];
+        for (int r = 0; r < 8; r++) v[r] = bv[r * RS + l8] * (int32_t)qc[r];
         idct_col(zune, v, w);
 #pragma unroll
         for (int r = 0; r < 8; r++) bv[r * RS + l8] = w[r];
       }
       wave_sync();
       // pass 2: row l8 -> 8 samples into the component's LDS plane
-#pragma unroll 1
-      for (int h = 0; h < 2; h++) {
-        if (!(h ? act[1] : act[0])) continue;
-        const int32_t *w = sm.blk + (slot + 32 * h) * LD + l8 * RS;
+      if (act) {
+        const int32_t *w = bv + l8 * RS;
         int32_t row[8];
         uint32_t px[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) row[i] = w[i];
         idct_row(zune, row, px);
-        const uint32_t c = h ? comp[1] : comp[0], br = h ? brow[1] : brow[0], bc = h ? bcol[1] : bcol[0];
         uint8_t *dst;
-        if (c == 0) {
-          dst = sm.yp + ((br - cur.ny_r0) * 8 + l8) * SM::YS + (bc - cc[0].b0) * 8;
+        if (comp == 0) {
+          dst = sm.yp + ((brow - cur.ny_r0) * 8 + l8) * SM::YS + (bcol - cc[0].b0) * 8;
         } else if (ring) {
-          dst = sm.cp[c - 1] + ((br % 3) * 8 + l8) * cstr + (bc - cc[1].b0) * 8;
+          dst = sm.cp[comp - 1] + ((brow % 3) * 8 + l8) * cstr + (bcol - cc[1].b0) * 8;
         } else {
-          dst = sm.cp[c - 1] + ((br - cur.c_r0) * 8 + l8) * cstr + (bc - cc[1].b0) * 8;
+          dst = sm.cp[comp - 1] + ((brow - cur.c_r0) * 8 + l8) * cstr + (bcol - cc[1].b0) * 8;
         }
         *(u32x2 *)dst = u32x2{dec_pack4(px[0], px[1], px[2], px[3]), dec_pack4(px[4], px[5], px[6], px[7])};
       }
       wave_sync();
     }
-    __syncthreads();  // planes complete
+    __syncthreads();  // planes complete, staging consumed
+    if (s + 1 < sb) stage(nxt);  // lands during the fill and the convolution
 
     // -- 2. fill: planar operand rows (p - 128) for the strip's 16 rows, columns [p0, pe)
-    for (uint32_t j = t; j < ((dbg & 2) ? 0u : kDecRows * nu); j += 256) {
-      const uint32_t r = j / nu, u = j - r * nu;
+    for (uint32_t j = t; j < ((dbg & 2) ? 0u : kDecRows * nu); j += kDecThreads) {
+      const uint32_t r = dec_div(j, m_nu), u = j - r * nu;
       const uint32_t xo = 8 * u, xa = p0 + xo;  // offset in the segment, absolute column
       const uint32_t y = s * kDecRows + r;       // image row
       const u32x2 yv = *(const u32x2 *)(sm.yp + r * SM::YS + xo);
@@ -521,32 +543,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
     __syncthreads();
 
-    // -- 3. convolution on the matrix cores, D = W . P per subtile (wave*2 + j)
+    // -- 3. convolution on the matrix cores, D = W . P for this wave's subtile
     // and channel: A = the weight digits (output column n, K group g), B =
     // the strip's pixels (row n, K group g), so lane (n, g) receives output
     // columns 4g .. 4g+3 of strip row n -- 4 adjacent pixels, stored
     // straight to HBM (12 bytes RGB / 4 bytes gray) without an LDS staging.
     const uint32_t y = s * kDecRows + n;  // this lane's image row
     const bool row_ok = y >= ps.row0 && y < ps.row0 + ps.rows;
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-      const uint32_t sub = wave * 2 + j;
-      if (x0 + sub * kDecSub >= x1 || steps[j] == 0 || (dbg & 4)) continue;  // wave-uniform
+    if (x0 + sub * kDecSub < x1 && steps != 0 && !(dbg & 4)) {  // wave-uniform
       uint32_t px[3] = {0, 0, 0};  // channel c of columns 4g .. 4g+3, packed
       for (uint32_t c = 0; c < C; c++) {
-        const uint8_t *brow = sm.ap[c] + n * SM::AS + (k0[j] - p0) + 16 * g;  // B: strip row n, K group g
+        const uint8_t *brow = sm.ap[c] + n * SM::AS + (k0 - p0) + 16 * g;  // B: strip row n, K group g
         i32x4 alo = *(const i32x4 *)(sm.corr + sub * kDecSub + 4 * g), amd = {0, 0, 0, 0}, ahi = {0, 0, 0, 0};
         {
           const i32x4 b = *(const i32x4 *)brow;
-          alo = __builtin_amdgcn_mfma_i32_16x16x64_i8(wlo[j][0], b, alo, 0, 0, 0);
-          amd = __builtin_amdgcn_mfma_i32_16x16x64_i8(wmid[j][0], b, amd, 0, 0, 0);
-          ahi = __builtin_amdgcn_mfma_i32_16x16x64_i8(whi[j][0], b, ahi, 0, 0, 0);
+          alo = __builtin_amdgcn_mfma_i32_16x16x64_i8(wlo[0], b, alo, 0, 0, 0);
+          amd = __builtin_amdgcn_mfma_i32_16x16x64_i8(wmid[0], b, amd, 0, 0, 0);
+          ahi = __builtin_amdgcn_mfma_i32_16x16x64_i8(whi[0], b, ahi, 0, 0, 0);
         }
-        if (KS > 1 && steps[j] > 1) {
+        if (KS > 1 && steps > 1) {
           const i32x4 b = *(const i32x4 *)(brow + 64);
-          alo = __builtin_amdgcn_mfma_i32_16x16x64_i8(wlo[j][KS - 1], b, alo, 0, 0, 0);
-          amd = __builtin_amdgcn_mfma_i32_16x16x64_i8(wmid[j][KS - 1], b, amd, 0, 0, 0);
-          ahi = __builtin_amdgcn_mfma_i32_16x16x64_i8(whi[j][KS - 1], b, ahi, 0, 0, 0);
+          alo = __builtin_amdgcn_mfma_i32_16x16x64_i8(wlo[KS - 1], b, alo, 0, 0, 0);
+          amd = __builtin_amdgcn_mfma_i32_16x16x64_i8(wmid[KS - 1], b, amd, 0, 0, 0);
+          ahi = __builtin_amdgcn_mfma_i32_16x16x64_i8(whi[KS - 1], b, ahi, 0, 0, 0);
         }
         uint32_t o[4];
 #pragma unroll
@@ -559,9 +578,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         px[1] = c == 1 ? w4 : px[1];
         px[2] = c == 2 ? w4 : px[2];
       }
-      if (!row_ok || (dbg & 8)) continue;
       const uint32_t xs = x0 + sub * kDecSub + 4 * g;  // first of the lane's 4 columns
-      if (xs >= x1) continue;
+      if (row_ok && !(dbg & 8) && xs < x1) {
       DG_GLOBAL uint8_t *d = gp<uint8_t>(ps.dst) + (size_t)(y - ps.row0) * ps.dst_stride + (size_t)xs * C;
       if (C == 1) {
         if (xs + 4 <= x1 && (((uintptr_t)d) & 3) == 0) {
@@ -569,8 +587,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         } else {
           for (uint32_t k = 0; k < 4 && xs + k < x1; k++) d[k] = (uint8_t)(px[0] >> (8 * k));
         }
-        continue;
-      }
+      } else {
       // [R0 G0 B0 R1] [G1 B1 R2 G2] [B2 R3 G3 B3]
       const uint32_t rg = __builtin_amdgcn_perm(px[1], px[0], 0x05010400u);   // R0 G0 R1 G1
       const uint32_t rg2 = __builtin_amdgcn_perm(px[1], px[0], 0x07030602u);  // R2 G2 R3 G3
@@ -587,8 +604,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         const uint32_t w[3] = {d0, d1, d2};
         for (uint32_t k = 0; k < 12 && xs + k / 3 < x1; k++) d[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
       }
+      }
+      }
     }
-    __syncthreads();  // the next strip's IDCT scratch aliases the operand rows
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's staging DMA for the next strip landed
+    __syncthreads();  // ... every wave's; and the next strip's IDCT scratch aliases the operand rows
     // (the next strip's IDCT writes yp / cp / the scratch aliasing ap, all
     // read before the barriers above; ob is next written after two barriers)
     cur = nxt;
@@ -598,9 +618,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 void launch_band_dec(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2],
                      const QuantTable *qpool, uint32_t strips_per_wg) {
   if (ncls[0])
-    hipLaunchKernelGGL((k_band_dec<kDecSeg0, 1>), dim3(ncls[0]), dim3(256), 0, st, imgs, list, qpool, strips_per_wg);
+    hipLaunchKernelGGL((k_band_dec<kDecSeg0, 1>), dim3(ncls[0]), dim3(kDecThreads), 0, st, imgs, list, qpool, strips_per_wg);
   if (ncls[1])
-    hipLaunchKernelGGL((k_band_dec<kDecSeg1, 2>), dim3(ncls[1]), dim3(256), 0, st, imgs, list + ncls[0], qpool,
+    hipLaunchKernelGGL((k_band_dec<kDecSeg1, 2>), dim3(ncls[1]), dim3(kDecThreads), 0, st, imgs, list + ncls[0], qpool,
                        strips_per_wg);
 }
 
