@@ -265,7 +265,8 @@ struct ImageDesc {
   uint32_t scan_len;        // raw bytes of entropy-coded data (EOI excluded)
   uint32_t nsub;            // subsequences (sized from the raw length)
   uint32_t sub_base;        // first SubState index
-  uint32_t sub_bits;        // bits per subsequence
+  uint32_t sub_bits;        // bits per subsequence (per image: option "sub_density")
+  uint32_t ckpt_base;       // first checkpoint record of this image (nsub * num_ckpt(sub_bits) of them)
   uint64_t ds;              // destuffed stream, word-interleaved (ds_word_index), >= 64 zero bytes past its end
   uint64_t mk;              // RST marker positions in ds (bits), ascending
   uint64_t chunk;           // destuff per-chunk records: uint32 {cnt, mkc, off, mkoff}

@@ -237,6 +237,17 @@ static uint32_t band_dec_mode(const ImageDesc &d, const ResizePass &ps) {
   return 0;
 }
 
+// k_resize_hm takes a band H pass when every 16-column subtile's window fits
+// one or two 64-wide K steps and the 16-aligned segment fits kHSegPx: returns
+// the K steps (0: the VALU band kernel runs it).
+static uint32_t h_mfma_steps(const ResizePass &ps) {
+  if (ps.kind != 1 || (ps.mode & (kHDirect | kHVFused | kHDecode)) || ps.C < 1 || ps.C > 4) return 0;
+  if (h_pass_span(ps) + 8.0 > (double)kHSegPx) return 0;
+  const double scale = (ps.in1 - ps.in0) / (double)ps.out_size;
+  const double window = 15.0 + std::ceil(15.0 * scale) + (double)ps.ksize + 2.0;
+  return window <= 64.0 ? 1u : (window <= 128.0 ? 2u : 0u);
+}
+
 dg_status Context::set_option(const std::string &k, int64_t v) {
   if (k == "sub_bits") {
     if (v != 0 && (v < 64 || v > 65536 || (v & (v - 1)))) return DG_ERR_INVALID;  // power of two
@@ -357,6 +368,15 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
   }
   if (k == "png_chunked") {  // 0: every PNG inflates serially (test switch)
     chunked_off_ = v == 0;
+    return DG_OK;
+  }
+  if (k == "sub_density") {  // bits-per-block threshold for shorter subsequences (0 = off)
+    if (v < 0 || v > 4096) return DG_ERR_INVALID;
+    sub_density_ = (double)v;
+    return DG_OK;
+  }
+  if (k == "h_mfma") {  // 0: band H passes with the VALU convolution (k_resize_hb, A/B)
+    h_mfma_ = v != 0;
     return DG_OK;
   }
   if (k == "band_dec") {  // 0: IDCT to planes + band H kernel (the split path, A/B)
@@ -777,6 +797,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   Layout IN;       // input arena (host path)
   std::vector<size_t> in_off(n, 0);
   size_t out_total = 0;
+  uint64_t ckpt_total = 0;  // checkpoint records of the batch (per-image sub_bits)
   b.out_dev_off.assign(n, 0);
   uint32_t sub_base = 0;
   b.descs.reserve(n);
@@ -934,7 +955,20 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     } else {
     // entropy data
     d.scan_len = (uint32_t)(h.scan_end - h.scan_off);
+    // Per-image subsequence size (option "sub_density" T > 0): a lane's
+    // decode time follows its symbols and blocks, not its bits, so images
+    // with few coded bits per block (flat, low quality: short EOB-heavy
+    // codes, ~2x the symbols per bit) take shorter ranges -- half below T
+    // bits per block, a quarter below T / 2 -- and their workgroups stop
+    // forming the entropy kernels' tail.
     d.sub_bits = sub_bits;
+    if (sub_density_ > 0 && sub_bits_ == 0) {
+      const double bpb = (double)d.scan_len * 8.0 / (double)std::max<uint32_t>(1, d.total_blocks);
+      if (bpb < sub_density_ * 0.5 && sub_bits >= 2048)
+        d.sub_bits = sub_bits / 4;
+      else if (bpb < sub_density_ && sub_bits >= 1024)
+        d.sub_bits = sub_bits / 2;
+    }
     // completed blocks go straight to plane pixels inside k_huff_write (not
     // with decode-once staging, whose k_huff_scatter writes coefficients)
     d.idct_fused = (idct_fused_ && !entropy_once_) ? 1u : 0u;
@@ -943,17 +977,19 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     // self-synchronisation distance, which is longest for 6-block MCUs
     // (4:2:0; p99.9 ~7 kbit on the bench corpus, tools/sync_stats.cpp)
     d.lead_bits = lead_bits_ >= 0 ? (uint32_t)lead_bits_ : (bpm >= 4 ? 6144u : 2048u);
-    d.nsub = std::max<uint32_t>(1, (uint32_t)(((uint64_t)d.scan_len * 8 + sub_bits - 1) / sub_bits));
+    d.nsub = std::max<uint32_t>(1, (uint32_t)(((uint64_t)d.scan_len * 8 + d.sub_bits - 1) / d.sub_bits));
     d.sub_base = sub_base;
     sub_base += d.nsub;
+    d.ckpt_base = (uint32_t)ckpt_total;
+    ckpt_total += (uint64_t)d.nsub * num_ckpt(d.sub_bits);
     d.nchunk = std::max<uint32_t>(1, (d.scan_len + kDestuffChunk - 1) / kDestuffChunk);
     uint32_t mcus = h.ncomp == 1 ? d.total_blocks : d.mcux * d.mcuy;
     d.mk_cap = (d.restart ? mcus / d.restart + 2 : 0) + 64;
     d.ds_lsw = 0;
-    while ((32u << d.ds_lsw) < sub_bits) d.ds_lsw++;
+    while ((32u << d.ds_lsw) < d.sub_bits) d.ds_lsw++;
     o.ds = L.take((size_t)ds_words_alloc(d.nsub, d.ds_lsw) * 4, 256);
-    if (entropy_once_ && sub_bits <= 8192) {  // decode-once staging (dg_entropy.h StageCtx)
-      d.stage_cap = (sub_bits / 2 + sub_bits / 8 + 64 + 3) / 4;
+    if (entropy_once_ && d.sub_bits <= 8192) {  // decode-once staging (dg_entropy.h StageCtx)
+      d.stage_cap = (d.sub_bits / 2 + d.sub_bits / 8 + 64 + 3) / 4;
       o.stage = L.take((size_t)((d.nsub + 63) / 64) * d.stage_cap * 64 * 16, 256);
       b.stage_on = true;
     }
@@ -1210,7 +1246,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     if (dd.fmt == kFmtJpeg) b.pf_n += dd.prog;
   b.pf_off = b.pf_n ? L.take((size_t)(b.pf_n + 1) * 4) : 0;
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
-  const size_t ckpt_off = L.take(b.total_subs * std::max<uint32_t>(1, num_ckpt(sub_bits)) * sizeof(Ckpt));
+  const size_t ckpt_off = L.take(std::max<uint64_t>(1, ckpt_total) * sizeof(Ckpt));
   // fused IDCT leftovers: at most one carried-in block per subsequence, plus
   // the blocks of flushes with < 8 active lanes -- the tail of a wave, or
   // every block of an image with fewer subsequences than that.  Sized for
@@ -1358,6 +1394,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   std::vector<WgItem> hb[2][2][4];  // band H items per (stage, fused fill, weight-count class)
   std::vector<WgItem> hvl[2];       // k_resize_hv items per H weight class
   std::vector<WgItem> decl[2];      // k_band_dec items per segment class
+  std::vector<WgItem> hm[2][2][2];  // k_resize_hm items per (stage, fused fill, K steps)
   for (int di = 0; di < (int)b.descs.size(); di++) {
     const ImageDesc &d = b.descs[di];
     const uint32_t I = (uint32_t)di;
@@ -1424,7 +1461,11 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         const uint32_t kk = ps.ksize + 1;
         const int cls = kk <= 8 ? 0 : kk <= 16 ? 1 : kk <= 32 ? 2 : 3;
         const int fused = (ps.mode & kHFused) ? 1 : 0;
-        for (uint32_t it = 0; it < cnt; it++) hb[s / 2][fused][cls].push_back({I, it});
+        const uint32_t ks = h_mfma_ ? h_mfma_steps(ps) : 0u;
+        if (ks)
+          for (uint32_t it = 0; it < cnt; it++) hm[s / 2][fused][ks - 1].push_back({I, it});
+        else
+          for (uint32_t it = 0; it < cnt; it++) hb[s / 2][fused][cls].push_back({I, it});
       } else {
         uint32_t cnt = (ps.width * ps.C + 15) / 16 * ps.rows;
         for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_RH0 + s].push_back({I, it});
@@ -1531,6 +1572,13 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     b.hvclass[c] = (uint32_t)hvl[c].size();
     b.lists[L_RHV].insert(b.lists[L_RHV].end(), hvl[c].begin(), hvl[c].end());
   }
+  for (int h = 0; h < 2; h++)
+    for (int f = 1; f >= 0; f--)  // launch order (launch_resize_hm): fused KS 1, KS 2, byte-fill KS 1, KS 2
+      for (int k = 0; k < 2; k++) {
+        b.hmclass[h][f][k] = (uint32_t)hm[h][f][k].size();
+        auto &l = b.lists[h ? L_RM2 : L_RM0];
+        l.insert(l.end(), hm[h][f][k].begin(), hm[h][f][k].end());
+      }
   for (int h = 0; h < 2; h++)
     for (int f = 1; f >= 0; f--)  // launch order: fused classes, then byte-fill classes
       for (int c = 0; c < 4; c++) {
@@ -1741,6 +1789,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_coef, 0));
   launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
   launch_band_dec(sl.st, dd, lst(L_DEC), b.decclass, qp, dec_strips_ | (dec_dbg_ << 16));
+  launch_resize_hm(sl.st, dd, lst(L_RM0), b.hmclass[0], 0);
   launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0);
   launch_resize_hv(sl.st, dd, lst(L_RHV), b.hvclass);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | ((debug_flags_ & 0xFF) << 8));
@@ -1748,6 +1797,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_resize_v(sl.st, dd, lst(L_RV1), cnt(L_RV1), 1);
   launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
+  launch_resize_hm(sl.st, dd, lst(L_RM2), b.hmclass[1], 2);
   launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2);
   launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;

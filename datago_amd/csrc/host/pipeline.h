@@ -92,6 +92,7 @@ struct Batch {
   uint32_t hclass[2][2][4] = {{{0}}};  // [stage/2][fused][class]
   uint32_t hvclass[2] = {0, 0};        // L_RHV items of H weight class <= 8, <= 16 (k_resize_hv)
   uint32_t decclass[2] = {0, 0};       // L_DEC items of the 320- / 640-pixel segment class (k_band_dec)
+  uint32_t hmclass[2][2][2] = {{{0}}};  // L_RM0 / L_RM2 items [stage/2][fused][K steps - 1] (k_resize_hm)
   size_t desc_off = 0, flags_off = 0;
   size_t meta_bytes = 0;
   size_t total_subs = 0;
@@ -141,6 +142,7 @@ enum ListId {
   L_UNF,                                                    // PNG unfilter bands (ticket order)
   L_RHV,                                                    // fused first H + V pass (k_resize_hv)
   L_DEC,                                                    // IDCT + colour + first H pass (k_band_dec)
+  L_RM0, L_RM2,                                             // band H passes on the matrix cores (k_resize_hm)
   L_COUNT
 };
 static_assert((int)L_COUNT <= 40, "Batch::lists");
@@ -244,6 +246,8 @@ class Context {
   int copy_threads_ = 8;                // option "copy_threads": host threads for a host-out batch's output copies
   bool hv_fused_ = false;               // option "hv_fused": first H + V pass fused (k_resize_hv) when it fits
   bool band_dec_ = false;               // option "band_dec": IDCT + colour + first H pass in k_band_dec
+  bool h_mfma_ = false;                 // option "h_mfma": band H passes on the matrix cores (k_resize_hm; measured slower: off)
+  double sub_density_ = 0;              // option "sub_density": bits per block below which subsequences shrink
   uint32_t dec_dbg_ = 0;                // option "dec_dbg": k_band_dec phase switches (timing experiments only)
   uint32_t dec_strips_ = kDecStripsDefault;  // option "dec_strips"
   bool idct_fused_ = false;             // option "idct_fused" (measured 7x slower k_huff_write: off)

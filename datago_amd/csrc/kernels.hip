@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   // previous workgroup and is not staged
   const bool stage = STAGE && im.stage != 0;
   DG_GLOBAL Ckpt *ck =
-      (!stage && t > 0 && active && nck && im.ckpt) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck
+      (!stage && t > 0 && active && nck && im.ckpt) ? (DG_GLOBAL Ckpt *)ckpt + im.ckpt_base + (size_t)s * nck
                                                      : nullptr;
   StageCtx sc;
   sc.on = stage && t > 0 && active;
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ 
   const uint32_t nck = num_ckpt(im.sub_bits);
   const bool stage = STAGE && im.stage != 0;
   DG_GLOBAL Ckpt *ck =
-      (!stage && active && nck && im.ckpt) ? (DG_GLOBAL Ckpt *)ckpt + (size_t)(im.sub_base + s) * nck : nullptr;
+      (!stage && active && nck && im.ckpt) ? (DG_GLOBAL Ckpt *)ckpt + im.ckpt_base + (size_t)s * nck : nullptr;
   StageCtx sc;
   sc.on = stage && active;
   sc.base = sc.on ? stage_range(im.stage, im.stage_cap, s) : nullptr;
@@ -1467,6 +1467,229 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   hband<KMAX, FUSED>(im, im.pass[stage], it.item0, seg, ob, ext);
 }
 
+// ---- band H pass on the matrix cores (k_resize_hm)
+//
+// Same work items as k_resize_hb (kHBandCols output columns x 8 * ps.bands
+// rows), in bands of 16 rows.  The fill stages the band's source segment in
+// LDS as planar signed bytes (p - 128), one plane per channel; the
+// convolution out[row][x] = sum_k src[row][k] * w_x[k] of a 16-column
+// subtile is the product of a banded K x 16 weight matrix with the 16 x K
+// band, v_mfma_i32_16x16x64_i8 over the subtile's window (KS steps of 64).
+// The i16 weight splits into three i8 digits, w = 2^14 a + 2^7 b + c (a in
+// [-2, 1], b and c in [0, 127]: fast_image_resize's precision puts the
+// largest weight of a pass in [2^14, 2^15)), the pixel offset comes back as
+// 128 * sum(w) in the accumulator's initial value: every product and sum is
+// an exact i32, so the bytes equal the VALU kernel's (and the oracle's) bit
+// for bit.  A = the weight digits (output column n = lane & 15, K group
+// g = lane >> 4), B = the pixels (band row n, K group g), so lane (n, g)
+// receives output columns 4g..4g+3 of band row n -- 4 adjacent pixels,
+// stored straight to HBM (C x 4 bytes) without an LDS staging pass.
+typedef int i32x4m __attribute__((ext_vector_type(4)));
+constexpr uint32_t kHmRows = 16;                      // band rows = MFMA M
+// planar rows: reads reach 64 * KS past a subtile's 16-aligned window start;
+// an odd multiple of 16 bytes keeps the 16 rows of a lane group on distinct banks
+constexpr uint32_t hm_row_stride(uint32_t need) {
+  uint32_t a = (need + 15) / 16 * 16;
+  while (((a / 16) & 1u) == 0) a += 16;
+  return a;
+}
+
+template <int KS, bool FUSED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_resize_hm(
+    const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list, int stage) {
+  constexpr uint32_t AS = hm_row_stride(kHSegPx + 64 * KS);
+  constexpr uint32_t NP = FUSED ? 3 : 4;  // planes (channels)
+  __shared__ __attribute__((aligned(16))) uint8_t ap[NP * kHmRows * AS];
+  __shared__ __attribute__((aligned(16))) int32_t corr[kHBandCols];
+  __shared__ uint32_t ext[2];
+  const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
+  const ImageDesc &im = imgs[it.image];
+  const ResizePass &ps = im.pass[stage];
+  const uint32_t tiles = (ps.width + kHBandCols - 1) / kHBandCols;
+  const uint32_t group = it.item0 / tiles, tile = it.item0 - group * tiles;
+  const uint32_t x0 = tile * kHBandCols;
+  const uint32_t x1 = x0 + kHBandCols < ps.width ? x0 + kHBandCols : ps.width;
+  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds) + 2 * ps.out0;
+  const uint32_t C = FUSED ? 3u : ps.C, ksize = ps.ksize;
+  const DG_GLOBAL int16_t *coef = gp<const int16_t>(ps.coef) + (size_t)ps.out0 * ksize;
+  const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  if (t == 0) {
+    ext[0] = 0xFFFFFFFFu;
+    ext[1] = 0;
+  }
+  __syncthreads();
+  if (t < kHBandCols && x0 + t < x1) {
+    const uint32_t st = (uint32_t)bounds[2 * (x0 + t)], n = (uint32_t)bounds[2 * (x0 + t) + 1];
+    atomicMin(&ext[0], st);
+    atomicMax(&ext[1], st + n);
+  }
+  __syncthreads();
+  const uint32_t p0 = ext[0] & ~15u;  // 16-aligned: the B operand reads are 16-byte LDS reads
+  const uint32_t pe = ext[1] < ps.in_size ? ext[1] : ps.in_size;
+  const int32_t prec = ps.precision;
+
+  // weights of this wave's two subtiles (2 * wave, 2 * wave + 1), set up once
+  const uint32_t n = lane & 15, g = lane >> 4;
+  i32x4m wlo[2][KS], wmd[2][KS], whi[2][KS];
+  uint32_t k0[2], steps[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const uint32_t sub = wave * 2 + j;
+    const uint32_t xs = x0 + sub * 16 + n;
+    const bool valid = xs < x1;
+    uint32_t st = 0, cnt = 0;
+    if (valid) {
+      st = (uint32_t)bounds[2 * xs];
+      cnt = (uint32_t)bounds[2 * xs + 1];
+    }
+    uint32_t mn = valid ? st : 0xFFFFFFFFu, mx = valid ? st + cnt : 0u;
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) {
+      const uint32_t a = (uint32_t)__shfl_xor((int)mn, m, 64), b = (uint32_t)__shfl_xor((int)mx, m, 64);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+    }
+    k0[j] = mn == 0xFFFFFFFFu ? p0 : (mn & ~15u);
+    steps[j] = mx > k0[j] ? (mx - k0[j] + 63) / 64 : 0;
+    if (steps[j] > (uint32_t)KS) steps[j] = KS;  // the host sends windows <= 64 * KS (h_mfma_class)
+    const DG_GLOBAL int16_t *kp = coef + (size_t)(valid ? xs : x0) * ksize;
+    int32_t sum = 0;  // of column n's weights: this lane's K groups, then over the four groups
+#pragma unroll
+    for (int s = 0; s < KS; s++) {
+      uint32_t lo[4] = {0, 0, 0, 0}, md[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
+      const int32_t kb = (int32_t)(k0[j] + 64 * s + 16 * g) - (int32_t)st;
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int32_t i = kb + e;
+        const int32_t w = (valid && i >= 0 && i < (int32_t)cnt) ? (int32_t)kp[i] : 0;
+        sum += w;
+        lo[e >> 2] |= (uint32_t)(w & 127) << (8 * (e & 3));
+        md[e >> 2] |= (uint32_t)((w >> 7) & 127) << (8 * (e & 3));
+        hi[e >> 2] |= (uint32_t)((w >> 14) & 0xFF) << (8 * (e & 3));
+      }
+      wlo[j][s] = i32x4m{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]};
+      wmd[j][s] = i32x4m{(int)md[0], (int)md[1], (int)md[2], (int)md[3]};
+      whi[j][s] = i32x4m{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    if (g == 0) corr[sub * 16 + n] = sum * 128 + (1 << (prec - 1));
+  }
+  // fill jobs (an octet of one row, or a 4-pixel unit) numbered across the band's rows
+  const uint32_t njob_row = FUSED ? (pe - p0 + 7) >> 3 : (pe - p0 + 3) >> 2;
+  const uint32_t inv_row = ((1u << 20) - 1u + njob_row) / (njob_row ? njob_row : 1u);
+  const uint32_t ybeg = group * kHBandRows * ps.bands, yend0 = ybeg + kHBandRows * ps.bands;
+  const uint32_t yend = yend0 < ps.rows ? yend0 : ps.rows;
+  __syncthreads();
+  for (uint32_t y0 = ybeg; y0 < yend; y0 += kHmRows) {
+    const uint32_t nrows = yend - y0 < kHmRows ? yend - y0 : kHmRows;
+    // phase 1: fill (rows past nrows keep stale bytes: their outputs are not stored)
+    const uint32_t njob = nrows * njob_row;
+    for (uint32_t j = t; j < njob; j += 256) {
+      const uint32_t r = __umul24(j, inv_row) >> 20, q = j - r * njob_row;
+      if (FUSED) {
+        int32_t Y[8], Cb[8], Cr[8];
+        upsample_ycc8(im, p0 + 8 * q, ps.row0 + y0 + r, Y, Cb, Cr);
+        uint32_t R[2] = {0, 0}, G[2] = {0, 0}, B[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          uint8_t rr, gg, bb;
+          ycc_px(im, Y[k], Cb[k], Cr[k], rr, gg, bb);
+          R[k >> 2] |= (uint32_t)rr << (8 * (k & 3));
+          G[k >> 2] |= (uint32_t)gg << (8 * (k & 3));
+          B[k >> 2] |= (uint32_t)bb << (8 * (k & 3));
+        }
+        uint8_t *d = ap + r * AS + 8 * q;
+        *(u32x2 *)d = u32x2{R[0] ^ 0x80808080u, R[1] ^ 0x80808080u};
+        *(u32x2 *)(d + kHmRows * AS) = u32x2{G[0] ^ 0x80808080u, G[1] ^ 0x80808080u};
+        *(u32x2 *)(d + 2 * kHmRows * AS) = u32x2{B[0] ^ 0x80808080u, B[1] ^ 0x80808080u};
+      } else {
+        uint32_t v[4];
+        const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0 + r) * ps.src_stride;
+        hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * q, v);
+        uint8_t *d = ap + r * AS + 4 * q;
+        for (uint32_t c = 0; c < C; c++) {
+          const uint32_t sh = 8 * c;
+          const uint32_t w = ((v[0] >> sh) & 0xFFu) | (((v[1] >> sh) & 0xFFu) << 8) | (((v[2] >> sh) & 0xFFu) << 16) |
+                             (((v[3] >> sh) & 0xFFu) << 24);
+          *(uint32_t *)(d + c * kHmRows * AS) = w ^ 0x80808080u;
+        }
+      }
+    }
+    __syncthreads();
+    // phase 2: convolve on the matrix cores, store 4 pixels per lane
+    const uint32_t yr = y0 + n;  // this lane's output row
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t sub = wave * 2 + j;
+      if (x0 + sub * 16 >= x1 || steps[j] == 0) continue;  // wave-uniform
+      uint32_t px[4] = {0, 0, 0, 0};  // channel c of columns 4g .. 4g+3
+      for (uint32_t c = 0; c < C; c++) {
+        const uint8_t *brow = ap + c * kHmRows * AS + n * AS + (k0[j] - p0) + 16 * g;
+        i32x4m alo = *(const i32x4m *)(corr + sub * 16 + 4 * g), amd = {0, 0, 0, 0}, ahi = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+          if (s > 0 && steps[j] <= (uint32_t)s) break;
+          const i32x4m b = *(const i32x4m *)(brow + 64 * s);
+          alo = __builtin_amdgcn_mfma_i32_16x16x64_i8(wlo[j][s], b, alo, 0, 0, 0);
+          amd = __builtin_amdgcn_mfma_i32_16x16x64_i8(wmd[j][s], b, amd, 0, 0, 0);
+          ahi = __builtin_amdgcn_mfma_i32_16x16x64_i8(whi[j][s], b, ahi, 0, 0, 0);
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int rr = 0; rr < 4; rr++) {
+          const int32_t v = ((ahi[rr] << 14) + (amd[rr] << 7) + alo[rr]) >> prec;
+          o[rr] = (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+        }
+        const uint32_t w4 = pack4(o[0], o[1], o[2], o[3]);
+        px[0] = c == 0 ? w4 : px[0];
+        px[1] = c == 1 ? w4 : px[1];
+        px[2] = c == 2 ? w4 : px[2];
+        px[3] = c == 3 ? w4 : px[3];
+      }
+      const uint32_t xs = x0 + sub * 16 + 4 * g;  // the lane's first column
+      if (n >= nrows || xs >= x1) continue;
+      DG_GLOBAL uint8_t *d = gp<uint8_t>(ps.dst) + (size_t)yr * ps.dst_stride + (size_t)xs * C;
+      // interleave the channels of the 4 pixels: C x 4 bytes
+      uint32_t w[4] = {0, 0, 0, 0};
+      if (C == 1) {
+        w[0] = px[0];
+      } else if (C == 2) {
+        w[0] = __builtin_amdgcn_perm(px[1], px[0], 0x05010400u);  // L0 A0 L1 A1
+        w[1] = __builtin_amdgcn_perm(px[1], px[0], 0x07030602u);  // L2 A2 L3 A3
+      } else if (C == 3) {
+        const uint32_t rg = __builtin_amdgcn_perm(px[1], px[0], 0x05010400u);   // R0 G0 R1 G1
+        const uint32_t rg2 = __builtin_amdgcn_perm(px[1], px[0], 0x07030602u);  // R2 G2 R3 G3
+        w[0] = __builtin_amdgcn_perm(px[2], rg, 0x02040100u);                   // R0 G0 B0 R1
+        const uint32_t gb = __builtin_amdgcn_perm(px[2], rg, 0x0c0c0503u);      // G1 B1 0 0
+        w[1] = __builtin_amdgcn_perm(rg2, gb, 0x05040100u);                     // G1 B1 R2 G2
+        w[2] = __builtin_amdgcn_perm(rg2, px[2], 0x03070602u);                  // B2 R3 G3 B3
+      } else {
+        const uint32_t rg = __builtin_amdgcn_perm(px[1], px[0], 0x05010400u);   // R0 G0 R1 G1
+        const uint32_t rg2 = __builtin_amdgcn_perm(px[1], px[0], 0x07030602u);  // R2 G2 R3 G3
+        const uint32_t ba = __builtin_amdgcn_perm(px[3], px[2], 0x05010400u);   // B0 A0 B1 A1
+        const uint32_t ba2 = __builtin_amdgcn_perm(px[3], px[2], 0x07030602u);  // B2 A2 B3 A3
+        w[0] = __builtin_amdgcn_perm(ba, rg, 0x05040100u);                      // R0 G0 B0 A0
+        w[1] = __builtin_amdgcn_perm(ba, rg, 0x07060302u);                      // R1 G1 B1 A1
+        w[2] = __builtin_amdgcn_perm(ba2, rg2, 0x05040100u);
+        w[3] = __builtin_amdgcn_perm(ba2, rg2, 0x07060302u);
+      }
+      if (xs + 4 <= x1 && (((uintptr_t)d) & 3) == 0) {
+        DG_GLOBAL uint32_t *d4 = (DG_GLOBAL uint32_t *)d;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+          if (k < C) d4[k] = w[k];
+      } else {
+        const uint32_t nb = (x1 - xs < 4 ? x1 - xs : 4) * C;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++)
+          if (k < nb) d[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+      }
+    }
+    __syncthreads();  // the next band's fill overwrites the planes
+  }
+}
+
 // Fused first H + V pass of a colour JPEG (ImageDesc pass[0] mode kHVFused):
 // one workgroup = kHBandCols columns x kHVRows V output rows.  It computes
 // the H rows those outputs' windows span, band by band exactly as
@@ -1844,6 +2067,16 @@ void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
                       int stage) {
   launch_hb_classes<true>(st, imgs, list, ncls[1], stage);
   launch_hb_classes<false>(st, imgs, list, ncls[0], stage);
+}
+void launch_resize_hm(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][2],
+                      int stage) {
+  DG_LAUNCH((k_resize_hm<1, true>), ncls[1][0], st, imgs, list, stage);
+  list += ncls[1][0];
+  DG_LAUNCH((k_resize_hm<2, true>), ncls[1][1], st, imgs, list, stage);
+  list += ncls[1][1];
+  DG_LAUNCH((k_resize_hm<1, false>), ncls[0][0], st, imgs, list, stage);
+  list += ncls[0][0];
+  DG_LAUNCH((k_resize_hm<2, false>), ncls[0][1], st, imgs, list, stage);
 }
 void launch_resize_hv(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2]) {
   DG_LAUNCH(k_resize_hv<8>, ncls[0], st, imgs, list);

@@ -232,8 +232,9 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "png_chunked" 0 = inflate every PNG with the serial kernel (test switch; default 1)
  *   "copy_threads" host threads copying a host-out batch's outputs to the caller's buffers (default 8)
  *   "hv_fused"     1 = fuse the first H and V passes of colour JPEGs where they fit (default 0; slower)
+ *   "h_mfma"       1 = band H passes on the matrix cores (k_resize_hm, i8 MFMA; default 0: measured slower); 0 = VALU kernel
  *   "band_dec"     1 = IDCT + upsampling + colour + the first H pass of a JPEG in one kernel (k_band_dec,
- *                 MFMA convolution; default 1); 0 = IDCT to planes + the band H kernel
+ *                 MFMA convolution; default 0: measured slower); 0 = IDCT to planes + the band H kernel
  *   "dec_strips"   k_band_dec: 16-row strips per workgroup (default 8)
  *   "reset_host_us" clears the host submit phase timers (stats "host_us_*")
  * Stats: "batches", "coalesced_batches", "coalesced_images", "resync_rounds", "fix_workgroups", "write_mismatch",
