@@ -38,7 +38,7 @@ EXPORTS = [
     "dg_poll", "dg_decode_one", "dg_submit_device", "dg_device_alloc", "dg_device_free",
     "dg_memcpy_h2d", "dg_memcpy_d2h", "dg_synchronize", "dg_last_batch_timings",
     "dg_ctx_set_option", "dg_ctx_get_stat", "dg_last_error", "dg_abi_version", "dg_sample_align",
-    "dg_wds_index", "dg_wds_key_hash",
+    "dg_wds_index", "dg_wds_key_hash", "dg_host_register", "dg_host_unregister",
 ]
 
 
@@ -113,6 +113,8 @@ def load() -> ctypes.CDLL:
     L.dg_memcpy_h2d.argtypes = [vp, vp, vp, sz]
     L.dg_memcpy_d2h.argtypes = [vp, vp, vp, sz]
     L.dg_synchronize.argtypes = [vp]
+    L.dg_host_register.argtypes = [vp, vp, sz]
+    L.dg_host_unregister.argtypes = [vp, vp]
     L.dg_last_batch_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), i32]
     L.dg_ctx_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
     L.dg_ctx_get_stat.argtypes = [vp, ctypes.c_char_p]
@@ -304,8 +306,9 @@ class Context:
             st, nb = self.output_size(d, forced[i] if forced else -1)
             outs.append(np.empty(max(nb, 1), np.uint8))
             caps.append(max(nb, 1))
-        bufs = [ctypes.create_string_buffer(d, len(d)) for d in datas]
-        srcs = _as_ptr_array([ctypes.addressof(b) for b in bufs])
+        # borrowed for the call (dg_submit copies them into pinned staging): no Python-side copy
+        bufs = [ctypes.c_char_p(d) for d in datas]
+        srcs = _as_ptr_array([ctypes.cast(b, ctypes.c_void_p).value or 0 for b in bufs])
         lens = (ctypes.c_size_t * max(1, n))(*[len(d) for d in datas])
         fb = (ctypes.c_int32 * max(1, n))(*(forced if forced else [-1] * n))
         optrs = _as_ptr_array([o.ctypes.data for o in outs])
@@ -327,13 +330,15 @@ class Context:
             res.append((DG_OK, outs[i][: m.nbytes].reshape(m.height, m.width, c), m))
         return res
 
-    def decode_one(self, data: bytes, forced_bucket: int = -1):
+    def decode_one(self, data: bytes, forced_bucket: int = -1, out: Optional[np.ndarray] = None):
         """dg_decode_one: one image; concurrent callers (threads) are coalesced
-        into shared GPU batches by the library."""
+        into shared GPU batches by the library.  `out`: a reused (ideally
+        host_register'ed) uint8 buffer of at least output_size bytes."""
         st, nb = self.output_size(data, forced_bucket)
         if st != DG_OK:
             return st, None, PayloadMeta()
-        out = np.empty(max(nb, 1), np.uint8)
+        if out is None or out.nbytes < nb:
+            out = np.empty(max(nb, 1), np.uint8)
         m = PayloadMeta()
         st = load().dg_decode_one(self._h, data, len(data), forced_bucket, out.ctypes.data, max(nb, 1),
                                   ctypes.byref(m))
@@ -417,3 +422,27 @@ class Context:
 
     def wait(self, ticket: int) -> None:
         _check(load().dg_wait(self._h, ticket))
+
+    def submit_host(self, datas: Sequence[bytes], outs: Sequence[np.ndarray], forced=None):
+        """Asynchronous host-in / host-out batch (dg_submit) into caller-owned
+        output arrays (reuse them: with dg_host_register'ed memory the outputs
+        arrive by DMA, without staging or page faults).  Returns (ticket,
+        metas, keepalive); call wait(ticket) before reading outs or metas."""
+        n = len(datas)
+        bufs = [ctypes.c_char_p(d) for d in datas]
+        srcs = _as_ptr_array([ctypes.cast(b, ctypes.c_void_p).value or 0 for b in bufs])
+        lens = (ctypes.c_size_t * max(1, n))(*[len(d) for d in datas])
+        fb = (ctypes.c_int32 * max(1, n))(*(forced if forced is not None else [-1] * n))
+        optrs = _as_ptr_array([o.ctypes.data for o in outs])
+        capa = (ctypes.c_uint64 * max(1, n))(*[o.nbytes for o in outs])
+        metas = (PayloadMeta * max(1, n))()
+        ticket = ctypes.c_uint64()
+        _check(load().dg_submit(self._h, n, srcs, lens, fb, optrs, capa, metas, ctypes.byref(ticket)))
+        return ticket.value, metas, (bufs, srcs, lens, fb, optrs, capa)
+
+    def host_register(self, arr: np.ndarray) -> None:
+        """dg_host_register: page-lock a reused output array (or arena)."""
+        _check(load().dg_host_register(self._h, arr.ctypes.data, arr.nbytes))
+
+    def host_unregister(self, arr: np.ndarray) -> None:
+        _check(load().dg_host_unregister(self._h, arr.ctypes.data))

@@ -237,6 +237,14 @@ dg_status dg_memcpy_d2h(dg_ctx *ctx, void *dst, const void *src, size_t bytes) {
   hipSetDevice(ctx->c.device());
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? DG_OK : DG_ERR_DEVICE;
 }
+dg_status dg_host_register(dg_ctx *ctx, void *ptr, size_t bytes) {
+  if (!ctx || !ptr || !bytes) return DG_ERR_INVALID;
+  return ctx->c.host_register(ptr, bytes);
+}
+dg_status dg_host_unregister(dg_ctx *ctx, void *ptr) {
+  if (!ctx || !ptr) return DG_ERR_INVALID;
+  return ctx->c.host_unregister(ptr);
+}
 dg_status dg_synchronize(dg_ctx *ctx) {
   if (!ctx) return DG_ERR_INVALID;
   hipSetDevice(ctx->c.device());

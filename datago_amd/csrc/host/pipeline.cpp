@@ -175,6 +175,46 @@ dg_status Context::init() {
   return DG_OK;
 }
 
+dg_status Context::host_register(void *ptr, size_t bytes) {
+  HIPCHK(hipSetDevice(device_));
+  if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) != hipSuccess) {
+    set_error("hipHostRegister failed");
+    return DG_ERR_DEVICE;
+  }
+  std::lock_guard<std::mutex> lk(reg_mu_);
+  registered_.push_back({(uintptr_t)ptr, bytes});
+  return DG_OK;
+}
+
+dg_status Context::host_unregister(void *ptr) {
+  {
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    for (size_t i = 0; i < registered_.size(); i++)
+      if (registered_[i].first == (uintptr_t)ptr) {
+        registered_.erase(registered_.begin() + (long)i);
+        break;
+      }
+  }
+  sync_all();  // no copy into the range may still be in flight
+  HIPCHK(hipSetDevice(device_));
+  return hipHostUnregister(ptr) == hipSuccess ? DG_OK : DG_ERR_INVALID;
+}
+
+bool Context::host_pinned(const void *ptr, size_t bytes) {
+  const uintptr_t a = (uintptr_t)ptr;
+  {
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    for (const auto &r : registered_)
+      if (a >= r.first && a + bytes <= r.first + r.second) return true;
+  }
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, ptr) != hipSuccess) {
+    (void)hipGetLastError();  // plain pageable memory: not an error
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
 dg_status Context::sync_all() {
   bool ok = true;
   for (hipStream_t q : {stream_, side_})
@@ -418,6 +458,7 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "sub_bits") return last_sub_bits_;
   if (k == "png_serial_fallbacks") return stat_png_serial_;
   if (k == "band_dec_images") return stat_band_dec_;
+  if (k == "direct_d2h") return stat_direct_d2h_;
   if (k == "png_chunks") return stat_png_chunks_;
   {  // host microseconds spent in dg_submit* since the last reset, per phase
     static const char *pn[6] = {"plan", "pools", "layout", "lists", "upload", "launch"};
@@ -799,6 +840,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   size_t out_total = 0;
   uint64_t ckpt_total = 0;  // checkpoint records of the batch (per-image sub_bits)
   b.out_dev_off.assign(n, 0);
+  b.out_direct.assign(n, 0);
   uint32_t sub_base = 0;
   b.descs.reserve(n);
   // first pass: sizes only (pointers are patched after allocation)
@@ -1644,6 +1686,11 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   if (host_io) {
     b.host_outs.assign(outs, outs + n);
     b.host_caps.assign(caps, caps + n);
+    // outputs into page-locked caller memory go there by DMA, not via the staging buffer
+    for (int i = 0; i < n; i++)
+      if (b.desc_of[i] >= 0 && !b.plans[i].encode && b.plans[i].out_bytes && outs[i] &&
+          host_pinned(outs[i], b.plans[i].out_bytes))
+        b.out_direct[i] = 1;
   }
   sl.batch = std::move(bp);
   phase(4);
@@ -1825,7 +1872,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   size_t total = align_up(back, 256);
   if (b.host_io)
     for (int i = 0; i < b.n; i++)
-      if (b.desc_of[i] >= 0 && !b.plans[i].encode) total += align_up(b.plans[i].out_bytes, 16);
+      if (b.desc_of[i] >= 0 && !b.plans[i].encode && !b.out_direct[i]) total += align_up(b.plans[i].out_bytes, 16);
   dg_status st = ensure_pinned(sl.out, total + 256, sl.st);
   if (st) return st;
   HIPCHK(hipMemcpyAsync(sl.out.p, M, back, hipMemcpyDeviceToHost, sl.st));
@@ -1833,6 +1880,11 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     size_t off = align_up(back, 256);
     for (int i = 0; i < b.n; i++) {
       if (b.desc_of[i] < 0 || b.plans[i].encode) continue;  // encoded: exact size copied in finish()
+      if (b.out_direct[i]) {  // DMA straight into the caller's page-locked buffer
+        HIPCHK(hipMemcpyAsync(b.host_outs[i], (char *)sl.scratch.p + b.out_dev_off[i], b.plans[i].out_bytes,
+                              hipMemcpyDeviceToHost, sl.st));
+        continue;
+      }
       HIPCHK(hipMemcpyAsync((char *)sl.out.p + off, (char *)sl.scratch.p + b.out_dev_off[i], b.plans[i].out_bytes,
                             hipMemcpyDeviceToHost, sl.st));
       off += align_up(b.plans[i].out_bytes, 16);
@@ -1957,7 +2009,9 @@ dg_status Context::finish(Slot &sl) {
       if (b.host_io && !status && nb) copies.push_back({b.host_outs[i], (char *)sl.out.p + b.enc_host_off[i], nb});
       continue;
     }
-    if (b.host_io) {
+    if (b.host_io && b.out_direct[i]) {
+      stat_direct_d2h_++;
+    } else if (b.host_io) {
       if (!status) copies.push_back({b.host_outs[i], (char *)sl.out.p + off, b.plans[i].out_bytes});
       off += align_up(b.plans[i].out_bytes, 16);
     }

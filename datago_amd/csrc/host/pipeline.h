@@ -100,6 +100,7 @@ struct Batch {
   std::vector<uint8_t *> host_outs;
   std::vector<uint64_t> host_caps;
   std::vector<size_t> out_dev_off;    // offset of each output in the scratch arena (host path)
+  std::vector<uint8_t> out_direct;    // host path: output DMA'd straight into the caller's pinned buffer
   dg_payload_meta *metas = nullptr;
   bool done = false;
   int resync_rounds = 0;
@@ -168,6 +169,9 @@ class Context {
   int device() const { return device_; }
   hipStream_t stream() const { return stream_; }
   dg_status sync_all();  // every stream of the context
+  dg_status host_register(void *ptr, size_t bytes);
+  dg_status host_unregister(void *ptr);
+  bool host_pinned(const void *ptr, size_t bytes);  // inside a registered range, or runtime-pinned memory
   dg_status set_option(const std::string &k, int64_t v);
   int64_t get_stat(const std::string &k);
   int timings(const char **names, float *ms, int cap);
@@ -264,6 +268,9 @@ class Context {
   int64_t stat_batches_ = 0, stat_resync_ = 0, stat_fix_ = 0, stat_mismatch_ = 0, stat_iters_ = 0;
   int64_t stat_unsettled_ = 0, stat_pool_flush_ = 0;
   std::vector<float> last_ms_;
+  std::mutex reg_mu_;
+  std::vector<std::pair<uintptr_t, size_t>> registered_;  // dg_host_register ranges
+  int64_t stat_direct_d2h_ = 0;                           // outputs copied straight into caller memory
 };
 
 }  // namespace dg

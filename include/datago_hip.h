@@ -193,6 +193,15 @@ dg_status dg_memcpy_h2d(dg_ctx *ctx, void *dst, const void *src, size_t bytes);
 dg_status dg_memcpy_d2h(dg_ctx *ctx, void *dst, const void *src, size_t bytes);
 dg_status dg_synchronize(dg_ctx *ctx);
 
+/* Page-lock a caller-owned host range (hipHostRegister) for the host-out path:
+ * outputs of dg_submit / dg_decode_one whose buffer lies inside a registered
+ * range (or in memory the HIP runtime already pins) are copied by DMA straight
+ * from HBM into it -- no pinned staging buffer, no host memcpy, no first-touch
+ * page faults.  Meant for a reused output-buffer pool (the Rust glue's payload
+ * arena); registering costs about as much as touching the pages once. */
+dg_status dg_host_register(dg_ctx *ctx, void *ptr, size_t bytes);
+dg_status dg_host_unregister(dg_ctx *ctx, void *ptr);
+
 /* Per-kernel timing of the last completed batch (HIP events on the context's
  * stream).  names[i] points to static strings; returns the number of stages. */
 int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_t cap);
