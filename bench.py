@@ -714,6 +714,8 @@ def main() -> int:
     # max over ranks; totals over ranks
     (dt_max,) = max_over_ranks([dt], world)
     per_rank_s = sum_over_ranks([dt if r == rank else 0.0 for r in range(world)], world)
+    # host CPU time each rank spent planning + submitting its batches (the 8-GPU host budget)
+    per_rank_host = sum_over_ranks([host_s["submit"] if r == rank else 0.0 for r in range(world)], world)
     px_all, alg_all, outpx_all = sum_over_ranks([float(px_total), alg_bytes, float(out_px)], world)
 
     # ---- isolated per-kernel times: batches one at a time (untimed, reported only)
@@ -995,6 +997,7 @@ def main() -> int:
             "output_mpix_s": round(outpx_all / dt_max / 1e6, 2),
             "images_per_s": round(B_ * a.steps * world / dt_max, 1),
             "host_submit_ms_per_step": round(1e3 * host_s["submit"] / a.steps, 3),  # Python + dg_submit_device planning
+            "host_submit_ms_per_step_per_rank": [round(1e3 * h_ / a.steps, 3) for h_ in per_rank_host],
             "host_submit_phases_ms_per_step": host_phases,
             "e2e_host_mpix_s": round(e2e, 2) if e2e else None,
             "e2e_host_detail": ({"note": "host JPEG bytes in -> host RGB out, a dg_host_register'ed output pool "
