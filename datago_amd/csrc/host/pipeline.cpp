@@ -410,6 +410,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     chunked_off_ = v == 0;
     return DG_OK;
   }
+  if (k == "lead_density") {
+    lead_density_ = v != 0;
+    return DG_OK;
+  }
   if (k == "sub_density") {  // bits-per-block threshold for shorter subsequences (0 = off)
     if (v < 0 || v > 4096) return DG_ERR_INVALID;
     sub_density_ = (double)v;
@@ -1019,6 +1023,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     // self-synchronisation distance, which is longest for 6-block MCUs
     // (4:2:0; p99.9 ~7 kbit on the bench corpus, tools/sync_stats.cpp)
     d.lead_bits = lead_bits_ >= 0 ? (uint32_t)lead_bits_ : (bpm >= 4 ? 6144u : 2048u);
+    // shorter ranges of symbol-dense images get a proportionally shorter lead-in (option
+    // "lead_density"): their codes are short, so the decoder self-synchronises in fewer bits
+    if (lead_density_ && lead_bits_ < 0 && d.sub_bits < sub_bits)
+      d.lead_bits = std::max<uint32_t>(1024u, d.lead_bits / (sub_bits / d.sub_bits));
     d.nsub = std::max<uint32_t>(1, (uint32_t)(((uint64_t)d.scan_len * 8 + d.sub_bits - 1) / d.sub_bits));
     d.sub_base = sub_base;
     sub_base += d.nsub;
@@ -1931,6 +1939,21 @@ dg_status Context::finish(Slot &sl) {
     const size_t ns = b.lists[L_SYNC].size(), nw = b.lists[L_HUFF].size();
     std::vector<uint64_t> rec(2 * (ns + nw));
     HIPCHK(hipMemcpy(rec.data(), sl.wgt.p, rec.size() * 8, hipMemcpyDeviceToHost));
+    if (const char *dump = getenv("DG_WG_DUMP")) {  // debug: one line per entropy workgroup
+      if (FILE *f = fopen(dump, "a")) {
+        uint64_t lo = ~0ull;
+        for (size_t i = 0; i < ns + nw; i++) lo = std::min(lo, rec[2 * i]);
+        for (size_t i = 0; i < ns + nw; i++) {
+          const WgItem &w = b.lists[i < ns ? L_SYNC : L_HUFF][i < ns ? i : i - ns];
+          const ImageDesc &d = b.descs[w.image];
+          fprintf(f, "%d %zu %u %u %llu %llu %u %u %u %u %u %u\n", i < ns ? 0 : 1, i, w.image, w.item0,
+                  (unsigned long long)(rec[2 * i] - lo), (unsigned long long)(rec[2 * i + 1] - lo), d.scan_len,
+                  d.total_blocks, d.sub_bits, d.nsub, d.lead_bits, d.width * d.height);
+        }
+        fprintf(f, "end\n");
+        fclose(f);
+      }
+    }
     for (int a = 0; a < 2; a++) {
       const size_t r0 = a ? ns : 0, n = a ? nw : ns;
       if (!n) continue;

@@ -252,6 +252,7 @@ class Context {
   bool band_dec_ = false;               // option "band_dec": IDCT + colour + first H pass in k_band_dec
   bool h_mfma_ = false;                 // option "h_mfma": band H passes on the matrix cores (k_resize_hm; measured slower: off)
   double sub_density_ = 0;              // option "sub_density": bits per block below which subsequences shrink
+  bool lead_density_ = false;           // option "lead_density": their lead-in shrinks by the same factor
   uint32_t dec_dbg_ = 0;                // option "dec_dbg": k_band_dec phase switches (timing experiments only)
   uint32_t dec_strips_ = kDecStripsDefault;  // option "dec_strips"
   bool idct_fused_ = false;             // option "idct_fused" (measured 7x slower k_huff_write: off)
