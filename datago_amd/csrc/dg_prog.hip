@@ -60,18 +60,25 @@ constexpr uint32_t kPBlk = 64;    // coefficient blocks per chunk
 
 constexpr uint32_t kDWin = 4096;  // destuffed window (bytes), speculative-table decoder
 
+// LDS of one scan workgroup.  The Huffman tables go last and a launch sizes
+// them for its scans: one (AC scans: one table each) or four (DC-first scans
+// of up to four components), so the AC launches, which hold the long serial
+// chains, fit 9 workgroups per CU instead of 5.
+template <int NT>
 struct ProgSmem {
-  HuffTable tabs[4];
   int16_t blk[kPBlk][64];
-  uint64_t nzm[kPBlk];  // refine scans: nonzero-history mask of each staged block (bit k = zigzag k)
-  uint64_t cor[kPBlk];  //   correction bits in stream order (one per history-nonzero band position)
-  uint32_t ncor[kPBlk]; //   how many
-  uint64_t nwp[kPBlk];  //   new coefficients +1 << Al
-  uint64_t nwn[kPBlk];  //   new coefficients -1 << Al
   union {
-    uint8_t win[kPWin + 16];                // serial decoder: stuffed bytes
+    struct {                                // serial decoder
+      alignas(16) uint8_t win[kPWin + 16];  //   stuffed bytes
+      uint64_t nzm[kPBlk];  // refine scans: nonzero-history mask of each staged block (bit k = zigzag k)
+      uint64_t cor[kPBlk];  //   correction bits in stream order (one per history-nonzero band position)
+      uint32_t ncor[kPBlk]; //   how many
+      uint64_t nwp[kPBlk];  //   new coefficients +1 << Al
+      uint64_t nwn[kPBlk];  //   new coefficients -1 << Al
+    };
     alignas(16) uint8_t dwin[kDWin + 64];   // speculative decoder: destuffed bytes + zero pad
   };
+  HuffTable tabs[NT];
 };
 
 // Every lane runs the same decode: make that explicit, so the state lives in
@@ -92,7 +99,8 @@ struct WReader {
 };
 
 // window starting at the 16-byte line holding byte p; all 64 lanes load
-__device__ __forceinline__ void wr_refill(WReader &r, ProgSmem &sm, uint32_t p) {
+template <class SM>
+__device__ __forceinline__ void wr_refill(WReader &r, SM &sm, uint32_t p) {
   __syncthreads();
   r.wabs = (r.d + p) & ~(uint64_t)15;
   const uint64_t end = r.d + r.len;
@@ -109,12 +117,14 @@ __device__ __forceinline__ void wr_refill(WReader &r, ProgSmem &sm, uint32_t p) 
 }
 
 // byte q (< len) of the scan, refilling the window when q is past it
-__device__ __forceinline__ uint32_t wr_byte(WReader &r, ProgSmem &sm, uint32_t q) {
+template <class SM>
+__device__ __forceinline__ uint32_t wr_byte(WReader &r, SM &sm, uint32_t q) {
   if (r.d + q - r.wabs >= kPWin) wr_refill(r, sm, q);
   return uni(sm.win[r.d + q - r.wabs]);
 }
 
-__device__ __forceinline__ void wr_fill(WReader &r, ProgSmem &sm) {
+template <class SM>
+__device__ __forceinline__ void wr_fill(WReader &r, SM &sm) {
   while (r.nbits <= 56) {
     // fast path: four bytes without an FF, inside the scan and the window
     if (!r.marker && r.nbits <= 32 && r.p + 4 <= r.len) {
@@ -154,7 +164,8 @@ __device__ __forceinline__ void wr_fill(WReader &r, ProgSmem &sm) {
   }
 }
 
-__device__ __forceinline__ uint32_t wr_get(WReader &r, ProgSmem &sm, uint32_t k) {
+template <class SM>
+__device__ __forceinline__ uint32_t wr_get(WReader &r, SM &sm, uint32_t k) {
   if (k == 0) return 0;
   if (r.nbits < (int32_t)k) wr_fill(r, sm);
   const uint32_t v = (uint32_t)(r.buf >> (64 - k));
@@ -177,7 +188,8 @@ __device__ __forceinline__ uint32_t prog_lookup(const HuffTable &t, uint32_t bit
   return 16u << 8;
 }
 
-__device__ __forceinline__ uint32_t wr_sym(WReader &r, ProgSmem &sm, const HuffTable &t) {
+template <class SM>
+__device__ __forceinline__ uint32_t wr_sym(WReader &r, SM &sm, const HuffTable &t) {
   if (r.nbits < 16) wr_fill(r, sm);
   const uint32_t e = prog_lookup(t, (uint32_t)(r.buf >> 32));
   const uint32_t l = e >> 8;
@@ -187,7 +199,8 @@ __device__ __forceinline__ uint32_t wr_sym(WReader &r, ProgSmem &sm, const HuffT
 }
 
 // restart (libjpeg process_restart): drop the buffered bits, continue after the next RSTn
-__device__ __forceinline__ void wr_restart(WReader &r, ProgSmem &sm) {
+template <class SM>
+__device__ __forceinline__ void wr_restart(WReader &r, SM &sm) {
   r.buf = 0;
   r.nbits = 0;
   uint32_t q = r.p;
@@ -206,7 +219,8 @@ struct ProgState {
 __device__ __forceinline__ uint32_t zz(uint32_t k) { return k < 63u ? k : 63u; }
 
 // one block of the scan (libjpeg jdphuff.c decode_mcu_{DC,AC}_{first,refine})
-__device__ __forceinline__ void prog_block(const ProgScan &sc, ProgSmem &sm, WReader &r, ProgState &ps, uint32_t ci,
+template <class SM>
+__device__ __forceinline__ void prog_block(const ProgScan &sc, SM &sm, WReader &r, ProgState &ps, uint32_t ci,
                                            int16_t *blk, uint64_t nz, uint64_t *mask) {
   const uint32_t ss = sc.ss, se = sc.se, al = sc.al;
   if (ss == 0) {
@@ -449,13 +463,18 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uin
 // Move the unread tail of the window to its front, then destuff 64 aligned
 // 16-byte lines of the scan at a time until the window is nearly full or
 // the scan's data ends.
-__device__ __forceinline__ void ds_refill(DStream &s, ProgSmem &sm, uint32_t lane) {
+template <class SM>
+__device__ __forceinline__ void ds_refill(DStream &s, SM &sm, uint32_t lane) {
   const uint32_t sb = uni((s.bp >> 3) & ~15u);
-  const uint32_t tail = s.dend > sb ? s.dend - sb : 0u;  // < 40 bytes (refill runs with < 24 unread)
-  __syncthreads();
-  const uint32_t t = lane < tail ? sm.dwin[sb + lane] : 0u;
-  __syncthreads();
-  if (lane < tail) sm.dwin[lane] = (uint8_t)t;
+  // < 40 bytes from the generic decoder (it refills with < 24 unread), up to
+  // ~180 from the refinement walk (it refills between blocks, >= 160 ahead)
+  const uint32_t tail = s.dend > sb ? s.dend - sb : 0u;
+  for (uint32_t c0 = 0; c0 < tail; c0 += 64) {  // forward, 64 bytes at a time: dst < src never overtakes
+    __syncthreads();
+    const uint32_t t = c0 + lane < tail ? sm.dwin[sb + c0 + lane] : 0u;
+    __syncthreads();
+    if (c0 + lane < tail) sm.dwin[c0 + lane] = (uint8_t)t;
+  }
   uint32_t bp = s.bp - sb * 8, dend = tail, q = s.q, prev = s.prev, done = s.done;
   const uint64_t end = s.src + s.len;
   while (!done && dend + 1024 + 16 <= kDWin) {
@@ -526,7 +545,8 @@ __device__ __forceinline__ void ds_refill(DStream &s, ProgSmem &sm, uint32_t lan
 }
 
 // lane's 32-bit peek at bit bp + lane of the window
-__device__ __forceinline__ uint32_t ds_peek(const ProgSmem &sm, uint32_t bp, uint32_t lane) {
+template <class SM>
+__device__ __forceinline__ uint32_t ds_peek(const SM &sm, uint32_t bp, uint32_t lane) {
   const uint32_t o = bp + lane, bi = o >> 3;
   const uint32_t *w = (const uint32_t *)sm.dwin;
   const uint32_t a = bi >> 2;
@@ -544,7 +564,8 @@ __device__ __forceinline__ uint32_t wrl(uint32_t v, uint32_t val, uint32_t at) {
   return threadIdx.x == at ? val : v;
 }
 
-__device__ __forceinline__ void prog_scan_spec(const ProgScan &sc, const ImageDesc &im, ProgSmem &sm, uint32_t lane,
+template <class SM>
+__device__ __forceinline__ void prog_scan_spec(const ProgScan &sc, const ImageDesc &im, SM &sm, uint32_t lane,
                                DG_GLOBAL int16_t *coef, uint32_t bpmu, uint32_t nunits, ProgDeps &pd) {
   const uint32_t upc = kPBlk / bpmu;
   const bool refine = sc.ah != 0;
@@ -580,10 +601,11 @@ __device__ __forceinline__ void prog_scan_spec(const ProgScan &sc, const ImageDe
     if (!s.done && (s.bp >> 3) + 24 > s.dend) ds_refill(s, sm, lane);
     if (s.done && (s.bp >> 3) > s.dend + 8) s.bp = (s.dend + 8) * 8;  // past the data: zeros forever
     peek = ds_peek(sm, s.bp, lane);
+    constexpr uint32_t kNT = sizeof(sm.tabs) / sizeof(HuffTable);  // tables the launch holds in LDS
     sp0 = huff_lookup(sm.tabs[0], peek);
-    if (nt > 1) sp1 = huff_lookup(sm.tabs[1], peek);
-    if (nt > 2) sp2 = huff_lookup(sm.tabs[2], peek);
-    if (nt > 3) sp3 = huff_lookup(sm.tabs[3], peek);
+    if (kNT > 1 && nt > 1) sp1 = huff_lookup(sm.tabs[kNT > 1 ? 1 : 0], peek);
+    if (kNT > 2 && nt > 2) sp2 = huff_lookup(sm.tabs[kNT > 2 ? 2 : 0], peek);
+    if (kNT > 3 && nt > 3) sp3 = huff_lookup(sm.tabs[kNT > 3 ? 3 : 0], peek);
   };
   // n (<= 32) bits at offset off (<= 63) of the round
   auto rd = [&](uint32_t off, uint32_t n) -> uint32_t { return n ? rdl(peek, off) >> (32u - n) : 0u; };
@@ -765,26 +787,225 @@ __device__ __forceinline__ void prog_scan_spec(const ProgScan &sc, const ImageDe
   }
 }
 
-__global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ imgs,
-                                                  const ProgScan *__restrict__ scans,
-                                                  const WgItem *__restrict__ list, const HuffTable *__restrict__ pool,
-                                                  uint32_t serial, DG_GLOBAL uint32_t *pflags) {
-  __shared__ ProgSmem sm;
-  const uint32_t lane = threadIdx.x;
-  // pipelined launch: scans are taken in list (level) order, so every scan a
-  // worker waits for was taken earlier by a worker that is running
-  uint32_t t = blockIdx.x;
-  if (pflags) {
-    uint32_t v = 0;
-    if (lane == 0) v = __hip_atomic_fetch_add((uint32_t *)pflags, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    t = uni(v);
+// huff_lookup (dg_entropy.h) for the 64 lanes of a round without divergent
+// branches: the sub-table and the canonical walk (codes longer than
+// kLutBits) run only when some lane needs them, behind wave-uniform tests,
+// so the walk's scalar state never lands in VGPRs at a divergent join.
+template <class T>
+__device__ __forceinline__ uint32_t huff_lookup_wave(const T &t, uint32_t bits) {
+  uint32_t e = t.lut[bits >> (32 - kLutBits)];
+  if (__ballot((e & 0x8000u) != 0u || e == 0u)) {
+    const uint32_t e2 = t.sub[e & (kMaxSubTables - 1)][(bits >> (32 - 16)) & ((1u << kSubBits) - 1)];
+    e = (e & 0x8000u) ? (e2 ? e2 : (16u << 8)) : e;
+    if (__ballot(e == 0u)) {  // more long prefixes than sub-tables: smallest l with pk < lim[l]
+      const uint32_t pk = bits >> 16;
+      uint32_t r = 16u << 8;
+#pragma unroll
+      for (int32_t l = 16; l > kLutBits; l--) {
+        const uint32_t v = ((uint32_t)l << 8) | t.vals[(t.valoff[l] + (int32_t)(pk >> (16 - l))) & 255];
+        r = pk < t.lim[l] ? v : r;
+      }
+      e = e ? e : r;
+    }
   }
-  const uint32_t self = list[t].item0;
+  return e;
+}
+
+// AC refinement scans (Ah > 0, Ss > 0; one component, so units are blocks):
+// most of a high-quality progressive file's bits -- the final luma
+// refinement alone is ~45% of the pool-largest file and its wave's decode is
+// the batch's long pole.  A function of its own (not inlined) so that its
+// symbol walk gets the register file to itself: inlined into the generic
+// decoder, the walk ran with SGPRs spilled to VGPR lanes and ~1500 cycles per
+// symbol.  Per symbol the walk does two readlanes (the code at offset o, the
+// 32 bits after it) and takes the sign and the correction bits of the
+// history-nonzero positions it passes straight out of those 32 bits; only
+// stretches of more than 31 correction bits (and EOB-run blocks) read the
+// round's peeks again.  Same semantics as the generic path (jdphuff.c
+// decode_mcu_AC_refine); returns pd.bad.
+template <class SM>
+__device__ __noinline__ uint32_t prog_refine_spec(const ProgScan &sc, const ImageDesc &im, SM &sm, uint32_t lane,
+                                                  DG_GLOBAL int16_t *coef, uint32_t nunits, ProgDeps pd) {
+  const uint32_t ss = uni(sc.ss), se = uni(sc.se), al = uni(sc.al);
+  const uint64_t band = (se < 63 ? (2ull << se) - 1ull : ~0ull) & ~((1ull << ss) - 1ull);
+  DStream s;
+  s.src = sc.data;
+  s.len = sc.len;
+  s.q = 0;
+  s.prev = 0;
+  s.dend = 0;
+  s.done = sc.len == 0;
+  s.bp = 0;
+  __syncthreads();
+  if (s.done) {
+    sm.dwin[lane] = 0;
+    __syncthreads();
+  }
+  uint32_t o = 0, peek = 0, sp0 = 0, aft = 0;
+  // A round: peeks and code lookups for the 64 bit offsets from bp.  The
+  // window is refilled only between blocks, with at least 160 bytes ahead: a
+  // block consumes at most 63 x (16-bit code + sign) + 63 correction bits +
+  // a 14-bit EOB run = 1148 bits, so no round inside a block needs a refill
+  // (and the walk has no call in it).
+  auto round = [&]() {
+    s.bp = uni(s.bp + o);
+    o = 0;
+    if (s.done && (s.bp >> 3) > s.dend + 8) s.bp = (s.dend + 8) * 8;  // past the data: zeros forever
+    peek = ds_peek(sm, s.bp, lane);
+    sp0 = huff_lookup_wave(sm.tabs[0], peek);
+    aft = ds_peek(sm, s.bp + (sp0 >> 8), lane);  // lane o: the 32 bits after the code at offset o
+  };
+  auto refill = [&]() {  // between blocks: keep >= 160 destuffed bytes ahead of the walk
+    if (!s.done && ((s.bp + o) >> 3) + 160 > s.dend) {
+      s.bp = uni(s.bp + o);
+      o = 0;
+      ds_refill(s, sm, lane);
+      round();
+    }
+  };
+  if (!s.done) {
+    ds_refill(s, sm, lane);
+  }
+  round();
+  uint32_t eobrun = 0;
+  for (uint32_t u0 = 0; u0 < nunits; u0 += kPBlk) {
+    const uint32_t nb = nunits - u0 < kPBlk ? nunits - u0 : kPBlk;
+    prog_wait(pd, prog_unit_mrow(im, sc, u0 + nb - 1) + 1);
+    if (pd.bad) break;  // (wave-uniform) the image is lost: no reads of blocks a producer may still write
+    uint32_t g = 0, lci, nzlo = 0, nzhi = 0;
+    if (lane < nb) {
+      g = prog_unit_block(im, sc, u0 + lane, 0, lci);
+      u32x4 *dst = (u32x4 *)sm.blk[lane];
+      const DG_GLOBAL u32x4 *src = (const DG_GLOBAL u32x4 *)(coef + (size_t)g * 64);
+      u32x4 x[8];
+#pragma unroll
+      for (int qq = 0; qq < 8; qq++) x[qq] = src[qq];
+#pragma unroll
+      for (int qq = 0; qq < 8; qq++) {
+        dst[qq] = x[qq];
+        const uint32_t ws[4] = {x[qq].x, x[qq].y, x[qq].z, x[qq].w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {  // coefficients 8qq + 2e, 8qq + 2e + 1
+          const uint32_t bits = ((ws[e] & 0xFFFFu) ? 1u : 0u) | ((ws[e] >> 16) ? 2u : 0u);
+          const int kk = qq * 8 + e * 2;
+          if (kk < 32) nzlo |= bits << kk;
+          else nzhi |= bits << (kk - 32);
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t corlo = 0, corhi = 0, ncor = 0, nplo = 0, nphi = 0, nnlo = 0, nnhi = 0;
+    for (uint32_t slot = 0; slot < nb; slot++) {
+      refill();
+      const uint64_t nz = ((uint64_t)rdl(nzhi, slot) << 32) | rdl(nzlo, slot);
+      const uint64_t nzb = nz & band, hz = ~nz & band;  // history-nonzero / history-zero positions of the band
+      // lane p: history-zero positions of the band below position p
+      const uint32_t zc = __builtin_amdgcn_mbcnt_hi((uint32_t)(hz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hz, 0u));
+      uint32_t zi = 0;  // zeros below k (k = ss: none)
+      uint64_t cb = 0, np = 0, nn = 0;
+      uint32_t cc = 0;
+      auto take = [&](uint32_t c) {  // c correction bits at offset o
+        while (c) {
+          if (o > 63) round();
+          const uint32_t n = c < 32 ? c : 32;
+          const uint32_t ou = uni(o);
+          cb = (cb << n) | (rdl(peek, ou) >> (32u - n));
+          o = ou + n;
+          cc += n;
+          c -= n;
+        }
+      };
+      uint32_t k = ss;
+      if (eobrun == 0) {
+        for (;;) {
+          o = uni(o);  // (o's phi can land in a VGPR after a round's lookups: keep the test scalar)
+          if (o > 47) round();
+          const uint32_t ou = uni(o);
+          const uint32_t e = rdl(sp0, ou), after = rdl(aft, ou);  // the code at o, the 32 bits after it
+          const uint32_t l = e >> 8, rr = (e >> 4) & 15u, sz = e & 15u;
+          if (!sz && rr != 15) {                     // EOBn: this block is the run's first
+            eobrun = (1u << rr) + (rr ? after >> (32u - rr) : 0u);
+            o = ou + l + rr;
+            break;
+          }
+          const uint32_t sg = (sz + 15u) >> 4;  // a new coefficient's sign bit comes first
+          // land on the (rr+1)-th history-zero position from k (ZRL: the 16th):
+          // the zero with index zi + rr, found by one compare over the lanes
+          // (lane p = position p holds the number of history-zero positions
+          // below p); the positions passed that are not zeros take a
+          // correction bit each
+          const uint32_t j = zi + rr;
+          const uint64_t m = __ballot(zc == j) & hz;
+          uint32_t pos, c;
+          if (m) {
+            pos = (uint32_t)__builtin_ctzll(m);
+            c = pos - k - rr;
+          } else {  // ran past Se
+            pos = se + 1;
+            c = (uint32_t)__builtin_popcountll(nzb & (~0ull << k));
+          }
+          zi = j + 1;
+          if (c + sg <= 32u) {  // the correction bits lie in `after` too
+            if (c) cb = (cb << c) | ((after << sg) >> (32u - c));
+            cc += c;
+            o = ou + l + sg + c;
+          } else {
+            o = ou + l + sg;
+            take(c);
+          }
+          const uint64_t bit = (uint64_t)sg << zz(pos);
+          const uint64_t neg = 0ull - (uint64_t)(after >> 31);  // all ones for a positive sign
+          np |= bit & neg;
+          nn |= bit & ~neg;
+          k = pos + 1;
+          if (k > se) break;
+        }
+      }
+      if (eobrun > 0) {
+        if (k <= se) take((uint32_t)__builtin_popcountll(nzb & (~0ull << k)));
+        eobrun--;
+      }
+      corlo = wrl(corlo, (uint32_t)cb, slot);
+      corhi = wrl(corhi, (uint32_t)(cb >> 32), slot);
+      ncor = wrl(ncor, cc, slot);
+      nplo = wrl(nplo, (uint32_t)np, slot);
+      nphi = wrl(nphi, (uint32_t)(np >> 32), slot);
+      nnlo = wrl(nnlo, (uint32_t)nn, slot);
+      nnhi = wrl(nnhi, (uint32_t)(nn >> 32), slot);
+    }
+    __syncthreads();
+    if (lane < nb) {
+      int16_t *bk = sm.blk[lane];
+      const int32_t p1 = 1 << al, m1 = -(1 << al);
+      const uint64_t bits = ((uint64_t)corhi << 32) | corlo;
+      int32_t i = (int32_t)ncor - 1;  // bit of the lowest history-nonzero position
+      for (uint64_t m = (((uint64_t)nzhi << 32) | nzlo) & band; m && i >= 0; m &= m - 1ull, i--) {
+        if (!((bits >> i) & 1u)) continue;
+        const uint32_t pos = (uint32_t)__builtin_ctzll(m);
+        const int32_t v = bk[pos];
+        if ((v & p1) == 0) bk[pos] = (int16_t)(v >= 0 ? v + p1 : v + m1);
+      }
+      for (uint64_t m = ((uint64_t)nphi << 32) | nplo; m; m &= m - 1ull) bk[__builtin_ctzll(m)] = (int16_t)p1;
+      for (uint64_t m = ((uint64_t)nnhi << 32) | nnlo; m; m &= m - 1ull) bk[__builtin_ctzll(m)] = (int16_t)m1;
+      DG_GLOBAL int16_t *dst = coef + (size_t)g * 64;
+      for (uint32_t k = ss; k <= se; k++) dst[k] = bk[k];
+    }
+    prog_publish(pd, prog_rows_done(im, sc, u0 + nb));
+    __syncthreads();
+  }
+  return pd.bad;
+}
+
+// One scan, start to end (all 64 lanes).
+template <int NT>
+__device__ __forceinline__ void prog_one(ProgSmem<NT> &sm, const ImageDesc *__restrict__ imgs,
+                                         const ProgScan *__restrict__ scans, const HuffTable *__restrict__ pool,
+                                         uint32_t serial, DG_GLOBAL uint32_t *pflags, uint32_t self, uint32_t lane) {
   const ProgScan &sc = scans[self];
   const ImageDesc &im = imgs[sc.image];
   ProgDeps pd;
   pd.flags = pflags;
-  pd.deps = sc.deps;
+  pd.deps = (sc.pflags & kProgChained) ? 0ull : sc.deps;  // chained: the deps ran before it in this item
   pd.first = sc.first;
   pd.self = self;
   pd.last = 0;
@@ -794,6 +1015,12 @@ __global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ 
   {
     const uint32_t words = (uint32_t)(sizeof(HuffTable) / 4);
     const uint32_t nt = (sc.ss == 0) ? (sc.ah == 0 ? sc.ns : 0) : 1;
+    if (nt > (uint32_t)NT) {  // the host routes scans by table count; never decode past the LDS tables
+      pd.bad = 1;
+      prog_finish(pd, imgs, sc, lane);
+      return;
+    }
+    __syncthreads();  // the previous scan of this item is done with the LDS
     for (uint32_t t = 0; t < nt; t++) {
       const uint32_t *src = (const uint32_t *)&pool[sc.ss == 0 ? sc.dc[t] : sc.ac];
       for (uint32_t w = lane; w < words; w += 64) ((uint32_t *)&sm.tabs[t])[w] = src[w];
@@ -811,6 +1038,11 @@ __global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ 
   }
   if (sc.restart == 0 && !(serial & 1u)) {
     __syncthreads();
+    if (sc.ah != 0 && sc.ss > 0 && sc.ns == 1 && !(serial & 4u)) {  // AC refinement: its own walk
+      pd.bad = prog_refine_spec(sc, im, sm, lane, coef, nunits, pd);
+      prog_finish(pd, imgs, sc, lane);
+      return;
+    }
     prog_scan_spec(sc, im, sm, lane, coef, bpmu, nunits, pd);
     prog_finish(pd, imgs, sc, lane);
     return;
@@ -897,6 +1129,36 @@ __global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ 
   prog_finish(pd, imgs, sc, lane);
 }
 
+// One workgroup (one wave) per work item: a single scan, or a chain of scans
+// of one image run back to back (ProgScan::next).  Pipelined launches hand
+// items out by an atomic ticket in list order, so every scan a worker waits
+// for was taken earlier by a worker that is running.  ptime (debug, option
+// wg_timing): s_memrealtime at the start and end of every scan.
+template <int NT>
+__global__ __launch_bounds__(64) void k_prog_scan(const ImageDesc *__restrict__ imgs,
+                                                  const ProgScan *__restrict__ scans,
+                                                  const WgItem *__restrict__ list, const HuffTable *__restrict__ pool,
+                                                  uint32_t serial, DG_GLOBAL uint32_t *pflags,
+                                                  DG_GLOBAL uint32_t *ticket, DG_GLOBAL uint64_t *ptime) {
+  __shared__ ProgSmem<NT> sm;
+  const uint32_t lane = threadIdx.x;
+  uint32_t t = blockIdx.x;
+  if (ticket) {
+    uint32_t v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add((uint32_t *)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = uni(v);
+  }
+  for (uint32_t self = uni(list[t].item0); self != kProgNoScan;) {
+    const uint64_t t0 = ptime ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    prog_one<NT>(sm, imgs, scans, pool, serial, pflags, self, lane);
+    if (ptime && lane == 0) {
+      ptime[2 * self] = t0;
+      ptime[2 * self + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    self = uni(scans[self].next);
+  }
+}
+
 // ------------------------------------------------------------ launchers
 
 void launch_prog_zero(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
@@ -904,8 +1166,15 @@ void launch_prog_zero(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
 }
 
 void launch_prog_scan(hipStream_t st, const ImageDesc *imgs, const ProgScan *scans, const WgItem *list, uint32_t n,
-                      const HuffTable *pool, uint32_t serial, uint32_t *pflags) {
-  if (n) hipLaunchKernelGGL(k_prog_scan, dim3(n), dim3(64), 0, st, imgs, scans, list, pool, serial, (DG_GLOBAL uint32_t *)pflags);
+                      const HuffTable *pool, uint32_t serial, uint32_t *pflags, uint32_t *ticket, uint64_t *ptime,
+                      int ntab) {
+  if (!n) return;
+  if (ntab <= 1)
+    hipLaunchKernelGGL(k_prog_scan<1>, dim3(n), dim3(64), 0, st, imgs, scans, list, pool, serial,
+                       (DG_GLOBAL uint32_t *)pflags, (DG_GLOBAL uint32_t *)ticket, (DG_GLOBAL uint64_t *)ptime);
+  else
+    hipLaunchKernelGGL(k_prog_scan<4>, dim3(n), dim3(64), 0, st, imgs, scans, list, pool, serial,
+                       (DG_GLOBAL uint32_t *)pflags, (DG_GLOBAL uint32_t *)ticket, (DG_GLOBAL uint64_t *)ptime);
 }
 
 }  // namespace dg

@@ -341,18 +341,20 @@ struct ProgScan {
   uint32_t comp[4];     // their component indices
   uint16_t dc[4];       // DC-first scans: Huffman pool index per scan component
   uint16_t ac;          // AC scans: Huffman pool index
-  uint16_t pad0;
+  uint16_t pflags;      // kProgChained: the scan runs after its deps in the same work item (no waits)
   uint32_t ss, se, ah, al;
   uint32_t restart;     // restart interval (MCUs; blocks when ns == 1), 0 = none
   uint32_t level;
   uint32_t first;       // batch index of the image's first scan
-  uint32_t pad1;
+  uint32_t next;        // next scan of the same work item (chain), kProgNoScan = none
   uint64_t deps;        // earlier scans of the image this one reads (bit e = scan first + e)
 };
 // Pipelined scans (one launch per batch): progress word of scan j =
 // flags[1 + j], in MCU rows whose blocks the scan has written (kProgDone
 // when finished); flags[0] hands out scans to workgroups in list order.
 constexpr uint32_t kProgDone = 0xFFFFFFFFu;
+constexpr uint32_t kProgNoScan = 0xFFFFFFFFu;
+constexpr uint16_t kProgChained = 1;
 constexpr uint32_t kProgMaxScans = 64;  // per image (deps is a 64-bit mask)
 constexpr uint32_t kProgZeroBytes = 65536;  // coefficient bytes zeroed per k_prog_zero workgroup
 

@@ -359,6 +359,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     prog_side_ = v != 0;
     return DG_OK;
   }
+  if (k == "prog_chain") {  // chain dependency groups costing <= this % of the batch's longest scan (0: off)
+    if (v < 0 || v > 100000) return DG_ERR_INVALID;
+    prog_chain_ = (int)v;
+    return DG_OK;
+  }
   if (k == "prog_pipe") {  // 0: one k_prog_scan launch per level (A/B)
     prog_pipe_ = v != 0;
     return DG_OK;
@@ -451,6 +456,8 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "fix_workgroups") return stat_fix_;
   if (k == "write_mismatch") return stat_mismatch_;
   if (k == "unsettled_batches") return stat_unsettled_;
+  if (k == "prog_items") return stat_prog_items_;
+  if (k == "prog_chains") return stat_prog_chains_;
   if (k == "pool_flushes") return stat_pool_flush_;
   if (k == "sync_iters_max") return stat_iters_;
   {  // wg_timing summaries, in nanoseconds: wg_{sync,write}_{span,mean,p90,max}
@@ -1294,7 +1301,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.pf_n = 0;
   for (const ImageDesc &dd : b.descs)
     if (dd.fmt == kFmtJpeg) b.pf_n += dd.prog;
-  b.pf_off = b.pf_n ? L.take((size_t)(b.pf_n + 1) * 4) : 0;
+  b.pf_off = b.pf_n ? L.take((size_t)(b.pf_n + 2) * 4) : 0;  // AC ticket, progress words, DC ticket
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
   const size_t ckpt_off = L.take(std::max<uint64_t>(1, ckpt_total) * sizeof(Ckpt));
   // fused IDCT leftovers: at most one carried-in block per subsequence, plus
@@ -1387,6 +1394,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         r.al = (uint32_t)sc.al;
         r.restart = (uint32_t)sc.restart;
         r.first = (uint32_t)first;
+        r.next = kProgNoScan;
+        r.pflags = 0;
         uint32_t lvl = 0;
         for (size_t e = 0; e < j; e++) {
           const JpegScan &pr = h.scans[e];
@@ -1584,29 +1593,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     if (lv >= b.prog_level_n.size()) b.prog_level_n.resize(lv + 1, 0);
     b.prog_level_n[lv]++;
   }
+  b.prog_dc_n = 0;
   if (prog_pipe_) {
-    // One pipelined launch takes scans in list order.  A scan waits only on
-    // earlier scans of its own image, so images may follow one another:
-    // largest coded size first (its slowest scan is the batch's long pole,
-    // and the launch has more scans than resident waves), each image's scans
-    // in level order.
-    std::vector<std::pair<uint64_t, uint32_t>> imgs;  // (coded bytes, first scan)
-    for (uint32_t j = 0; j < (uint32_t)b.pscans.size(); j++) {
-      if (j == 0 || b.pscans[j].image != b.pscans[j - 1].image) imgs.push_back({0, j});
-      imgs.back().first += b.pscans[j].len;
-    }
-    std::stable_sort(imgs.begin(), imgs.end(), [](const auto &a, const auto &c) { return a.first > c.first; });
-    b.lists[L_PROG].clear();
-    for (const auto &im : imgs) {
-      const uint32_t j0 = im.second;
-      uint32_t j1 = j0;
-      while (j1 < b.pscans.size() && b.pscans[j1].image == b.pscans[j0].image) j1++;
-      uint32_t maxlv = 0;
-      for (uint32_t j = j0; j < j1; j++) maxlv = std::max(maxlv, b.pscans[j].level);
-      for (uint32_t lv = 0; lv <= maxlv; lv++)
-        for (uint32_t j = j0; j < j1; j++)
-          if (b.pscans[j].level == lv) b.lists[L_PROG].push_back(WgItem{b.pscans[j].image, j});
-    }
+    plan_prog_items(b);
   } else {  // one launch per level: scans grouped by level
     std::vector<uint32_t> at(b.prog_level_n.size(), 0);
     for (size_t lv = 1; lv < at.size(); lv++) at[lv] = at[lv - 1] + b.prog_level_n[lv - 1];
@@ -1661,9 +1650,11 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   if (st) return st;
   char *P = (char *)sl.stage.p;
   memset(P + b.flags_off, 0, sizeof(BatchFlags));
+  b.ptime_off = 0;
   if (wg_timing_) {
     const size_t nrec = b.lists[L_SYNC].size() + b.lists[L_HUFF].size();
-    st = ensure(sl.wgt, nrec * 16 + 64, sl.st);
+    b.ptime_off = b.pscans.empty() ? 0 : nrec * 16 + 64;  // per-scan {start, end} after the entropy records
+    st = ensure(sl.wgt, nrec * 16 + 64 + b.pscans.size() * 16, sl.st);
     if (st) return st;
     BatchFlags *bf = (BatchFlags *)(P + b.flags_off);
     bf->wgtime = (uint64_t)(uintptr_t)sl.wgt.p;
@@ -1725,6 +1716,117 @@ int Context::pick_slot() {
   }
   next_slot_ = (i + 1) % total;
   return i;
+}
+
+// Work items of the pipelined progressive launch (dg_prog.hip k_prog_scan).
+// Scans of one image that share no (component, coefficient band) never wait
+// on each other, so the connected groups of the dependency graph -- for a
+// colour file the DC scans, and the AC scans of each component -- can each
+// run back to back in one wave (a chain, ProgScan::next).  A chained scan
+// never waits: its deps ran before it in the same wave.  That is the whole
+// point: with one wave per scan, an image's later scans sit resident for its
+// whole duration waiting on their producers' rows (10 waves per image for
+// libjpeg's default script), and the batch's LDS-bound residency went to
+// waiting waves.  A group whose decode costs more than prog_chain % of the
+// batch's longest single scan (the long pole when every scan is pipelined)
+// keeps one wave per scan and the row pipeline, so chaining never lengthens
+// the batch.  Cost model: coded bytes + blocks / 2.  Items needing more than
+// one Huffman table in LDS (DC-first scans of several components) go last
+// (prog_dc_n) and run in a launch of their own with four tables.  Order:
+// pipelined scans first (image by image, largest first, each in level order:
+// a scan only ever waits on one with a lower ticket), then chains, costliest
+// first.
+void Context::plan_prog_items(Batch &b) {
+  auto &list = b.lists[L_PROG];
+  list.clear();
+  const uint32_t n = (uint32_t)b.pscans.size();
+  if (!n) return;
+  std::vector<double> cost(n);
+  double longest = 0;
+  for (uint32_t j = 0; j < n; j++) {
+    const ProgScan &sc = b.pscans[j];
+    const ImageDesc &d = b.descs[sc.image];
+    uint64_t blocks;
+    if (sc.ns == 1) {
+      const uint32_t c = sc.comp[0];
+      blocks = (uint64_t)((d.cdsw[c] + 7) / 8) * ((d.cdsh[c] + 7) / 8);
+    } else {
+      blocks = (uint64_t)d.mcux * d.mcuy * d.bpm;
+    }
+    cost[j] = (double)sc.len + 0.5 * (double)blocks;
+    longest = std::max(longest, cost[j]);
+  }
+  std::vector<uint32_t> par(n);
+  for (uint32_t j = 0; j < n; j++) par[j] = j;
+  auto find = [&](uint32_t x) {
+    while (par[x] != x) x = par[x] = par[par[x]];
+    return x;
+  };
+  for (uint32_t j = 0; j < n; j++)
+    for (uint64_t m = b.pscans[j].deps; m; m &= m - 1ull) {
+      const uint32_t e = b.pscans[j].first + (uint32_t)__builtin_ctzll(m), a = find(j), c = find(e);
+      if (a != c) par[std::max(a, c)] = std::min(a, c);
+    }
+  struct Group {
+    std::vector<uint32_t> scans;  // ascending: every dep of a scan comes before it
+    double cost = 0;
+    bool dc = false;
+  };
+  std::vector<Group> groups;
+  std::vector<int32_t> gi(n, -1);
+  for (uint32_t j = 0; j < n; j++) {
+    const uint32_t r = find(j);
+    if (gi[r] < 0) {
+      gi[r] = (int32_t)groups.size();
+      groups.emplace_back();
+    }
+    Group &g = groups[gi[r]];
+    const ProgScan &sc = b.pscans[j];
+    g.scans.push_back(j);
+    g.cost += cost[j];
+    g.dc |= (sc.ss == 0 && sc.ah == 0 ? sc.ns : (sc.ss == 0 ? 0u : 1u)) > 1;
+  }
+  const double limit = longest * (double)prog_chain_ / 100.0;
+  std::vector<uint32_t> split[2];            // pipelined scans, AC / DC launch
+  std::vector<std::pair<double, uint32_t>> chains[2];  // (cost, group)
+  std::vector<double> img_cost(b.descs.size(), 0.0);
+  for (uint32_t j = 0; j < n; j++) img_cost[b.pscans[j].image] += cost[j];
+  for (uint32_t g = 0; g < (uint32_t)groups.size(); g++) {
+    Group &G = groups[g];
+    if (prog_chain_ > 0 && G.cost <= limit) {
+      for (size_t i = 0; i < G.scans.size(); i++) {
+        ProgScan &sc = b.pscans[G.scans[i]];
+        sc.pflags |= kProgChained;
+        sc.next = i + 1 < G.scans.size() ? G.scans[i + 1] : kProgNoScan;
+      }
+      chains[G.dc].push_back({G.cost, g});
+    } else {
+      for (uint32_t j : G.scans) split[G.dc].push_back(j);
+    }
+  }
+  for (int dc = 0; dc < 2; dc++) {
+    std::stable_sort(split[dc].begin(), split[dc].end(), [&](uint32_t x, uint32_t y) {
+      const ProgScan &a = b.pscans[x], &c = b.pscans[y];
+      if (a.image != c.image) {
+        if (img_cost[a.image] != img_cost[c.image]) return img_cost[a.image] > img_cost[c.image];
+        return a.image < c.image;
+      }
+      if (a.level != c.level) return a.level < c.level;
+      return x < y;
+    });
+    std::stable_sort(chains[dc].begin(), chains[dc].end(),
+                     [](const auto &x, const auto &y) { return x.first > y.first; });
+  }
+  for (int dc = 0; dc < 2; dc++) {
+    for (uint32_t j : split[dc]) list.push_back(WgItem{b.pscans[j].image, j});
+    for (const auto &c : chains[dc]) {
+      const uint32_t j = groups[c.second].scans[0];
+      list.push_back(WgItem{b.pscans[j].image, j});
+    }
+  }
+  b.prog_dc_n = (uint32_t)(split[1].size() + chains[1].size());
+  stat_prog_items_ += list.size();
+  stat_prog_chains_ += chains[0].size() + chains[1].size();
 }
 
 dg_status Context::launch_all(Slot &sl, bool from_fix) {
@@ -1801,19 +1903,33 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   // (the main stream waits for it before the IDCT), except with stage timing
   // on, where every stage runs on the main stream so its events bracket it.
   const bool pside = side_stream_ && prog_side_ && !timing_ && !b.pscans.empty();
+  bool dc_side = false;  // DC items on the side stream, AC items on the main one
   if (!from_fix && !b.pscans.empty()) {
     hipStream_t pst = pside ? sl.side : sl.st;
     launch_prog_zero(pst, dd, lst(L_PROG_ZERO), cnt(L_PROG_ZERO));
     const ProgScan *ps = (const ProgScan *)(M + b.pscan_off);
     const uint32_t prog_dbg = ((uint32_t)(debug_flags_ >> 19) & 1u) << 1;  // forced wait timeouts (tests)
+    uint64_t *pt = b.ptime_off ? (uint64_t *)((char *)sl.wgt.p + b.ptime_off) : nullptr;
     if (prog_pipe_) {
+      // AC items (one Huffman table in LDS) and DC items (four) in launches of
+      // their own; no scan of one waits on a scan of the other
       uint32_t *pf = (uint32_t *)((char *)sl.scratch.p + b.pf_off);
-      HIPCHK(hipMemsetAsync(pf, 0, (size_t)(b.pf_n + 1) * 4, pst));
-      launch_prog_scan(pst, dd, ps, lst(L_PROG), cnt(L_PROG), hp, (prog_serial_ ? 1u : 0u) | prog_dbg, pf);
+      HIPCHK(hipMemsetAsync(pf, 0, (size_t)(b.pf_n + 2) * 4, pst));
+      const uint32_t nac = cnt(L_PROG) - b.prog_dc_n, sflags = (prog_serial_ ? 1u : 0u) | prog_dbg;
+      hipStream_t dst = pst;
+      if (!pside && side_stream_ && !timing_ && b.prog_dc_n && nac) {  // DC items beside the AC launch
+        HIPCHK(hipEventRecord(sl.ev_zero, pst));
+        HIPCHK(hipStreamWaitEvent(sl.side, sl.ev_zero, 0));
+        dst = sl.side;
+        dc_side = true;
+      }
+      launch_prog_scan(pst, dd, ps, lst(L_PROG), nac, hp, sflags, pf, pf, pt, 1);
+      launch_prog_scan(dst, dd, ps, lst(L_PROG) + nac, b.prog_dc_n, hp, sflags, pf, pf + b.pf_n + 1, pt, 4);
+      if (dc_side) HIPCHK(hipEventRecord(sl.ev_prog, sl.side));
     } else {
       uint32_t at = 0;
       for (uint32_t nl : b.prog_level_n) {
-        launch_prog_scan(pst, dd, ps, lst(L_PROG) + at, nl, hp, prog_serial_ ? 1u : 0u, nullptr);
+        launch_prog_scan(pst, dd, ps, lst(L_PROG) + at, nl, hp, prog_serial_ ? 1u : 0u, nullptr, nullptr, pt, 4);
         at += nl;
       }
     }
@@ -1835,7 +1951,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     launch_huff_write(sl.st, dm, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots, qp, (uint32_t)write_pair_);
   if (next()) return DG_ERR_DEVICE;
   if (next()) return DG_ERR_DEVICE;  // coeffs (side stream)
-  if (pside) HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_prog, 0));  // progressive coefficients
+  if (pside || dc_side) HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_prog, 0));  // progressive coefficients
   if (b.any_fused) launch_idct_list(sl.st, dd, qp, fl, std::min<uint32_t>(2048u, (b.idct_cap + 31) / 32));
   launch_idct(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);
   if (next()) return DG_ERR_DEVICE;
@@ -1934,6 +2050,25 @@ dg_status Context::finish(Slot &sl) {
     stat_resync_++;
     dg_status st = launch_all(sl, true);
     if (st) return st;
+  }
+  if (b.ptime_off) {  // debug: one line per progressive scan (option wg_timing, env DG_PROG_DUMP)
+    std::vector<uint64_t> rec(2 * b.pscans.size());
+    HIPCHK(hipMemcpy(rec.data(), (char *)sl.wgt.p + b.ptime_off, rec.size() * 8, hipMemcpyDeviceToHost));
+    if (const char *dump = getenv("DG_PROG_DUMP")) {
+      if (FILE *f = fopen(dump, "a")) {
+        uint64_t lo = ~0ull;
+        for (size_t i = 0; i < b.pscans.size(); i++) lo = std::min(lo, rec[2 * i]);
+        for (size_t i = 0; i < b.pscans.size(); i++) {
+          const ProgScan &sc = b.pscans[i];
+          const ImageDesc &d = b.descs[sc.image];
+          fprintf(f, "%zu %u %u %u %u %u %u %u %u %u %u %llu %llu %u %u\n", i, sc.image, sc.ns, sc.comp[0], sc.ss, sc.se,
+                  sc.ah, sc.al, sc.len, sc.level, (uint32_t)sc.pflags, (unsigned long long)(rec[2 * i] - lo),
+                  (unsigned long long)(rec[2 * i + 1] - lo), d.total_blocks, d.width * d.height);
+        }
+        fprintf(f, "end\n");
+        fclose(f);
+      }
+    }
   }
   if (b.flags.wgtime) {
     const size_t ns = b.lists[L_SYNC].size(), nw = b.lists[L_HUFF].size();

@@ -73,7 +73,9 @@ struct Batch {
   uint32_t uf_maxbpp = 1;   // widest filter unit of the batch's PNGs (k_png_unfilter's LDS)
   size_t uf_flags_off = 0;  // their flags + ticket in the scratch arena (zeroed per batch)
   uint32_t pf_n = 0;        // progressive scans (progress words, one pipelined k_prog_scan launch)
-  size_t pf_off = 0;        // ticket + progress words in the scratch arena (zeroed per batch)
+  size_t pf_off = 0;        // AC ticket, progress words, DC ticket in the scratch arena (zeroed per batch)
+  size_t ptime_off = 0;     // debug (wg_timing): per-scan {start, end} in the wgt buffer, 0 = none
+  uint32_t prog_dc_n = 0;   // the last prog_dc_n items of L_PROG need four Huffman tables (DC-first scans)
   std::vector<uint8_t> blob;
   size_t blob_off = 0;
   bool any_png = false, any_alpha = false, any_enc = false;
@@ -185,6 +187,7 @@ class Context {
   dg_status ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user = nullptr);
   dg_status upload_pools();
   dg_status launch_all(Slot &sl, bool from_fix);
+  void plan_prog_items(Batch &b);
   dg_status finish(Slot &sl);
   Slot *find(uint64_t ticket);
   int pick_slot();
@@ -259,6 +262,7 @@ class Context {
   bool progressive_ = false;            // option "progressive"
   bool prog_serial_ = false;            // option "prog_serial": serial reader for every scan (A/B)
   bool prog_pipe_ = true;               // option "prog_pipe": all scans in one pipelined launch (0: one launch per level)
+  int prog_chain_ = 100;                // option "prog_chain": chain dependency groups costing <= this % of the longest scan
   bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first
   bool entropy_once_ = false;           // option "entropy_once": decode-once staging + k_huff_scatter
   int64_t stat_png_serial_ = 0, stat_png_chunks_ = 0;
@@ -268,6 +272,7 @@ class Context {
   // stats
   int64_t stat_batches_ = 0, stat_resync_ = 0, stat_fix_ = 0, stat_mismatch_ = 0, stat_iters_ = 0;
   int64_t stat_unsettled_ = 0, stat_pool_flush_ = 0;
+  int64_t stat_prog_items_ = 0, stat_prog_chains_ = 0;  // pipelined progressive launches: work items, chains
   std::vector<float> last_ms_;
   std::mutex reg_mu_;
   std::vector<std::pair<uintptr_t, size_t>> registered_;  // dg_host_register ranges

@@ -62,13 +62,18 @@ void launch_band_dec(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
 // final copy / gray->RGB expansion: 256 output pixels per workgroup
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 // progressive JPEG (dg_prog.hip): zero coefficients (kProgZeroBytes per
-// workgroup), then one wave per scan: all scans in one launch with pflags
-// (zeroed, 1 + scans words; dg_types.h ProgScan), or one level per launch
-// with pflags null.  serial bit 0: serial bit reader for every scan; bit 1 (test
-// switch): every scan with dependencies times out on its first wait
+// workgroup), then one wave per work item (a scan, or a chain of scans linked
+// by ProgScan::next): pipelined launches with pflags (progress words, zeroed,
+// 1 + scans; dg_types.h ProgScan) and ticket (a zeroed counter handing out the
+// items in list order), or one level per launch with both null.  ntab: Huffman
+// tables in LDS (1: AC scans only; 4: any scan).  ptime (debug, may be null):
+// {start, end} s_memrealtime per scan.  serial bit 0: serial bit reader for
+// every scan; bit 1 (test switch): every scan with unchained dependencies
+// times out on its first wait
 void launch_prog_zero(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 void launch_prog_scan(hipStream_t st, const ImageDesc *imgs, const ProgScan *scans, const WgItem *list, uint32_t n,
-                      const HuffTable *pool, uint32_t serial, uint32_t *pflags);
+                      const HuffTable *pool, uint32_t serial, uint32_t *pflags, uint32_t *ticket, uint64_t *ptime,
+                      int ntab);
 
 }  // namespace dg
 

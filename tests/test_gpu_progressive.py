@@ -176,6 +176,7 @@ def test_progressive_wait_timeout_is_unsupported_and_isolated():
     L = _lib()
     ctx = L.Context(0)
     ctx.set_option("progressive", 1)
+    ctx.set_option("prog_chain", 0)  # every scan its own wave: chained scans never wait
     prog = [_prog(4701, 300, 200), _prog(4702, 640, 480, 90, "4:4:4")]
     base = [synth.make_jpeg(4703, 320, 240), synth.make_jpeg(4704, 123, 77, 70, "4:2:2")]
     ctx.set_option("debug_flags", DBG_FORCE_PROG_TIMEOUT)
@@ -189,3 +190,28 @@ def test_progressive_wait_timeout_is_unsupported_and_isolated():
         ost, ref = O.jpeg_decode(d)
         assert np.array_equal(arr.reshape(ref.shape), ref)
     assert all(r[0] == 0 for r in ctx.decode_batch(prog))
+
+
+@pytest.mark.parametrize("chain", [0, 100, 100000])
+def test_progressive_chains_bit_exact(chain):
+    """Work items of the pipelined launch (option prog_chain): every scan its
+    own wave (0), the default (dependency groups chained in one wave unless
+    they cost more than the batch's longest scan, so the largest image stays
+    pipelined), and every group chained (100000).  The outputs are the
+    oracle's in every mode, gray and colour, with and without restarts
+    (restart scans use the serial reader inside a chain too)."""
+    L = _lib()
+    ctx = L.Context(0)
+    ctx.set_option("progressive", 1)
+    ctx.set_option("prog_chain", chain)
+    datas = [_prog(4801, 1700, 1300, 93)] + _cases(48, 14, 420)
+    res = ctx.decode_batch(datas)
+    for i, (data, (st, arr, _)) in enumerate(zip(datas, res)):
+        assert st == 0, (i, L.last_error())
+        ost, ref = O.jpeg_decode(data)
+        assert np.array_equal(arr.reshape(ref.shape), ref), i
+    items, chains = ctx.stat("prog_items"), ctx.stat("prog_chains")
+    if chain == 0:
+        assert chains == 0
+    else:
+        assert 0 < chains <= items
