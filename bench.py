@@ -107,6 +107,10 @@ def parse():
                          "not the headline config)")
     ap.add_argument("--progressive-frac", type=float, default=0.0,
                     help="jpeg workload: share of the pool written as progressive JPEGs (not the headline config)")
+    ap.add_argument("--no-prog-split", action="store_true",
+                    help="progressive-frac runs: dg_wait every batch whole (no dg_wait_ready / deferred completion)")
+    ap.add_argument("--prog-ring", type=int, default=4096,
+                    help="progressive-frac runs: output slots for progressive members awaiting completion")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     if a.pool <= 0:
@@ -634,6 +638,22 @@ def main() -> int:
             return seq[k * B_:(k + 1) * B_]
         return [(k * B_ + j) % len(pool) for j in range(B_)]
 
+    # Progressive members of a submission run in the library's progressive
+    # aggregate (datago_hip.h dg_wait_ready): the loop waits for the other
+    # members only (dg_wait_ready) and completes a batch's progressive members
+    # later (dg_wait), so their outputs live in a ring of their own, reused
+    # once the batch that held a slot is complete.  Everything is complete
+    # before the timed region ends.
+    split = a.progressive_frac > 0 and not a.no_prog_split
+    prog_of = [synth.is_progressive_jpeg(d) for d in pool] if split else [False] * len(pool)
+    ring = {"next": 0, "owner": [], "done": set(), "deferred": []}
+    if split:
+        ring_sz = max([(out_bytes[i] + 15) // 16 * 16 for i in range(len(pool)) if prog_of[i]] or [16])
+        ring["n"] = a.prog_ring
+        ring["size"] = ring_sz
+        ring["base"] = ctx.alloc(a.prog_ring * ring_sz)
+        ring["owner"] = [-1] * a.prog_ring
+
     def submit(k: int):
         idx = batch_idx(k)
         hp = [h_base + offs[i] for i in idx]
@@ -642,36 +662,70 @@ def main() -> int:
         outs, caps, oo = [], [], 0
         slot = k % a.inflight  # one output arena per batch in flight
         for i in idx:
-            outs.append(d_out[slot] + oo)
+            if prog_of[i]:
+                r = ring["next"] % ring["n"]
+                ring["next"] += 1
+                while ring["owner"][r] >= 0 and ring["owner"][r] not in ring["done"]:
+                    finish_deferred(ring["deferred"].pop(0))  # oldest first
+                ring["owner"][r] = k
+                outs.append(ring["base"] + r * ring["size"])
+            else:
+                outs.append(d_out[slot] + oo)
+                oo += (out_bytes[i] + 15) // 16 * 16
             caps.append(out_bytes[i])
-            oo += (out_bytes[i] + 15) // 16 * 16
         ticket, metas = ctx.submit_device(hp, dp, lens, outs, caps, [forced_pool[i] for i in idx])
-        return ticket, metas, idx
+        return ticket, metas, idx, k
+
+    def check(metas, idx, which):
+        for j, i in enumerate(idx):
+            if which(i) and metas[j].status != 0:
+                raise RuntimeError(f"image {i} status {metas[j].status}: {L.last_error()}")
 
     def complete(pend):
-        ticket, metas, idx = pend
+        ticket, metas, idx, k = pend
         ctx.wait(ticket)
-        for j, i in enumerate(idx):
-            if metas[j].status != 0:
-                raise RuntimeError(f"image {i} status {metas[j].status}: {L.last_error()}")
+        check(metas, idx, lambda i: True)
+        ring["done"].add(k)
         return idx
+
+    def finish_deferred(pend, on_done=None):
+        ticket, metas, idx, k = pend
+        ctx.wait(ticket)
+        check(metas, idx, lambda i: prog_of[i])
+        ring["done"].add(k)
+        if on_done or ring.get("on_done"):
+            (on_done or ring["on_done"])([i for i in idx if prog_of[i]])
+
+    def ready(pend):  # split mode: the batch's other members; its progressive ones later
+        ticket, metas, idx, k = pend
+        ctx.wait_ready(ticket)
+        check(metas, idx, lambda i: not prog_of[i])
+        if any(prog_of[i] for i in idx):
+            ring["deferred"].append(pend)
+        else:
+            ring["done"].add(k)
+        return [i for i in idx if not prog_of[i]]
 
     host_s = {"submit": 0.0}
 
     def run(k0: int, n: int, on_done=None):
         pend = []  # batch k + inflight - 1 is submitted before batch k is waited on
+        done_fn = ready if split else complete
+        ring["on_done"] = on_done
         for k in range(k0, k0 + n):
             ts = time.perf_counter()
             pend.append(submit(k))
             host_s["submit"] += time.perf_counter() - ts
             if len(pend) >= a.inflight:
-                idx = complete(pend.pop(0))
+                idx = done_fn(pend.pop(0))
                 if on_done:
                     on_done(idx)
         while pend:
-            idx = complete(pend.pop(0))
+            idx = done_fn(pend.pop(0))
             if on_done:
                 on_done(idx)
+        while ring["deferred"]:
+            finish_deferred(ring["deferred"].pop(0))
 
     run(0, max(1, a.warmup))
     host_s["submit"] = 0.0

@@ -35,7 +35,7 @@ EXPORTS = [
     "dg_bucket_table_build", "dg_bucket_table_free", "dg_bucket_count", "dg_bucket_get",
     "dg_closest_bucket", "dg_bucket_find_key", "dg_aspect_ratio_to_str", "dg_probe",
     "dg_ctx_create", "dg_ctx_destroy", "dg_ctx_buckets", "dg_output_size", "dg_submit", "dg_wait",
-    "dg_poll", "dg_decode_one", "dg_submit_device", "dg_device_alloc", "dg_device_free",
+    "dg_poll", "dg_wait_ready", "dg_decode_one", "dg_submit_device", "dg_device_alloc", "dg_device_free",
     "dg_memcpy_h2d", "dg_memcpy_d2h", "dg_synchronize", "dg_last_batch_timings",
     "dg_ctx_set_option", "dg_ctx_get_stat", "dg_last_error", "dg_abi_version", "dg_sample_align",
     "dg_wds_index", "dg_wds_key_hash", "dg_host_register", "dg_host_unregister",
@@ -107,6 +107,7 @@ def load() -> ctypes.CDLL:
                                    ctypes.POINTER(u64), ctypes.POINTER(PayloadMeta), ctypes.POINTER(u64)]
     L.dg_wait.argtypes = [vp, u64]
     L.dg_poll.argtypes = [vp, u64]
+    L.dg_wait_ready.argtypes = [vp, u64, ctypes.POINTER(i32)]
     L.dg_decode_one.argtypes = [vp, ctypes.c_char_p, sz, i32, vp, u64, ctypes.POINTER(PayloadMeta)]
     L.dg_device_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
     L.dg_device_free.argtypes = [vp, vp]
@@ -422,6 +423,16 @@ class Context:
 
     def wait(self, ticket: int) -> None:
         _check(load().dg_wait(self._h, ticket))
+
+    def wait_ready(self, ticket: int) -> int:
+        """dg_wait_ready: every non-progressive member done; returns how many
+        progressive members still run (complete them with wait(ticket))."""
+        pend = ctypes.c_int32()
+        _check(load().dg_wait_ready(self._h, ticket, ctypes.byref(pend)))
+        return pend.value
+
+    def poll(self, ticket: int) -> int:
+        return load().dg_poll(self._h, ticket)
 
     def submit_host(self, datas: Sequence[bytes], outs: Sequence[np.ndarray], forced=None):
         """Asynchronous host-in / host-out batch (dg_submit) into caller-owned

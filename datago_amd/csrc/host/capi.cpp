@@ -197,18 +197,21 @@ dg_status dg_output_size(dg_ctx *ctx, const uint8_t *bytes, size_t len, int32_t 
 dg_status dg_submit(dg_ctx *ctx, int32_t n, const uint8_t *const *srcs, const size_t *lens, const int32_t *forced,
                     uint8_t *const *outs, const uint64_t *caps, dg_payload_meta *metas, uint64_t *ticket) {
   if (!ctx || !ticket) return DG_ERR_INVALID;
-  return ctx->c.submit(n, srcs, nullptr, lens, forced, outs, caps, metas, true, ticket);
+  return ctx->c.submit_user(n, srcs, nullptr, lens, forced, outs, caps, metas, true, ticket);
 }
 
 dg_status dg_submit_device(dg_ctx *ctx, int32_t n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs,
                            const size_t *lens, const int32_t *forced, uint8_t *const *d_outs,
                            const uint64_t *caps, dg_payload_meta *metas, uint64_t *ticket) {
   if (!ctx || !ticket || (n > 0 && !d_srcs)) return DG_ERR_INVALID;
-  return ctx->c.submit(n, h_srcs, d_srcs, lens, forced, d_outs, caps, metas, false, ticket);
+  return ctx->c.submit_user(n, h_srcs, d_srcs, lens, forced, d_outs, caps, metas, false, ticket);
 }
 
-dg_status dg_wait(dg_ctx *ctx, uint64_t ticket) { return ctx ? ctx->c.wait(ticket) : DG_ERR_INVALID; }
-dg_status dg_poll(dg_ctx *ctx, uint64_t ticket) { return ctx ? ctx->c.poll(ticket) : DG_ERR_INVALID; }
+dg_status dg_wait(dg_ctx *ctx, uint64_t ticket) { return ctx ? ctx->c.wait_user(ticket) : DG_ERR_INVALID; }
+dg_status dg_poll(dg_ctx *ctx, uint64_t ticket) { return ctx ? ctx->c.poll_user(ticket) : DG_ERR_INVALID; }
+dg_status dg_wait_ready(dg_ctx *ctx, uint64_t ticket, int32_t *pending) {
+  return ctx ? ctx->c.wait_ready(ticket, pending) : DG_ERR_INVALID;
+}
 
 dg_status dg_decode_one(dg_ctx *ctx, const uint8_t *src, size_t len, int32_t forced, uint8_t *out, uint64_t cap,
                         dg_payload_meta *meta) {

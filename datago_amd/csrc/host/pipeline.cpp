@@ -163,6 +163,7 @@ dg_status Context::init() {
     sl.ev.resize(kNumStages + 1);
     for (auto &e : sl.ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    if (&sl - slots_ >= kMaxInflight) continue;  // progressive slots: make_prog_streams below
     HIPCHK(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&sl.side, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_meta, hipEventDisableTiming));
@@ -171,6 +172,39 @@ dg_status Context::init() {
     HIPCHK(hipEventCreateWithFlags(&sl.ev_prog, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_png0, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_png1, hipEventDisableTiming));
+  }
+  return make_prog_streams();
+}
+
+// Streams of the progressive slots (option "prog_queue").  A progressive
+// batch holds its stream for ~0.1-1 s; HIP maps streams onto the process's
+// few hardware queues (GPU_MAX_HW_QUEUES, 4), and kernels behind it in the
+// same queue wait for it -- a baseline slot's stream sharing that queue then
+// stalls behind the refinement chains.  0: plain streams; 1 / 2: highest /
+// lowest priority; 3: a CU mask over every CU (a masked stream gets a
+// hardware queue of its own).
+dg_status Context::make_prog_streams() {
+  HIPCHK(hipSetDevice(device_));
+  int least = 0, greatest = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  for (int j = 0; j < kProgSlots; j++) {
+    Slot &sl = slots_[kMaxInflight + j];
+    for (hipStream_t *q : {&sl.st, &sl.side}) {
+      if (*q) {
+        HIPCHK(hipStreamSynchronize(*q));
+        HIPCHK(hipStreamDestroy(*q));
+        *q = nullptr;
+      }
+      if (prog_queue_ == 1 || prog_queue_ == 2) {
+        HIPCHK(hipStreamCreateWithPriority(q, hipStreamNonBlocking, prog_queue_ == 1 ? greatest : least));
+      } else if (prog_queue_ == 3) {
+        std::vector<uint32_t> mask((ncu_ + 31) / 32, 0xFFFFFFFFu);
+        if (ncu_ % 32) mask.back() = (1u << (ncu_ % 32)) - 1u;
+        HIPCHK(hipExtStreamCreateWithCUMask(q, (uint32_t)mask.size(), mask.data()));
+      } else {
+        HIPCHK(hipStreamCreateWithFlags(q, hipStreamNonBlocking));
+      }
+    }
   }
   return DG_OK;
 }
@@ -330,16 +364,48 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "progressive") {
-    // Progressive JPEGs on the GPU (dg_prog.hip).  Off by default: a
-    // refinement scan decodes serially in one wave, so one large progressive
-    // image holds its whole batch for ~0.1-2 s; the default
-    // returns DG_ERR_UNSUPPORTED and the caller's CPU decoder takes them.
+    // Progressive JPEGs on the GPU (dg_prog.hip; default on).  A refinement
+    // scan decodes serially in one wave, so a large file takes ~0.1-1 s: the
+    // progressive members of a submission run apart from the rest (prog_split)
+    // in aggregate batches on slots of their own.  0: DG_ERR_UNSUPPORTED (the
+    // caller's CPU decoder takes them).
     progressive_ = v != 0;
     return DG_OK;
   }
-  if (k == "prog_lanes") {  // progressive batches in flight beside the baseline ones (dg_decode_one); 0: mixed in
-    if (v < 0 || v > kMaxInflight - 1) return DG_ERR_INVALID;
+  if (k == "prog_lanes") {  // dg_decode_one: progressive batches in flight on the progressive slots; 0: mixed in
+    if (v < 0 || v > kProgSlots) return DG_ERR_INVALID;
     prog_lanes_ = (int)v;
+    return DG_OK;
+  }
+  if (k == "prog_queue") {  // progressive slots' streams: 0 plain, 1 high / 2 low priority, 3 CU-masked
+    if (v < 0 || v > 3) return DG_ERR_INVALID;
+    {
+      std::lock_guard<std::mutex> lk(pmu_);
+      if (!pagg_.empty()) flush_pagg_locked();
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int j = 0; j < kProgSlots; j++) {
+      Slot &sl = slots_[kMaxInflight + j];
+      if (sl.batch && !sl.batch->done) {
+        dg_status st = finish(sl);
+        if (st) return st;
+      }
+    }
+    prog_queue_ = (int)v;
+    return make_prog_streams();
+  }
+  if (k == "prog_split") {  // dg_submit: progressive members into the progressive aggregate (0: decoded in the batch)
+    prog_split_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "prog_batch") {  // progressive aggregate: launched once it holds this many images
+    if (v < 1 || v > 65536) return DG_ERR_INVALID;
+    prog_batch_ = (int)v;
+    return DG_OK;
+  }
+  if (k == "prog_flush_us") {  // ... or once it is this old at a submit / poll / wait_ready
+    if (v < 0 || v > 100000000) return DG_ERR_INVALID;
+    prog_flush_us_ = (int)v;
     return DG_OK;
   }
   if (k == "sync_pair") {  // k_huff_sync: a second AC symbol per single step from the same peek (A/B)
@@ -457,6 +523,8 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "write_mismatch") return stat_mismatch_;
   if (k == "unsettled_batches") return stat_unsettled_;
   if (k == "prog_items") return stat_prog_items_;
+  if (k == "prog_aggregates") return stat_prog_aggs_;
+  if (k == "prog_aggregate_images") return stat_prog_agg_images_;
   if (k == "prog_chains") return stat_prog_chains_;
   if (k == "pool_flushes") return stat_pool_flush_;
   if (k == "sync_iters_max") return stat_iters_;
@@ -550,7 +618,7 @@ static constexpr size_t kPoolKeep = 4096;
 static constexpr size_t kPoolMax = 65535;
 
 dg_status Context::flush_pools() {
-  for (int s = 0; s < kMaxInflight; s++) {  // batches in flight still read (and may resync with) the pools
+  for (int s = 0; s < kAllSlots; s++) {  // batches in flight still read (and may resync with) the pools
     Slot &o = slots_[s];
     if (o.batch && !o.batch->done) {
       dg_status st = finish(o);
@@ -739,14 +807,15 @@ struct Layout {
 
 dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
                           const int32_t *forced, uint8_t *const *outs, const uint64_t *caps,
-                          dg_payload_meta *metas, bool host_io, uint64_t *ticket) {
+                          dg_payload_meta *metas, bool host_io, uint64_t *ticket, dg_payload_meta *const *mptrs,
+                          int force_slot) {
   std::lock_guard<std::mutex> lk(mu_);
-  if (n < 0 || (n > 0 && (!h_srcs || !lens || !outs || !caps || !metas))) {
+  if (n < 0 || (n > 0 && (!h_srcs || !lens || !outs || !caps || (!metas && !mptrs)))) {
     set_error("null argument");
     return DG_ERR_INVALID;
   }
   HIPCHK(hipSetDevice(device_));
-  Slot &sl = slots_[pick_slot()];
+  Slot &sl = slots_[force_slot >= 0 ? force_slot : pick_slot()];
   if (sl.batch && !sl.batch->done) {  // this slot's previous batch must complete first
     dg_status st = finish(sl);
     if (st) return st;
@@ -758,7 +827,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   HIPCHK(hipEventCreateWithFlags(&b.fin->e, hipEventDisableTiming));
   b.n = n;
   b.host_io = host_io;
-  b.metas = metas;
+  b.mptr.resize(n);
+  for (int i = 0; i < n; i++) b.mptr[i] = mptrs ? mptrs[i] : &metas[i];
   b.plans.resize(n);
   b.desc_of.assign(n, -1);
   auto phase_t0 = std::chrono::steady_clock::now();
@@ -771,7 +841,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   for (int i = 0; i < n; i++) plan_image(h_srcs[i], lens[i], forced ? forced[i] : -1, b.plans[i]);
   for (int i = 0; i < n; i++) {
     ImagePlan &p = b.plans[i];
-    dg_payload_meta &m = metas[i];
+    dg_payload_meta &m = *b.mptr[i];
     memset(&m, 0, sizeof(m));
     m.status = p.status;
     m.bucket = p.bucket;
@@ -820,10 +890,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     }
     if (worst == -2) {
       p.status = DG_ERR_UNSUPPORTED;
-      metas[i].status = DG_ERR_UNSUPPORTED;
+      b.mptr[i]->status = DG_ERR_UNSUPPORTED;
     } else if (worst < 0) {
       p.status = DG_ERR_CORRUPT;
-      metas[i].status = DG_ERR_CORRUPT;
+      b.mptr[i]->status = DG_ERR_CORRUPT;
     }
   }
   dg_status st = upload_pools();
@@ -1702,20 +1772,28 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
 }
 
 // A slot for the next batch: the next in turn, whose batch the caller then
-// finishes first.  With progressive lanes (dg_decode_one), a slot still busy
-// with its batch -- possibly a long progressive one -- is passed over for an
-// idle slot, so baseline batches keep cycling while it runs.  (Idle-first for
-// every batch measured 4% slower on the PNG workload: out-of-turn reuse.)
+// finishes first.  Progressive batches have slots of their own
+// (pick_prog_slot), so every baseline slot cycles at the baseline pace.
 int Context::pick_slot() {
-  const int total = std::min(kMaxInflight, nslots_ + (progressive_ ? prog_lanes_ : 0));
-  int i = next_slot_ % total;
-  const Slot &s = slots_[i];
-  if (progressive_ && prog_lanes_ > 0 && s.batch && !s.batch->done && hipEventQuery(s.done) != hipSuccess) {
-    for (int j = 0; j < total; j++)
-      if (!slots_[j].batch || slots_[j].batch->done) return j;
-  }
-  next_slot_ = (i + 1) % total;
+  const int i = next_slot_ % nslots_;
+  next_slot_ = (i + 1) % nslots_;
   return i;
+}
+
+// A progressive slot: the first idle one, else the next in turn (whose batch
+// the caller then waits for: backpressure on the progressive lane only).
+int Context::pick_prog_slot() {
+  for (int j = 0; j < kProgSlots; j++) {
+    const int k = kMaxInflight + (next_pslot_ + j) % kProgSlots;
+    const Slot &s = slots_[k];
+    if (!s.batch || s.batch->done || hipEventQuery(s.done) == hipSuccess) {
+      next_pslot_ = (next_pslot_ + j + 1) % kProgSlots;
+      return k;
+    }
+  }
+  const int k = kMaxInflight + next_pslot_;
+  next_pslot_ = (next_pslot_ + 1) % kProgSlots;
+  return k;
 }
 
 // Work items of the pipelined progressive launch (dg_prog.hip k_prog_scan).
@@ -2160,10 +2238,10 @@ dg_status Context::finish(Slot &sl) {
     }
     if (!status && b.unsettled && b.plans[i].fmt == kFmtJpeg && !b.plans[i].hdr.progressive)
       status = DG_ERR_UNSUPPORTED;
-    if (status) b.metas[i].status = status;
+    if (status) b.mptr[i]->status = status;
     if (b.plans[i].encode) {
       const uint32_t nb = back[b.desc_of[i]].enc.enc_bytes;
-      b.metas[i].nbytes = nb;
+      b.mptr[i]->nbytes = nb;
       if (b.host_io && !status && nb) copies.push_back({b.host_outs[i], (char *)sl.out.p + b.enc_host_off[i], nb});
       continue;
     }
@@ -2206,7 +2284,7 @@ dg_status Context::wait(uint64_t ticket) {
   return finish(*sl);
 }
 
-dg_status Context::flush_batch(std::vector<OneReq *> &batch) {
+dg_status Context::flush_batch(std::vector<OneReq *> &batch, bool prog) {
   const int n = (int)batch.size();
   std::vector<const uint8_t *> srcs(n);
   std::vector<size_t> lens(n);
@@ -2222,8 +2300,13 @@ dg_status Context::flush_batch(std::vector<OneReq *> &batch) {
     caps[i] = batch[i]->cap;
   }
   uint64_t t = 0;
+  int slot = -1;
+  if (prog) {
+    std::lock_guard<std::mutex> lk(mu_);
+    slot = pick_prog_slot();
+  }
   dg_status st = submit(n, srcs.data(), nullptr, lens.data(), forced.data(), outs.data(), caps.data(), metas.data(),
-                        true, &t);
+                        true, &t, nullptr, slot);
   if (!st) st = wait(t);
   for (int i = 0; i < n; i++) {
     *batch[i]->meta = metas[i];
@@ -2237,7 +2320,7 @@ dg_status Context::decode_one(const uint8_t *src, size_t len, int32_t forced, ui
   OneReq r{src, len, forced, out, cap, meta, false, DG_OK, false};
   if (coalesce_max_ <= 1) {
     std::vector<OneReq *> one{&r};
-    flush_batch(one);
+    flush_batch(one, false);
     return r.st;
   }
   // Progressive JPEGs decode their scans serially (one wave per scan, ~0.1-1 s
@@ -2270,7 +2353,7 @@ dg_status Context::decode_one(const uint8_t *src, size_t len, int32_t forced, ui
       stat_coalesced_batches_++;
       stat_coalesced_images_ += (int64_t)batch.size();
       lk.unlock();
-      flush_batch(batch);
+      flush_batch(batch, r.prog);
       lk.lock();
       for (OneReq *x : batch) x->done = true;
       (r.prog ? pinflight_ : inflight_)--;
@@ -2294,6 +2377,210 @@ dg_status Context::poll(uint64_t ticket) {
   if (!sl || sl->batch->done) return DG_OK;
   hipError_t e = hipEventQuery(sl->done);
   if (e == hipErrorNotReady) return DG_ERR_NOT_READY;
+  return DG_OK;
+}
+
+// ---- progressive split (dg_submit / dg_submit_device / dg_wait / dg_poll / dg_wait_ready)
+//
+// A refinement scan is one serial chain (dg_prog.hip): a large progressive
+// file takes ~0.1-1 s, and a batch lasts as long as its longest chain.  So a
+// submission with progressive members is split: its other members run as a
+// batch of their own (back at the baseline pace), and its progressive members
+// join the open progressive aggregate, which is submitted as one batch on a
+// progressive slot once it holds prog_batch images, once it is older than
+// prog_flush_us at a submit / poll / wait_ready, or as soon as a caller blocks
+// on one of its members (dg_wait).  An aggregate of ~1024 files keeps
+// thousands of scan chains in flight at once, where a 256-image batch with a
+// few progressive members idles the GPU behind one chain.  dg_wait(ticket)
+// completes both parts (the ABI's contract is unchanged); dg_wait_ready
+// returns once the non-progressive part is done and leaves the progressive
+// members' metas at DG_ERR_NOT_READY until a later dg_wait(ticket).
+
+// Launch the open aggregate early (before prog_batch images) only when it is
+// older than prog_flush_us AND a progressive slot is idle: while both run,
+// the aggregate keeps growing (a larger launch hides more of its long pole).
+bool Context::pagg_stale_locked() {
+  if (pagg_.empty() || std::chrono::steady_clock::now() - pagg_t0_ < std::chrono::microseconds(prog_flush_us_))
+    return false;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int j = 0; j < kProgSlots; j++) {
+    const Slot &sl = slots_[kMaxInflight + j];
+    if (!sl.batch || sl.batch->done || hipEventQuery(sl.done) == hipSuccess) return true;
+  }
+  return false;
+}
+
+dg_status Context::flush_pagg_locked() {
+  if (pagg_.empty()) return DG_OK;
+  const int n = (int)pagg_.size();
+  std::vector<const uint8_t *> h(n), d(n);
+  std::vector<size_t> lens(n);
+  std::vector<int32_t> forced(n);
+  std::vector<uint8_t *> outs(n);
+  std::vector<uint64_t> caps(n);
+  std::vector<dg_payload_meta *> mp(n);
+  for (int i = 0; i < n; i++) {
+    const PEntry &e = pagg_[i];
+    h[i] = e.host.data();
+    d[i] = e.dsrc;
+    lens[i] = e.len;
+    forced[i] = e.forced;
+    outs[i] = e.out;
+    caps[i] = e.cap;
+    mp[i] = e.meta;
+  }
+  int slot;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    slot = pick_prog_slot();
+  }
+  uint64_t t = 0;
+  dg_status st = submit(n, h.data(), pagg_host_ ? nullptr : d.data(), lens.data(), forced.data(), outs.data(),
+                        caps.data(), nullptr, pagg_host_, &t, mp.data(), slot);
+  if (st) {
+    for (PEntry &e : pagg_) e.meta->status = st;
+    t = 0;
+  }
+  stat_prog_aggs_++;
+  stat_prog_agg_images_ += n;
+  pgen_[pagg_gen_] = {t, pagg_refs_};
+  pagg_refs_ = 0;
+  pagg_gen_++;
+  pagg_.clear();
+  return st;
+}
+
+dg_status Context::submit_user(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
+                               const int32_t *forced, uint8_t *const *outs, const uint64_t *caps,
+                               dg_payload_meta *metas, bool host_io, uint64_t *ticket) {
+  if (!ticket) return DG_ERR_INVALID;
+  std::vector<uint8_t> isp(n > 0 ? n : 0, 0);
+  int np = 0;
+  if (progressive_ && prog_split_ && n > 0 && h_srcs && lens && outs && caps && metas && (host_io || d_srcs))
+    for (int i = 0; i < n; i++) {
+      isp[i] = h_srcs[i] && jpeg_sniff_progressive(h_srcs[i], lens[i]) ? 1 : 0;
+      np += isp[i];
+    }
+  if (!np) {
+    dg_status st = submit(n, h_srcs, d_srcs, lens, forced, outs, caps, metas, host_io, ticket);
+    std::lock_guard<std::mutex> lk(pmu_);
+    if (pagg_stale_locked()) flush_pagg_locked();
+    return st;
+  }
+  SplitRec rec;
+  if (np < n) {  // the other members: a batch of their own
+    std::vector<const uint8_t *> h, d;
+    std::vector<size_t> ln;
+    std::vector<int32_t> fb;
+    std::vector<uint8_t *> ou;
+    std::vector<uint64_t> cp;
+    std::vector<dg_payload_meta *> mp;
+    for (int i = 0; i < n; i++) {
+      if (isp[i]) continue;
+      h.push_back(h_srcs[i]);
+      d.push_back(d_srcs ? d_srcs[i] : nullptr);
+      ln.push_back(lens[i]);
+      fb.push_back(forced ? forced[i] : -1);
+      ou.push_back(outs[i]);
+      cp.push_back(caps[i]);
+      mp.push_back(&metas[i]);
+    }
+    dg_status st = submit((int)h.size(), h.data(), host_io ? nullptr : d.data(), ln.data(), fb.data(), ou.data(),
+                          cp.data(), nullptr, host_io, &rec.tb, mp.data());
+    if (st) return st;
+  }
+  std::lock_guard<std::mutex> lk(pmu_);
+  if (!pagg_.empty() && pagg_host_ != host_io) flush_pagg_locked();  // an aggregate is host- or device-fed
+  if (pagg_.empty()) pagg_t0_ = std::chrono::steady_clock::now();
+  pagg_host_ = host_io;
+  for (int i = 0; i < n; i++) {
+    if (!isp[i]) continue;
+    PEntry e;
+    e.host.assign(h_srcs[i], h_srcs[i] + lens[i]);  // the caller's host bytes are only valid during the call
+    e.dsrc = host_io ? nullptr : d_srcs[i];
+    e.len = lens[i];
+    e.forced = forced ? forced[i] : -1;
+    e.out = outs[i];
+    e.cap = caps[i];
+    e.meta = &metas[i];
+    memset(e.meta, 0, sizeof(*e.meta));
+    e.meta->status = DG_ERR_NOT_READY;
+    e.meta->bucket = -1;
+    pagg_.push_back(std::move(e));
+  }
+  rec.gen = pagg_gen_;
+  rec.nprog = np;
+  pagg_refs_++;
+  {
+    std::lock_guard<std::mutex> lk2(mu_);
+    *ticket = next_ticket_++;  // a ticket of its own, in the batch tickets' sequence
+  }
+  split_[*ticket] = rec;
+  dg_status st = DG_OK;
+  if ((int)pagg_.size() >= prog_batch_ || pagg_stale_locked()) st = flush_pagg_locked();
+  return st;
+}
+
+dg_status Context::wait_user(uint64_t ticket) {
+  SplitRec rec;
+  uint64_t tp = 0;
+  {
+    std::lock_guard<std::mutex> lk(pmu_);
+    auto it = split_.find(ticket);
+    if (it == split_.end()) return wait(ticket);
+    rec = it->second;
+    if (rec.gen == pagg_gen_) flush_pagg_locked();  // someone blocks on the open aggregate: launch it now
+    tp = pgen_[rec.gen].first;
+  }
+  dg_status st = rec.tb ? wait(rec.tb) : DG_OK;
+  dg_status st2 = tp ? wait(tp) : DG_OK;
+  std::lock_guard<std::mutex> lk(pmu_);
+  if (split_.erase(ticket)) {
+    auto g = pgen_.find(rec.gen);
+    if (g != pgen_.end() && --g->second.second <= 0) pgen_.erase(g);
+  }
+  return st ? st : st2;
+}
+
+dg_status Context::wait_ready(uint64_t ticket, int32_t *pending) {
+  SplitRec rec;
+  {
+    std::lock_guard<std::mutex> lk(pmu_);
+    if (pagg_stale_locked()) flush_pagg_locked();
+    auto it = split_.find(ticket);
+    if (it == split_.end()) {
+      if (pending) *pending = 0;
+      return wait(ticket);
+    }
+    rec = it->second;
+  }
+  dg_status st = rec.tb ? wait(rec.tb) : DG_OK;
+  if (pending) {  // progressive members not complete yet (their metas read DG_ERR_NOT_READY)
+    std::lock_guard<std::mutex> lk(pmu_);
+    uint64_t tp = 0;
+    if (rec.gen != pagg_gen_) {
+      auto g = pgen_.find(rec.gen);
+      tp = g != pgen_.end() ? g->second.first : 0;
+    }
+    *pending = (rec.gen == pagg_gen_ || (tp && poll(tp) == DG_ERR_NOT_READY)) ? rec.nprog : 0;
+  }
+  return st;
+}
+
+dg_status Context::poll_user(uint64_t ticket) {
+  SplitRec rec;
+  uint64_t tp = 0;
+  {
+    std::lock_guard<std::mutex> lk(pmu_);
+    if (pagg_stale_locked()) flush_pagg_locked();
+    auto it = split_.find(ticket);
+    if (it == split_.end()) return poll(ticket);
+    rec = it->second;
+    if (rec.gen == pagg_gen_) return DG_ERR_NOT_READY;
+    tp = pgen_[rec.gen].first;
+  }
+  if (rec.tb && poll(rec.tb) == DG_ERR_NOT_READY) return DG_ERR_NOT_READY;
+  if (tp && poll(tp) == DG_ERR_NOT_READY) return DG_ERR_NOT_READY;
   return DG_OK;
 }
 

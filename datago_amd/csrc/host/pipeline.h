@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <memory>
 #include <condition_variable>
 #include <mutex>
@@ -103,7 +104,7 @@ struct Batch {
   std::vector<uint64_t> host_caps;
   std::vector<size_t> out_dev_off;    // offset of each output in the scratch arena (host path)
   std::vector<uint8_t> out_direct;    // host path: output DMA'd straight into the caller's pinned buffer
-  dg_payload_meta *metas = nullptr;
+  std::vector<dg_payload_meta *> mptr;  // each image's meta (the caller's; a split submission's are scattered)
   bool done = false;
   int resync_rounds = 0;
   bool unsettled = false;             // resync hit kMaxResyncRounds: JPEGs go back as DG_ERR_UNSUPPORTED
@@ -114,8 +115,12 @@ struct Batch {
 
 // One in-flight batch's device/pinned buffers.  Three (option "slots", 1 to
 // kMaxInflight) slots let the host plan and upload batch k+1 while the GPU
-// still runs batches k and k-1.
+// still runs batches k and k-1.  kProgSlots more run progressive batches only
+// (dg_submit's progressive aggregates, dg_decode_one's progressive lanes), so a
+// ~0.1-1 s refinement chain never holds a baseline slot.
 constexpr int kMaxInflight = 4;
+constexpr int kProgSlots = 2;
+constexpr int kAllSlots = kMaxInflight + kProgSlots;
 struct Slot {
   DevBuf scratch, meta, input;
   DevBuf wgt;  // debug: per-workgroup timestamps of the entropy kernels (option "wg_timing")
@@ -156,11 +161,23 @@ class Context {
   ~Context();
   dg_status init();
 
+  // One batch in one slot (mptrs: per-image meta pointers instead of the
+  // metas array; force_slot: a progressive slot instead of the next in turn).
   dg_status submit(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
                    const int32_t *forced, uint8_t *const *outs, const uint64_t *caps, dg_payload_meta *metas,
-                   bool host_io, uint64_t *ticket);
+                   bool host_io, uint64_t *ticket, dg_payload_meta *const *mptrs = nullptr, int force_slot = -1);
   dg_status wait(uint64_t ticket);
   dg_status poll(uint64_t ticket);
+  // The C ABI's dg_submit / dg_submit_device / dg_wait / dg_poll /
+  // dg_wait_ready: a submission with progressive members is split (option
+  // "prog_split"): the rest run as a batch of their own, the progressive
+  // members join an aggregate batch on a progressive slot.
+  dg_status submit_user(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
+                        const int32_t *forced, uint8_t *const *outs, const uint64_t *caps, dg_payload_meta *metas,
+                        bool host_io, uint64_t *ticket);
+  dg_status wait_user(uint64_t ticket);
+  dg_status poll_user(uint64_t ticket);
+  dg_status wait_ready(uint64_t ticket, int32_t *pending);
   // One image, coalesced with concurrent callers into shared GPU batches
   // (SURVEY §8(b).6): returns the image's status.
   dg_status decode_one(const uint8_t *src, size_t len, int32_t forced, uint8_t *out, uint64_t cap,
@@ -188,9 +205,13 @@ class Context {
   dg_status upload_pools();
   dg_status launch_all(Slot &sl, bool from_fix);
   void plan_prog_items(Batch &b);
+  dg_status flush_pagg_locked();  // pmu_ held
+  bool pagg_stale_locked();       // the open aggregate is older than prog_flush_us
   dg_status finish(Slot &sl);
   Slot *find(uint64_t ticket);
   int pick_slot();
+  int pick_prog_slot();
+  dg_status make_prog_streams();
 
   int device_;
   bool has_cfg_ = false;
@@ -217,13 +238,42 @@ class Context {
   std::vector<OneReq *> pending_, ppending_;  // baseline / progressive callers waiting for a batch
   int callers_ = 0, inflight_ = 0, inflight_reqs_ = 0, pinflight_ = 0;
   int prog_lanes_ = 1;  // option "prog_lanes": progressive batches in flight beside the baseline ones
+  // progressive aggregate of split submissions (options "prog_split", "prog_batch", "prog_flush_us")
+  struct PEntry {
+    std::vector<uint8_t> host;  // the coded file (the header parser walks every scan at flush time)
+    const uint8_t *dsrc;        // device copy (dg_submit_device) or null
+    size_t len;
+    int32_t forced;
+    uint8_t *out;
+    uint64_t cap;
+    dg_payload_meta *meta;
+  };
+  struct SplitRec {
+    uint64_t tb = 0;   // internal ticket of the non-progressive members (0: none)
+    uint64_t gen = 0;  // aggregate generation holding the progressive members
+    int32_t nprog = 0;
+  };
+  std::mutex pmu_;
+  std::vector<PEntry> pagg_;
+  bool pagg_host_ = true;
+  uint64_t pagg_gen_ = 1;
+  std::chrono::steady_clock::time_point pagg_t0_;
+  std::unordered_map<uint64_t, std::pair<uint64_t, int>> pgen_;  // flushed generation -> (ticket, split refs)
+  std::unordered_map<uint64_t, SplitRec> split_;                 // user ticket -> parts
+  int pagg_refs_ = 0;      // split records referring to the open aggregate
+  int next_pslot_ = 0;
+  bool prog_split_ = true;
+  int prog_batch_ = 1024;
+  int prog_flush_us_ = 20000;
+  int prog_queue_ = 0;      // option "prog_queue" (make_prog_streams)
+  int64_t stat_prog_aggs_ = 0, stat_prog_agg_images_ = 0;
   bool multi_lead_ = true;   // option "multi_lead": multi-symbol AC steps in k_huff_sync's state-only decodes
   int write_pair_ = 3;       // option "write_pair": up to this many more AC symbols per k_huff_write step from one peek
   bool sync_pair_ = false;   // option "sync_pair": the same in k_huff_sync (measured slower beside multi_lead: off)
   bool prog_side_ = false;  // option "prog_side": progressive scans on the side stream (measured slower: off)
   int coalesce_max_ = 64, coalesce_us_ = 500;
   int64_t stat_coalesced_batches_ = 0, stat_coalesced_images_ = 0;
-  dg_status flush_batch(std::vector<OneReq *> &batch);
+  dg_status flush_batch(std::vector<OneReq *> &batch, bool prog);
 
   std::vector<HuffTable> hpool_;
   std::unordered_map<std::string, int> hpool_idx_;
@@ -232,7 +282,7 @@ class Context {
   size_t hpool_uploaded_ = 0, qpool_uploaded_ = 0;
   DevBuf d_hpool_, d_qpool_;
 
-  Slot slots_[kMaxInflight];
+  Slot slots_[kAllSlots];  // [0, kMaxInflight): baseline batches; then kProgSlots progressive ones
   uint32_t ncu_ = 256;  // compute units: persistent-worker grids
   int nslots_ = 3;  // option "slots": batches in flight (each slot: own streams + scratch; 3 measured +3-4% over 2)
   int next_slot_ = 0;
@@ -259,7 +309,7 @@ class Context {
   uint32_t dec_dbg_ = 0;                // option "dec_dbg": k_band_dec phase switches (timing experiments only)
   uint32_t dec_strips_ = kDecStripsDefault;  // option "dec_strips"
   bool idct_fused_ = false;             // option "idct_fused" (measured 7x slower k_huff_write: off)
-  bool progressive_ = false;            // option "progressive"
+  bool progressive_ = true;             // option "progressive"
   bool prog_serial_ = false;            // option "prog_serial": serial reader for every scan (A/B)
   bool prog_pipe_ = true;               // option "prog_pipe": all scans in one pipelined launch (0: one launch per level)
   int prog_chain_ = 100;                // option "prog_chain": chain dependency groups costing <= this % of the longest scan

@@ -158,6 +158,29 @@ def corpus_cache_dir() -> str:
     return os.environ.get("DATAGO_CORPUS_CACHE") or os.path.join(tempfile.gettempdir(), "datago_amd_corpus")
 
 
+def is_progressive_jpeg(data: bytes) -> bool:
+    """SOF2 before the first SOS (what the library's sniff checks)."""
+    i, n = 2, len(data)
+    if n < 4 or data[0] != 0xFF or data[1] != 0xD8:
+        return False
+    while i + 4 <= n:
+        if data[i] != 0xFF:
+            return False
+        m = data[i + 1]
+        if m == 0xFF:
+            i += 1
+            continue
+        if m == 0xC2:
+            return True
+        if m in (0xC0, 0xC1, 0xDA) or m == 0xD9:
+            return False
+        if 0xD0 <= m <= 0xD7 or m == 0x01:
+            i += 2
+            continue
+        i += 2 + ((data[i + 2] << 8) | data[i + 3])
+    return False
+
+
 def _pool_job(seed: int, i: int, spec, progressive_frac: float, restart_marker_rows: int = 0):
     step = int(round(1.0 / progressive_frac)) if progressive_frac > 0 else 0
     return (seed * 1_000_003 + i, spec[i], int(restart_marker_rows), bool(step) and i % step == 0)

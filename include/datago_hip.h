@@ -41,19 +41,20 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 2  /* 2: dg_image_config.decode_semantics */
+#define DG_ABI_VERSION 3  /* 2: dg_image_config.decode_semantics; 3: dg_wait_ready, progressive on by default */
 
 typedef enum dg_status {
   DG_OK = 0,
-  DG_ERR_UNSUPPORTED = 1, /* valid image the GPU path does not decode (progressive,
-                             arithmetic, 12-bit, CMYK, non-JPEG...): caller keeps its CPU path */
+  DG_ERR_UNSUPPORTED = 1, /* valid image the GPU path does not decode (arithmetic, 12-bit,
+                             CMYK, 16-bit PNG, non-JPEG/PNG...): caller keeps its CPU path */
   DG_ERR_CORRUPT = 2,     /* maps to image::ImageError::Decoding: drop the sample */
   DG_ERR_OOM = 3,         /* device or host allocation failed */
   DG_ERR_BAD_BUCKET = 4,  /* forced aspect-ratio key/index not in the table (the reference panics) */
   DG_ERR_INVALID = 5,     /* invalid argument / config (the reference asserts) */
   DG_ERR_SMALL_BUFFER = 6,/* caller's output buffer is too small; meta holds the size needed */
   DG_ERR_DEVICE = 7,      /* HIP runtime error */
-  DG_ERR_NOT_READY = 8    /* dg_poll: batch still running */
+  DG_ERR_NOT_READY = 8    /* dg_poll: batch still running; meta.status of a progressive member
+                             dg_wait_ready left running */
 } dg_status;
 
 /* Image formats reported by dg_probe. */
@@ -167,6 +168,17 @@ dg_status dg_submit(dg_ctx *ctx, int32_t n, const uint8_t *const *srcs, const si
                     dg_payload_meta *metas, uint64_t *ticket);
 dg_status dg_wait(dg_ctx *ctx, uint64_t ticket);
 dg_status dg_poll(dg_ctx *ctx, uint64_t ticket);
+/* Progressive JPEGs of a submission (option "prog_split", default on) do not
+ * run in its batch: a refinement scan is one serial chain (~0.1-1 s for a
+ * large file), so they join a progressive aggregate that runs on slots of its
+ * own (launched at "prog_batch" images, after "prog_flush_us", or when a
+ * caller blocks on one of them in dg_wait).  dg_wait(ticket) completes every
+ * member as before.  dg_wait_ready(ticket) returns once every other member is
+ * complete (outputs and metas valid); *pending (may be NULL) = progressive
+ * members still running, whose metas read status DG_ERR_NOT_READY until a
+ * later dg_wait(ticket) -- so a loader hands its baseline samples on at the
+ * baseline pace and the progressive ones when their aggregate is done. */
+dg_status dg_wait_ready(dg_ctx *ctx, uint64_t ticket, int32_t *pending);
 
 /* Synchronous single image (image_payload_from_path equivalent).  Calls from
  * concurrent threads are coalesced into shared GPU batches (one 0.3 MP image
@@ -220,11 +232,16 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *                 force an entropy write-pass mismatch / a resync that never settles; bit 18 / 19 = force
  *                 a PNG unfilter band wait / a progressive scan wait to time out (tests of the per-image
  *                 DG_ERR_UNSUPPORTED those failures return)
- *   "progressive" 1 = decode progressive JPEGs on the GPU (default 0: DG_ERR_UNSUPPORTED, the
- *                 caller's CPU decoder takes them; a refinement scan is one serial chain, so a large
- *                 file holds its batch for ~0.1-1 s: worth it for progressive-heavy corpora)
+ *   "progressive" 1 = decode progressive JPEGs on the GPU (default 1; 0: DG_ERR_UNSUPPORTED, the
+ *                 caller's CPU decoder takes them)
+ *   "prog_split"  1 = progressive members of a dg_submit run in the progressive aggregate (default 1,
+ *                 see dg_wait_ready); 0 = in the submission's own batch
+ *   "prog_batch"  progressive aggregate: launched once it holds this many images (default 1024)
+ *   "prog_flush_us" ... or once it is this old at a dg_submit / dg_poll / dg_wait_ready (default 20000)
  *   "prog_lanes"  dg_decode_one: progressive files coalesce into batches of their own, this many in
- *                 flight beside the baseline batches (default 1; 0 = mixed into the baseline batches)
+ *                 flight on the progressive slots (0..2, default 1; 0 = mixed into the baseline batches)
+ *   "prog_chain"  progressive work items: dependency groups costing <= this % of the batch's longest scan
+ *                 run back to back in one wave (default 100; 0 = one wave per scan)
  *   "prog_pipe"   1 = all scans of a batch in one pipelined launch (default); 0 = one launch per level
  *   "prog_serial" 1 = serial bit reader for every scan (A/B; scans with restart intervals always use it)
  *   "prog_side"   1 = progressive scans on the slot's side stream (default 0: measured slower)
@@ -232,9 +249,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "write_pair"  k_huff_write: up to this many more AC symbols per step out of one 32-bit peek (0..3,
  *                 default 3)
  *   "sync_pair"   1 = the same in k_huff_sync after a single-symbol step (default 0: measured slower)
- *   "slots"       baseline batches in flight, 1..4 (default 3); with "progressive" = 1 and "prog_lanes" > 0
- *                 the context cycles through slots + prog_lanes slots (at most 4), each with its own scratch
- *                 arena, pinned staging and streams
+ *   "slots"       baseline batches in flight, 1..4 (default 3), each with its own scratch arena, pinned
+ *                 staging and streams; progressive batches use two slots of their own
  *   "hb_bands"    band H kernel: 8-row bands per workgroup, 1..64 (default 16)
  *   "entropy_lpt" 1 = dispatch the slowest entropy workgroups first (default 1)
  *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)
@@ -249,7 +265,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  * Stats: "batches", "coalesced_batches", "coalesced_images", "resync_rounds", "fix_workgroups", "write_mismatch",
  * "unsettled_batches", "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool" (tables pooled now),
  * "pool_flushes" (times the table pools were started over), "png_chunks", "png_serial_fallbacks",
- * "band_dec_images" (images whose first H pass ran in k_band_dec);
+ * "band_dec_images" (images whose first H pass ran in k_band_dec), "prog_items", "prog_chains" (work items / chains
+ * of the pipelined progressive launches), "prog_aggregates", "prog_aggregate_images";
  * -1 if unknown.
  *
  * Entropy-decode self-checks: an image whose write pass disagrees with the sync pass, or every sequential JPEG of

@@ -46,7 +46,7 @@ def test_no_torch_types_in_abi():
 
 
 def test_abi_version(L):
-    assert L.dg_abi_version() == 2  # 2: dg_image_config.decode_semantics
+    assert L.dg_abi_version() == 3  # 2: dg_image_config.decode_semantics; 3: dg_wait_ready
 
 
 @pytest.mark.parametrize("cfg", list(B.CONFIGS.keys()))

@@ -90,11 +90,25 @@ def test_progressive_truncated_is_corrupt():
     assert res[0][0] == L.DG_ERR_CORRUPT and res[1][0] == L.DG_OK
 
 
-def test_progressive_off_by_default_is_unsupported():
+def test_progressive_option_off_is_unsupported():
     L = _lib()
     ctx = L.Context(0)
+    ctx.set_option("progressive", 0)
     res = ctx.decode_batch([_prog(45, 64, 48), synth.make_jpeg(46, 64, 48)])
     assert res[0][0] == L.DG_ERR_UNSUPPORTED and res[1][0] == L.DG_OK
+
+
+def test_progressive_on_by_default():
+    """Progressive files decode inline by default (worker_files.rs:14-16 ->
+    image -> zune-jpeg decodes them), through the split submission."""
+    L = _lib()
+    ctx = L.Context(0)
+    datas = [_prog(45, 64, 48), synth.make_jpeg(46, 64, 48)]
+    for data, (st, arr, _) in zip(datas, ctx.decode_batch(datas)):
+        assert st == 0
+        ost, ref = O.jpeg_decode(data)
+        assert np.array_equal(arr.reshape(ref.shape), ref)
+    assert ctx.stat("prog_aggregates") == 1 and ctx.stat("prog_aggregate_images") == 1
 
 
 def test_progressive_speculative_equals_serial_reader():
@@ -215,3 +229,95 @@ def test_progressive_chains_bit_exact(chain):
         assert chains == 0
     else:
         assert 0 < chains <= items
+
+
+def _resized_ref(data, t):
+    w, h = O.jpeg_info(data)[1:3]
+    tw, th = t.target_size(w, h)
+    ost, dec = O.jpeg_decode(data)
+    return O.crop_and_resize(dec, tw, th, O.MODE_FIR)
+
+
+def _mixed(seed, n, every=3):
+    out = []
+    for i in range(n):
+        rng = np.random.default_rng(seed + i)
+        out.append(synth.make_jpeg(seed + i, int(rng.integers(64, 700)), int(rng.integers(64, 700)),
+                                   int(rng.integers(50, 97)), ["4:2:0", "4:2:2", "4:4:4"][i % 3],
+                                   progressive=i % every == 1))
+    return out
+
+
+def test_split_wait_ready_then_wait():
+    """dg_submit with progressive members (prog_split, the default): the other
+    members form a batch of their own and are complete after dg_wait_ready;
+    the progressive ones are pending (meta status DG_ERR_NOT_READY) until
+    dg_wait, and then every output equals the oracle's."""
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+    ctx.set_option("prog_flush_us", 10_000_000)  # launched only by the dg_wait below
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    datas = _mixed(8100, 12)
+    isp = [i % 3 == 1 for i in range(len(datas))]
+    outs = [np.zeros(max(ctx.output_size(d)[1], 1), np.uint8) for d in datas]
+    ticket, metas, keep = ctx.submit_host(datas, outs)
+    pending = ctx.wait_ready(ticket)
+    assert pending == sum(isp)
+    for i, d in enumerate(datas):
+        if isp[i]:
+            assert metas[i].status == L.DG_ERR_NOT_READY, i
+        else:
+            assert metas[i].status == 0, i
+            ref = _resized_ref(d, t)
+            assert np.array_equal(outs[i][: ref.size].reshape(ref.shape), ref), i
+    ctx.wait(ticket)
+    for i, d in enumerate(datas):
+        assert metas[i].status == 0, i
+        ref = _resized_ref(d, t)
+        assert np.array_equal(outs[i][: ref.size].reshape(ref.shape), ref), i
+    assert ctx.stat("prog_aggregates") == 1
+
+
+def test_split_aggregates_across_submissions():
+    """Progressive members of several submissions share one aggregate batch
+    (prog_batch, prog_flush_us large): waited on out of order, every output
+    is the oracle's; a later submission starts a new aggregate."""
+    L = _lib()
+    ctx = L.Context(0)
+    ctx.set_option("prog_flush_us", 10_000_000)
+    ctx.set_option("prog_batch", 1000)
+    subs = [_mixed(8200 + 50 * k, 7, every=2) for k in range(3)]
+    held = []
+    for datas in subs:
+        outs = [np.zeros(max(ctx.output_size(d)[1], 1), np.uint8) for d in datas]
+        ticket, metas, keep = ctx.submit_host(datas, outs)
+        held.append((ticket, metas, keep, outs, datas))
+    for ticket, metas, keep, outs, datas in held:
+        assert ctx.wait_ready(ticket) == sum(i % 2 == 1 for i in range(len(datas)))
+    for ticket, metas, keep, outs, datas in reversed(held):
+        ctx.wait(ticket)
+        for i, d in enumerate(datas):
+            assert metas[i].status == 0
+            ost, ref = O.jpeg_decode(d)
+            assert np.array_equal(outs[i][: ref.size].reshape(ref.shape), ref), i
+    assert ctx.stat("prog_aggregates") == 1
+    assert ctx.stat("prog_aggregate_images") == sum(sum(i % 2 == 1 for i in range(len(d))) for d in subs)
+    res = ctx.decode_batch(_mixed(8400, 4, every=2))
+    assert all(r[0] == 0 for r in res) and ctx.stat("prog_aggregates") == 2
+
+
+def test_split_device_path_and_batch_limit():
+    """dg_submit_device (coded bytes in HBM, outputs in HBM) splits the same
+    way; an aggregate that reaches prog_batch images launches at once."""
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+    ctx.set_option("prog_batch", 2)
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    datas = _mixed(8500, 9)
+    res = ctx.decode_batch_torch(datas)
+    for i, (d, (st, ten, _)) in enumerate(zip(datas, res)):
+        assert st == 0, i
+        assert np.array_equal(ten.cpu().numpy(), _resized_ref(d, t)), i
+    assert ctx.stat("prog_aggregates") == 1  # launched by the submission that reached prog_batch
