@@ -163,9 +163,10 @@ dg_status Context::init() {
     sl.ev.resize(kNumStages + 1);
     for (auto &e : sl.ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-    if (&sl - slots_ >= kMaxInflight) continue;  // progressive slots: make_prog_streams below
-    HIPCHK(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&sl.side, hipStreamNonBlocking));
+    if (&sl - slots_ < kMaxInflight) {  // progressive slots: make_prog_streams below
+      HIPCHK(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
+      HIPCHK(hipStreamCreateWithFlags(&sl.side, hipStreamNonBlocking));
+    }
     HIPCHK(hipEventCreateWithFlags(&sl.ev_meta, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_coef, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_zero, hipEventDisableTiming));

@@ -265,7 +265,7 @@ class Context {
   bool prog_split_ = true;
   int prog_batch_ = 1024;
   int prog_flush_us_ = 20000;
-  int prog_queue_ = 0;      // option "prog_queue" (make_prog_streams)
+  int prog_queue_ = 2;      // option "prog_queue" (make_prog_streams): low priority, a queue of its own
   int64_t stat_prog_aggs_ = 0, stat_prog_agg_images_ = 0;
   bool multi_lead_ = true;   // option "multi_lead": multi-symbol AC steps in k_huff_sync's state-only decodes
   int write_pair_ = 3;       // option "write_pair": up to this many more AC symbols per k_huff_write step from one peek
