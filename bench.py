@@ -109,7 +109,7 @@ def parse():
                     help="jpeg workload: share of the pool written as progressive JPEGs (not the headline config)")
     ap.add_argument("--no-prog-split", action="store_true",
                     help="progressive-frac runs: dg_wait every batch whole (no dg_wait_ready / deferred completion)")
-    ap.add_argument("--prog-ring", type=int, default=4096,
+    ap.add_argument("--prog-ring", type=int, default=8192,
                     help="progressive-frac runs: output slots for progressive members awaiting completion")
     ap.add_argument("--out", default="")
     a = ap.parse_args()

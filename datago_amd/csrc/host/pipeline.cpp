@@ -105,8 +105,9 @@ Context::Context(int device, const dg_image_config *cfg) : device_(device) {
 Context::~Context() {
   hipSetDevice(device_);
   sync_all();
-  for (DevBuf *b : {&d_hpool_, &d_qpool_})
-    if (b->p) hipFree(b->p);
+  for (int g = 0; g < kPoolGens; g++)
+    for (DevBuf *b : {&d_hpool_[g], &d_qpool_[g]})
+      if (b->p) hipFree(b->p);
   for (Slot &sl : slots_) {
     for (auto e : sl.ev) hipEventDestroy(e);
     if (sl.done) hipEventDestroy(sl.done);
@@ -610,28 +611,32 @@ dg_status Context::ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user) {
 // Table pools.  Huffman and quantisation tables are de-duplicated by content
 // into per-context pools that the kernels index with 16-bit slots.  Pools are
 // not grow-only: once a pool holds more than kPoolKeep tables (a long-running
-// loader over per-image-optimised JPEGs adds ~4 new tables per image), the
-// next submit drains the batches in flight and starts the pools over, so a
-// valid image never fails for lack of pool space.  Only a single batch that
-// alone needs more than kPoolMax tables sends its overflow images back as
+// loader over per-image-optimised JPEGs adds ~4 new tables per image; a
+// progressive file ~10-12, one per scan), the next submit starts the pools
+// over in the next of kPoolGens device generations, waiting only for batches
+// that still read that generation (round 2 drained every batch in flight
+// here -- with progressive aggregates that was a ~1 s stall of every slot,
+// and it serialised the aggregates).  Only a single batch that alone needs
+// more than kPoolMax tables sends its overflow images back as
 // DG_ERR_UNSUPPORTED (the caller's CPU path), never as CORRUPT.
-static constexpr size_t kPoolKeep = 4096;
+static constexpr size_t kPoolKeep = 16384;
 static constexpr size_t kPoolMax = 65535;
 
 dg_status Context::flush_pools() {
-  for (int s = 0; s < kAllSlots; s++) {  // batches in flight still read (and may resync with) the pools
+  const int next = (pool_gen_ + 1) % kPoolGens;
+  for (int s = 0; s < kAllSlots; s++) {  // batches in flight still reading (and may resync with) that generation
     Slot &o = slots_[s];
-    if (o.batch && !o.batch->done) {
+    if (o.batch && !o.batch->done && o.batch->pool_gen == next) {
       dg_status st = finish(o);
       if (st) return st;
     }
   }
-  if (dg_status st = sync_all()) return st;
   hpool_.clear();
   hpool_idx_.clear();
   qpool_.clear();
   qpool_idx_.clear();
   hpool_uploaded_ = qpool_uploaded_ = 0;
+  pool_gen_ = next;
   stat_pool_flush_++;
   return DG_OK;
 }
@@ -664,26 +669,20 @@ int Context::pool_quant(const uint16_t *q) {
 }
 
 dg_status Context::upload_pools() {
+  DevBuf &hb = d_hpool_[pool_gen_], &qb = d_qpool_[pool_gen_];
+  if (!hb.p) {  // each generation is allocated once, at full capacity: no reallocation, no device sync
+    if (dg_status st = ensure(hb, kPoolMax * sizeof(HuffTable))) return st;
+    if (dg_status st = ensure(qb, kPoolMax * sizeof(QuantTable))) return st;
+  }
+  // appends only: entries below *_uploaded_ may be in use by batches in flight
   if (hpool_.size() != hpool_uploaded_) {
-    size_t bytes = hpool_.size() * sizeof(HuffTable);
-    if (d_hpool_.cap < bytes) {
-      dg_status st = ensure(d_hpool_, bytes * 2);
-      if (st) return st;
-      hpool_uploaded_ = 0;
-    }
-    HIPCHK(hipMemcpyAsync((char *)d_hpool_.p + hpool_uploaded_ * sizeof(HuffTable), &hpool_[hpool_uploaded_],
+    HIPCHK(hipMemcpyAsync((char *)hb.p + hpool_uploaded_ * sizeof(HuffTable), &hpool_[hpool_uploaded_],
                           (hpool_.size() - hpool_uploaded_) * sizeof(HuffTable), hipMemcpyHostToDevice, stream_));
     HIPCHK(hipStreamSynchronize(stream_));  // the host vector may reallocate later
     hpool_uploaded_ = hpool_.size();
   }
   if (qpool_.size() != qpool_uploaded_) {
-    size_t bytes = qpool_.size() * sizeof(QuantTable);
-    if (d_qpool_.cap < bytes) {
-      dg_status st = ensure(d_qpool_, bytes * 2);
-      if (st) return st;
-      qpool_uploaded_ = 0;
-    }
-    HIPCHK(hipMemcpyAsync((char *)d_qpool_.p + qpool_uploaded_ * sizeof(QuantTable), &qpool_[qpool_uploaded_],
+    HIPCHK(hipMemcpyAsync((char *)qb.p + qpool_uploaded_ * sizeof(QuantTable), &qpool_[qpool_uploaded_],
                           (qpool_.size() - qpool_uploaded_) * sizeof(QuantTable), hipMemcpyHostToDevice, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
     qpool_uploaded_ = qpool_.size();
@@ -899,6 +898,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   dg_status st = upload_pools();
   if (st) return st;
+  b.pool_gen = pool_gen_;
+  b.hp = (const HuffTable *)d_hpool_[pool_gen_].p;
+  b.qp = (const QuantTable *)d_qpool_[pool_gen_].p;
 
   phase(1);
   // ---- 3. layout
@@ -1915,8 +1917,8 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   ImageDesc *dm = (ImageDesc *)(M + b.desc_off);
   BatchFlags *fl = (BatchFlags *)(M + b.flags_off);
   SubState *subs = (SubState *)((char *)sl.scratch.p + sl.subs_off);
-  const HuffTable *hp = (const HuffTable *)d_hpool_.p;
-  const QuantTable *qp = (const QuantTable *)d_qpool_.p;
+  const HuffTable *hp = b.hp;  // the pool generation this batch was planned against
+  const QuantTable *qp = b.qp;
   auto lst = [&](int l) { return (const WgItem *)(M + b.list_off[l]); };
   auto cnt = [&](int l) { return (uint32_t)b.lists[l].size(); };
   auto ev = [&](int i) -> dg_status {
@@ -1996,7 +1998,8 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
       HIPCHK(hipMemsetAsync(pf, 0, (size_t)(b.pf_n + 2) * 4, pst));
       const uint32_t nac = cnt(L_PROG) - b.prog_dc_n, sflags = (prog_serial_ ? 1u : 0u) | prog_dbg;
       hipStream_t dst = pst;
-      if (!pside && side_stream_ && !timing_ && b.prog_dc_n && nac) {  // DC items beside the AC launch
+      if (!pside && side_stream_ && b.prog_dc_n && nac) {  // DC items beside the AC launch (also when timing:
+                                                          // the IDCT stage then holds what the DC items outlast)
         HIPCHK(hipEventRecord(sl.ev_zero, pst));
         HIPCHK(hipStreamWaitEvent(sl.side, sl.ev_zero, 0));
         dst = sl.side;

@@ -105,6 +105,9 @@ struct Batch {
   std::vector<size_t> out_dev_off;    // offset of each output in the scratch arena (host path)
   std::vector<uint8_t> out_direct;    // host path: output DMA'd straight into the caller's pinned buffer
   std::vector<dg_payload_meta *> mptr;  // each image's meta (the caller's; a split submission's are scattered)
+  const HuffTable *hp = nullptr;       // the table pools (generation pool_gen) this batch's kernels read
+  const QuantTable *qp = nullptr;
+  int pool_gen = 0;
   bool done = false;
   int resync_rounds = 0;
   bool unsettled = false;             // resync hit kMaxResyncRounds: JPEGs go back as DG_ERR_UNSUPPORTED
@@ -280,7 +283,13 @@ class Context {
   std::vector<QuantTable> qpool_;
   std::unordered_map<std::string, int> qpool_idx_;
   size_t hpool_uploaded_ = 0, qpool_uploaded_ = 0;
-  DevBuf d_hpool_, d_qpool_;
+  // Device copies of the pools: kPoolGens generations, each allocated once at
+  // full capacity.  Starting the pools over moves to the next generation and
+  // waits only for batches still reading that (oldest) one, never for the
+  // batches in flight on the current ones.
+  static constexpr int kPoolGens = 4;
+  DevBuf d_hpool_[kPoolGens], d_qpool_[kPoolGens];
+  int pool_gen_ = 0;
 
   Slot slots_[kAllSlots];  // [0, kMaxInflight): baseline batches; then kProgSlots progressive ones
   uint32_t ncu_ = 256;  // compute units: persistent-worker grids

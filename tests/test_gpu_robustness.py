@@ -175,7 +175,7 @@ def test_table_pools_never_fill():
             if lo <= i < lo + batch:
                 assert np.array_equal(res[i - lo][1], want[i]), i
     assert ctx.stat("pool_flushes") >= 1
-    assert ctx.stat("qpool") <= 4096 + batch
+    assert ctx.stat("qpool") <= 16384 + batch  # kPoolKeep
 
 
 def test_forced_write_mismatch_is_a_per_image_status():
