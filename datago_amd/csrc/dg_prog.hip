@@ -467,7 +467,7 @@ template <class SM>
 __device__ __forceinline__ void ds_refill(DStream &s, SM &sm, uint32_t lane) {
   const uint32_t sb = uni((s.bp >> 3) & ~15u);
   // < 40 bytes from the generic decoder (it refills with < 24 unread), up to
-  // ~180 from the refinement walk (it refills between blocks, >= 160 ahead)
+  // ~210 from the refinement walk (it refills between blocks, >= 192 ahead)
   const uint32_t tail = s.dend > sb ? s.dend - sb : 0u;
   for (uint32_t c0 = 0; c0 < tail; c0 += 64) {  // forward, 64 bytes at a time: dst < src never overtakes
     __syncthreads();
@@ -843,10 +843,11 @@ __device__ __noinline__ uint32_t prog_refine_spec(const ProgScan &sc, const Imag
   }
   uint32_t o = 0, peek = 0, sp0 = 0, aft = 0;
   // A round: peeks and code lookups for the 64 bit offsets from bp.  The
-  // window is refilled only between blocks, with at least 160 bytes ahead: a
+  // window is refilled only between blocks, with at least 192 bytes ahead: a
   // block consumes at most 63 x (16-bit code + sign) + 63 correction bits +
-  // a 14-bit EOB run = 1148 bits, so no round inside a block needs a refill
-  // (and the walk has no call in it).
+  // a 14-bit EOB run = 1148 bits, and a round reads at most 128 bits past its
+  // walk position, so no round inside a block needs a refill (and the walk
+  // has no call in it).
   auto round = [&]() {
     s.bp = uni(s.bp + o);
     o = 0;
@@ -855,8 +856,8 @@ __device__ __noinline__ uint32_t prog_refine_spec(const ProgScan &sc, const Imag
     sp0 = huff_lookup_wave(sm.tabs[0], peek);
     aft = ds_peek(sm, s.bp + (sp0 >> 8), lane);  // lane o: the 32 bits after the code at offset o
   };
-  auto refill = [&]() {  // between blocks: keep >= 160 destuffed bytes ahead of the walk
-    if (!s.done && ((s.bp + o) >> 3) + 160 > s.dend) {
+  auto refill = [&]() {  // between blocks: keep >= 192 destuffed bytes ahead of the walk
+    if (!s.done && ((s.bp + o) >> 3) + 192 > s.dend) {
       s.bp = uni(s.bp + o);
       o = 0;
       ds_refill(s, sm, lane);
@@ -949,7 +950,7 @@ __device__ __noinline__ uint32_t prog_refine_spec(const ProgScan &sc, const Imag
             if (c) cb = (cb << c) | ((after << sg) >> (32u - c));
             cc += c;
             o = ou + l + sg + c;
-          } else {
+          } else {  // (a 64-bit window from a second per-lane peek measured slower: 795 -> 886 ms)
             o = ou + l + sg;
             take(c);
           }

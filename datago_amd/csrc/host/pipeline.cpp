@@ -108,6 +108,7 @@ Context::~Context() {
   for (int g = 0; g < kPoolGens; g++)
     for (DevBuf *b : {&d_hpool_[g], &d_qpool_[g]})
       if (b->p) hipFree(b->p);
+  free_retired();
   for (Slot &sl : slots_) {
     for (auto e : sl.ev) hipEventDestroy(e);
     if (sl.done) hipEventDestroy(sl.done);
@@ -563,15 +564,34 @@ int Context::timings(const char **names, float *ms, int cap) {
 
 // Grow a device buffer.  `user`: the only stream that can still be using it
 // (a slot's own buffers); nullptr = shared by every stream (the table pools).
+// Growing a buffer never frees the old one on the spot: hipFree / hipHostFree
+// synchronise the whole device, which would make a baseline batch's growth
+// wait for a ~1 s progressive aggregate on another slot (and serialised the
+// aggregates).  The caller guarantees the old buffer is idle (a slot's
+// previous batch is finished before its buffers are reused), so it is only
+// retired and freed later: at destruction, or once retired buffers pass
+// kRetiredMax, after a sync of every stream.
+static constexpr size_t kRetiredMax = (size_t)16 << 30;
+
+void Context::retire(void *p, size_t bytes, bool pinned) {
+  (pinned ? retired_pinned_ : retired_dev_).push_back(p);
+  retired_bytes_ += bytes;
+  if (retired_bytes_ > kRetiredMax && sync_all() == DG_OK) free_retired();
+}
+
+void Context::free_retired() {
+  for (void *p : retired_dev_) hipFree(p);
+  for (void *p : retired_pinned_) hipHostFree(p);
+  retired_dev_.clear();
+  retired_pinned_.clear();
+  retired_bytes_ = 0;
+}
+
 dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
+  (void)user;
   if (b.cap >= bytes) return DG_OK;
   if (b.p) {
-    if (user) {
-      HIPCHK(hipStreamSynchronize(user));
-    } else if (dg_status st = sync_all()) {
-      return st;
-    }
-    HIPCHK(hipFree(b.p));
+    retire(b.p, b.cap, false);
     b.p = nullptr;
     b.cap = 0;
   }
@@ -587,14 +607,10 @@ dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
 }
 
 dg_status Context::ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user) {
+  (void)user;
   if (b.cap >= bytes) return DG_OK;
   if (b.p) {
-    if (user) {
-      HIPCHK(hipStreamSynchronize(user));
-    } else if (dg_status st = sync_all()) {
-      return st;
-    }
-    HIPCHK(hipHostFree(b.p));
+    retire(b.p, b.cap, true);
     b.p = nullptr;
     b.cap = 0;
   }

@@ -204,6 +204,10 @@ class Context {
   dg_status flush_pools();
   int pool_quant(const uint16_t *q);
   dg_status ensure(DevBuf &b, size_t bytes, hipStream_t user = nullptr);
+  void retire(void *p, size_t bytes, bool pinned);
+  void free_retired();
+  std::vector<void *> retired_dev_, retired_pinned_;  // grown-out buffers, freed later (ensure)
+  size_t retired_bytes_ = 0;
   dg_status ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user = nullptr);
   dg_status upload_pools();
   dg_status launch_all(Slot &sl, bool from_fix);
