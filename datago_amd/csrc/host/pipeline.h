@@ -270,7 +270,7 @@ class Context {
   int pagg_refs_ = 0;      // split records referring to the open aggregate
   int next_pslot_ = 0;
   bool prog_split_ = true;
-  int prog_batch_ = 1024;
+  int prog_batch_ = 2048;
   int prog_flush_us_ = 20000;
   int prog_queue_ = 2;      // option "prog_queue" (make_prog_streams): low priority, a queue of its own
   int64_t stat_prog_aggs_ = 0, stat_prog_agg_images_ = 0;

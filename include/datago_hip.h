@@ -236,7 +236,7 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *                 caller's CPU decoder takes them)
  *   "prog_split"  1 = progressive members of a dg_submit run in the progressive aggregate (default 1,
  *                 see dg_wait_ready); 0 = in the submission's own batch
- *   "prog_batch"  progressive aggregate: launched once it holds this many images (default 1024)
+ *   "prog_batch"  progressive aggregate: launched once it holds this many images (default 2048)
  *   "prog_flush_us" ... or once it is this old at a dg_submit / dg_poll / dg_wait_ready (default 20000)
  *   "prog_lanes"  dg_decode_one: progressive files coalesce into batches of their own, this many in
  *                 flight on the progressive slots (0..2, default 1; 0 = mixed into the baseline batches)
