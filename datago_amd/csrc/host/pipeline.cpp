@@ -200,9 +200,13 @@ dg_status Context::make_prog_streams() {
       }
       if (prog_queue_ == 1 || prog_queue_ == 2) {
         HIPCHK(hipStreamCreateWithPriority(q, hipStreamNonBlocking, prog_queue_ == 1 ? greatest : least));
-      } else if (prog_queue_ == 3) {
-        std::vector<uint32_t> mask((ncu_ + 31) / 32, 0xFFFFFFFFu);
-        if (ncu_ % 32) mask.back() = (1u << (ncu_ % 32)) - 1u;
+      } else if (prog_queue_ == 3) {  // prog_cus of the CUs, spread evenly (every ncu/prog_cus-th)
+        std::vector<uint32_t> mask((ncu_ + 31) / 32, 0u);
+        const uint32_t want = prog_cus_ > 0 && (uint32_t)prog_cus_ < ncu_ ? (uint32_t)prog_cus_ : ncu_;
+        for (uint32_t k = 0; k < want; k++) {
+          const uint32_t cu = (uint32_t)(((uint64_t)k * ncu_) / want);
+          mask[cu / 32] |= 1u << (cu % 32);
+        }
         HIPCHK(hipExtStreamCreateWithCUMask(q, (uint32_t)mask.size(), mask.data()));
       } else {
         HIPCHK(hipStreamCreateWithFlags(q, hipStreamNonBlocking));
@@ -396,6 +400,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     }
     prog_queue_ = (int)v;
     return make_prog_streams();
+  }
+  if (k == "prog_cus") {  // prog_queue 3: CUs the progressive streams may use (0 = all); set before prog_queue
+    if (v < 0 || v > 4096) return DG_ERR_INVALID;
+    prog_cus_ = (int)v;
+    return DG_OK;
   }
   if (k == "prog_split") {  // dg_submit: progressive members into the progressive aggregate (0: decoded in the batch)
     prog_split_ = v != 0;
@@ -885,7 +894,15 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   phase(0);
   // ---- 2. table pools
-  if (hpool_.size() > kPoolKeep || qpool_.size() > kPoolKeep) {
+  size_t hneed = 0, qneed = 0;  // upper bound of the tables this batch adds
+  for (int i = 0; i < n; i++) {
+    const ImagePlan &p = b.plans[i];
+    if (p.status || p.fmt != kFmtJpeg) continue;
+    hneed += p.hdr.progressive ? p.hdr.tables.size() : 2u * (size_t)p.hdr.ncomp;
+    qneed += (size_t)p.hdr.ncomp;
+  }
+  if (hpool_.size() > kPoolKeep || qpool_.size() > kPoolKeep ||
+      (hpool_.size() && hpool_.size() + hneed > kPoolMax) || (qpool_.size() && qpool_.size() + qneed > kPoolMax)) {
     dg_status st = flush_pools();
     if (st) return st;
   }

@@ -122,7 +122,10 @@ struct Batch {
 // (dg_submit's progressive aggregates, dg_decode_one's progressive lanes), so a
 // ~0.1-1 s refinement chain never holds a baseline slot.
 constexpr int kMaxInflight = 4;
-constexpr int kProgSlots = 2;
+#ifndef DG_PROG_SLOTS
+#define DG_PROG_SLOTS 2
+#endif
+constexpr int kProgSlots = DG_PROG_SLOTS;  // (-DDG_PROG_SLOTS=n: experiment builds)
 constexpr int kAllSlots = kMaxInflight + kProgSlots;
 struct Slot {
   DevBuf scratch, meta, input;
@@ -272,6 +275,7 @@ class Context {
   bool prog_split_ = true;
   int prog_batch_ = 2048;
   int prog_flush_us_ = 20000;
+  int prog_cus_ = 0;        // option "prog_cus" (prog_queue 3: CU mask width, 0 = all)
   int prog_queue_ = 2;      // option "prog_queue" (make_prog_streams): low priority, a queue of its own
   int64_t stat_prog_aggs_ = 0, stat_prog_agg_images_ = 0;
   bool multi_lead_ = true;   // option "multi_lead": multi-symbol AC steps in k_huff_sync's state-only decodes
