@@ -355,7 +355,8 @@ struct ProgScan {
 constexpr uint32_t kProgDone = 0xFFFFFFFFu;
 constexpr uint32_t kProgNoScan = 0xFFFFFFFFu;
 constexpr uint16_t kProgChained = 1;
-constexpr uint32_t kProgMaxScans = 64;  // per image (deps is a 64-bit mask)
+constexpr uint32_t kProgMaxScans = 256;    // per image (the parser's limit)
+constexpr uint32_t kProgMaxDepScans = 64;  // deps is a 64-bit mask: images with more scans run chained only
 constexpr uint32_t kProgZeroBytes = 65536;  // coefficient bytes zeroed per k_prog_zero workgroup
 
 // One workgroup's work: an image and the first item it handles.

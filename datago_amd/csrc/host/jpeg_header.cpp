@@ -175,7 +175,7 @@ void parse_jpeg_header(const uint8_t *d, size_t n, JpegHeader &h) {
         sc.off = h.scan_off;
         sc.end = q;
         h.scans.push_back(sc);
-        if (h.scans.size() > kProgMaxScans) return fail(h, JH_UNSUPPORTED, "more than 64 progressive scans");
+        if (h.scans.size() > kProgMaxScans) return fail(h, JH_UNSUPPORTED, "more than 256 progressive scans");
         p = q;
         if (d[q + 1] == 0xD9) break;  // EOI
         continue;

@@ -1511,7 +1511,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
             for (int y = 0; y < sc.ns; y++) share |= pr.comp[x] == sc.comp[y];
           if (share) {
             lvl = std::max(lvl, b.pscans[first + e].level + 1);
-            r.deps |= 1ull << e;
+            if (h.scans.size() <= kProgMaxDepScans) r.deps |= 1ull << e;  // larger files: chained only
           }
         }
         r.level = lvl;
@@ -1876,11 +1876,24 @@ void Context::plan_prog_items(Batch &b) {
     while (par[x] != x) x = par[x] = par[par[x]];
     return x;
   };
-  for (uint32_t j = 0; j < n; j++)
-    for (uint64_t m = b.pscans[j].deps; m; m &= m - 1ull) {
-      const uint32_t e = b.pscans[j].first + (uint32_t)__builtin_ctzll(m), a = find(j), c = find(e);
+  // groups: scans of one image sharing a component and an overlapping band
+  // (the deps relation, computed directly: files with more than
+  // kProgMaxDepScans scans have no deps mask and run chained only)
+  std::vector<uint8_t> nodeps(b.descs.size(), 0);
+  for (uint32_t j = 0; j < n; j++) {
+    const ProgScan &sj = b.pscans[j];
+    if (sj.image < nodeps.size() && b.descs[sj.image].prog > kProgMaxDepScans) nodeps[sj.image] = 1;
+    for (uint32_t e = sj.first; e < j; e++) {
+      const ProgScan &se_ = b.pscans[e];
+      if (se_.se < sj.ss || sj.se < se_.ss) continue;
+      bool share = false;
+      for (uint32_t x = 0; x < se_.ns && x < 4; x++)
+        for (uint32_t y = 0; y < sj.ns && y < 4; y++) share |= se_.comp[x] == sj.comp[y];
+      if (!share) continue;
+      const uint32_t a = find(j), c = find(e);
       if (a != c) par[std::max(a, c)] = std::min(a, c);
     }
+  }
   struct Group {
     std::vector<uint32_t> scans;  // ascending: every dep of a scan comes before it
     double cost = 0;
@@ -1907,7 +1920,7 @@ void Context::plan_prog_items(Batch &b) {
   for (uint32_t j = 0; j < n; j++) img_cost[b.pscans[j].image] += cost[j];
   for (uint32_t g = 0; g < (uint32_t)groups.size(); g++) {
     Group &G = groups[g];
-    if (prog_chain_ > 0 && G.cost <= limit) {
+    if ((prog_chain_ > 0 && G.cost <= limit) || nodeps[b.pscans[G.scans[0]].image]) {
       for (size_t i = 0; i < G.scans.size(); i++) {
         ProgScan &sc = b.pscans[G.scans[i]];
         sc.pflags |= kProgChained;

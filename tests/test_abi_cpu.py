@@ -103,3 +103,15 @@ def test_probe(L):
     Image.new("RGB", (7, 5)).save(buf, format="PNG")
     st, info = _lib.probe(buf.getvalue())
     assert st == 0 and info.format == _lib.DG_FMT_PNG and (info.width, info.height) == (7, 5)
+
+
+def test_probe_accepts_more_than_64_progressive_scans(L):
+    """The header parser takes up to 256 scans (the deps-mask cap
+    of 64 no longer refuses files; such files run chained on the GPU)."""
+    import ctypes
+    from test_gpu_progressive import _many_scan_jpeg
+    d = _many_scan_jpeg(9100)
+    assert d.count(b"\xff\xda") == 65
+    info = _lib.ProbeInfo()
+    assert L.dg_probe(d, len(d), ctypes.byref(info)) == 0
+    assert info.progressive == 1 and info.gpu_supported == 1

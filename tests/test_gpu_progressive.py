@@ -321,3 +321,112 @@ def test_split_device_path_and_batch_limit():
         assert st == 0, i
         assert np.array_equal(ten.cpu().numpy(), _resized_ref(d, t)), i
     assert ctx.stat("prog_aggregates") == 1  # launched by the submission that reached prog_batch
+
+
+def _huff_codes(bits, vals):
+    """Canonical Huffman codes (T.81 Annex C) of a DHT (bits[16], vals)."""
+    codes, code, k = {}, 0, 0
+    for length in range(1, 17):
+        for _ in range(bits[length - 1]):
+            codes[vals[k]] = (code, length)
+            code += 1
+            k += 1
+        code <<= 1
+    return codes
+
+
+class _Bits:
+    def __init__(self):
+        self.out, self.acc, self.n = bytearray(), 0, 0
+
+    def put(self, v, n):
+        for i in range(n - 1, -1, -1):
+            self.acc = (self.acc << 1) | ((v >> i) & 1)
+            self.n += 1
+            if self.n == 8:
+                self.out.append(self.acc)
+                if self.acc == 0xFF:
+                    self.out.append(0)
+                self.acc, self.n = 0, 0
+
+    def done(self):
+        if self.n:
+            self.put((1 << (8 - self.n)) - 1, 8 - self.n)
+        return bytes(self.out)
+
+
+def _many_scan_jpeg(seed, bw=8, bh=5):
+    """A gray progressive JPEG with 65 scans (DC first at Al=1, one AC-first
+    scan per zigzag position 1..63, DC refinement): more than the 64 scans a
+    deps mask can describe.  Coefficients are drawn directly (quantiser 1),
+    Huffman tables are the standard luminance ones (the oracle encoder's)."""
+    import ctypes
+    from oracle import oracle as O2
+    lib = O2.lib()
+    dcb = list((ctypes.c_uint8 * 16).in_dll(lib, "oe_dc_luma_bits"))
+    dcv = list((ctypes.c_uint8 * 12).in_dll(lib, "oe_dc_vals"))
+    acb = list((ctypes.c_uint8 * 16).in_dll(lib, "oe_ac_luma_bits"))
+    acv = list((ctypes.c_uint8 * 162).in_dll(lib, "oe_ac_luma_vals"))
+    dcc, acc = _huff_codes(dcb, dcv), _huff_codes(acb, acv)
+    rng = np.random.default_rng(seed)
+    nb = bw * bh
+    coef = np.zeros((nb, 64), np.int32)
+    coef[:, 0] = rng.integers(-300, 300, nb)
+    coef[:, 1:] = rng.integers(-6, 7, (nb, 63)) * (rng.random((nb, 63)) < 0.35)
+
+    def seg(m, body):
+        return bytes([0xFF, m]) + (len(body) + 2).to_bytes(2, "big") + body
+
+    def mag(v):
+        s = int(abs(v)).bit_length()
+        return s, (v if v >= 0 else v + (1 << s) - 1) & ((1 << s) - 1)
+
+    def sos(ss, se, ah, al):
+        return seg(0xDA, bytes([1, 1, 0x00, ss, se, (ah << 4) | al]))
+
+    out = bytearray(b"\xFF\xD8")
+    out += seg(0xDB, bytes([0]) + bytes([1] * 64))
+    out += seg(0xC2, bytes([8]) + (bh * 8).to_bytes(2, "big") + (bw * 8).to_bytes(2, "big") + bytes([1, 1, 0x11, 0]))
+    out += seg(0xC4, bytes([0x00]) + bytes(dcb) + bytes(dcv))
+    out += seg(0xC4, bytes([0x10]) + bytes(acb) + bytes(acv))
+    b, pred = _Bits(), 0
+    for i in range(nb):  # DC first, Al = 1
+        v = int(coef[i, 0]) >> 1
+        s, m = mag(v - pred)
+        pred = v
+        b.put(*dcc[s])
+        b.put(m, s)
+    out += sos(0, 0, 0, 1) + b.done()
+    for k in range(1, 64):  # one AC-first scan per coefficient
+        b = _Bits()
+        for i in range(nb):
+            v = int(coef[i, k])
+            if v == 0:
+                b.put(*acc[0x00])  # EOB
+            else:
+                s, m = mag(v)
+                b.put(*acc[s])
+                b.put(m, s)
+        out += sos(k, k, 0, 0) + b.done()
+    b = _Bits()
+    for i in range(nb):  # DC refinement: bit 0
+        b.put(int(coef[i, 0]) & 1, 1)
+    out += sos(0, 0, 1, 0) + b.done() + b"\xFF\xD9"
+    return bytes(out)
+
+
+@pytest.mark.parametrize("chain", [0, 100])
+def test_progressive_more_than_64_scans(chain):
+    """Files with more scans than a deps mask holds decode, their
+    dependency groups always chained; equal to the oracle and to PIL."""
+    L = _lib()
+    ctx = L.Context(0)
+    ctx.set_option("prog_chain", chain)
+    datas = [_many_scan_jpeg(9100 + i, 8 + 3 * i, 5 + i) for i in range(3)] + [_prog(9200, 300, 200)]
+    for data, (st, arr, _) in zip(datas, ctx.decode_batch(datas)):
+        assert st == 0, L.last_error()
+        ost, ref = O.jpeg_decode(data)
+        assert ost == 0
+        pil = np.asarray(Image.open(io.BytesIO(data)))
+        assert np.array_equal(ref.reshape(pil.shape), pil)
+        assert np.array_equal(arr.reshape(ref.shape), ref)
