@@ -187,22 +187,29 @@ dg_status Context::init() {
 // lowest priority; 3: a CU mask over every CU (a masked stream gets a
 // hardware queue of its own).
 dg_status Context::make_prog_streams() {
+  return make_streams(kMaxInflight, kProgSlots, prog_queue_, prog_cus_);
+}
+
+// (Re)create the main and side streams of slots [first, first + count):
+// mode 0 plain, 1 / 2 highest / lowest priority, 3 a CU mask over `cus` CUs
+// (0 = all).  Modes 1-3 get hardware queues of their own.
+dg_status Context::make_streams(int first, int count, int mode, int cus) {
   HIPCHK(hipSetDevice(device_));
   int least = 0, greatest = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-  for (int j = 0; j < kProgSlots; j++) {
-    Slot &sl = slots_[kMaxInflight + j];
+  for (int j = first; j < first + count; j++) {
+    Slot &sl = slots_[j];
     for (hipStream_t *q : {&sl.st, &sl.side}) {
       if (*q) {
         HIPCHK(hipStreamSynchronize(*q));
         HIPCHK(hipStreamDestroy(*q));
         *q = nullptr;
       }
-      if (prog_queue_ == 1 || prog_queue_ == 2) {
-        HIPCHK(hipStreamCreateWithPriority(q, hipStreamNonBlocking, prog_queue_ == 1 ? greatest : least));
-      } else if (prog_queue_ == 3) {  // prog_cus of the CUs, spread evenly (every ncu/prog_cus-th)
+      if (mode == 1 || mode == 2) {
+        HIPCHK(hipStreamCreateWithPriority(q, hipStreamNonBlocking, mode == 1 ? greatest : least));
+      } else if (mode == 3) {  // cus of the CUs, spread evenly (every ncu/cus-th)
         std::vector<uint32_t> mask((ncu_ + 31) / 32, 0u);
-        const uint32_t want = prog_cus_ > 0 && (uint32_t)prog_cus_ < ncu_ ? (uint32_t)prog_cus_ : ncu_;
+        const uint32_t want = cus > 0 && (uint32_t)cus < ncu_ ? (uint32_t)cus : ncu_;
         for (uint32_t k = 0; k < want; k++) {
           const uint32_t cu = (uint32_t)(((uint64_t)k * ncu_) / want);
           mask[cu / 32] |= 1u << (cu % 32);
@@ -400,6 +407,19 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     }
     prog_queue_ = (int)v;
     return make_prog_streams();
+  }
+  if (k == "slot_queue") {  // baseline slots' streams: 0 plain, 1 high / 2 low priority, 3 CU-masked (own queues)
+    if (v < 0 || v > 3) return DG_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int j = 0; j < kMaxInflight; j++) {
+      Slot &sl = slots_[j];
+      if (sl.batch && !sl.batch->done) {
+        dg_status st = finish(sl);
+        if (st) return st;
+      }
+    }
+    slot_queue_ = (int)v;
+    return make_streams(0, kMaxInflight, slot_queue_, 0);
   }
   if (k == "prog_cus") {  // prog_queue 3: CUs the progressive streams may use (0 = all); set before prog_queue
     if (v < 0 || v > 4096) return DG_ERR_INVALID;
