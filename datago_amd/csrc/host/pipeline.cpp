@@ -165,10 +165,7 @@ dg_status Context::init() {
     sl.ev.resize(kNumStages + 1);
     for (auto &e : sl.ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-    if (&sl - slots_ < kMaxInflight) {  // progressive slots: make_prog_streams below
-      HIPCHK(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
-      HIPCHK(hipStreamCreateWithFlags(&sl.side, hipStreamNonBlocking));
-    }
+
     HIPCHK(hipEventCreateWithFlags(&sl.ev_meta, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_coef, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_zero, hipEventDisableTiming));
@@ -176,6 +173,7 @@ dg_status Context::init() {
     HIPCHK(hipEventCreateWithFlags(&sl.ev_png0, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_png1, hipEventDisableTiming));
   }
+  if (dg_status st = make_streams(0, kMaxInflight, slot_queue_, 0)) return st;
   return make_prog_streams();
 }
 

@@ -276,7 +276,7 @@ class Context {
   bool prog_split_ = true;
   int prog_batch_ = 2048;
   int prog_flush_us_ = 20000;
-  int slot_queue_ = 0;      // option "slot_queue" (make_streams for the baseline slots)
+  int slot_queue_ = 1;      // option "slot_queue" (make_streams for the baseline slots): high priority
   int prog_cus_ = 0;        // option "prog_cus" (prog_queue 3: CU mask width, 0 = all)
   int prog_queue_ = 2;      // option "prog_queue" (make_prog_streams): low priority, a queue of its own
   int64_t stat_prog_aggs_ = 0, stat_prog_agg_images_ = 0;
