@@ -121,7 +121,7 @@ struct Batch {
 // still runs batches k and k-1.  kProgSlots more run progressive batches only
 // (dg_submit's progressive aggregates, dg_decode_one's progressive lanes), so a
 // ~0.1-1 s refinement chain never holds a baseline slot.
-constexpr int kMaxInflight = 4;
+constexpr int kMaxInflight = 6;
 #ifndef DG_PROG_SLOTS
 #define DG_PROG_SLOTS 2
 #endif
