@@ -72,9 +72,9 @@ def parse():
                     help="per-stage HBM bytes from a PMC run of this configuration (tools/pmc_traffic.py)")
     ap.add_argument("--wg-timing", action="store_true", help="debug: per-workgroup timing of the entropy kernels")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="batches in flight (context slots / output arenas); 0 = 3 for jpeg (84.7-85.7 -> 87.4-89.2 "
-                         "Gpx/s vs 2, profiles/r02/inflight), 2 for wds, 4 for png (its inflate chains leave most of "
-                         "the GPU idle: 2347 -> 2958 Mpx/s measured)")
+                    help="batches in flight (context slots / output arenas); 0 = 4 for jpeg (3 vs 4: 94.6 vs 96.8 "
+                         "Gpx/s mean of 3 alternating runs, profiles/r03/slots), 2 for wds, 4 for png (its inflate "
+                         "chains leave most of the GPU idle: 2347 -> 2958 Mpx/s measured)")
     ap.add_argument("--entropy-once", type=int, default=-1, help="decode-once entropy staging (-1 = library default)")
     ap.add_argument("--entropy-lpt", type=int, default=-1, help="slow entropy workgroups first (-1 = library default)")
     ap.add_argument("--hb-bands", type=int, default=0, help="band H kernel: 8-row bands per workgroup (0 = default)")
@@ -118,7 +118,7 @@ def parse():
     if a.samples <= 0:
         a.samples = 1_000_000 if a.workload == "cfg4" else 100_000
     if a.inflight <= 0:
-        a.inflight = 4 if a.workload == "png" else 3 if a.workload in ("jpeg", "cfg4") else 2
+        a.inflight = 4 if a.workload in ("png", "jpeg", "cfg4") else 2
     if a.batch <= 0:
         a.batch = 1024 if a.workload == "wds" else 256
     if a.size <= 0:  # BASELINE.json configs[2]: "decode + resize to 512"
@@ -599,8 +599,7 @@ def main() -> int:
         ctx.set_option("entropy_lpt", a.entropy_lpt)
     if a.entropy_once >= 0:
         ctx.set_option("entropy_once", a.entropy_once)
-    if a.inflight != 3:
-        ctx.set_option("slots", a.inflight)
+    ctx.set_option("slots", a.inflight)
     # ---- pool -> HBM (one arena, 16-byte aligned entries; wds: the shards themselves)
     if wds:
         host_arena = np.concatenate([tar_arena, np.zeros(64, np.uint8)])

@@ -303,7 +303,7 @@ class Context {
 
   Slot slots_[kAllSlots];  // [0, kMaxInflight): baseline batches; then kProgSlots progressive ones
   uint32_t ncu_ = 256;  // compute units: persistent-worker grids
-  int nslots_ = 3;  // option "slots": batches in flight (each slot: own streams + scratch; 3 measured +3-4% over 2)
+  int nslots_ = 4;  // option "slots": batches in flight (each slot: own streams + scratch; 4 measured +2% over 3 with own queues)
   int next_slot_ = 0;
   uint64_t next_ticket_ = 1;
 

@@ -256,7 +256,7 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "write_pair"  k_huff_write: up to this many more AC symbols per step out of one 32-bit peek (0..3,
  *                 default 3)
  *   "sync_pair"   1 = the same in k_huff_sync after a single-symbol step (default 0: measured slower)
- *   "slots"       baseline batches in flight, 1..6 (default 3), each with its own scratch arena, pinned
+ *   "slots"       baseline batches in flight, 1..6 (default 4), each with its own scratch arena, pinned
  *                 staging and streams; progressive batches use two slots of their own
  *   "hb_bands"    band H kernel: 8-row bands per workgroup, 1..64 (default 16)
  *   "entropy_lpt" 1 = dispatch the slowest entropy workgroups first (default 1)

@@ -185,7 +185,7 @@ def test_entropy_decode_once_matches(sub_bits):
 def test_band_and_slot_options_validated():
     L = _lib()
     ctx = L.Context(0)
-    for k, v in (("hb_bands", 0), ("hb_bands", 65), ("slots", 0), ("slots", 5)):
+    for k, v in (("hb_bands", 0), ("hb_bands", 65), ("slots", 0), ("slots", 7)):
         with pytest.raises(Exception):
             ctx.set_option(k, v)
 
