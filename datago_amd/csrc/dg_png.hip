@@ -835,15 +835,23 @@ __device__ __forceinline__ uint32_t lane_sym(LaneBits &r, const LaneTab<B, LutPt
   return 0xFFFFu;
 }
 
-constexpr uint32_t kInfLdsPerLane = (512 + 128) * 2;  // 80 KiB per 64-lane workgroup: 2 per CU
+// LDS bytes per lane: an LB-bit literal/length and a DB-bit distance lookup
+template <uint32_t LB, uint32_t DB>
+constexpr uint32_t inf_lds_per_lane() {
+  return ((1u << LB) + (1u << DB)) * 2u;
+}
 
 // One lane per chunk: decode from the chunk's candidate block start until a
 // block ends exactly where a later chunk's candidate starts (or the stream
 // ends), writing uint16 entries: bytes, or 256 + window index for bytes that
-// lie before the chunk (resolved by k_inf_resolve).
-__global__ __launch_bounds__(64) void k_inf_decode(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
+// lie before the chunk (resolved by k_inf_resolve). WG lanes per workgroup;
+// the lookups take WG * inf_lds_per_lane<LB, DB>() bytes of LDS (64 lanes,
+// 9/7 bits: 80 KiB, two workgroups per CU).
+template <uint32_t WG, uint32_t LB, uint32_t DB>
+__global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
                                                    uint32_t nch) {
-  const uint32_t gi = blockIdx.x * 64 + threadIdx.x;
+  constexpr uint32_t kInfLdsPerLane = inf_lds_per_lane<LB, DB>();
+  const uint32_t gi = blockIdx.x * WG + threadIdx.x;
   if (gi >= nch) return;
   InfChunk &c = ch[gi];
   c.len = 0;
@@ -861,8 +869,8 @@ __global__ __launch_bounds__(64) void k_inf_decode(const ImageDesc *__restrict__
   // LDS: per lane a 9-bit literal/length and a 7-bit distance lookup
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   DG_LDS uint16_t *lds = (DG_LDS uint16_t *)(DG_LDS uint8_t *)smem_raw + threadIdx.x * kInfLdsPerLane / 2;
-  LaneTab<9, DG_LDS uint16_t *> tl{lds, (DG_GLOBAL uint16_t *)(tb + 2624), 0, 0, {0, 0, 0}};
-  LaneTab<7, DG_LDS uint16_t *> td{lds + 512, (DG_GLOBAL uint16_t *)(tb + 3264), 0, 0, {0, 0, 0}};
+  LaneTab<LB, DG_LDS uint16_t *> tl{lds, (DG_GLOBAL uint16_t *)(tb + 2624), 0, 0, {0, 0, 0}};
+  LaneTab<DB, DG_LDS uint16_t *> td{lds + (1u << LB), (DG_GLOBAL uint16_t *)(tb + 3264), 0, 0, {0, 0, 0}};
   LaneTab<6, DG_GLOBAL uint16_t *> tc{(DG_GLOBAL uint16_t *)(tb + 3328), (DG_GLOBAL uint16_t *)(tb + 3520), 0, 0,
                                       {0, 0, 0}};
   const uint32_t zbits_total = pd.zlen * 8u;
@@ -1523,14 +1531,31 @@ void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
 void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_inf_find, dim3(nwg), dim3(64), 0, st, imgs, ch, list);
 }
-void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch) {
+template <uint32_t WG, uint32_t LB, uint32_t DB>
+static void launch_inf_decode_t(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch) {
+  constexpr uint32_t lds = WG * inf_lds_per_lane<LB, DB>();
   static bool attr = false;  // > 64 KiB of dynamic LDS
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_inf_decode, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              64 * kInfLdsPerLane);
+    (void)hipFuncSetAttribute((const void *)k_inf_decode<WG, LB, DB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
     attr = true;
   }
-  if (nch) hipLaunchKernelGGL(k_inf_decode, dim3((nch + 63) / 64), dim3(64), 64 * kInfLdsPerLane, st, imgs, ch, nch);
+  if (nch) hipLaunchKernelGGL((k_inf_decode<WG, LB, DB>), dim3((nch + WG - 1) / WG), dim3(WG), lds, st, imgs, ch, nch);
+}
+// variant: 64-lane workgroups with 0 = 9/7-bit lookups (80 KiB, 2 per CU);
+// 1 = 8/6 bits (40 KiB, 4 per CU); 2 = 7/6 bits (24 KiB, 6 per CU);
+// 3 = 7/5 bits (20 KiB, 8 per CU); 4 = 6/5 bits (12 KiB); 5 = 6/4 bits
+// (10 KiB). 32-lane workgroups measured no faster
+// than 64-lane ones of the same LDS (profiles/r03/infdec)
+void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch, uint32_t variant) {
+  switch (variant) {
+    case 1: launch_inf_decode_t<64, 8, 6>(st, imgs, ch, nch); break;
+    case 2: launch_inf_decode_t<64, 7, 6>(st, imgs, ch, nch); break;
+    case 3: launch_inf_decode_t<64, 7, 5>(st, imgs, ch, nch); break;
+    case 4: launch_inf_decode_t<64, 6, 5>(st, imgs, ch, nch); break;
+    case 5: launch_inf_decode_t<64, 6, 4>(st, imgs, ch, nch); break;
+    default: launch_inf_decode_t<64, 9, 7>(st, imgs, ch, nch); break;
+  }
 }
 void launch_inf_resolve(hipStream_t st, ImageDesc *imgs, const InfChunk *ch, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_inf_resolve, dim3(nwg), dim3(1024), 0, st, imgs, ch, list);

@@ -520,6 +520,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     sub_density_ = (double)v;
     return DG_OK;
   }
+  if (k == "inf_decode") {  // k_inf_decode lookup bits (literal/length, distance): 0 9/7, 1 8/6, 2 7/6, 3 7/5, 4 6/5, 5 6/4
+    if (v < 0 || v > 5) return DG_ERR_INVALID;
+    inf_decode_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "h_mfma") {  // 0: band H passes with the VALU convolution (k_resize_hb, A/B)
     h_mfma_ = v != 0;
     return DG_OK;
@@ -2011,7 +2016,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
       }
       InfChunk *ich = (InfChunk *)(M + b.ichunk_off);
       launch_inf_find(sl.st, dd, ich, lst(L_INF_FIND), cnt(L_INF_FIND));
-      launch_inf_decode(sl.st, dd, ich, (uint32_t)b.ichunks.size());
+      launch_inf_decode(sl.st, dd, ich, (uint32_t)b.ichunks.size(), inf_decode_);
       launch_inf_resolve(sl.st, dm, ich, lst(L_INF_RES), cnt(L_INF_RES));
       launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG), beside ? 1 : 2);
       if (beside) HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_png1, 0));

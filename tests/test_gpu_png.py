@@ -196,10 +196,12 @@ def test_png_large_full_size_properties(ctx512):
     assert st == 0 and (arr.shape[1], arr.shape[0]) == t.target_size(1800, 1200)
 
 
-def test_chunked_inflate_matches_serial_and_oracle():
+@pytest.mark.parametrize("inf_decode", [0, 1, 2, 3, 4, 5])
+def test_chunked_inflate_matches_serial_and_oracle(inf_decode):
     """Large streams take the chunk-parallel inflate (block-header search,
     one lane per chunk, window markers); it must equal the oracle and the
-    serial kernel (option png_chunked=0) byte for byte."""
+    serial kernel (option png_chunked=0) byte for byte, for every
+    k_inf_decode shape (option inf_decode: lanes per workgroup, lookup bits)."""
     L = _lib()
     rng = np.random.default_rng(31)
     datas = []
@@ -211,6 +213,7 @@ def test_chunked_inflate_matches_serial_and_oracle():
     datas.append(synth.make_png(77, 1200, 900, "RGBA", level=6))
     datas.append(synth.make_png(78, 1600, 1000, "L", level=6, filters="random"))
     a = L.Context(0)
+    a.set_option("inf_decode", inf_decode)
     b = L.Context(0)
     b.set_option("png_chunked", 0)
     ra, rb = a.decode_batch(datas), b.decode_batch(datas)
