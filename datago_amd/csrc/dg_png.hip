@@ -1143,14 +1143,13 @@ __device__ __forceinline__ uint32_t shfl_up1(uint32_t v) {
 // tile k-1; tile k-2 is complete, is stored to HBM, and its buffer receives
 // tile k+1.  Each lane takes kUfU units per step (lane l at step t owns units
 // kUfU*(t-l) ..), so one shuffle round trip serves kUfU units.
-constexpr uint32_t kUfU = 2;
-constexpr uint32_t kUfTile = 64 * kUfU;
+// kUfU is a template parameter (option uf_units, 1 or 2; default 2).
 // LDS of one worker: 3 tiles of 64 rows plus 3 previous-band rows, each
 // kUfTile * bpp + 4 bytes (dword misalignment; an odd number of words, so
 // lane rows fall on distinct banks).  Sized for the batch's widest filter
 // unit (dynamic LDS), so batches of 1-3-byte units run more workers per CU.
-__host__ __device__ constexpr uint32_t uf_pitch(uint32_t bpp) { return kUfTile * bpp + 4; }
-__host__ __device__ constexpr uint32_t uf_smem_bytes(uint32_t bpp) { return (3 * 64 + 3) * uf_pitch(bpp); }
+__host__ __device__ constexpr uint32_t uf_pitch(uint32_t bpp, uint32_t u) { return 64 * u * bpp + 4; }
+__host__ __device__ constexpr uint32_t uf_smem_bytes(uint32_t bpp, uint32_t u) { return (3 * 64 + 3) * uf_pitch(bpp, u); }
 struct UnfilterSmem {
   uint8_t *base;
   uint32_t pitch;
@@ -1208,10 +1207,11 @@ __device__ __forceinline__ bool uf_wait(const DG_GLOBAL uint32_t *flag, uint32_t
 // Rows [y0, y0 + 64) of one filtered plane (the image, or one Adam7 pass) of
 // H rows of 1 + rb bytes at raw_a -> rows of rb bytes at stride us at unf_a.
 // `pred` is the previous band's progress flag (null for the first band).
-template <uint32_t BPP>
+template <uint32_t BPP, uint32_t kUfU>
 __device__ void unfilter_band(const UnfilterSmem &sm, ImageDesc &im, uint64_t raw_a, uint64_t unf_a, uint32_t rb,
                               uint32_t us, uint32_t H, uint32_t y0, DG_GLOBAL uint32_t *self,
                               const DG_GLOBAL uint32_t *pred, bool force_timeout) {
+  constexpr uint32_t kUfTile = 64 * kUfU;
   const uint32_t lane = threadIdx.x;
   const uint32_t units = rb / BPP;  // BPP == 1 covers sub-byte samples (filter unit = 1 byte)
   const uint32_t tb = kUfTile * BPP;
@@ -1360,10 +1360,11 @@ __device__ void unfilter_band(const UnfilterSmem &sm, ImageDesc &im, uint64_t ra
 // ticket order (bands of all planes round-robin, band 0 of every plane first),
 // so a band's predecessor was always taken earlier by a running worker and
 // every wait ends (no dependence on which workgroups are resident).
+template <uint32_t U>
 __global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ tasks,
                                                      uint32_t ntasks, uint32_t *__restrict__ flags_,
                                                      uint32_t *__restrict__ ticket, uint32_t dbg) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t uf_smem[];  // uf_smem_bytes(batch's widest unit)
+  extern __shared__ __attribute__((aligned(16))) uint8_t uf_smem[];  // uf_smem_bytes(batch's widest unit, U)
   __shared__ uint32_t s_ticket;
   DG_GLOBAL uint32_t *flags = gp<uint32_t>((uint64_t)(uintptr_t)flags_);
   for (;;) {
@@ -1397,12 +1398,12 @@ __global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ img
     // test switch (debug_flags bit 18): band 1 of every plane times out on its first wait
     const bool force = (dbg & 1u) && band == 1;
     if (!uni(im.status)) {  // (an image whose inflate failed has nothing to unfilter)
-      const UnfilterSmem sm{uf_smem, uf_pitch(pd.bpp <= 4 ? pd.bpp : 4)};
+      const UnfilterSmem sm{uf_smem, uf_pitch(pd.bpp <= 4 ? pd.bpp : 4, U)};
       switch (pd.bpp) {
-        case 1: unfilter_band<1>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
-        case 2: unfilter_band<2>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
-        case 3: unfilter_band<3>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
-        default: unfilter_band<4>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
+        case 1: unfilter_band<1, U>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
+        case 2: unfilter_band<2, U>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
+        case 3: unfilter_band<3, U>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
+        default: unfilter_band<4, U>(sm, im, ra, ua, rb, us, H, band * 64, self, pred, force); break;
       }
     }
     uf_publish(self, kUfDone);  // the next band's tiles read this band's last row from HBM
@@ -1560,19 +1561,30 @@ void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint
 void launch_inf_resolve(hipStream_t st, ImageDesc *imgs, const InfChunk *ch, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_inf_resolve, dim3(nwg), dim3(1024), 0, st, imgs, ch, list);
 }
-void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
-                         uint32_t ncu, uint32_t maxbpp, uint32_t dbg) {
+template <uint32_t U>
+static void launch_png_unfilter_t(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks,
+                                  uint32_t *flags, uint32_t ncu, uint32_t maxbpp, uint32_t dbg) {
   // flags: ntasks progress words + the ticket counter, zeroed by the caller
   static bool attr = false;  // > 64 KiB of dynamic LDS
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_png_unfilter, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)uf_smem_bytes(4));
+    (void)hipFuncSetAttribute((const void *)k_png_unfilter<U>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)uf_smem_bytes(4, U));
     attr = true;
   }
-  const uint32_t bpp = maxbpp < 1 ? 1u : maxbpp > 4 ? 4u : maxbpp, lds = uf_smem_bytes(bpp);
+  const uint32_t bpp = maxbpp < 1 ? 1u : maxbpp > 4 ? 4u : maxbpp, lds = uf_smem_bytes(bpp, U);
   const uint32_t per_cu = std::max<uint32_t>(1u, (160u * 1024u - 64u) / (lds + 64u));  // workers resident per CU
   const uint32_t g = std::min(ntasks, ncu * per_cu);
-  if (g) hipLaunchKernelGGL(k_png_unfilter, dim3(g), dim3(64), lds, st, imgs, tasks, ntasks, flags, flags + ntasks, dbg);
+  if (g)
+    hipLaunchKernelGGL(k_png_unfilter<U>, dim3(g), dim3(64), lds, st, imgs, tasks, ntasks, flags, flags + ntasks, dbg);
+}
+// units: filter units per lane per diagonal step (tiles of 64 * units columns;
+// 1 halves the LDS per worker, 2 halves the shuffle round trips per unit)
+void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
+                         uint32_t ncu, uint32_t maxbpp, uint32_t dbg, uint32_t units) {
+  if (units == 1)
+    launch_png_unfilter_t<1>(st, imgs, tasks, ntasks, flags, ncu, maxbpp, dbg);
+  else
+    launch_png_unfilter_t<2>(st, imgs, tasks, ntasks, flags, ncu, maxbpp, dbg);
 }
 void launch_png_expand(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_png_expand, dim3(nwg), dim3(256), 0, st, imgs, list);

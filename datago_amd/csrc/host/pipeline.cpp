@@ -520,6 +520,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     sub_density_ = (double)v;
     return DG_OK;
   }
+  if (k == "uf_units") {  // PNG unfilter: filter units per lane per step (1: half the LDS per worker)
+    if (v < 1 || v > 2) return DG_ERR_INVALID;
+    uf_units_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "inf_decode") {  // k_inf_decode lookup bits (literal/length, distance): 0 9/7, 1 8/6, 2 7/6, 3 7/5, 4 6/5, 5 6/4
     if (v < 0 || v > 5) return DG_ERR_INVALID;
     inf_decode_ = (uint32_t)v;
@@ -2029,7 +2034,8 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
     if (b.uf_n) {
       uint32_t *uf = (uint32_t *)((char *)sl.scratch.p + b.uf_flags_off);
       HIPCHK(hipMemsetAsync(uf, 0, (size_t)(b.uf_n + 1) * 4, sl.st));
-      launch_png_unfilter(sl.st, dm, lst(L_UNF), cnt(L_UNF), uf, ncu_, b.uf_maxbpp, (uint32_t)(debug_flags_ >> 18) & 1u);
+      launch_png_unfilter(sl.st, dm, lst(L_UNF), cnt(L_UNF), uf, ncu_, b.uf_maxbpp, (uint32_t)(debug_flags_ >> 18) & 1u,
+                          uf_units_);
     }
     launch_png_expand(sl.st, dd, lst(L_EXPAND), cnt(L_EXPAND));
   }

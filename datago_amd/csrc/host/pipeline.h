@@ -322,6 +322,7 @@ class Context {
   int copy_threads_ = 8;                // option "copy_threads": host threads for a host-out batch's output copies
   bool hv_fused_ = false;               // option "hv_fused": first H + V pass fused (k_resize_hv) when it fits
   bool band_dec_ = false;               // option "band_dec": IDCT + colour + first H pass in k_band_dec
+  uint32_t uf_units_ = 2;               // option "uf_units": PNG unfilter units per lane per step (1 or 2)
   uint32_t inf_decode_ = 2;             // option "inf_decode": k_inf_decode lookup bits (2 = 7/6, 24 KiB LDS per wave)
   bool h_mfma_ = false;                 // option "h_mfma": band H passes on the matrix cores (k_resize_hm; measured slower: off)
   double sub_density_ = 0;              // option "sub_density": bits per block below which subsequences shrink

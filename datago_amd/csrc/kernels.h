@@ -86,7 +86,8 @@ void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
 // tasks: (image, pass << 24 | band) in ticket order; flags: ntasks + 1 zeroed words;
 // dbg bit 0: band 1 of every plane times out on its first wait (test switch)
 void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
-                         uint32_t ncu, uint32_t maxbpp, uint32_t dbg);
+                         uint32_t ncu, uint32_t maxbpp, uint32_t dbg,
+                         uint32_t units);
 // 256 pixels per workgroup
 void launch_png_expand(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 // alpha program at `point` (0 before call 1, 1 between the calls, 2 after call 2): 256 pixels per workgroup

@@ -248,13 +248,15 @@ def test_png_adam7_bit_exact(ctx_dec, ctx512):
         assert np.array_equal(arr, O.crop_and_resize(ref, tw, th, O.MODE_FIR))
 
 
-def test_serial_inflate_beside_chunked_and_unfilter_unit_widths():
+@pytest.mark.parametrize("uf_units", [2, 1])
+def test_serial_inflate_beside_chunked_and_unfilter_unit_widths(uf_units):
     """Round-2 scheduling paths: small streams (masks) inflate on the side
     stream beside the chunk-parallel kernels (option side_stream 1, mode 0 +
     fallbacks mode 1) or after them on the main stream (side_stream 0, mode
     2); and the pipelined unfilter sizes its LDS for the batch's widest filter
     unit (L-only batches: 6 workers per CU, RGBA: 1).  Every variant equals
-    the oracle byte for byte; tall images give many pipelined bands."""
+    the oracle byte for byte; tall images give many pipelined bands.  Both
+    unfilter tile widths (option uf_units: 64 or 128 filter units) run."""
     L = _lib()
     rng = np.random.default_rng(47)
     big = [synth.pil_png(synth.synth_pixels(rng, 1300, 1700), compress_level=6),  # chunked
@@ -265,6 +267,7 @@ def test_serial_inflate_beside_chunked_and_unfilter_unit_widths():
     for side in (1, 0):
         ctx = L.Context(0)
         ctx.set_option("side_stream", side)
+        ctx.set_option("uf_units", uf_units)
         for name, datas in batches.items():
             for k, (d, (st, arr, _)) in enumerate(zip(datas, ctx.decode_batch(datas))):
                 ost, ref = O.png_decode(d)
