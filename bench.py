@@ -80,8 +80,9 @@ def parse():
     ap.add_argument("--hb-bands", type=int, default=0, help="band H kernel: 8-row bands per workgroup (0 = default)")
     ap.add_argument("--ckpt", type=int, default=-1, help="entropy checkpoints (-1 = library default)")
     ap.add_argument("--idct-fused", type=int, default=-1, help="IDCT inside the entropy write kernel (-1 = default)")
-    ap.add_argument("--decode-semantics", type=int, default=0,
-                    help="JPEG pixel semantics: 0 libjpeg-turbo (pinned, default), 1 zune-jpeg 0.5.12 restated")
+    ap.add_argument("--decode-semantics", type=int, default=1, choices=(0, 1),
+                    help="JPEG pixel semantics: 1 zune-jpeg 0.5.12 restated (default: the reference's decoder, the "
+                         "mode INTEGRATION.md sets for the drop-in), 0 libjpeg-turbo (pinned to PIL)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall seconds of the CPU-baseline sample (x cores of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=3, help="host-memory (PCIe-inclusive) steps")
@@ -185,9 +186,10 @@ def reference_toolchain() -> str:
 
 def _cpu_work(args):
     from oracle import oracle as O
-    data, tw, th, enc = args
+    data, tw, th, enc, sem = args
     t = time.perf_counter()
-    st, dec = O.decode_any(data)
+    with O.semantics(sem):
+        st, dec = O.decode_any(data)
     out = O.crop_and_resize(dec, tw, th, O.MODE_FIR) if (dec.shape[1], dec.shape[0]) != (tw, th) else dec
     if enc:
         O.jpeg_encode(out, 92)
@@ -243,20 +245,20 @@ def pillow_baseline(pool, targets, seconds: float, encode: bool = False):
                       f"{cores} processes ({basis}), {wall:.1f} s"}
 
 
-def cpu_baseline(pool, targets, seconds: float, encode: bool = False):
+def cpu_baseline(pool, targets, seconds: float, encode: bool = False, sem: int = 1):
     """Oracle (scalar C restatement of the reference path: decode +
-    crop_and_resize) on the host cores, one image per task like the
-    reference's tokio worker (worker_files.rs:74-141)."""
+    crop_and_resize, in the GPU run's decode semantics) on the host cores, one
+    image per task like the reference's tokio worker (worker_files.rs:74-141)."""
     import multiprocessing as mp
     from oracle import oracle as O
     O.lib()
     cores, basis = host_cores()
     # size the sample from a one-image probe so the run takes ~`seconds`
-    px, dt = _cpu_work((pool[0], *targets[0], encode))
+    px, dt = _cpu_work((pool[0], *targets[0], encode, sem))
     per_px = dt / max(px, 1)
     mean_px = np.mean([w * h for (w, h) in [image_dims(d)[:2] for d in pool[:32]]])
     n = int(max(cores, min(64 * len(pool), seconds * cores / max(per_px * mean_px, 1e-9))))
-    jobs = [(pool[i % len(pool)], *targets[i % len(pool)], encode) for i in range(n)]
+    jobs = [(pool[i % len(pool)], *targets[i % len(pool)], encode, sem) for i in range(n)]
     p = mp.get_context("fork").Pool(cores)
     try:
         p.map(_cpu_work, jobs[:cores], chunksize=1)  # workers up and the oracle loaded
@@ -269,7 +271,8 @@ def cpu_baseline(pool, targets, seconds: float, encode: bool = False):
     tot_px = sum(r[0] for r in res)
     return {"value": round(tot_px / wall / 1e6, 2), "unit": "Mpixel/s", "cores": cores, "kind": "port",
             "sample": f"{n} images of the same pool ({tot_px / 1e6:.1f} Mpx) through oracle/ (scalar C "
-                      f"decode + FIR-mode Lanczos3 crop_and_resize{' + JPEG q92 encode' if encode else ''}), "
+                      f"decode in {'zune-jpeg' if sem else 'libjpeg-turbo'} semantics + FIR-mode Lanczos3 "
+                      f"crop_and_resize{' + JPEG q92 encode' if encode else ''}), "
                       f"{cores} processes ({basis}), {wall:.1f} s",
             "cpu_model": cpu_model(), "reference_toolchain": reference_toolchain()}
 
@@ -580,8 +583,7 @@ def main() -> int:
         ctx.set_option("wg_timing", 1)
     if a.hb_bands:
         ctx.set_option("hb_bands", a.hb_bands)
-    if a.decode_semantics:
-        ctx.set_option("decode_semantics", a.decode_semantics)
+    ctx.set_option("decode_semantics", a.decode_semantics)
     if a.ckpt >= 0:
         ctx.set_option("ckpt", a.ckpt)
     if a.hv_fused >= 0:
@@ -994,6 +996,11 @@ def main() -> int:
                                    (f"configs[4]{'' if a.encode else ' without re-encode'}: RGB PNG (PIL, zlib 6) "
                                     "+ L8 mask PNG pairs, mask aligned to the image's bucket, decode + crop/resize "
                                     f"to 1024/32{' + JPEG q92 re-encode of every payload' if a.encode else ''}"),
+                       "decode_semantics": {"value": a.decode_semantics,
+                                            "name": "zune-jpeg 0.5.12" if a.decode_semantics else "libjpeg-turbo",
+                                            "note": "JPEG pixel stages (IDCT, upsampling, colour); 1 is the "
+                                                    "reference's decoder and the mode INTEGRATION.md sets for the "
+                                                    "drop-in (dg_image_config.decode_semantics)"},
                        "pre_encode_images": bool(a.encode),
                        "progressive_frac": a.progressive_frac, **({"ctx_opt": a.ctx_opt} if a.ctx_opt else {}),
                        "restart_marker_rows": a.rst_rows,
@@ -1071,7 +1078,7 @@ def main() -> int:
                               for q in ("span", "mean", "p90", "max")} if a.wg_timing else None),
         }
         if world == 1 and not a.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(pool, targets, a.cpu_seconds, a.encode)
+            result["cpu_baseline"] = cpu_baseline(pool, targets, a.cpu_seconds, a.encode, a.decode_semantics)
             result["cpu_baseline_pillow"] = pillow_baseline(pool, targets, a.cpu_seconds, a.encode)
         else:
             result["cpu_baseline"] = None

@@ -608,12 +608,18 @@ int Context::timings(const char **names, float *ms, int cap) {
 // previous batch is finished before its buffers are reused), so it is only
 // retired and freed later: at destruction, or once retired buffers pass
 // kRetiredMax, after a sync of every stream.
-static constexpr size_t kRetiredMax = (size_t)16 << 30;
+// Device and page-locked host memory have limits of their own: several ranks
+// per host each keeping GiBs of grown-out buffers page-locked would pin a lot
+// of the host's memory.  Retired buffers are also freed at the first idle
+// moment (a wait that leaves no batch in flight, free_retired_if_idle).
+static constexpr size_t kRetiredDevMax = (size_t)4 << 30;
+static constexpr size_t kRetiredPinMax = (size_t)512 << 20;
 
 void Context::retire(void *p, size_t bytes, bool pinned) {
   (pinned ? retired_pinned_ : retired_dev_).push_back(p);
-  retired_bytes_ += bytes;
-  if (retired_bytes_ > kRetiredMax && sync_all() == DG_OK) free_retired();
+  (pinned ? retired_pin_bytes_ : retired_dev_bytes_) += bytes;
+  if ((retired_dev_bytes_ > kRetiredDevMax || retired_pin_bytes_ > kRetiredPinMax) && sync_all() == DG_OK)
+    free_retired();
 }
 
 void Context::free_retired() {
@@ -621,7 +627,15 @@ void Context::free_retired() {
   for (void *p : retired_pinned_) hipHostFree(p);
   retired_dev_.clear();
   retired_pinned_.clear();
-  retired_bytes_ = 0;
+  retired_dev_bytes_ = retired_pin_bytes_ = 0;
+}
+
+// mu_ held.  hipFree synchronises the device, so only when nothing is in flight.
+void Context::free_retired_if_idle() {
+  if (retired_dev_.empty() && retired_pinned_.empty()) return;
+  for (const Slot &s : slots_)
+    if (s.batch && !s.batch->done) return;
+  free_retired();
 }
 
 dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
@@ -861,15 +875,31 @@ struct Layout {
 dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
                           const int32_t *forced, uint8_t *const *outs, const uint64_t *caps,
                           dg_payload_meta *metas, bool host_io, uint64_t *ticket, dg_payload_meta *const *mptrs,
-                          int force_slot) {
-  std::lock_guard<std::mutex> lk(mu_);
+                          int force_slot, bool defer_meta) {
+  std::unique_lock<std::mutex> lk(mu_);
   if (n < 0 || (n > 0 && (!h_srcs || !lens || !outs || !caps || (!metas && !mptrs)))) {
     set_error("null argument");
     return DG_ERR_INVALID;
   }
   HIPCHK(hipSetDevice(device_));
   Slot &sl = slots_[force_slot >= 0 ? force_slot : pick_slot()];
-  if (sl.batch && !sl.batch->done) {  // this slot's previous batch must complete first
+  // This slot's previous batch must complete first.  Its GPU work is waited
+  // for without the context lock: a progressive slot's batch can run ~1 s,
+  // and every other dg_submit / dg_wait / dg_poll of the context would stall
+  // behind it.  Re-checked after relocking: another thread may
+  // have finished that batch, or queued one of its own on the slot.
+  while (sl.batch && !sl.batch->done) {
+    if (hipEventQuery(sl.batch->fin->e) == hipErrorNotReady) {
+      std::shared_ptr<BatchEvent> fin = sl.batch->fin;
+      lk.unlock();
+      const hipError_t e = hipEventSynchronize(fin->e);
+      lk.lock();
+      if (e != hipSuccess) {
+        set_error(std::string("HIP error: ") + hipGetErrorString(e) + " waiting for a slot's batch");
+        return DG_ERR_DEVICE;
+      }
+      continue;
+    }
     dg_status st = finish(sl);
     if (st) return st;
   }
@@ -882,6 +912,15 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.host_io = host_io;
   b.mptr.resize(n);
   for (int i = 0; i < n; i++) b.mptr[i] = mptrs ? mptrs[i] : &metas[i];
+  if (defer_meta) {
+    // A progressive aggregate's members: the callers' metas keep reading
+    // DG_ERR_NOT_READY until finish() publishes the batch's own copies
+    // (dg_wait_ready's contract; the GPU is still decoding while planning
+    // fills in status and dimensions).
+    b.pub = b.mptr;
+    b.local_meta.assign(n, dg_payload_meta{});
+    for (int i = 0; i < n; i++) b.mptr[i] = &b.local_meta[i];
+  }
   b.plans.resize(n);
   b.desc_of.assign(n, -1);
   auto phase_t0 = std::chrono::steady_clock::now();
@@ -2332,6 +2371,7 @@ dg_status Context::finish(Slot &sl) {
     }
   }
   parallel_copy(copies, copy_threads_);
+  for (size_t i = 0; i < b.pub.size(); i++) *b.pub[i] = b.local_meta[i];  // defer_meta: publish now
   b.done = true;
   return DG_OK;
 }
@@ -2360,7 +2400,9 @@ dg_status Context::wait(uint64_t ticket) {
   Slot *sl = find(ticket);
   if (!sl) return ticket < next_ticket_ ? DG_OK : DG_ERR_INVALID;
   if (sl->batch->done) return DG_OK;
-  return finish(*sl);
+  const dg_status st = finish(*sl);
+  if (!st) free_retired_if_idle();
+  return st;
 }
 
 dg_status Context::flush_batch(std::vector<OneReq *> &batch, bool prog) {
@@ -2515,14 +2557,14 @@ dg_status Context::flush_pagg_locked() {
   }
   uint64_t t = 0;
   dg_status st = submit(n, h.data(), pagg_host_ ? nullptr : d.data(), lens.data(), forced.data(), outs.data(),
-                        caps.data(), nullptr, pagg_host_, &t, mp.data(), slot);
-  if (st) {
+                        caps.data(), nullptr, pagg_host_, &t, mp.data(), slot, true);
+  if (st) {  // no batch: the members fail now, and dg_wait on any of their tickets returns st
     for (PEntry &e : pagg_) e.meta->status = st;
     t = 0;
   }
   stat_prog_aggs_++;
   stat_prog_agg_images_ += n;
-  pgen_[pagg_gen_] = {t, pagg_refs_};
+  pgen_[pagg_gen_] = PGen{t, pagg_refs_, st};
   pagg_refs_ = 0;
   pagg_gen_++;
   pagg_.clear();
@@ -2542,8 +2584,11 @@ dg_status Context::submit_user(int n, const uint8_t *const *h_srcs, const uint8_
     }
   if (!np) {
     dg_status st = submit(n, h_srcs, d_srcs, lens, forced, outs, caps, metas, host_io, ticket);
-    std::lock_guard<std::mutex> lk(pmu_);
-    if (pagg_stale_locked()) flush_pagg_locked();
+    // a stale aggregate is launched by whoever comes by, but a baseline
+    // submitter never queues behind a thread that holds the aggregate (its
+    // launch may wait for a busy progressive slot)
+    std::unique_lock<std::mutex> lk(pmu_, std::try_to_lock);
+    if (lk.owns_lock() && pagg_stale_locked()) flush_pagg_locked();
     return st;
   }
   SplitRec rec;
@@ -2595,28 +2640,34 @@ dg_status Context::submit_user(int n, const uint8_t *const *h_srcs, const uint8_
     *ticket = next_ticket_++;  // a ticket of its own, in the batch tickets' sequence
   }
   split_[*ticket] = rec;
-  dg_status st = DG_OK;
-  if ((int)pagg_.size() >= prog_batch_ || pagg_stale_locked()) st = flush_pagg_locked();
-  return st;
+  // The caller's members are queued and its ticket is live.  An aggregate
+  // launch started here may carry other submissions' members too: its
+  // failure is recorded for their dg_wait (pgen_) and in their metas, never
+  // returned from this call, whose non-progressive part is already in flight.
+  if ((int)pagg_.size() >= prog_batch_ || pagg_stale_locked()) flush_pagg_locked();
+  return DG_OK;
 }
 
 dg_status Context::wait_user(uint64_t ticket) {
   SplitRec rec;
   uint64_t tp = 0;
+  dg_status agg_st = DG_OK;
   {
     std::lock_guard<std::mutex> lk(pmu_);
     auto it = split_.find(ticket);
     if (it == split_.end()) return wait(ticket);
     rec = it->second;
     if (rec.gen == pagg_gen_) flush_pagg_locked();  // someone blocks on the open aggregate: launch it now
-    tp = pgen_[rec.gen].first;
+    const PGen &g = pgen_[rec.gen];
+    tp = g.ticket;
+    agg_st = g.st;
   }
   dg_status st = rec.tb ? wait(rec.tb) : DG_OK;
-  dg_status st2 = tp ? wait(tp) : DG_OK;
+  dg_status st2 = tp ? wait(tp) : agg_st;
   std::lock_guard<std::mutex> lk(pmu_);
   if (split_.erase(ticket)) {
     auto g = pgen_.find(rec.gen);
-    if (g != pgen_.end() && --g->second.second <= 0) pgen_.erase(g);
+    if (g != pgen_.end() && --g->second.refs <= 0) pgen_.erase(g);
   }
   return st ? st : st2;
 }
@@ -2639,9 +2690,15 @@ dg_status Context::wait_ready(uint64_t ticket, int32_t *pending) {
     uint64_t tp = 0;
     if (rec.gen != pagg_gen_) {
       auto g = pgen_.find(rec.gen);
-      tp = g != pgen_.end() ? g->second.first : 0;
+      tp = g != pgen_.end() ? g->second.ticket : 0;
     }
-    *pending = (rec.gen == pagg_gen_ || (tp && poll(tp) == DG_ERR_NOT_READY)) ? rec.nprog : 0;
+    bool busy = rec.gen == pagg_gen_ || (tp && poll(tp) == DG_ERR_NOT_READY);
+    // The aggregate's kernels are done: complete it (outputs copied to host
+    // buffers, statuses written, metas published) before reporting 0 pending,
+    // so pending == 0 means the progressive members are ready to read.  The
+    // event has completed, so this does not block (bar a rare entropy resync).
+    if (!busy && tp) wait(tp);
+    *pending = busy ? rec.nprog : 0;
   }
   return st;
 }
@@ -2656,7 +2713,7 @@ dg_status Context::poll_user(uint64_t ticket) {
     if (it == split_.end()) return poll(ticket);
     rec = it->second;
     if (rec.gen == pagg_gen_) return DG_ERR_NOT_READY;
-    tp = pgen_[rec.gen].first;
+    tp = pgen_[rec.gen].ticket;
   }
   if (rec.tb && poll(rec.tb) == DG_ERR_NOT_READY) return DG_ERR_NOT_READY;
   if (tp && poll(tp) == DG_ERR_NOT_READY) return DG_ERR_NOT_READY;

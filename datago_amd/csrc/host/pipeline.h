@@ -105,6 +105,8 @@ struct Batch {
   std::vector<size_t> out_dev_off;    // offset of each output in the scratch arena (host path)
   std::vector<uint8_t> out_direct;    // host path: output DMA'd straight into the caller's pinned buffer
   std::vector<dg_payload_meta *> mptr;  // each image's meta (the caller's; a split submission's are scattered)
+  std::vector<dg_payload_meta> local_meta;  // defer_meta: the metas planning and finish() write ...
+  std::vector<dg_payload_meta *> pub;       // ... copied to the callers' (pub) only when finish() completes
   const HuffTable *hp = nullptr;       // the table pools (generation pool_gen) this batch's kernels read
   const QuantTable *qp = nullptr;
   int pool_gen = 0;
@@ -171,7 +173,8 @@ class Context {
   // metas array; force_slot: a progressive slot instead of the next in turn).
   dg_status submit(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
                    const int32_t *forced, uint8_t *const *outs, const uint64_t *caps, dg_payload_meta *metas,
-                   bool host_io, uint64_t *ticket, dg_payload_meta *const *mptrs = nullptr, int force_slot = -1);
+                   bool host_io, uint64_t *ticket, dg_payload_meta *const *mptrs = nullptr, int force_slot = -1,
+                   bool defer_meta = false);
   dg_status wait(uint64_t ticket);
   dg_status poll(uint64_t ticket);
   // The C ABI's dg_submit / dg_submit_device / dg_wait / dg_poll /
@@ -209,8 +212,9 @@ class Context {
   dg_status ensure(DevBuf &b, size_t bytes, hipStream_t user = nullptr);
   void retire(void *p, size_t bytes, bool pinned);
   void free_retired();
+  void free_retired_if_idle();
   std::vector<void *> retired_dev_, retired_pinned_;  // grown-out buffers, freed later (ensure)
-  size_t retired_bytes_ = 0;
+  size_t retired_dev_bytes_ = 0, retired_pin_bytes_ = 0;
   dg_status ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user = nullptr);
   dg_status upload_pools();
   dg_status launch_all(Slot &sl, bool from_fix);
@@ -269,7 +273,12 @@ class Context {
   bool pagg_host_ = true;
   uint64_t pagg_gen_ = 1;
   std::chrono::steady_clock::time_point pagg_t0_;
-  std::unordered_map<uint64_t, std::pair<uint64_t, int>> pgen_;  // flushed generation -> (ticket, split refs)
+  struct PGen {
+    uint64_t ticket = 0;  // the aggregate's batch (0: its launch failed)
+    int refs = 0;         // split records still referring to it
+    dg_status st = DG_OK; // launch status, returned by dg_wait of its members
+  };
+  std::unordered_map<uint64_t, PGen> pgen_;  // flushed generation -> aggregate
   std::unordered_map<uint64_t, SplitRec> split_;                 // user ticket -> parts
   int pagg_refs_ = 0;      // split records referring to the open aggregate
   int next_pslot_ = 0;

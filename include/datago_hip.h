@@ -175,9 +175,15 @@ dg_status dg_poll(dg_ctx *ctx, uint64_t ticket);
  * caller blocks on one of them in dg_wait).  dg_wait(ticket) completes every
  * member as before.  dg_wait_ready(ticket) returns once every other member is
  * complete (outputs and metas valid); *pending (may be NULL) = progressive
- * members still running, whose metas read status DG_ERR_NOT_READY until a
- * later dg_wait(ticket) -- so a loader hands its baseline samples on at the
- * baseline pace and the progressive ones when their aggregate is done. */
+ * members still running, whose metas read status DG_ERR_NOT_READY (even while
+ * their aggregate is already decoding) until they are complete.  *pending == 0
+ * means they are: outputs copied, metas published -- by that dg_wait_ready
+ * call when the aggregate's kernels are done, or by a later dg_wait(ticket) --
+ * so a loader hands its baseline samples on at the baseline pace and the
+ * progressive ones when their aggregate is done, polling dg_wait_ready or
+ * blocking in dg_wait.  dg_submit's status covers the caller's submission
+ * only: an aggregate launch it triggers that fails is reported in the members'
+ * metas and by dg_wait on their tickets. */
 dg_status dg_wait_ready(dg_ctx *ctx, uint64_t ticket, int32_t *pending);
 
 /* Synchronous single image (image_payload_from_path equivalent).  Calls from

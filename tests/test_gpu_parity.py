@@ -1,9 +1,14 @@
 """GPU parity: the HIP path (through the C ABI) vs the oracle, bit-exact.
 
-Decode: libjpeg-turbo semantics (oracle pinned against PIL).  Resize: the
-oracle's MODE_FIR restatement of fast_image_resize (tolerance 0: the kernels
-use the same f64 coefficient math and i16 quantisation).  Sizes are small
-enough for the scalar oracle to finish in seconds.
+Decode: both decode semantics (context option / dg_image_config
+`decode_semantics`): 0 = libjpeg-turbo (oracle pinned against PIL) and 1 =
+zune-jpeg 0.5.12, the reference's own decoder and the mode INTEGRATION.md
+sets for the Rust drop-in (oracle SEM_ZUNE restatement, parity unpinned
+against the crate itself: DESIGN.md §4).  Tests parametrised with `sem` run
+in both.  Resize: the oracle's MODE_FIR restatement of fast_image_resize
+(tolerance 0: the kernels use the same f64 coefficient math and i16
+quantisation).  Sizes are small enough for the scalar oracle to finish in
+seconds.
 """
 import hashlib
 import io
@@ -29,6 +34,24 @@ def _lib():
     return L
 
 
+SEMS = [0, 1]  # decode_semantics: libjpeg-turbo, zune-jpeg (the drop-in's mode)
+SEM_IDS = ["libjpeg", "zune"]
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    """Contexts by (bucket size or 0 for decode-only, decode semantics), made once per module."""
+    cache = {}
+
+    def get(size, sem):
+        if (size, sem) not in cache:
+            kw = dict(crop_and_resize=True, default_image_size=size, downsampling_ratio=16 if size == 512 else 32,
+                      min_aspect_ratio=0.5, max_aspect_ratio=2.0) if size else {}
+            cache[(size, sem)] = _lib().Context(0, decode_semantics=sem, **kw)
+        return cache[(size, sem)]
+    return get
+
+
 @pytest.fixture(scope="module")
 def ctx_dec():
     return _lib().Context(0)
@@ -52,10 +75,15 @@ def _golden_files():
     return [(n, open(os.path.join(GOLD, "jpeg", n + ".jpg"), "rb").read()) for n in names]
 
 
-def _oracle_resized(data, tw, th):
-    st, dec = O.jpeg_decode(data)
+def _oracle_decoded(data, sem=0):
+    with O.semantics(sem):
+        st, dec = O.jpeg_decode(data)
     assert st == 0
-    return O.crop_and_resize(dec, tw, th, O.MODE_FIR)
+    return dec
+
+
+def _oracle_resized(data, tw, th, sem=0):
+    return O.crop_and_resize(_oracle_decoded(data, sem), tw, th, O.MODE_FIR)
 
 
 def _rand_jpegs(seed, n, maxdim=700, rst=False):
@@ -82,12 +110,13 @@ def test_decode_only_golden_bit_exact(ctx_dec):
     assert ctx_dec.stat("write_mismatch") == 0
 
 
-def test_decode_only_random_bit_exact_vs_oracle(ctx_dec):
+@pytest.mark.parametrize("sem", SEMS, ids=SEM_IDS)
+def test_decode_only_random_bit_exact_vs_oracle(ctxs, sem):
     datas = _rand_jpegs(1, 24, rst=True)
-    res = ctx_dec.decode_batch(datas)
+    res = ctxs(0, sem).decode_batch(datas)
     for i, (d, (st, arr, meta)) in enumerate(zip(datas, res)):
-        ost, ref = O.jpeg_decode(d)
-        assert st == 0 and ost == 0
+        ref = _oracle_decoded(d, sem)
+        assert st == 0
         assert arr.shape == ref.shape, i
         assert np.array_equal(arr, ref), (i, int((arr != ref).sum()))
         assert (meta.original_width, meta.original_height) == (ref.shape[1], ref.shape[0])
@@ -108,18 +137,20 @@ def test_crop_resize_golden_bit_exact(ctx512):
         assert d.max() == 0, (name, int(d.max()), int((d > 0).sum()))
 
 
-def test_crop_resize_random_1024(ctx1024):
+@pytest.mark.parametrize("sem", SEMS, ids=SEM_IDS)
+def test_crop_resize_random_1024(ctxs, sem):
+    ctx = ctxs(1024, sem)
     datas = _rand_jpegs(2, 16, maxdim=1400)
-    res = ctx1024.decode_batch(datas)
+    res = ctx.decode_batch(datas)
     t = B.ARAwareTransform(1024, 32, 0.5, 2.0)
     for i, (data, (st, arr, meta)) in enumerate(zip(datas, res)):
         assert st == 0
         w, h = O.jpeg_info(data)[1:3]
         tw, th = t.target_size(w, h)
-        ref = _oracle_resized(data, tw, th)
+        ref = _oracle_resized(data, tw, th, sem)
         assert arr.shape == ref.shape
         assert np.array_equal(arr, ref), (i, (w, h), (tw, th))
-    assert ctx1024.stat("write_mismatch") == 0
+    assert ctx.stat("write_mismatch") == 0
 
 
 def test_fractional_crop_case(ctx512):
@@ -145,13 +176,13 @@ def test_subsequence_sizes_agree(ctx_dec):
         assert ctx.stat("write_mismatch") == 0
 
 
-@pytest.mark.parametrize("bands,slots", [(1, 1), (3, 2), (8, 3), (64, 4)])
-def test_band_and_slot_options_bit_exact(bands, slots):
+@pytest.mark.parametrize("bands,slots,sem", [(1, 1, 0), (3, 2, 1), (8, 3, 0), (64, 4, 1)])
+def test_band_and_slot_options_bit_exact(bands, slots, sem):
     # the band H kernel's rows per workgroup (hb_bands) and the batches in
     # flight (slots) change only the partitioning: outputs stay bit-exact
     L = _lib()
     ctx = L.Context(0, crop_and_resize=True, default_image_size=1024, downsampling_ratio=32,
-                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0, decode_semantics=sem)
     ctx.set_option("hb_bands", bands)
     ctx.set_option("slots", slots)
     datas = _rand_jpegs(5, 6, maxdim=1300)
@@ -160,7 +191,7 @@ def test_band_and_slot_options_bit_exact(bands, slots):
         for data, (st, arr, meta) in zip(datas, ctx.decode_batch(datas)):
             assert st == 0
             w, h = O.jpeg_info(data)[1:3]
-            assert np.array_equal(arr, _oracle_resized(data, *t.target_size(w, h))), (bands, slots, (w, h))
+            assert np.array_equal(arr, _oracle_resized(data, *t.target_size(w, h), sem)), (bands, slots, (w, h))
 
 
 @pytest.mark.parametrize("sub_bits", [0, 512, 2048, 8192])
@@ -283,15 +314,16 @@ H_CLASS_CASES = [
 ]
 
 
+@pytest.mark.parametrize("sem", SEMS, ids=SEM_IDS)
 @pytest.mark.parametrize("case", H_CLASS_CASES, ids=lambda c: f"{c[0]}x{c[1]}_{c[2]}_{'L' if c[3] else 'RGB'}")
-def test_h_pass_classes_bit_exact(ctx512, case):
+def test_h_pass_classes_bit_exact(ctxs, case, sem):
     w, h, ss, gray = case
     data = synth.make_jpeg(40 + w % 97, w, h, 88, ss, gray=gray)
-    st, arr, meta = ctx512.decode_one(data)
+    st, arr, meta = ctxs(512, sem).decode_one(data)
     assert st == 0
     t = B.ARAwareTransform(512, 16, 0.5, 2.0)
     tw, th = t.target_size(w, h)
-    ref = _oracle_resized(data, tw, th)
+    ref = _oracle_resized(data, tw, th, sem)
     assert arr.shape == ref.shape
     d = np.abs(arr.astype(int) - ref.astype(int))
     assert d.max() == 0, (int(d.max()), int((d > 0).sum()), np.argwhere(d > 0)[:4].tolist())
@@ -312,16 +344,17 @@ CROP_CASES = [
 ]
 
 
+@pytest.mark.parametrize("sem", SEMS, ids=SEM_IDS)
 @pytest.mark.parametrize("case", CROP_CASES, ids=lambda c: f"{c[0]}x{c[1]}_{'L' if c[2] else 'RGB'}")
-def test_crop_folding_bit_exact(ctx512, case):
+def test_crop_folding_bit_exact(ctxs, case, sem):
     w, h, gray = case
     data = synth.make_jpeg(60 + w % 89 + h % 7, w, h, 90, "4:2:0", gray=gray)
-    st, arr, meta = ctx512.decode_one(data)
+    st, arr, meta = ctxs(512, sem).decode_one(data)
     assert st == 0
     t = B.ARAwareTransform(512, 16, 0.5, 2.0)
     tw, th = t.target_size(w, h)
     assert (meta.width, meta.height) == (tw, th)
-    ref = _oracle_resized(data, tw, th)
+    ref = _oracle_resized(data, tw, th, sem)
     assert arr.shape == ref.shape
     d = np.abs(arr.astype(int) - ref.astype(int))
     assert d.max() == 0, (int(d.max()), int((d > 0).sum()))
@@ -386,21 +419,38 @@ FULL_CASES = [  # (content, w, h, quality, subsampling, gray): configs[1] sizes,
 ]
 
 
-def test_full_size_regimes_bit_exact_vs_oracle(ctx1024):
+@pytest.mark.parametrize("sem", SEMS, ids=SEM_IDS)
+def test_full_size_regimes_bit_exact_vs_oracle(ctxs, sem):
     """Full configs[1]-size images end to end (decode + bucket + crop/resize at
-    1024/32), every regime in one batch, bit-exact against the oracle."""
+    1024/32), every regime in one batch, bit-exact against the oracle in
+    both decode semantics."""
+    ctx = ctxs(1024, sem)
     datas = []
     for i, (kind, w, h, q, ss, gray) in enumerate(FULL_CASES):
         rng = np.random.default_rng(900 + i)
         datas.append(synth.encode_jpeg(_content(kind, rng, w, h, gray), q, ss))
-    res = ctx1024.decode_batch(datas)
+    res = ctx.decode_batch(datas)
     t = B.ARAwareTransform(1024, 32, 0.5, 2.0)
     for k, (data, (st, arr, meta)) in enumerate(zip(datas, res)):
         assert st == 0, (k, FULL_CASES[k])
-        st2, dec = O.jpeg_decode(data)
+        dec = _oracle_decoded(data, sem)
         ref = O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR)
         assert np.array_equal(arr, ref), FULL_CASES[k]
-    assert ctx1024.stat("write_mismatch") == 0
+    assert ctx.stat("write_mismatch") == 0
+
+
+def test_zune_bench_pool_sample_bit_exact(ctxs):
+    """A slice of the bench's own configs[1] pool (bench.py's corpus: seeded
+    mixed aspect ratios, short side 256..2048, q 75..95, 80/10/10 % 4:2:0 /
+    4:2:2 / 4:4:4, 5 % gray) at 1024/32 in zune mode, the mode the headline
+    is measured in: every output bit-exact against the SEM_ZUNE oracle."""
+    ctx = ctxs(1024, 1)
+    datas = synth.mixed_corpus(2, 4096, lo=0, hi=16)  # bench.py's configs[1] pool (seed 2, 4,096 images)
+    t = B.ARAwareTransform(1024, 32, 0.5, 2.0)
+    for k, (data, (st, arr, meta)) in enumerate(zip(datas, ctx.decode_batch(datas))):
+        assert st == 0, k
+        dec = _oracle_decoded(data, 1)
+        assert np.array_equal(arr, O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR)), k
 
 
 @pytest.mark.parametrize("sub_bits", [512, 8192])

@@ -279,6 +279,40 @@ def test_split_wait_ready_then_wait():
     assert ctx.stat("prog_aggregates") == 1
 
 
+def test_split_aggregate_launched_before_wait_ready():
+    """An aggregate launched while the caller still holds its ticket
+    (prog_batch 1: the submission itself launches it) keeps its members'
+    metas at DG_ERR_NOT_READY while the GPU decodes -- planning writes the
+    batch's own copies, finish() publishes them -- and dg_wait_ready reports
+    pending 0 only once outputs and statuses are in place."""
+    import time
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0)
+    ctx.set_option("prog_batch", 1)
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    datas = _mixed(8150, 9)
+    isp = [i % 3 == 1 for i in range(len(datas))]
+    outs = [np.zeros(max(ctx.output_size(d)[1], 1), np.uint8) for d in datas]
+    ticket, metas, keep = ctx.submit_host(datas, outs)
+    assert ctx.stat("prog_aggregates") >= 1  # launched inside the submission
+    for i in range(len(datas)):
+        if isp[i]:
+            assert metas[i].status == L.DG_ERR_NOT_READY and metas[i].width == 0, i
+    deadline = time.time() + 60
+    pending = ctx.wait_ready(ticket)
+    while pending and time.time() < deadline:
+        time.sleep(0.01)
+        pending = ctx.wait_ready(ticket)
+    assert pending == 0
+    for i, d in enumerate(datas):  # complete without dg_wait: outputs copied, metas published
+        assert metas[i].status == 0, i
+        ref = _resized_ref(d, t)
+        assert (metas[i].width, metas[i].height) == (ref.shape[1], ref.shape[0]), i
+        assert np.array_equal(outs[i][: ref.size].reshape(ref.shape), ref), i
+    ctx.wait(ticket)  # still valid after the members completed
+
+
 def test_split_aggregates_across_submissions():
     """Progressive members of several submissions share one aggregate batch
     (prog_batch, prog_flush_us large): waited on out of order, every output

@@ -118,3 +118,24 @@ def test_incomplete_progressive_refinement_decodes_in_zune_mode():
     for k, (d, (st, arr, _)) in enumerate(zip(datas, zu.decode_batch(datas))):
         assert st == 0, (k, L.last_error())
         assert np.array_equal(arr, _oracle(d, O.SEM_ZUNE)), k
+
+
+def test_zune_complete_progressive_full_size_1024():
+    """Complete (not truncated) progressive files in zune mode, configs[1]
+    sizes, decode + bucket + crop/resize at 1024/32 through the default split
+    submission (the progressive aggregate), mixed with baseline files: every
+    output bit-exact against the SEM_ZUNE oracle."""
+    from datago_amd import _lib as L
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=1024, downsampling_ratio=32, min_aspect_ratio=0.5,
+                    max_aspect_ratio=2.0, decode_semantics=1)
+    dims = [(2048, 1536, "4:2:0", True), (1100, 1900, "4:2:2", True), (1500, 1500, "4:4:4", True),
+            (1999, 1001, "4:2:0", False), (777, 1333, "4:2:0", True), (2300, 1100, "4:2:0", False)]
+    datas = [synth.make_jpeg(7600 + i, w, h, 90, ss, gray=(i == 4), progressive=p) for i, (w, h, ss, p) in
+             enumerate(dims)]
+    t = B.ARAwareTransform(1024, 32, 0.5, 2.0)
+    for k, (d, (st, arr, meta)) in enumerate(zip(datas, ctx.decode_batch(datas))):
+        assert st == 0, (k, L.last_error())
+        dec = _oracle(d, O.SEM_ZUNE)
+        ref = O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR)
+        assert np.array_equal(arr, ref), (k, dims[k])
+    assert ctx.stat("prog_aggregate_images") == sum(p for *_, p in dims)
