@@ -513,6 +513,29 @@ def jpeg_pool(a, rank: int, world: int, workers: int, dist):
 
 # ------------------------------------------------------------------- main
 
+def pin_rank_cores(local: int, local_world: int):
+    """Give each rank of this node a disjoint, contiguous share of the CPUs
+    the job may use (before anything touches the GPU or starts threads): the
+    ranks' host planning, Python loop and pool workers then never compete for
+    a core, and contiguous ids keep a rank on one socket on the usual
+    GPU-per-socket layouts.  DG_NO_PIN=1 disables it.  Returns the CPU list."""
+    if local_world <= 1 or os.environ.get("DG_NO_PIN"):
+        return None
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+    per = len(cpus) // local_world
+    if per < 1:
+        return None
+    mine = cpus[local * per:(local + 1) * per]
+    try:
+        os.sched_setaffinity(0, mine)
+    except OSError:
+        return None
+    return mine
+
+
 def main() -> int:
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -520,6 +543,7 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    pinned = pin_rank_cores(local, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
     if world != a.gpus and rank == 0:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; measuring {world} ranks", file=sys.stderr)
     import torch
@@ -765,7 +789,13 @@ def main() -> int:
     ctx.set_option("timing", 0)
     # host planning phases of the timed steps only (read before the untimed legs add to them)
     host_phases = {q: round(ctx.stat("host_us_" + q) / 1e3 / a.steps, 3)
-                   for q in ("plan", "pools", "layout", "lists", "upload", "launch")}
+                   for q in ("plan", "pools", "layout", "lists", "upload", "launch", "slotwait")}
+    host_phases_cpu = {q: round(ctx.stat("host_cpu_us_" + q) / 1e3 / a.steps, 3)
+                       for q in ("plan", "pools", "layout", "lists", "upload", "launch")}
+    ph_all = sum_over_ranks([host_phases[q] if r == rank else 0.0 for r in range(world)
+                             for q in ("plan", "pools", "layout", "lists", "upload", "launch", "slotwait")] +
+                            [host_phases_cpu[q] if r == rank else 0.0 for r in range(world)
+                             for q in ("plan", "pools", "layout", "lists", "upload", "launch")], world)
     # max over ranks; totals over ranks
     (dt_max,) = max_over_ranks([dt], world)
     per_rank_s = sum_over_ranks([dt if r == rank else 0.0 for r in range(world)], world)
@@ -1059,6 +1089,16 @@ def main() -> int:
             "host_submit_ms_per_step": round(1e3 * host_s["submit"] / a.steps, 3),  # Python + dg_submit_device planning
             "host_submit_ms_per_step_per_rank": [round(1e3 * h_ / a.steps, 3) for h_ in per_rank_host],
             "host_submit_phases_ms_per_step": host_phases,
+            # per rank: wall ms per step in each dg_submit_device phase, the thread's CPU ms in the same
+            # phases (wall >> cpu = blocking: allocation, driver locks, copies), and the slot wait
+            "host_submit_phases_per_rank": [
+                {"wall": {q: round(ph_all[r * 7 + j], 3) for j, q in
+                          enumerate(("plan", "pools", "layout", "lists", "upload", "launch", "slotwait"))},
+                 "cpu": {q: round(ph_all[7 * world + r * 6 + j], 3) for j, q in
+                         enumerate(("plan", "pools", "layout", "lists", "upload", "launch"))}}
+                for r in range(world)],
+            "rank_cpus": (f"{len(pinned)} CPUs per rank, disjoint contiguous shares of the job's affinity set"
+                          if pinned else "unpinned"),
             "e2e_host_mpix_s": round(e2e, 2) if e2e else None,
             "e2e_host_detail": ({"note": "host JPEG bytes in -> host RGB out, a dg_host_register'ed output pool "
                                          "reused, batches pipelined; outputs DMA'd from HBM into the pool",

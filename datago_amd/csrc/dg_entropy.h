@@ -18,6 +18,7 @@
 // whose range contains its position.
 #pragma once
 #include "dg_pixel.h"
+#include "dg_plane.h"
 #include "dg_types.h"
 
 namespace dg {
@@ -352,14 +353,7 @@ __device__ __forceinline__ void wc_coop_flush(WriteCtx &w, bool pending) {
 #pragma unroll
           for (int i = 0; i < 8; i++) row[i] = h[i];
           idct_row(zune, row, px);
-          // byte packing by v_perm (see pack4 in kernels.hip: shift/or packing miscompiles)
-          const uint32_t lo = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[3], px[2], 0x0c0c0400u),
-                                                    __builtin_amdgcn_perm(px[1], px[0], 0x0c0c0400u), 0x05040100u);
-          const uint32_t hi = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[7], px[6], 0x0c0c0400u),
-                                                    __builtin_amdgcn_perm(px[5], px[4], 0x0c0c0400u), 0x05040100u);
-          DG_GLOBAL uint8_t *dst =
-              (DG_GLOBAL uint8_t *)(uintptr_t)im.plane[c] + (size_t)(by * 8 + part) * (im.cbw[c] * 8) + bx * 8;
-          *(DG_GLOBAL u32x2 *)dst = u32x2{lo, hi};
+          store_plane_row8(im, c, by * 8 + part, bx, px);  // plain plane or chroma records (dg_plane.h)
         }
         *row4 = zero;
       }

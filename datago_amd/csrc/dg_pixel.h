@@ -15,15 +15,26 @@ namespace dg {
 // jidctint.c (CONST_BITS 13, PASS1_BITS 2).
 constexpr int32_t kConstBits = 13, kPass1Bits = 2;
 
+// a * b where both fit a signed 24-bit value (M24): the device's full-rate
+// v_mul_i32_i24 (v_mul_lo_u32 is quarter rate) gives the same low 32 bits
+template <bool M24>
+DG_HD int32_t imul(int32_t a, int32_t b) {
+#if defined(DG_DEVICE)
+  if (M24) return __mul24(a, b);
+#endif
+  return a * b;
+}
+
+template <bool M24 = false>
 DG_HD void idct_1d(const int32_t i0, const int32_t i1, const int32_t i2, const int32_t i3,
                    const int32_t i4, const int32_t i5, const int32_t i6, const int32_t i7,
                    int32_t o[8]) {
   int32_t z1, z2, z3, z4, z5, t0, t1, t2, t3, t10, t11, t12, t13;
   z2 = i2;
   z3 = i6;
-  z1 = (z2 + z3) * 4433;
-  t2 = z1 + z3 * (-15137);
-  t3 = z1 + z2 * 6270;
+  z1 = imul<M24>(z2 + z3, 4433);
+  t2 = z1 + imul<M24>(z3, -15137);
+  t3 = z1 + imul<M24>(z2, 6270);
   t0 = (int32_t)((uint32_t)(i0 + i4) << kConstBits);
   t1 = (int32_t)((uint32_t)(i0 - i4) << kConstBits);
   t10 = t0 + t3;
@@ -38,15 +49,15 @@ DG_HD void idct_1d(const int32_t i0, const int32_t i1, const int32_t i2, const i
   z2 = t1 + t2;
   z3 = t0 + t2;
   z4 = t1 + t3;
-  z5 = (z3 + z4) * 9633;
-  t0 = t0 * 2446;
-  t1 = t1 * 16819;
-  t2 = t2 * 25172;
-  t3 = t3 * 12299;
-  z1 = z1 * (-7373);
-  z2 = z2 * (-20995);
-  z3 = z3 * (-16069);
-  z4 = z4 * (-3196);
+  z5 = imul<M24>(z3 + z4, 9633);
+  t0 = imul<M24>(t0, 2446);
+  t1 = imul<M24>(t1, 16819);
+  t2 = imul<M24>(t2, 25172);
+  t3 = imul<M24>(t3, 12299);
+  z1 = imul<M24>(z1, -7373);
+  z2 = imul<M24>(z2, -20995);
+  z3 = imul<M24>(z3, -16069);
+  z4 = imul<M24>(z4, -3196);
   z3 += z5;
   z4 += z5;
   t0 += z1 + z3;
@@ -79,11 +90,12 @@ DG_HD uint8_t idct_out(int32_t x) {
 // IDCT `idct_int`: stb_image's factorisation with 12-bit constants; o[k] are
 // the pre-bias sums, pass 1 takes (o + 512) >> 10, pass 2
 // (o + 65536 + (128 << 17)) >> 17 clamped to 0..255.
+template <bool M24 = false>
 DG_HD void idct_1d_stb(const int32_t s0, const int32_t s1, const int32_t s2, const int32_t s3,
                        const int32_t s4, const int32_t s5, const int32_t s6, const int32_t s7, int32_t o[8]) {
   int32_t p2 = s2, p3 = s6;
-  int32_t p1 = (p2 + p3) * 2217;
-  const int32_t u2 = p1 + p3 * -7567, u3 = p1 + p2 * 3135;
+  int32_t p1 = imul<M24>(p2 + p3, 2217);
+  const int32_t u2 = p1 + imul<M24>(p3, -7567), u3 = p1 + imul<M24>(p2, 3135);
   const int32_t t0e = (int32_t)((uint32_t)(s0 + s4) << 12), t1e = (int32_t)((uint32_t)(s0 - s4) << 12);
   const int32_t x0 = t0e + u3, x3 = t0e - u3, x1 = t1e + u2, x2 = t1e - u2;
   int32_t t0 = s7, t1 = s5, t2 = s3, t3 = s1;
@@ -91,15 +103,15 @@ DG_HD void idct_1d_stb(const int32_t s0, const int32_t s1, const int32_t s2, con
   int32_t p4 = t1 + t3;
   p1 = t0 + t3;
   p2 = t1 + t2;
-  const int32_t p5 = (p3 + p4) * 4816;
-  t0 *= 1223;
-  t1 *= 8410;
-  t2 *= 12586;
-  t3 *= 6149;
-  p1 = p5 + p1 * -3685;
-  p2 = p5 + p2 * -10497;
-  p3 = p3 * -8034;
-  p4 = p4 * -1597;
+  const int32_t p5 = imul<M24>(p3 + p4, 4816);
+  t0 = imul<M24>(t0, 1223);
+  t1 = imul<M24>(t1, 8410);
+  t2 = imul<M24>(t2, 12586);
+  t3 = imul<M24>(t3, 6149);
+  p1 = p5 + imul<M24>(p1, -3685);
+  p2 = p5 + imul<M24>(p2, -10497);
+  p3 = imul<M24>(p3, -8034);
+  p4 = imul<M24>(p4, -1597);
   t3 += p1 + p4;
   t2 += p2 + p3;
   t1 += p2 + p4;
@@ -136,14 +148,17 @@ DG_HD void idct_col(bool zune, const int32_t v[8], int32_t ws[8]) {
     for (int r = 0; r < 8; r++) ws[r] = sat16(descale(o[r], kConstBits - kPass1Bits));
   }
 }
+// Pass 2's inputs are the 16-bit-saturated workspace, so every product's
+// operands fit 24 bits (sums of up to four of them times constants < 2^15):
+// full-rate 24-bit multiplies, bit-exact.
 DG_HD void idct_row(bool zune, const int32_t w[8], uint32_t px[8]) {
   int32_t o[8];
   if (zune) {
-    idct_1d_stb(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+    idct_1d_stb<true>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
 #pragma unroll
     for (int i = 0; i < 8; i++) px[i] = idct_stb_out(o[i]);
   } else {
-    idct_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+    idct_1d<true>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
 #pragma unroll
     for (int i = 0; i < 8; i++) px[i] = idct_out(o[i]);
   }

@@ -271,6 +271,7 @@ struct ImageDesc {
   uint64_t mk;              // RST marker positions in ds (bits), ascending
   uint64_t chunk;           // destuff per-chunk records: uint32 {cnt, mkc, off, mkoff}
   uint32_t nchunk;          // raw chunks of kDestuffChunk bytes
+  uint32_t ds_state0;       // k_destuff_one: index of chunk 0's state word (batch-wide, list order)
   uint32_t ds_bits;         // destuffed length in bits (written by k_destuff_scan)
   uint32_t nmk;             // RST markers (written by k_destuff_scan)
   uint32_t slotmap;         // Huffman slot of (component c, dc=0/ac=1) at nibble 2c+ac
@@ -315,7 +316,7 @@ struct ImageDesc {
   // ---- format, PNG, alpha handling, final conversion
   uint32_t fmt;             // kFmtJpeg / kFmtPng
   uint32_t prog;            // progressive JPEG: scans decoded by k_prog_scan (0: sequential)
-  uint32_t prog_pad;
+  uint32_t crec;            // bit c: component c's plane holds chroma records (dg_plane.h; option "chroma_rec")
   uint32_t copy_mode;       // k_copy: 0 same channels, 1 L->RGB, 2 RGBA->RGB blend over gray,
                             // 3 LA->RGB of a resized LA image (GrayImage over the LA bytes, B3),
                             // 4 LA->RGB of an unresized LumaA8 (alpha dropped)

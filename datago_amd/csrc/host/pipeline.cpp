@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <time.h>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -35,6 +36,12 @@ void set_error(const std::string &s) { g_last_error = s; }
   } while (0)
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+static double thread_cpu_us() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (double)ts.tv_sec * 1e6 + (double)ts.tv_nsec * 1e-3;
+}
 
 // Boundary-repair rounds (finish()) before a batch is declared unsettled.
 static constexpr int kMaxResyncRounds = 64;
@@ -351,6 +358,12 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     coalesce_max_ = (int)v;
     return DG_OK;
   }
+  if (k == "coalesce_inflight") {  // dg_decode_one: coalesced baseline batches in flight (0 = "slots")
+    if (v < 0 || v > kMaxInflight) return DG_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(cmu_);
+    coalesce_inflight_ = (int)v;
+    return DG_OK;
+  }
   if (k == "coalesce_us") {
     if (v < 0 || v > 1000000) return DG_ERR_INVALID;
     std::lock_guard<std::mutex> lk(cmu_);
@@ -485,8 +498,17 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     idct_fused_ = v != 0;
     return DG_OK;
   }
-  if (k == "reset_host_us") {  // zero the host_us_* stats
+  if (k == "destuff_one") {
+    destuff_one_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "chroma_rec") {
+    chroma_rec_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "reset_host_us") {  // zero the host_us_* / host_cpu_us_* stats
     for (double &x : host_us_) x = 0;
+    for (double &x : host_cpu_us_) x = 0;
     return DG_OK;
   }
   if (k == "hv_fused") {  // fused first H + V pass of colour JPEGs where it fits (default 0: slower)
@@ -579,10 +601,12 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "band_dec_images") return stat_band_dec_;
   if (k == "direct_d2h") return stat_direct_d2h_;
   if (k == "png_chunks") return stat_png_chunks_;
-  {  // host microseconds spent in dg_submit* since the last reset, per phase
-    static const char *pn[6] = {"plan", "pools", "layout", "lists", "upload", "launch"};
-    for (int q = 0; q < 6; q++)
+  {  // host microseconds spent in dg_submit* since the last reset, per phase: wall and thread CPU
+    static const char *pn[7] = {"plan", "pools", "layout", "lists", "upload", "launch", "slotwait"};
+    for (int q = 0; q < 7; q++) {
       if (k == std::string("host_us_") + pn[q]) return (int64_t)host_us_[q];
+      if (q < 6 && k == std::string("host_cpu_us_") + pn[q]) return (int64_t)host_cpu_us_[q];
+    }
   }
   if (k == "hpool") return (int64_t)hpool_.size();
   if (k == "qpool") return (int64_t)qpool_.size();
@@ -876,6 +900,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
                           const int32_t *forced, uint8_t *const *outs, const uint64_t *caps,
                           dg_payload_meta *metas, bool host_io, uint64_t *ticket, dg_payload_meta *const *mptrs,
                           int force_slot, bool defer_meta) {
+  const auto wait_t0 = std::chrono::steady_clock::now();
   std::unique_lock<std::mutex> lk(mu_);
   if (n < 0 || (n > 0 && (!h_srcs || !lens || !outs || !caps || (!metas && !mptrs)))) {
     set_error("null argument");
@@ -903,6 +928,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     dg_status st = finish(sl);
     if (st) return st;
   }
+  // context lock + the slot's previous batch (stat "host_us_slotwait")
+  host_us_[6] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - wait_t0).count();
   std::unique_ptr<Batch> bp(new Batch());
   Batch &b = *bp;
   b.ticket = next_ticket_++;
@@ -923,11 +950,18 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   b.plans.resize(n);
   b.desc_of.assign(n, -1);
+  // host time per submit phase: wall ("host_us_<phase>") and this thread's CPU
+  // time ("host_cpu_us_<phase>"); wall well above CPU = blocking (allocation,
+  // copies, driver locks), not planning work
   auto phase_t0 = std::chrono::steady_clock::now();
-  auto phase = [&](int k) {  // host time per submit phase (stats "host_us_<phase>")
+  double cpu_t0 = thread_cpu_us();
+  auto phase = [&](int k) {
     const auto now = std::chrono::steady_clock::now();
+    const double c = thread_cpu_us();
     host_us_[k] += std::chrono::duration<double, std::micro>(now - phase_t0).count();
+    host_cpu_us_[k] += c - cpu_t0;
     phase_t0 = now;
+    cpu_t0 = c;
   };
   // ---- 1. plan every image (host, header only)
   for (int i = 0; i < n; i++) plan_image(h_srcs[i], lens[i], forced ? forced[i] : -1, b.plans[i]);
@@ -1363,7 +1397,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       d.pass[0].mode |= dm;
       if (dm) stat_band_dec_++;
       if (!dm)
-        for (uint32_t c = 0; c < d.ncomp; c++) o.plane[c] = L.take((size_t)d.cbw[c] * 8 * d.cbh[c] * 8);
+        for (uint32_t c = 0; c < d.ncomp; c++) {
+          // half-rate chroma as 8-byte records (dg_plane.h, option "chroma_rec"): twice the bytes
+          const bool rec = chroma_rec_ && d.ncomp == 3 && d.hmax == 2 * d.ch[c];
+          if (rec) d.crec |= 1u << c;
+          o.plane[c] = L.take((size_t)d.cbw[c] * 8 * d.cbh[c] * 8 * (rec ? 2 : 1));
+        }
     }
     if (colour && !d.color_fused) o.pix = L.take((size_t)d.pix_stride * H);
     // final write: the last pass writes straight into the output when the
@@ -1475,6 +1514,11 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   for (const ImageDesc &dd : b.descs)
     if (dd.fmt == kFmtJpeg) b.pf_n += dd.prog;
   b.pf_off = b.pf_n ? L.take((size_t)(b.pf_n + 2) * 4) : 0;  // AC ticket, progress words, DC ticket
+  // k_destuff_one: a ticket word + one state word per destuff chunk (zeroed per batch)
+  b.ds_n = 0;
+  for (const ImageDesc &dd : b.descs)
+    if (dd.fmt == kFmtJpeg && !dd.prog) b.ds_n += dd.nchunk;
+  b.ds_state_off = (destuff_one_ && b.ds_n) ? L.take((size_t)(b.ds_n + 1) * 8) : 0;
   const size_t subs_off = L.take(b.total_subs * sizeof(SubState));
   const size_t ckpt_off = L.take(std::max<uint64_t>(1, ckpt_total) * sizeof(Ckpt));
   // fused IDCT leftovers: at most one carried-in block per subsequence, plus
@@ -1650,6 +1694,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     } else {
     for (uint32_t w = 0; w < d.nsub; w += kSubPerWg) b.lists[L_HUFF].push_back({I, w});
     for (uint32_t w = 0; w < d.nsub; w += kSubPerWg - 1) b.lists[L_SYNC].push_back({I, w});
+    b.descs[di].ds_state0 = (uint32_t)b.lists[L_DESTUFF].size();  // k_destuff_one's state words, list order
     for (uint32_t c = 0; c < d.nchunk; c++) b.lists[L_DESTUFF].push_back({I, c});
     b.lists[L_SCAN].push_back({I, 0});
     }
@@ -2088,9 +2133,15 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
 
     launch_coeffs(cs, dm, lst(L_COEF), cnt(L_COEF));
     HIPCHK(hipEventRecord(sl.ev_coef, cs));
-    launch_destuff_count(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
-    launch_destuff_scan(sl.st, dm, lst(L_SCAN), cnt(L_SCAN));
-    launch_destuff_write(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
+    if (b.ds_state_off) {  // one pass, decoupled look-back (option "destuff_one")
+      uint64_t *dst = (uint64_t *)((char *)sl.scratch.p + b.ds_state_off);
+      HIPCHK(hipMemsetAsync(dst, 0, (size_t)(b.ds_n + 1) * 8, sl.st));
+      launch_destuff_one(sl.st, dm, lst(L_DESTUFF), cnt(L_DESTUFF), dst);
+    } else {
+      launch_destuff_count(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
+      launch_destuff_scan(sl.st, dm, lst(L_SCAN), cnt(L_SCAN));
+      launch_destuff_write(sl.st, dd, lst(L_DESTUFF), cnt(L_DESTUFF));
+    }
   }
   if (next()) return DG_ERR_DEVICE;
   // progressive JPEG: zero, then the scans (one pipelined launch, or level by
@@ -2463,7 +2514,7 @@ dg_status Context::decode_one(const uint8_t *src, size_t len, int32_t forced, ui
     const bool ready = !q.empty() && ((int)q.size() >= coalesce_max_ ||
                                       (int)(pending_.size() + ppending_.size()) >= waiting ||
                                       std::chrono::steady_clock::now() >= deadline);
-    const bool room = r.prog ? pinflight_ < prog_lanes_ : inflight_ < nslots_;
+    const bool room = r.prog ? pinflight_ < prog_lanes_ : inflight_ < (coalesce_inflight_ ? coalesce_inflight_ : nslots_);
     if (ready && room && std::find(q.begin(), q.end(), &r) != q.end()) {
       std::vector<OneReq *> batch;
       const size_t take = std::min(q.size(), (size_t)coalesce_max_);

@@ -73,6 +73,8 @@ struct Batch {
   uint32_t uf_n = 0;        // PNG unfilter bands (progress flags, L_UNF tasks)
   uint32_t uf_maxbpp = 1;   // widest filter unit of the batch's PNGs (k_png_unfilter's LDS)
   size_t uf_flags_off = 0;  // their flags + ticket in the scratch arena (zeroed per batch)
+  uint32_t ds_n = 0;          // destuff chunks of the batch (k_destuff_one state words)
+  size_t ds_state_off = 0;    // their ticket + state words in the scratch arena (zeroed per batch), 0 = three-pass destuff
   uint32_t pf_n = 0;        // progressive scans (progress words, one pipelined k_prog_scan launch)
   size_t pf_off = 0;        // AC ticket, progress words, DC ticket in the scratch arena (zeroed per batch)
   size_t ptime_off = 0;     // debug (wg_timing): per-scan {start, end} in the wgt buffer, 0 = none
@@ -294,6 +296,7 @@ class Context {
   bool sync_pair_ = false;   // option "sync_pair": the same in k_huff_sync (measured slower beside multi_lead: off)
   bool prog_side_ = false;  // option "prog_side": progressive scans on the side stream (measured slower: off)
   int coalesce_max_ = 64, coalesce_us_ = 500;
+  int coalesce_inflight_ = 0;  // option "coalesce_inflight": coalesced batches in flight (0 = nslots_)
   int64_t stat_coalesced_batches_ = 0, stat_coalesced_images_ = 0;
   dg_status flush_batch(std::vector<OneReq *> &batch, bool prog);
 
@@ -327,9 +330,12 @@ class Context {
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
   int decode_sem_ = 0;                  // option "decode_semantics"
   bool ckpt_ = true;                    // option "ckpt"
-  double host_us_[6] = {0, 0, 0, 0, 0, 0};  // submit phases (stats "host_us_*"; option "reset_host_us")
+  double host_us_[7] = {0, 0, 0, 0, 0, 0, 0};  // submit phases + slot wait (stats "host_us_*"; option "reset_host_us")
+  double host_cpu_us_[6] = {0, 0, 0, 0, 0, 0};  // the same phases' thread CPU time (stats "host_cpu_us_*")
   int copy_threads_ = 8;                // option "copy_threads": host threads for a host-out batch's output copies
   bool hv_fused_ = false;               // option "hv_fused": first H + V pass fused (k_resize_hv) when it fits
+  bool destuff_one_ = true;             // option "destuff_one": single-pass destuff with decoupled look-back
+  bool chroma_rec_ = true;              // option "chroma_rec": half-rate chroma planes as 8-byte records (dg_plane.h)
   bool band_dec_ = false;               // option "band_dec": IDCT + colour + first H pass in k_band_dec
   uint32_t uf_units_ = 2;               // option "uf_units": PNG unfilter units per lane per step (1 or 2)
   uint32_t inf_decode_ = 2;             // option "inf_decode": k_inf_decode lookup bits (2 = 7/6, 24 KiB LDS per wave)

@@ -10,6 +10,7 @@ namespace dg {
 void launch_destuff_count(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 void launch_destuff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+void launch_destuff_one(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, uint64_t *state);
 // Entropy decode (one 256-thread workgroup per 256 subsequences of one image)
 // (sync/fix: 255 useful subsequences per workgroup, see kernels.hip)
 struct Ckpt;

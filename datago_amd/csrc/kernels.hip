@@ -20,6 +20,7 @@
 
 #include "dg_entropy.h"
 #include "dg_pixel.h"
+#include "dg_plane.h"
 #include "kernels.h"
 
 #pragma clang fp contract(off)
@@ -243,6 +244,136 @@ __global__ __launch_bounds__(256) void k_destuff_write(const ImageDesc *__restri
   if ((uint32_t)t < total - tail0) {
     const uint32_t q = O + tail0 + t;
     ds[(size_t)ds_word_index(q >> 2, lsw) * 4 + (q & 3)] = buf[tail0 + t];
+  }
+}
+
+// Destuff in one pass (option "destuff_one"): count, prefix and write of a
+// chunk in one workgroup, instead of k_destuff_count + k_destuff_scan +
+// k_destuff_write (three launches, the raw scan read twice).  A chunk's
+// output offset is the sum of its image's earlier chunks' kept bytes, found
+// by decoupled look-back: each chunk publishes its own counts as soon as it
+// has them (state word: bit 62 aggregate ready, bit 63 inclusive prefix
+// ready, markers in bits 32..61, kept bytes in 0..31), then walks back over
+// its predecessors' words, adding aggregates until it meets an inclusive
+// prefix, and publishes its own inclusive prefix.  Chunks are taken in list
+// order from a batch ticket (state[0]), so every predecessor was taken by a
+// workgroup that is running or done: each wait ends.  A wait that does not
+// end within ~1 s (a hardware or launch anomaly, never a property of the
+// data) marks the image DG_ERR_UNSUPPORTED instead of hanging.  Wave 0 runs
+// the look-back with every lane on the same addresses (no lane-divergent
+// branch around the polling loop, see uf_wait in dg_png.hip).
+constexpr uint64_t kDsAgg = 1ull << 62, kDsIncl = 1ull << 63;
+
+__global__ __launch_bounds__(256) void k_destuff_one(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
+                                                     uint64_t *__restrict__ state) {
+  __shared__ uint32_t sk[256], sm[256];
+  __shared__ uint8_t buf[kDestuffChunk];
+  __shared__ uint32_t s_item, s_ok, s_ek, s_em;
+  const int t = threadIdx.x;
+  if (t == 0) s_item = atomicAdd((uint32_t *)state, 1u);
+  __syncthreads();
+  const WgItem it = list[s_item];
+  ImageDesc &im = imgs[it.image];
+  const uint32_t c = it.item0;
+  const Destuff16 d = destuff16(gp<const uint8_t>(im.scan), im.scan_len, c * kDestuffChunk + t * 16);
+  sk[t] = d.kept;
+  sm[t] = d.mks;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    uint32_t a = t >= off ? sk[t - off] : 0u, b = t >= off ? sm[t - off] : 0u;
+    __syncthreads();
+    sk[t] += a;
+    sm[t] += b;
+    __syncthreads();
+  }
+  const uint32_t total = sk[255], mtotal = sm[255];
+  uint64_t *cs = state + 1 + im.ds_state0;  // this image's chunk words
+  if (t < 64) {  // wave 0, every lane on the same values
+    const uint64_t own = ((uint64_t)(mtotal & 0x3FFFFFFFu) << 32) | total;
+    uint32_t ek = 0, em = 0, ok = 1;
+    if (c == 0) {
+      __hip_atomic_store(cs, own | kDsIncl, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(cs + c, own | kDsAgg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t j = c - 1;
+      for (;;) {
+        const uint64_t v = __hip_atomic_load(cs + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (v & (kDsAgg | kDsIncl)) {
+          ek += (uint32_t)v;
+          em += (uint32_t)(v >> 32) & 0x3FFFFFFFu;
+          if ((v & kDsIncl) || j == 0) break;
+          j--;
+          continue;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // ~1 s at 100 MHz
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      const uint64_t incl = ((uint64_t)((em + mtotal) & 0x3FFFFFFFu) << 32) | (uint64_t)(ek + total);
+      __hip_atomic_store(cs + c, incl | kDsIncl, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t == 0) {
+      s_ek = ek;
+      s_em = em;
+      s_ok = ok;
+    }
+  }
+  __syncthreads();
+  if (!s_ok) {
+    if (t == 0) atomicCAS((int *)&im.status, 0, 1);  // DG_ERR_UNSUPPORTED (an earlier CORRUPT stays)
+    return;  // uniform
+  }
+  const uint32_t O = s_ek;        // chunk's first output byte
+  uint32_t o = sk[t] - d.kept;    // this thread's first byte within the chunk
+  if (d.km == 0xFFFFu) {
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++) buf[o + j] = (uint8_t)(d.r[j >> 2] >> (8 * (j & 3)));
+  } else {
+    uint32_t mo = s_em + sm[t] - d.mks;
+    DG_GLOBAL uint32_t *mk = gp<uint32_t>(im.mk);
+    for (uint32_t j = 0; j < 16; j++) {
+      if ((d.mm >> j) & 1u) {
+        if (mo < im.mk_cap) mk[mo] = (O + o) * 8;
+        mo++;
+      }
+      if ((d.km >> j) & 1u) buf[o++] = (uint8_t)(d.r[j >> 2] >> (8 * (j & 3)));
+    }
+  }
+  __syncthreads();
+  DG_GLOBAL uint8_t *ds = gp<uint8_t>(im.ds);
+  DG_GLOBAL uint32_t *ds4 = (DG_GLOBAL uint32_t *)ds;
+  const uint32_t lsw = im.ds_lsw;
+  const uint32_t mis = (4u - (O & 3u)) & 3u;
+  const uint32_t head = mis < total ? mis : total;
+  const uint32_t nd = (total - head) >> 2;
+  if ((uint32_t)t < head) {
+    const uint32_t q = O + t;
+    ds[(size_t)ds_word_index(q >> 2, lsw) * 4 + (q & 3)] = buf[t];
+  }
+  const uint32_t w0 = (O + head) >> 2;
+  for (uint32_t q = t; q < nd; q += 256) {
+    const uint32_t b0 = head + 4 * q;
+    ds4[ds_word_index(w0 + q, lsw)] = (uint32_t)buf[b0] | ((uint32_t)buf[b0 + 1] << 8) |
+                                      ((uint32_t)buf[b0 + 2] << 16) | ((uint32_t)buf[b0 + 3] << 24);
+  }
+  const uint32_t tail0 = head + 4 * nd;
+  if ((uint32_t)t < total - tail0) {
+    const uint32_t q = O + tail0 + t;
+    ds[(size_t)ds_word_index(q >> 2, lsw) * 4 + (q & 3)] = buf[tail0 + t];
+  }
+  if (c + 1 == im.nchunk) {  // the image's last chunk: stream length, marker count, zero padding
+    const uint32_t ck = O + total, cm = s_em + mtotal;
+    if (t == 0) {
+      im.ds_bits = ck * 8;
+      im.nmk = cm < im.mk_cap ? cm : im.mk_cap;
+    }
+    if (t < 64) {
+      const uint32_t q = ck + t;
+      ds[(size_t)ds_word_index(q >> 2, lsw) * 4 + (q & 3)] = 0;
+    }
   }
 }
 
@@ -691,11 +822,13 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
   const uint32_t bx0 = chunk * kIdctBlocks + slot, bx1 = bx0 + 32;
   const bool v0 = bx0 < cbw, v1 = bx1 < cbw;
   const DG_GLOBAL int16_t *coef = gp<const int16_t>(im.coef);
+  const uint32_t chc = im.ch[c];
   auto block_index = [&](uint32_t bx) -> uint32_t {
     if (im.ncomp == 1) return by * im.cbw[0] + bx;
-    uint32_t my = by / im.cv[c], vy = by - my * im.cv[c];
-    uint32_t mx = bx / im.ch[c], hx = bx - mx * im.ch[c];
-    return (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * im.ch[c] + hx;
+    uint32_t my = by / im.cv[c], vy = by - my * im.cv[c];  // uniform
+    // per lane: sampling factors are 1..4, and 1 / 2 need no division
+    uint32_t mx = chc == 1 ? bx : chc == 2 ? bx >> 1 : bx / chc, hx = bx - mx * chc;
+    return (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * chc + hx;
   };
   u32x4 r0 = {0, 0, 0, 0}, r1 = {0, 0, 0, 0};
   if (v0) r0 = *(const DG_GLOBAL u32x4 *)(coef + (size_t)block_index(bx0) * 64 + lane * 8);
@@ -723,9 +856,9 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
   {
     int32_t v0[8], v1[8], w0[8], w1[8];
 #pragma unroll
-    for (int r = 0; r < 8; r++) {
-      v0[r] = bv0[r * RS + lane] * qc[r];
-      v1[r] = bv1[r * RS + lane] * qc[r];
+    for (int r = 0; r < 8; r++) {  // int16 coefficient x uint16 quantiser: 24-bit operands, exact
+      v0[r] = __mul24(bv0[r * RS + lane], qc[r]);
+      v1[r] = __mul24(bv1[r * RS + lane], qc[r]);
     }
     idct_col(zune, v0, w0);
     idct_col(zune, v1, w1);
@@ -740,6 +873,8 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
   // pass 2: row `lane`
   const uint32_t pst = cbw * 8;
   DG_GLOBAL uint8_t *plane = gp<uint8_t>(im.plane[c]) + (size_t)(by * 8 + lane) * pst;
+  const bool rec = plane_is_rec(im, c);  // uniform per workgroup
+  uint32_t pv[2][8];
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     const int32_t *w = (h ? bv1 : bv0) + lane * RS;
@@ -749,10 +884,39 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
 #pragma unroll
     for (int i = 0; i < 8; i++) row[i] = w[i];
     idct_row(zune, row, px);
+    if (rec) {
+      crec_clamp((int32_t)crec_lim(im, c) - 1 - (int32_t)((h ? bx1 : bx0) * 8), px, pv[h]);
+      continue;
+    }
     // pack4, not shifts: shift/or packing of clamped values lets hipcc form
     // v_ashr_pk_u8_i32 and OR the next byte into its stale upper half
     const uint32_t lo = pack4(px[0], px[1], px[2], px[3]), hi = pack4(px[4], px[5], px[6], px[7]);
     if (v) *(DG_GLOBAL u32x2 *)(plane + (size_t)(h ? bx1 : bx0) * 8) = u32x2{lo, hi};
+  }
+  if (!rec) return;
+  // Chroma records (dg_plane.h): the workgroup's 64 blocks are consecutive
+  // in the row, so a block's outer edge samples come from its neighbours'
+  // edge columns through LDS and both records of a row go out as one 16-byte
+  // store; only the first and last block of the chunk hand their edge to
+  // (and leave their own to) the neighbouring workgroups.
+  __shared__ uint8_t efirst[kIdctBlocks * 8], elast[kIdctBlocks * 8];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int i = slot + 32 * h;
+    efirst[i * 8 + lane] = (uint8_t)pv[h][0];
+    elast[i * 8 + lane] = (uint8_t)pv[h][7];
+  }
+  __syncthreads();
+  DG_GLOBAL uint8_t *rrow = crec_row(im, c, by * 8 + lane);
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    if (!(h ? v1 : v0)) continue;
+    const int i = slot + 32 * h;
+    const uint32_t bx = h ? bx1 : bx0;
+    const bool in_l = i > 0, in_r = i + 1 < (int)kIdctBlocks && bx + 1 < cbw;
+    const uint32_t l = in_l ? elast[(i - 1) * 8 + lane] : pv[h][0];
+    const uint32_t r = in_r ? efirst[(i + 1) * 8 + lane] : pv[h][7];
+    store_crec_pair(rrow, bx, cbw, pv[h], l, r, in_l || bx == 0, in_r || bx + 1 == cbw);
   }
 }
 
@@ -809,8 +973,7 @@ __global__ __launch_bounds__(256) void k_idct_list(const ImageDesc *__restrict__
 #pragma unroll
       for (int i = 0; i < 8; i++) row[i] = bv[lane * RS + i];
       idct_row(im.sem != 0, row, px);
-      DG_GLOBAL uint8_t *dst = gp<uint8_t>(im.plane[c]) + (size_t)(by * 8 + lane) * (im.cbw[c] * 8) + bx * 8;
-      *(DG_GLOBAL u32x2 *)dst = u32x2{pack4(px[0], px[1], px[2], px[3]), pack4(px[4], px[5], px[6], px[7])};
+      store_plane_row8(im, c, by * 8 + lane, bx, px);
     }
     __syncthreads();
   }
@@ -826,7 +989,42 @@ __global__ __launch_bounds__(256) void k_idct_list(const ImageDesc *__restrict__
 // the host keeps every JPEG plane below 4 GiB (pipeline.cpp, plan_image).
 template <class P>
 __device__ __forceinline__ void upsample8(P pl, uint32_t stride, uint32_t hr, uint32_t vr,
-                                          uint32_t dsw, uint32_t dsh, uint32_t x0, uint32_t y, int32_t o[8]) {
+                                          uint32_t dsw, uint32_t dsh, uint32_t x0, uint32_t y, int32_t o[8],
+                                          bool rec = false) {
+  if (rec) {  // chroma records (dg_plane.h): six clamped columns per row in one load, no edge cases
+    const uint32_t c0 = x0 >> 1;
+    int32_t cs[6];
+    const bool fancy = dsw > 2;
+    if (vr == 1 || !fancy) {
+      load_crec6(pl, stride, vr == 1 ? y : y >> 1, c0, cs);
+      if (!fancy) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) o[k] = cs[1 + (k >> 1)];
+        return;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int32_t a = cs[k + 1] * 3;
+        o[2 * k] = (a + cs[k] + 1) >> 2;
+        o[2 * k + 1] = (a + cs[k + 2] + 2) >> 2;
+      }
+      return;
+    }
+    const uint32_t r = y >> 1;
+    int32_t rn = (y & 1) ? (int32_t)r + 1 : (int32_t)r - 1;
+    rn = rn < 0 ? 0 : (rn > (int32_t)dsh - 1 ? (int32_t)dsh - 1 : rn);
+    int32_t fr[6];
+    load_crec6(pl, stride, r, c0, cs);
+    load_crec6(pl, stride, (uint32_t)rn, c0, fr);
+#pragma unroll
+    for (int k = 0; k < 6; k++) cs[k] = cs[k] * 3 + fr[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      o[2 * k] = (cs[k + 1] * 3 + cs[k] + 8) >> 4;
+      o[2 * k + 1] = (cs[k + 1] * 3 + cs[k + 2] + 7) >> 4;
+    }
+    return;
+  }
   if (hr == 1) {  // 4:4:4 component (vr is 1 too for the supported samplings)
     u32x2 v = *(const DG_GLOBAL u32x2 *)(pl + (size_t)__umul24(y, stride) + x0);
 #pragma unroll
@@ -923,7 +1121,34 @@ __device__ __forceinline__ void upsample8(P pl, uint32_t stride, uint32_t hr, ui
 // the last pair is ((3 * in[n-2] + in[n-1] + 2) >> 2, in[n-1]).
 template <class P>
 __device__ __forceinline__ void upsample8_zune(P pl, uint32_t stride, uint32_t hr, uint32_t vr, uint32_t ph,
-                                               uint32_t x0, uint32_t y, int32_t o[8]) {
+                                               uint32_t x0, uint32_t y, int32_t o[8], bool rec = false) {
+  if (rec) {  // chroma records (dg_plane.h), columns clamped to [0, n-1]
+    const uint32_t n = stride, c0 = x0 >> 1;
+    int32_t cs[6];
+    if (vr == 1) {
+      load_crec6(pl, stride, y, c0, cs);
+    } else {
+      const uint32_t r = y >> 1;
+      const uint32_t rn = (y & 1) ? (r + 1 < ph ? r + 1 : r) : (r > 0 ? r - 1 : 0);
+      int32_t fr[6];
+      load_crec6(pl, stride, r, c0, cs);
+      load_crec6(pl, stride, rn, c0, fr);
+#pragma unroll
+      for (int k = 0; k < 6; k++) cs[k] = (3 * cs[k] + 2 + fr[k]) >> 2;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // column 0: cs[0] == cs[1], so the even output is cs[1] as zune's
+      const int32_t a = 3 * cs[k + 1] + 2;
+      int32_t ev = (a + cs[k]) >> 2, od = (a + cs[k + 2]) >> 2;
+      if (c0 + (uint32_t)k + 1 == n) {
+        ev = (3 * cs[k] + cs[k + 1] + 2) >> 2;
+        od = cs[k + 1];
+      }
+      o[2 * k] = ev;
+      o[2 * k + 1] = od;
+    }
+    return;
+  }
   if (hr == 1) {
     u32x2 v = *(const DG_GLOBAL u32x2 *)(pl + (size_t)__umul24(y, stride) + x0);
 #pragma unroll
@@ -975,19 +1200,19 @@ __device__ __forceinline__ void upsample_ycc8(const ImageDesc &im, uint32_t x0, 
                                              int32_t Cb[8], int32_t Cr[8]) {
   if (im.sem) {
     upsample8_zune(gp<const uint8_t>(im.plane[0]), im.cbw[0] * 8, im.hmax / im.ch[0], im.vmax / im.cv[0],
-                   im.cbh[0] * 8, x0, y, Y);
+                   im.cbh[0] * 8, x0, y, Y, plane_is_rec(im, 0));
     upsample8_zune(gp<const uint8_t>(im.plane[1]), im.cbw[1] * 8, im.hmax / im.ch[1], im.vmax / im.cv[1],
-                   im.cbh[1] * 8, x0, y, Cb);
+                   im.cbh[1] * 8, x0, y, Cb, plane_is_rec(im, 1));
     upsample8_zune(gp<const uint8_t>(im.plane[2]), im.cbw[2] * 8, im.hmax / im.ch[2], im.vmax / im.cv[2],
-                   im.cbh[2] * 8, x0, y, Cr);
+                   im.cbh[2] * 8, x0, y, Cr, plane_is_rec(im, 2));
     return;
   }
   upsample8(gp<const uint8_t>(im.plane[0]), im.cbw[0] * 8, im.hmax / im.ch[0], im.vmax / im.cv[0], im.cdsw[0],
-            im.cdsh[0], x0, y, Y);
+            im.cdsh[0], x0, y, Y, plane_is_rec(im, 0));
   upsample8(gp<const uint8_t>(im.plane[1]), im.cbw[1] * 8, im.hmax / im.ch[1], im.vmax / im.cv[1], im.cdsw[1],
-            im.cdsh[1], x0, y, Cb);
+            im.cdsh[1], x0, y, Cb, plane_is_rec(im, 1));
   upsample8(gp<const uint8_t>(im.plane[2]), im.cbw[2] * 8, im.hmax / im.ch[2], im.vmax / im.cv[2], im.cdsw[2],
-            im.cdsh[2], x0, y, Cr);
+            im.cdsh[2], x0, y, Cr, plane_is_rec(im, 2));
 }
 
 __device__ __forceinline__ void ycc_px(const ImageDesc &im, int32_t y, int32_t cb, int32_t cr, uint8_t &r,
@@ -1054,6 +1279,13 @@ __global__ __launch_bounds__(256) void k_coeffs(ImageDesc *__restrict__ imgs, co
   const double recip = 1.0 / filter_scale;
   DG_GLOBAL int32_t *bounds = gp<int32_t>(ps.bounds);  // {start, size} per output
   DG_GLOBAL int16_t *coef = gp<int16_t>(ps.coef);
+  // Each tap's Lanczos value is evaluated twice (the sum, then the
+  // quantisation), not four times: the largest normalised weight of an output
+  // is its largest (smallest, for a negative sum) raw weight divided by the
+  // sum -- division by one value is monotone in IEEE arithmetic, so this is
+  // exactly the max of the quotients -- and each output's sum waits for the
+  // second loop in the first 8 bytes of its own coefficient row (ksize >= 7
+  // taps of 2 bytes; the same thread owns output o in both loops).
   double maxw = 0.0;
   for (uint32_t o = t; o < out_size; o += 256) {
     // fast_image_resize precompute_coefficients for output o (see fir_weights)
@@ -1061,13 +1293,15 @@ __global__ __launch_bounds__(256) void k_coeffs(ImageDesc *__restrict__ imgs, co
     double fl = floor(center - support), cl = ceil(center + support);
     int32_t xmin = fl < 0.0 ? 0 : (int32_t)fl;
     int32_t xmax = cl > (double)in_size ? (int32_t)in_size : (int32_t)cl;
-    double c = center - 0.5, ww = 0.0;
+    double c = center - 0.5, ww = 0.0, vhi = -INFINITY, vlo = INFINITY;
     int32_t first = -1, last = -1;
     for (int32_t x = xmin; x < xmax; x++) {
       double v = lanczos3(((double)x - c) * recip);
       if (v != 0.0) {
         if (first < 0) first = x;
         last = x;
+        vhi = v > vhi ? v : vhi;
+        vlo = v < vlo ? v : vlo;
       }
       ww += v;
     }
@@ -1075,10 +1309,16 @@ __global__ __launch_bounds__(256) void k_coeffs(ImageDesc *__restrict__ imgs, co
     int32_t n = first < 0 ? 0 : last - first + 1;
     bounds[2 * o] = st;
     bounds[2 * o + 1] = n;
-    for (int32_t i = 0; i < n; i++) {
-      double v = lanczos3(((double)(st + i) - c) * recip);
-      if (ww != 0.0) v /= ww;
-      if (v > maxw) maxw = v;
+    {
+      const uint64_t bits = __builtin_bit_cast(uint64_t, ww);
+      DG_GLOBAL uint16_t *kw = (DG_GLOBAL uint16_t *)(coef + (size_t)o * ksize);
+#pragma unroll
+      for (int q = 0; q < 4; q++) kw[q] = (uint16_t)(bits >> (16 * q));
+    }
+    if (n > 0) {  // the taps [st, st + n) hold every nonzero weight; zeros inside it are 0 / ww = 0
+      const double hi = ww > 0.0 ? vhi / ww : ww < 0.0 ? vlo / ww : vhi;
+      const double cand = hi > 0.0 ? hi : 0.0;  // a zero weight inside the window still compares
+      if (cand > maxw) maxw = cand;
     }
   }
   red[t] = maxw;
@@ -1091,13 +1331,14 @@ __global__ __launch_bounds__(256) void k_coeffs(ImageDesc *__restrict__ imgs, co
   if (t == 0) ps.precision = precision;
   for (uint32_t o = t; o < out_size; o += 256) {
     double center = in0 + ((double)o + 0.5) * scale;
-    double fl = floor(center - support), cl = ceil(center + support);
-    int32_t xmin = fl < 0.0 ? 0 : (int32_t)fl;
-    int32_t xmax = cl > (double)in_size ? (int32_t)in_size : (int32_t)cl;
-    double c = center - 0.5, ww = 0.0;
-    for (int32_t x = xmin; x < xmax; x++) ww += lanczos3(((double)x - c) * recip);
-    const int32_t st = bounds[2 * o], n = bounds[2 * o + 1];
+    double c = center - 0.5;
     DG_GLOBAL int16_t *k = coef + (size_t)o * ksize;
+    uint64_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) bits |= (uint64_t)(uint16_t)k[q] << (16 * q);
+    const double ww = __builtin_bit_cast(double, bits);
+    const int32_t st = bounds[2 * o], n = bounds[2 * o + 1];
+    for (int32_t i = n; i < 4; i++) k[i] = 0;  // taps past n keep no stale sum bits
     for (int32_t i = 0; i < n; i++) {
       double v = lanczos3(((double)(st + i) - c) * recip);
       if (ww != 0.0) v /= ww;
@@ -1232,6 +1473,116 @@ __device__ __forceinline__ void hfill_color8(const ImageDesc &im, uint32_t y, ui
   d4[1] = u32x4{v[4], v[5], v[6], v[7]};
 }
 
+// Fill classes of the fused colour fill: the common JPEG layouts get a fill
+// specialised at compile time (no per-pixel branches on sampling, semantics,
+// record format or colour space, no edge clamping: the chroma records carry
+// their clamped edges); everything else takes the generic hfill_color8.
+// Chosen once per workgroup (uniform per image).
+enum FillClass : int {
+  FC_GENERIC = 0,
+  FC_420 = 1, FC_420_Z = 2,  // Y h2v2, Cb/Cr h1v1 as chroma records; libjpeg fancy / zune
+  FC_422 = 3, FC_422_Z = 4,  // Y h2v1, Cb/Cr h1v1 as chroma records
+  FC_444 = 5, FC_444_Z = 6,  // all components at full rate (plain planes)
+};
+
+__device__ __forceinline__ int fill_class(const ImageDesc &im) {
+  if (im.ncomp != 3 || im.colorspace != CS_YCC) return FC_GENERIC;
+  const bool z = im.sem != 0;
+  if (im.ch[0] == 1 && im.cv[0] == 1 && im.ch[1] == 1 && im.cv[1] == 1 && im.ch[2] == 1 && im.cv[2] == 1 &&
+      im.crec == 0)
+    return z ? FC_444_Z : FC_444;
+  if (im.ch[0] != 2 || im.ch[1] != 1 || im.cv[1] != 1 || im.ch[2] != 1 || im.cv[2] != 1 || im.crec != 6u)
+    return FC_GENERIC;
+  if (!z && (im.cdsw[1] <= 2 || im.cdsw[2] <= 2)) return FC_GENERIC;  // libjpeg's box filter for tiny widths
+  if (im.cv[0] == 2) return z ? FC_420_Z : FC_420;
+  if (im.cv[0] == 1) return z ? FC_422_Z : FC_422;
+  return FC_GENERIC;
+}
+
+template <int FC>
+__device__ __forceinline__ void hfill_fc8(const ImageDesc &im, uint32_t y, uint32_t x0, uint32_t *d) {
+  constexpr bool Z = FC == FC_420_Z || FC == FC_422_Z || FC == FC_444_Z;
+  constexpr int SS = (FC == FC_420 || FC == FC_420_Z) ? 2 : (FC == FC_422 || FC == FC_422_Z) ? 1 : 0;
+  const DG_GLOBAL uint8_t *pY = gp<const uint8_t>(im.plane[0]);
+  const DG_GLOBAL uint8_t *pB = gp<const uint8_t>(im.plane[1]);
+  const DG_GLOBAL uint8_t *pR = gp<const uint8_t>(im.plane[2]);
+  const uint32_t sY = im.cbw[0] * 8;
+  int32_t Yv[8], Cb[8], Cr[8];
+  auto unpack8 = [](u32x2 v, int32_t o[8]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      o[k] = (v.x >> (8 * k)) & 0xFF;
+      o[k + 4] = (v.y >> (8 * k)) & 0xFF;
+    }
+  };
+  unpack8(*(const DG_GLOBAL u32x2 *)(pY + (size_t)__umul24(y, sY) + x0), Yv);
+  if (SS == 0) {
+    const uint32_t sC = im.cbw[1] * 8;
+    unpack8(*(const DG_GLOBAL u32x2 *)(pB + (size_t)__umul24(y, sC) + x0), Cb);
+    unpack8(*(const DG_GLOBAL u32x2 *)(pR + (size_t)__umul24(y, sC) + x0), Cr);
+  } else {
+    const uint32_t sC = im.cbw[1] * 8, c0 = x0 >> 1;
+    int32_t b[6], r[6];
+    if (SS == 1) {
+      load_crec6(pB, sC, y, c0, b);
+      load_crec6(pR, sC, y, c0, r);
+    } else {
+      const uint32_t rr = y >> 1, last = Z ? im.cbh[1] * 8 - 1 : im.cdsh[1] - 1;
+      const uint32_t rn = (y & 1) ? (rr + 1 <= last ? rr + 1 : last) : (rr > 0 ? rr - 1 : 0);
+      int32_t b1[6], r1[6];
+      load_crec6(pB, sC, rr, c0, b);
+      load_crec6(pR, sC, rr, c0, r);
+      load_crec6(pB, sC, rn, c0, b1);
+      load_crec6(pR, sC, rn, c0, r1);
+#pragma unroll
+      for (int k = 0; k < 6; k++) {
+        b[k] = Z ? (3 * b[k] + 2 + b1[k]) >> 2 : 3 * b[k] + b1[k];
+        r[k] = Z ? (3 * r[k] + 2 + r1[k]) >> 2 : 3 * r[k] + r1[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (Z) {  // zune: (3a + b + 2) >> 2 both phases; the padded row's last pair is its quirk
+        const int32_t ab = 3 * b[k + 1] + 2, ar = 3 * r[k + 1] + 2;
+        int32_t eb = (ab + b[k]) >> 2, ob = (ab + b[k + 2]) >> 2, er = (ar + r[k]) >> 2, orr = (ar + r[k + 2]) >> 2;
+        if (c0 + (uint32_t)k + 1 == sC) {
+          eb = (3 * b[k] + b[k + 1] + 2) >> 2;
+          ob = b[k + 1];
+          er = (3 * r[k] + r[k + 1] + 2) >> 2;
+          orr = r[k + 1];
+        }
+        Cb[2 * k] = eb;
+        Cb[2 * k + 1] = ob;
+        Cr[2 * k] = er;
+        Cr[2 * k + 1] = orr;
+      } else if (SS == 2) {  // libjpeg h2v2 fancy over column sums
+        Cb[2 * k] = (b[k + 1] * 3 + b[k] + 8) >> 4;
+        Cb[2 * k + 1] = (b[k + 1] * 3 + b[k + 2] + 7) >> 4;
+        Cr[2 * k] = (r[k + 1] * 3 + r[k] + 8) >> 4;
+        Cr[2 * k + 1] = (r[k + 1] * 3 + r[k + 2] + 7) >> 4;
+      } else {  // libjpeg h2v1 fancy
+        Cb[2 * k] = (b[k + 1] * 3 + b[k] + 1) >> 2;
+        Cb[2 * k + 1] = (b[k + 1] * 3 + b[k + 2] + 2) >> 2;
+        Cr[2 * k] = (r[k + 1] * 3 + r[k] + 1) >> 2;
+        Cr[2 * k + 1] = (r[k + 1] * 3 + r[k + 2] + 2) >> 2;
+      }
+    }
+  }
+  uint32_t v[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint8_t rr, gg, bb;
+    if (Z)
+      ycc_to_rgb_zune(Yv[k], Cb[k], Cr[k], rr, gg, bb);
+    else
+      ycc_to_rgb(Yv[k], Cb[k], Cr[k], rr, gg, bb);
+    v[k] = (uint32_t)rr | ((uint32_t)gg << 8) | ((uint32_t)bb << 16);
+  }
+  u32x4 *d4 = (u32x4 *)d;
+  d4[0] = u32x4{v[0], v[1], v[2], v[3]};
+  d4[1] = u32x4{v[4], v[5], v[6], v[7]};
+}
+
 // 4 source pixels at p (p % 4 == 0) of an interleaved C-byte row of `in_size`
 // pixels in rows of `stride` (multiple of 4) bytes
 __device__ __forceinline__ void hfill_bytes4(const DG_GLOBAL uint8_t *row, uint32_t C, uint32_t stride,
@@ -1342,7 +1693,7 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
 // conversion from the planes, C = 3); otherwise the fill copies interleaved
 // bytes of C = 1..4 channels.  Separate kernels so each allocates registers
 // for its own path only.
-template <int KMAX, bool FUSED>
+template <int KMAX, bool FUSED, int FC = FC_GENERIC>
 __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps, uint32_t item, uint32_t *seg,
                                       uint8_t *ob, uint32_t *ext) {
   // one workgroup: a tile of kHBandCols output columns x ps.bands bands of
@@ -1416,7 +1767,10 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
     for (uint32_t j = t; j < njob; j += 256) {
       const uint32_t r = __umul24(j, inv_row) >> 20, q = j - r * njob_row;
       if (FUSED) {
-        hfill_color8(im, ps.row0 + y0 + r, p0 + 8 * q, seg + r * kHSegStride + 8 * q);
+        if (FC == FC_GENERIC)
+          hfill_color8(im, ps.row0 + y0 + r, p0 + 8 * q, seg + r * kHSegStride + 8 * q);
+        else
+          hfill_fc8<FC>(im, ps.row0 + y0 + r, p0 + 8 * q, seg + r * kHSegStride + 8 * q);
       } else {
         const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0 + r) * ps.src_stride;
         hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * q, seg + r * kHSegStride + 4 * q);
@@ -1464,6 +1818,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   __shared__ uint32_t ext[2];
   const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
   const ImageDesc &im = imgs[it.image];
+  if (FUSED) {  // a fused fill reads the planes: specialised per layout (uniform per workgroup)
+    switch (fill_class(im)) {
+      case FC_420: hband<KMAX, FUSED, FC_420>(im, im.pass[stage], it.item0, seg, ob, ext); return;
+      case FC_420_Z: hband<KMAX, FUSED, FC_420_Z>(im, im.pass[stage], it.item0, seg, ob, ext); return;
+      case FC_422: hband<KMAX, FUSED, FC_422>(im, im.pass[stage], it.item0, seg, ob, ext); return;
+      case FC_422_Z: hband<KMAX, FUSED, FC_422_Z>(im, im.pass[stage], it.item0, seg, ob, ext); return;
+      case FC_444: hband<KMAX, FUSED, FC_444>(im, im.pass[stage], it.item0, seg, ob, ext); return;
+      case FC_444_Z: hband<KMAX, FUSED, FC_444_Z>(im, im.pass[stage], it.item0, seg, ob, ext); return;
+      default: break;
+    }
+  }
   hband<KMAX, FUSED>(im, im.pass[stage], it.item0, seg, ob, ext);
 }
 
@@ -1995,6 +2360,9 @@ void launch_destuff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, ui
 }
 void launch_destuff_write(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   DG_LAUNCH(k_destuff_write, nwg, st, imgs, list);
+}
+void launch_destuff_one(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, uint64_t *state) {
+  DG_LAUNCH(k_destuff_one, nwg, st, imgs, list, state);
 }
 // sync / fix hold only the batch's largest table count in LDS (4 for a
 // typical colour JPEG instead of kMaxSlots = 6): 16 KiB instead of 23 KiB
