@@ -498,6 +498,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     idct_fused_ = v != 0;
     return DG_OK;
   }
+  if (k == "h_pairs") {
+    h_pairs_ = v != 0;
+    return DG_OK;
+  }
   if (k == "destuff_one") {
     destuff_one_ = v != 0;
     return DG_OK;
@@ -1736,8 +1740,11 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         // k_resize_hb<K> reads taps in even-aligned pairs: a window starting
         // at an odd segment position spans ksize + 1 positions
         const uint32_t kk = ps.ksize + 1;
-        const int cls = kk <= 8 ? 0 : kk <= 16 ? 1 : kk <= 32 ? 2 : 3;
+        int cls = kk <= 8 ? 0 : kk <= 16 ? 1 : kk <= 32 ? 2 : 3;
         const int fused = (ps.mode & kHFused) ? 1 : 0;
+        // the pair layout's 8- and 16-tap kernels hold narrower segments (hseg_px in kernels.hip)
+        if (fused && h_pairs_)
+          while (cls < 2 && h_pass_span(ps) > (cls == 0 ? 192.0 : 384.0)) cls++;
         const uint32_t ks = h_mfma_ ? h_mfma_steps(ps) : 0u;
         if (ks)
           for (uint32_t it = 0; it < cnt; it++) hm[s / 2][fused][ks - 1].push_back({I, it});
@@ -2208,7 +2215,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
   launch_band_dec(sl.st, dd, lst(L_DEC), b.decclass, qp, dec_strips_ | (dec_dbg_ << 16));
   launch_resize_hm(sl.st, dd, lst(L_RM0), b.hmclass[0], 0);
-  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0);
+  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0, h_pairs_);
   launch_resize_hv(sl.st, dd, lst(L_RHV), b.hvclass);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
@@ -2216,7 +2223,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_hm(sl.st, dd, lst(L_RM2), b.hmclass[1], 2);
-  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2);
+  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2, h_pairs_);
   launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3);

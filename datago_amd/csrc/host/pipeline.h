@@ -334,6 +334,7 @@ class Context {
   double host_cpu_us_[6] = {0, 0, 0, 0, 0, 0};  // the same phases' thread CPU time (stats "host_cpu_us_*")
   int copy_threads_ = 8;                // option "copy_threads": host threads for a host-out batch's output copies
   bool hv_fused_ = false;               // option "hv_fused": first H + V pass fused (k_resize_hv) when it fits
+  bool h_pairs_ = true;                 // option "h_pairs": fused band H kernels with the i16-pair LDS layout
   bool destuff_one_ = true;             // option "destuff_one": single-pass destuff with decoupled look-back
   bool chroma_rec_ = true;              // option "chroma_rec": half-rate chroma planes as 8-byte records (dg_plane.h)
   bool band_dec_ = false;               // option "band_dec": IDCT + colour + first H pass in k_band_dec

@@ -1458,16 +1458,19 @@ constexpr uint32_t kHVSegStride = kHVSegPx + 8;  // (kHVSegPx, kHVTapsMax, kHVRo
 constexpr uint32_t kHVOut = 8;                    // k_resize_hv: V rows produced per round
 
 // job j of the fill: 8 source pixels from the planes, p0 % 8 == 0
-__device__ __forceinline__ void hfill_color8(const ImageDesc &im, uint32_t y, uint32_t x0, uint32_t *d) {
+__device__ __forceinline__ void hcolor8(const ImageDesc &im, uint32_t y, uint32_t x0, uint32_t v[8]) {
   int32_t Y[8], Cb[8], Cr[8];
   upsample_ycc8(im, x0, y, Y, Cb, Cr);
-  uint32_t v[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     uint8_t r, g, b;
     ycc_px(im, Y[k], Cb[k], Cr[k], r, g, b);
     v[k] = (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
   }
+}
+__device__ __forceinline__ void hfill_color8(const ImageDesc &im, uint32_t y, uint32_t x0, uint32_t *d) {
+  uint32_t v[8];
+  hcolor8(im, y, x0, v);
   u32x4 *d4 = (u32x4 *)d;
   d4[0] = u32x4{v[0], v[1], v[2], v[3]};
   d4[1] = u32x4{v[4], v[5], v[6], v[7]};
@@ -1500,7 +1503,7 @@ __device__ __forceinline__ int fill_class(const ImageDesc &im) {
 }
 
 template <int FC>
-__device__ __forceinline__ void hfill_fc8(const ImageDesc &im, uint32_t y, uint32_t x0, uint32_t *d) {
+__device__ __forceinline__ void hcolor_fc8(const ImageDesc &im, uint32_t y, uint32_t x0, uint32_t v[8]) {
   constexpr bool Z = FC == FC_420_Z || FC == FC_422_Z || FC == FC_444_Z;
   constexpr int SS = (FC == FC_420 || FC == FC_420_Z) ? 2 : (FC == FC_422 || FC == FC_422_Z) ? 1 : 0;
   const DG_GLOBAL uint8_t *pY = gp<const uint8_t>(im.plane[0]);
@@ -1568,7 +1571,6 @@ __device__ __forceinline__ void hfill_fc8(const ImageDesc &im, uint32_t y, uint3
       }
     }
   }
-  uint32_t v[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     uint8_t rr, gg, bb;
@@ -1578,9 +1580,33 @@ __device__ __forceinline__ void hfill_fc8(const ImageDesc &im, uint32_t y, uint3
       ycc_to_rgb(Yv[k], Cb[k], Cr[k], rr, gg, bb);
     v[k] = (uint32_t)rr | ((uint32_t)gg << 8) | ((uint32_t)bb << 16);
   }
-  u32x4 *d4 = (u32x4 *)d;
-  d4[0] = u32x4{v[0], v[1], v[2], v[3]};
-  d4[1] = u32x4{v[4], v[5], v[6], v[7]};
+}
+
+// 8 fused-fill pixels (RGB in bytes 0..2 of v[k]) of segment pixels 8q..8q+7
+// into the band's LDS: one dword per pixel (seg), or, with the pair layout
+// (PAIRS), per pixel pair (2k, 2k+1) the R and G pairs as i16 x 2 in one
+// 8-byte word (segrg) and the B pair in one dword (segb), the operands
+// v_dot2_i32_i16 takes as they are: no byte selects in the convolution.
+template <bool PAIRS>
+__device__ __forceinline__ void hput8(const uint32_t v[8], uint32_t *seg, u32x2 *segrg, uint32_t *segb) {
+  if (!PAIRS) {
+    u32x4 *d4 = (u32x4 *)seg;
+    d4[0] = u32x4{v[0], v[1], v[2], v[3]};
+    d4[1] = u32x4{v[4], v[5], v[6], v[7]};
+    return;
+  }
+  uint32_t rg[8], bq[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t a = v[2 * k], b = v[2 * k + 1];
+    rg[2 * k] = __builtin_amdgcn_perm(b, a, 0x0c040c00u);      // [a.R, 0, b.R, 0]
+    rg[2 * k + 1] = __builtin_amdgcn_perm(b, a, 0x0c050c01u);  // [a.G, 0, b.G, 0]
+    bq[k] = __builtin_amdgcn_perm(b, a, 0x0c060c02u);          // [a.B, 0, b.B, 0]
+  }
+  u32x4 *r4 = (u32x4 *)segrg;
+  r4[0] = u32x4{rg[0], rg[1], rg[2], rg[3]};
+  r4[1] = u32x4{rg[4], rg[5], rg[6], rg[7]};
+  *(u32x4 *)segb = u32x4{bq[0], bq[1], bq[2], bq[3]};
 }
 
 // 4 source pixels at p (p % 4 == 0) of an interleaved C-byte row of `in_size`
@@ -1689,13 +1715,61 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
     }
 }
 
+// The convolution of hconv_rows for C = 3 over the pair layout (hput8): per
+// tap pair and row one 8-byte and one 4-byte LDS read give the R, G and B
+// operands of the three v_dot2_i32_i16 as they are.
+template <int KMAX>
+__device__ __forceinline__ void hconv_pairs(const u32x2 *segrg, const uint32_t *segb, uint32_t sp, uint32_t off,
+                                            const uint32_t *kw2, uint32_t ksize, uint32_t r0, uint32_t nrows,
+                                            int32_t prec, uint8_t *ob, uint32_t col) {
+  constexpr uint32_t R = kHBandRows / 2;
+  const int32_t bias = 1 << (prec - 1);
+  int32_t a[R][3];
+#pragma unroll
+  for (uint32_t r = 0; r < R; r++) a[r][0] = a[r][1] = a[r][2] = bias;
+  const uint32_t pe0 = off >> 1;
+#pragma unroll
+  for (int j = 0; j < (KMAX + 1) / 2; j++) {
+    if ((uint32_t)(2 * j) >= ksize + 1) break;
+    const s16x2 w = __builtin_bit_cast(s16x2, kw2[j]);
+#pragma unroll
+    for (uint32_t r = 0; r < R; r++) {
+      const uint32_t i = (r0 + 2 * r) * sp + pe0 + j;
+      const u32x2 rg = *(const u32x2 *)((const uint32_t *)segrg + 2 * i);
+      const uint32_t bq = segb[i];
+      const uint32_t rv = rg.x, gv = rg.y;
+      a[r][0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, rv), w, a[r][0], false);
+      a[r][1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, gv), w, a[r][1], false);
+      a[r][2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, bq), w, a[r][2], false);
+    }
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < R; r++)
+    if (r0 + 2 * r < nrows) {
+      uint8_t *o = ob + (r0 + 2 * r) * (kHBandCols * 4) + col * 3;
+#pragma unroll
+      for (int c = 0; c < 3; c++) o[c] = clip_shift(a[r][c], prec);
+    }
+}
+
+// LDS source segment (pixels per row) of a band H kernel.  The pair layout
+// (6 bytes per pixel) is sized per weight class: a window of <= 8 taps means
+// a downscale of at most 1x, <= 16 taps at most 7/3 x, so 128 output columns
+// read at most ~160 / ~344 source pixels (h_pass_span); the byte layout and
+// the wider classes keep kHSegPx.
+constexpr uint32_t hseg_px(int kmax, bool pairs) {
+  return !pairs ? kHSegPx : kmax == 8 ? 192u : kmax == 16 ? 384u : kHSegPx;
+}
+
 // FUSED: the first pass of a colour JPEG (fill = upsample + colour
 // conversion from the planes, C = 3); otherwise the fill copies interleaved
 // bytes of C = 1..4 channels.  Separate kernels so each allocates registers
 // for its own path only.
-template <int KMAX, bool FUSED, int FC = FC_GENERIC>
+template <int KMAX, bool FUSED, int FC = FC_GENERIC, bool PAIRS = false>
 __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps, uint32_t item, uint32_t *seg,
-                                      uint8_t *ob, uint32_t *ext) {
+                                      uint8_t *ob, uint32_t *ext, u32x2 *segrg = nullptr, uint32_t *segb = nullptr) {
+  constexpr uint32_t SEGPX = hseg_px(KMAX, PAIRS);
+  constexpr uint32_t SP = SEGPX / 2 + 4;  // pair layout: pairs per row (even: 16-byte aligned octets)
   // one workgroup: a tile of kHBandCols output columns x ps.bands bands of
   // kHBandRows rows; the column tile's weights, source extent and descriptor
   // reads are set up once and reused for every band
@@ -1728,7 +1802,7 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
   __syncthreads();
   const uint32_t p0 = ext[0] & ~7u;
   uint32_t p1 = ext[1];
-  if (p1 - p0 > kHSegPx) p1 = p0 + kHSegPx;  // host sizing guarantees this never triggers
+  if (p1 - p0 > SEGPX) p1 = p0 + SEGPX;  // host sizing guarantees this never triggers
   const uint32_t pe = p1 < ps.in_size ? p1 : ps.in_size;
   uint32_t kw2[KMAX > 0 ? (KMAX + 1) / 2 : 1];  // weights (w_2j, w_2j+1) as i16 x 2
   const DG_GLOBAL int16_t *kp = coef + (size_t)(valid ? x : x0) * ksize;
@@ -1767,10 +1841,13 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
     for (uint32_t j = t; j < njob; j += 256) {
       const uint32_t r = __umul24(j, inv_row) >> 20, q = j - r * njob_row;
       if (FUSED) {
+        uint32_t v[8];
         if (FC == FC_GENERIC)
-          hfill_color8(im, ps.row0 + y0 + r, p0 + 8 * q, seg + r * kHSegStride + 8 * q);
+          hcolor8(im, ps.row0 + y0 + r, p0 + 8 * q, v);
         else
-          hfill_fc8<FC>(im, ps.row0 + y0 + r, p0 + 8 * q, seg + r * kHSegStride + 8 * q);
+          hcolor_fc8<FC>(im, ps.row0 + y0 + r, p0 + 8 * q, v);
+        hput8<PAIRS>(v, seg + r * kHSegStride + 8 * q, PAIRS ? segrg + r * SP + 4 * q : nullptr,
+                     PAIRS ? segb + r * SP + 4 * q : nullptr);
       } else {
         const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0 + r) * ps.src_stride;
         hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * q, seg + r * kHSegStride + 4 * q);
@@ -1779,7 +1856,9 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
     __syncthreads();
     // phase 2: convolve (thread: column col, rows r0, r0 + 2, ...)
     if (valid) {
-      if (FUSED || C == 3)
+      if (PAIRS)
+        hconv_pairs<KMAX>(segrg, segb, SP, off, kw2, ksize, r0, nrows, prec, ob, col);
+      else if (FUSED || C == 3)
         hconv_rows<KMAX, 3>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
       else if (C == 1)
         hconv_rows<KMAX, 1>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
@@ -1810,26 +1889,31 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
 // Register budget for 5 waves per SIMD (<= 96 VGPRs; every variant fits
 // without scratch: 66-95 VGPRs).  A 4-wave budget measured slower
 // (resize_h1 2.81-2.90 vs 2.69-2.74 ms) and is no longer built.
-template <int KMAX, bool FUSED>
+template <int KMAX, bool FUSED, bool PAIRS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_resize_hb(
     const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list, int stage) {
-  __shared__ __attribute__((aligned(16))) uint32_t seg[kHBandRows * kHSegStride];
+  static_assert(!PAIRS || (FUSED && KMAX > 0), "the pair layout is for fused fills with register weights");
+  constexpr uint32_t SP = hseg_px(KMAX, PAIRS) / 2 + 4;
+  __shared__ __attribute__((aligned(16))) uint32_t seg[PAIRS ? 4 : kHBandRows * kHSegStride];
+  __shared__ __attribute__((aligned(16))) u32x2 segrg[PAIRS ? kHBandRows * SP : 2];
+  __shared__ __attribute__((aligned(16))) uint32_t segb[PAIRS ? kHBandRows * SP : 4];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kHBandRows * kHBandCols * 4];
   __shared__ uint32_t ext[2];
   const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
   const ImageDesc &im = imgs[it.image];
+  const ResizePass &ps = im.pass[stage];
   if (FUSED) {  // a fused fill reads the planes: specialised per layout (uniform per workgroup)
     switch (fill_class(im)) {
-      case FC_420: hband<KMAX, FUSED, FC_420>(im, im.pass[stage], it.item0, seg, ob, ext); return;
-      case FC_420_Z: hband<KMAX, FUSED, FC_420_Z>(im, im.pass[stage], it.item0, seg, ob, ext); return;
-      case FC_422: hband<KMAX, FUSED, FC_422>(im, im.pass[stage], it.item0, seg, ob, ext); return;
-      case FC_422_Z: hband<KMAX, FUSED, FC_422_Z>(im, im.pass[stage], it.item0, seg, ob, ext); return;
-      case FC_444: hband<KMAX, FUSED, FC_444>(im, im.pass[stage], it.item0, seg, ob, ext); return;
-      case FC_444_Z: hband<KMAX, FUSED, FC_444_Z>(im, im.pass[stage], it.item0, seg, ob, ext); return;
+      case FC_420: hband<KMAX, FUSED, FC_420, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
+      case FC_420_Z: hband<KMAX, FUSED, FC_420_Z, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
+      case FC_422: hband<KMAX, FUSED, FC_422, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
+      case FC_422_Z: hband<KMAX, FUSED, FC_422_Z, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
+      case FC_444: hband<KMAX, FUSED, FC_444, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
+      case FC_444_Z: hband<KMAX, FUSED, FC_444_Z, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
       default: break;
     }
   }
-  hband<KMAX, FUSED>(im, im.pass[stage], it.item0, seg, ob, ext);
+  hband<KMAX, FUSED, FC_GENERIC, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb);
 }
 
 // ---- band H pass on the matrix cores (k_resize_hm)
@@ -2419,22 +2503,25 @@ void launch_coeffs(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t
 void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
   DG_LAUNCH(k_resize_h, nwg, st, imgs, list, stage);
 }
-template <bool FUSED>
+template <bool FUSED, bool PAIRS>
 static void launch_hb_classes(hipStream_t st, const ImageDesc *imgs, const WgItem *&list, const uint32_t ncls[4],
                               int stage) {
-  DG_LAUNCH((k_resize_hb<8, FUSED>), ncls[0], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<8, FUSED, PAIRS>), ncls[0], st, imgs, list, stage);
   list += ncls[0];
-  DG_LAUNCH((k_resize_hb<16, FUSED>), ncls[1], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<16, FUSED, PAIRS>), ncls[1], st, imgs, list, stage);
   list += ncls[1];
-  DG_LAUNCH((k_resize_hb<32, FUSED>), ncls[2], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<32, FUSED>), ncls[2], st, imgs, list, stage);  // pairs: 35 KiB of LDS, 4 waves/SIMD
   list += ncls[2];
   DG_LAUNCH((k_resize_hb<0, FUSED>), ncls[3], st, imgs, list, stage);
   list += ncls[3];
 }
 void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][4],
-                      int stage) {
-  launch_hb_classes<true>(st, imgs, list, ncls[1], stage);
-  launch_hb_classes<false>(st, imgs, list, ncls[0], stage);
+                      int stage, bool pairs) {
+  if (pairs)
+    launch_hb_classes<true, true>(st, imgs, list, ncls[1], stage);
+  else
+    launch_hb_classes<true, false>(st, imgs, list, ncls[1], stage);
+  launch_hb_classes<false, false>(st, imgs, list, ncls[0], stage);
 }
 void launch_resize_hm(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][2],
                       int stage) {
