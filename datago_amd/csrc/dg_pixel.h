@@ -136,14 +136,17 @@ DG_HD uint8_t idct_stb_out(int32_t o) {
 // passes; no valid coefficient block comes near the limits).  Pass 2 of one
 // row of workspace values: 8 output samples.  Both decode semantics.
 DG_HD int32_t sat16(int32_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+// M24: the caller knows every input is below 2^20 in magnitude (sums of up
+// to four stay within 24 bits), so the products may use 24-bit multiplies.
+template <bool M24 = false>
 DG_HD void idct_col(bool zune, const int32_t v[8], int32_t ws[8]) {
   int32_t o[8];
   if (zune) {
-    idct_1d_stb(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
+    idct_1d_stb<M24>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
 #pragma unroll
     for (int r = 0; r < 8; r++) ws[r] = sat16(idct_stb_pass1(o[r]));
   } else {
-    idct_1d(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
+    idct_1d<M24>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
 #pragma unroll
     for (int r = 0; r < 8; r++) ws[r] = sat16(descale(o[r], kConstBits - kPass1Bits));
   }

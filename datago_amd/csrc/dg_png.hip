@@ -787,16 +787,56 @@ __device__ bool lane_build(const DG_GLOBAL uint8_t *lens, uint32_t n, LaneTab<B,
 
 struct LaneBits {
   uint64_t bb;
-  uint32_t nb, wp, zwords;
-  uint32_t w1;  // next word, loaded one refill ahead
+  uint32_t nb, wp, zwords;  // wp: index of the next stream word to shift into bb
+  uint32_t w1;              // Q = false: that word, loaded one refill ahead
+  u32x4 cur, nxt;           // Q = true: the aligned quad holding word wp, and the quad after it
 };
 
+// 16-byte aligned quad of stream words at word index i (i % 4 == 0); words
+// past the stream read as zero
+__device__ __forceinline__ u32x4 lb_quad(const DG_GLOBAL uint32_t *z, uint32_t zwords, uint32_t i) {
+  if (i + 4 <= zwords) return *(const DG_GLOBAL u32x4 *)(z + i);
+  u32x4 q = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++)
+    if (i + k < zwords) q[k] = z[i + k];
+  return q;
+}
+
+// Q: prefetch 4 to 8 words (16 to 32 symbols of a literal-heavy stream) ahead
+// in two aligned 16-byte quads instead of one word (about 4 symbols): the
+// per-lane decode is a dependent chain, and one word ahead left each refill
+// waiting out most of a global load's latency.
+template <bool Q>
+__device__ __forceinline__ void lb_seek(LaneBits &r, const DG_GLOBAL uint32_t *z, uint32_t wp) {
+  r.wp = wp;
+  if (Q) {
+    r.cur = lb_quad(z, r.zwords, wp & ~3u);
+    r.nxt = lb_quad(z, r.zwords, (wp & ~3u) + 4u);
+  } else {
+    r.w1 = wp < r.zwords ? z[wp] : 0u;
+  }
+}
+
+template <bool Q = false>
 __device__ __forceinline__ void lb_refill(LaneBits &r, const DG_GLOBAL uint32_t *z) {
   if (r.nb < 32) {
-    r.bb |= (uint64_t)r.w1 << r.nb;
-    r.nb += 32;
-    r.wp++;
-    r.w1 = r.wp < r.zwords ? z[r.wp] : 0u;
+    if (Q) {
+      const uint32_t k = r.wp & 3u;
+      const uint32_t w = k == 0 ? r.cur.x : k == 1 ? r.cur.y : k == 2 ? r.cur.z : r.cur.w;
+      r.bb |= (uint64_t)w << r.nb;
+      r.nb += 32;
+      r.wp++;
+      if ((r.wp & 3u) == 0) {
+        r.cur = r.nxt;
+        r.nxt = lb_quad(z, r.zwords, r.wp + 4u);
+      }
+    } else {
+      r.bb |= (uint64_t)r.w1 << r.nb;
+      r.nb += 32;
+      r.wp++;
+      r.w1 = r.wp < r.zwords ? z[r.wp] : 0u;
+    }
   }
 }
 __device__ __forceinline__ uint32_t lb_get(LaneBits &r, uint32_t k) {
@@ -847,7 +887,7 @@ constexpr uint32_t inf_lds_per_lane() {
 // lie before the chunk (resolved by k_inf_resolve). WG lanes per workgroup;
 // the lookups take WG * inf_lds_per_lane<LB, DB>() bytes of LDS (64 lanes,
 // 9/7 bits: 80 KiB, two workgroups per CU).
-template <uint32_t WG, uint32_t LB, uint32_t DB>
+template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false>
 __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
                                                    uint32_t nch) {
   constexpr uint32_t kInfLdsPerLane = inf_lds_per_lane<LB, DB>();
@@ -878,11 +918,10 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
   r.zwords = (pd.zlen + 3) / 4;
   {
     const uint32_t p = c.start;
-    r.wp = p >> 5;
     r.bb = 0;
     r.nb = 0;
-    r.w1 = r.wp < r.zwords ? z[r.wp] : 0u;
-    lb_refill(r, z);
+    lb_seek<Q>(r, z, p >> 5);
+    lb_refill<Q>(r, z);
     lb_get(r, p & 31u);
   }
   const uint32_t cap = c.cap;
@@ -902,7 +941,7 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
       status = 1;
       break;
     }
-    lb_refill(r, z);
+    lb_refill<Q>(r, z);
     const uint32_t last = lb_get(r, 1), type = lb_get(r, 2);
     if (type == 3) {
       status = 1;
@@ -910,7 +949,7 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
     }
     if (type == 0) {
       lb_get(r, r.nb & 7u);
-      lb_refill(r, z);
+      lb_refill<Q>(r, z);
       const uint32_t len = lb_get(r, 16), nlen = lb_get(r, 16);
       if ((len ^ 0xFFFFu) != nlen) {
         status = 1;
@@ -925,11 +964,10 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
       for (uint32_t j = 0; j < len; j++) out[q + j] = zb[bpos + j];
       q += len;
       const uint32_t np = (bpos + len) * 8u;
-      r.wp = np >> 5;
       r.bb = 0;
       r.nb = 0;
-      r.w1 = r.wp < r.zwords ? z[r.wp] : 0u;
-      lb_refill(r, z);
+      lb_seek<Q>(r, z, np >> 5);
+      lb_refill<Q>(r, z);
       lb_get(r, np & 31u);
       if (last) break;
       continue;
@@ -939,7 +977,7 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
       lane_build(lens, 288, tl);
       lane_build(lens + 288, 30, td);
     } else {
-      lb_refill(r, z);
+      lb_refill<Q>(r, z);
       const uint32_t nlen = lb_get(r, 5) + 257, ndist = lb_get(r, 5) + 1, ncode = lb_get(r, 4) + 4;
       if (nlen > 286 || ndist > 30) {
         status = 1;
@@ -947,7 +985,7 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
       }
       for (uint32_t s = 0; s < 19; s++) lens[s] = 0;
       for (uint32_t i = 0; i < ncode; i++) {
-        lb_refill(r, z);
+        lb_refill<Q>(r, z);
         lens[c_clorder[i]] = (uint8_t)lb_get(r, 3);
       }
       if (!lane_build(lens, 19, tc)) {
@@ -957,7 +995,7 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
       uint32_t i = 0, prev = 0;
       const uint32_t total = nlen + ndist;
       while (i < total && !status) {
-        lb_refill(r, z);
+        lb_refill<Q>(r, z);
         const uint32_t s = lane_sym(r, tc);
         uint32_t v = s, rep = 1;
         if (s < 16) {
@@ -990,7 +1028,7 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
     }
     // symbols of the block
     for (;;) {
-      lb_refill(r, z);
+      lb_refill<Q>(r, z);
       const uint32_t s = lane_sym(r, tl);
       if (s < 256) {
         if (q >= cap) {
@@ -1006,13 +1044,13 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
         break;
       }
       const uint32_t len = c_lbase[s - 257] + lb_get(r, c_lext[s - 257]);
-      lb_refill(r, z);
+      lb_refill<Q>(r, z);
       const uint32_t ds = lane_sym(r, td);
       if (ds >= 30) {
         status = 1;
         break;
       }
-      lb_refill(r, z);
+      lb_refill<Q>(r, z);
       const uint32_t dist = c_dbase[ds] + lb_get(r, c_dext[ds]);
       if (q + len > cap) {
         status = 2;
@@ -1532,21 +1570,23 @@ void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
 void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_inf_find, dim3(nwg), dim3(64), 0, st, imgs, ch, list);
 }
-template <uint32_t WG, uint32_t LB, uint32_t DB>
+template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false>
 static void launch_inf_decode_t(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch) {
   constexpr uint32_t lds = WG * inf_lds_per_lane<LB, DB>();
   static bool attr = false;  // > 64 KiB of dynamic LDS
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_inf_decode<WG, LB, DB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void *)k_inf_decode<WG, LB, DB, Q>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     attr = true;
   }
-  if (nch) hipLaunchKernelGGL((k_inf_decode<WG, LB, DB>), dim3((nch + WG - 1) / WG), dim3(WG), lds, st, imgs, ch, nch);
+  if (nch)
+    hipLaunchKernelGGL((k_inf_decode<WG, LB, DB, Q>), dim3((nch + WG - 1) / WG), dim3(WG), lds, st, imgs, ch, nch);
 }
 // variant: 64-lane workgroups with 0 = 9/7-bit lookups (80 KiB, 2 per CU);
 // 1 = 8/6 bits (40 KiB, 4 per CU); 2 = 7/6 bits (24 KiB, 6 per CU);
 // 3 = 7/5 bits (20 KiB, 8 per CU); 4 = 6/5 bits (12 KiB); 5 = 6/4 bits
-// (10 KiB). 32-lane workgroups measured no faster
+// (10 KiB); 6 / 7 = 2 / 1 with the stream prefetched two 16-byte quads
+// ahead (lb_refill<true>). 32-lane workgroups measured no faster
 // than 64-lane ones of the same LDS (profiles/r03/infdec)
 void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch, uint32_t variant) {
   switch (variant) {
@@ -1555,6 +1595,8 @@ void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint
     case 3: launch_inf_decode_t<64, 7, 5>(st, imgs, ch, nch); break;
     case 4: launch_inf_decode_t<64, 6, 5>(st, imgs, ch, nch); break;
     case 5: launch_inf_decode_t<64, 6, 4>(st, imgs, ch, nch); break;
+    case 6: launch_inf_decode_t<64, 7, 6, true>(st, imgs, ch, nch); break;   // 2 + quad prefetch
+    case 7: launch_inf_decode_t<64, 8, 6, true>(st, imgs, ch, nch); break;   // 1 + quad prefetch
     default: launch_inf_decode_t<64, 9, 7>(st, imgs, ch, nch); break;
   }
 }

@@ -498,6 +498,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     idct_fused_ = v != 0;
     return DG_OK;
   }
+  if (k == "idct_thread") {
+    idct_thread_ = v != 0;
+    return DG_OK;
+  }
   if (k == "h_pairs") {
     h_pairs_ = v != 0;
     return DG_OK;
@@ -551,8 +555,9 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     uf_units_ = (uint32_t)v;
     return DG_OK;
   }
-  if (k == "inf_decode") {  // k_inf_decode lookup bits (literal/length, distance): 0 9/7, 1 8/6, 2 7/6, 3 7/5, 4 6/5, 5 6/4
-    if (v < 0 || v > 5) return DG_ERR_INVALID;
+  if (k == "inf_decode") {  // k_inf_decode lookup bits (literal/length, distance): 0 9/7, 1 8/6, 2 7/6, 3 7/5, 4 6/5,
+                            // 5 6/4; 6, 7 = 2, 1 with the stream prefetched two quads ahead
+    if (v < 0 || v > 7) return DG_ERR_INVALID;
     inf_decode_ = (uint32_t)v;
     return DG_OK;
   }
@@ -2207,7 +2212,10 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (next()) return DG_ERR_DEVICE;  // coeffs (side stream)
   if (pside || dc_side) HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_prog, 0));  // progressive coefficients
   if (b.any_fused) launch_idct_list(sl.st, dd, qp, fl, std::min<uint32_t>(2048u, (b.idct_cap + 31) / 32));
-  launch_idct(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);
+  if (idct_thread_)
+    launch_idct_t(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);
+  else
+    launch_idct(sl.st, dd, lst(L_IDCT), cnt(L_IDCT), qp);
   if (next()) return DG_ERR_DEVICE;
   launch_color(sl.st, dd, lst(L_COLOR), cnt(L_COLOR));
   if (next()) return DG_ERR_DEVICE;

@@ -334,8 +334,10 @@ class Context {
   double host_cpu_us_[6] = {0, 0, 0, 0, 0, 0};  // the same phases' thread CPU time (stats "host_cpu_us_*")
   int copy_threads_ = 8;                // option "copy_threads": host threads for a host-out batch's output copies
   bool hv_fused_ = false;               // option "hv_fused": first H + V pass fused (k_resize_hv) when it fits
-  bool h_pairs_ = true;                 // option "h_pairs": fused band H kernels with the i16-pair LDS layout
-  bool destuff_one_ = true;             // option "destuff_one": single-pass destuff with decoupled look-back
+  bool idct_thread_ = true;             // option "idct_thread": one lane per block (k_idct_t) instead of 8 (k_idct)
+  bool h_pairs_ = false;                // option "h_pairs": fused band H kernels with the i16-pair LDS layout (measured neutral: off)
+  bool destuff_one_ = false;            // option "destuff_one": single-pass destuff with decoupled look-back
+                                        // (configs[1] 0.66 vs 0.43 ms three-pass: off)
   bool chroma_rec_ = true;              // option "chroma_rec": half-rate chroma planes as 8-byte records (dg_plane.h)
   bool band_dec_ = false;               // option "band_dec": IDCT + colour + first H pass in k_band_dec
   uint32_t uf_units_ = 2;               // option "uf_units": PNG unfilter units per lane per step (1 or 2)

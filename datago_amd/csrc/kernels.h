@@ -35,6 +35,7 @@ void launch_idct_list(hipStream_t st, const ImageDesc *imgs, const QuantTable *q
 void launch_huff_scatter(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                          const SubState *subs);
 // dequant + IDCT: 64 blocks of one block row per workgroup
+void launch_idct_t(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, const QuantTable *qpool);
 void launch_idct(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                  const QuantTable *qpool);
 // upsample + colour convert: 256 x 4-pixel quads per workgroup

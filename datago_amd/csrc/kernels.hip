@@ -260,8 +260,15 @@ __global__ __launch_bounds__(256) void k_destuff_write(const ImageDesc *__restri
 // workgroup that is running or done: each wait ends.  A wait that does not
 // end within ~1 s (a hardware or launch anomaly, never a property of the
 // data) marks the image DG_ERR_UNSUPPORTED instead of hanging.  Wave 0 runs
-// the look-back with every lane on the same addresses (no lane-divergent
-// branch around the polling loop, see uf_wait in dg_png.hip).
+// the look-back, 64 predecessors per round (one per lane), with wave-uniform
+// control flow around the polling loop (see uf_wait in dg_png.hip).  A first
+// version walked back one chunk per load (one L2 round trip each) and took
+// 9.9 ms per batch instead of 0.44.  The state words carry their values
+// with the flags, so they need atomicity and agent-scope coherence but no
+// ordering of other memory: relaxed atomics.  Release/acquire at agent
+// scope write back / invalidate the XCD's L2 on every publish and poll
+// (MI355X's L2s are per XCD), and took 6.6 ms per batch even with the
+// 64-wide look-back.
 constexpr uint64_t kDsAgg = 1ull << 62, kDsIncl = 1ull << 63;
 
 __global__ __launch_bounds__(256) void k_destuff_one(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
@@ -288,32 +295,48 @@ __global__ __launch_bounds__(256) void k_destuff_one(ImageDesc *__restrict__ img
   }
   const uint32_t total = sk[255], mtotal = sm[255];
   uint64_t *cs = state + 1 + im.ds_state0;  // this image's chunk words
-  if (t < 64) {  // wave 0, every lane on the same values
+  if (t < 64) {  // wave 0
     const uint64_t own = ((uint64_t)(mtotal & 0x3FFFFFFFu) << 32) | total;
     uint32_t ek = 0, em = 0, ok = 1;
     if (c == 0) {
-      __hip_atomic_store(cs, own | kDsIncl, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cs, own | kDsIncl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      __hip_atomic_store(cs + c, own | kDsAgg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cs + c, own | kDsAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // Look back 64 predecessors at a time, one per lane (lane l: chunk
+      // base - 1 - l): the nearest inclusive prefix ends the walk, every
+      // chunk between it and this one must have published its aggregate (a
+      // window with a gap before its first inclusive word is read again).
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      uint32_t j = c - 1;
+      const uint32_t lane = t;
+      uint32_t base = c;  // chunks [.., base) still to add
       for (;;) {
-        const uint64_t v = __hip_atomic_load(cs + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if (v & (kDsAgg | kDsIncl)) {
-          ek += (uint32_t)v;
-          em += (uint32_t)(v >> 32) & 0x3FFFFFFFu;
-          if ((v & kDsIncl) || j == 0) break;
-          j--;
+        const int32_t j = (int32_t)base - 1 - (int32_t)lane;
+        const uint64_t v = j >= 0 ? __hip_atomic_load(cs + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kDsIncl;
+        const uint64_t incl = __ballot((v & kDsIncl) != 0), none = __ballot((v & (kDsAgg | kDsIncl)) == 0);
+        const uint32_t stop = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;  // first lane with a prefix
+        const uint64_t before = stop >= 64 ? ~0ull : ((2ull << stop) - 1ull);  // lanes 0..stop
+        if ((none & before) == 0) {  // lanes 0..stop all published: take them
+          const bool take = lane <= stop && j >= 0;
+          uint32_t vk = take ? (uint32_t)v : 0u, vm = take ? (uint32_t)(v >> 32) & 0x3FFFFFFFu : 0u;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) {
+            vk += __shfl_xor(vk, o);
+            vm += __shfl_xor(vm, o);
+          }
+          ek += vk;
+          em += vm;
+          if (stop < 64) break;
+          base -= 64;  // all 64 were aggregates: the next window
           continue;
         }
         if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // ~1 s at 100 MHz
           ok = 0;
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
       }
       const uint64_t incl = ((uint64_t)((em + mtotal) & 0x3FFFFFFFu) << 32) | (uint64_t)(ek + total);
-      __hip_atomic_store(cs + c, incl | kDsIncl, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cs + c, incl | kDsIncl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (t == 0) {
       s_ek = ek;
@@ -919,6 +942,99 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
     store_crec_pair(rrow, bx, cbw, pv[h], l, r, in_l || bx == 0, in_r || bx + 1 == cbw);
   }
 }
+
+// Thread-per-block IDCT (option "idct_thread"): one wave = the 64
+// consecutive blocks of one block row of one component (the L_IDCT items of
+// k_idct), one lane per block.  A lane loads its block's 128 coefficient
+// bytes (eight 16-byte loads), dequantises them into 64 registers in natural
+// order (the zigzag permutation is a compile-time register renaming), runs
+// the 8 column and 8 row transforms in registers and stores its 8 pixel
+// rows; the 64 lanes' rows are 512 contiguous bytes of a plane row.  No LDS,
+// no barriers, about half k_idct's VALU work per block (k_idct spends 8 lanes
+// per block and three LDS round trips on the transposes).  Chroma records
+// take their neighbour blocks' edge samples from the adjacent lanes
+// (ds_bpermute); only lanes 0 and 63 hand their edges to the neighbouring
+// waves by the byte-store protocol of dg_plane.h.
+__global__ __launch_bounds__(64) void k_idct_t(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
+                                              const QuantTable *__restrict__ qpool) {
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  uint32_t item = it.item0, c = 0;
+  for (; c < im.ncomp; c++) {
+    const uint32_t ck = (im.cbw[c] + kIdctBlocks - 1) / kIdctBlocks;
+    const uint32_t n = im.cbh[c] * ck;
+    if (item < n) break;
+    item -= n;
+  }
+  const uint32_t ck = (im.cbw[c] + kIdctBlocks - 1) / kIdctBlocks;
+  const uint32_t by = item / ck, chunk = item - by * ck;
+  const uint32_t lane = threadIdx.x, cbw = im.cbw[c];
+  const uint32_t bx = chunk * kIdctBlocks + lane;
+  const bool v = bx < cbw;
+  // Decode semantics as a runtime flag: with it as a template constant the
+  // whole block's transforms become one straight-line region and the
+  // scheduler interleaves all eight columns (185 VGPRs, 2 waves per SIMD);
+  // the per-transform branch keeps it at 94.
+  const bool zune = im.sem != 0;
+  const uint32_t chc = im.ch[c];
+  uint32_t bidx;
+  if (im.ncomp == 1) {
+    bidx = by * cbw + bx;
+  } else {
+    const uint32_t my = by / im.cv[c], vy = by - my * im.cv[c];
+    const uint32_t mx = chc == 1 ? bx : chc == 2 ? bx >> 1 : bx / chc, hx = bx - mx * chc;
+    bidx = (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * chc + hx;
+  }
+  const DG_GLOBAL uint16_t *q = gp<const uint16_t>((uint64_t)(uintptr_t)qpool[im.qpool[c]].q);
+  int32_t x[64];
+  {
+    u32x4 w[8];
+    const DG_GLOBAL u32x4 *src = (const DG_GLOBAL u32x4 *)(gp<const int16_t>(im.coef) + (size_t)(v ? bidx : 0) * 64);
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = v ? src[i] : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 64; k++) {
+      const uint32_t word = w[k >> 3][(k >> 1) & 3];
+      const int32_t z = (int32_t)(int16_t)(k & 1 ? word >> 16 : word & 0xFFFFu);
+      const int nat = kZigzagToNatural[k];
+      x[nat] = __mul24(z, (int32_t)q[nat]);  // int16 x uint16: 24-bit operands, exact
+    }
+  }
+#pragma unroll
+  for (int col = 0; col < 8; col++) {
+    int32_t in[8], o[8];
+#pragma unroll
+    for (int r = 0; r < 8; r++) in[r] = x[r * 8 + col];
+    idct_col(zune, in, o);
+#pragma unroll
+    for (int r = 0; r < 8; r++) x[r * 8 + col] = o[r];
+  }
+  const bool rec = plane_is_rec(im, c);
+  const int32_t e = rec ? (int32_t)crec_lim(im, c) - 1 - (int32_t)(bx * 8) : 7;
+  DG_GLOBAL uint8_t *plane = gp<uint8_t>(im.plane[c]);
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    uint32_t px[8];
+    idct_row(zune, x + r * 8, px);
+    const uint32_t y = by * 8 + (uint32_t)r;
+    if (!rec) {
+      if (v)
+        *(DG_GLOBAL u32x2 *)(plane + (size_t)y * (cbw * 8) + bx * 8) =
+            u32x2{pack4(px[0], px[1], px[2], px[3]), pack4(px[4], px[5], px[6], px[7])};
+      continue;
+    }
+    uint32_t vv[8];
+    crec_clamp(e, px, vv);
+    // neighbours' edge columns from the adjacent lanes (every lane takes part)
+    const uint32_t l = (uint32_t)__shfl_up((int)vv[7], 1), rr = (uint32_t)__shfl_down((int)vv[0], 1);
+    if (v) {
+      const bool have_l = lane > 0 || bx == 0, have_r = (lane + 1 < 64u && bx + 1 < cbw) || bx + 1 == cbw;
+      store_crec_pair(crec_row(im, c, y), bx, cbw, vv, lane > 0 ? l : vv[0], bx + 1 < cbw ? rr : vv[7], have_l,
+                      have_r);
+    }
+  }
+}
+
 
 // Fused-IDCT leftovers (option "idct_fused"): the blocks k_huff_write could
 // not turn into pixels itself -- a block completed by a range that did not
@@ -2490,6 +2606,9 @@ void launch_idct_list(hipStream_t st, const ImageDesc *imgs, const QuantTable *q
 void launch_huff_scatter(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                          const SubState *subs) {
   DG_LAUNCH(k_huff_scatter, nwg, st, imgs, list, subs);
+}
+void launch_idct_t(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, const QuantTable *qpool) {
+  if (nwg) hipLaunchKernelGGL(k_idct_t, dim3(nwg), dim3(64), 0, st, imgs, list, qpool);
 }
 void launch_idct(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, const QuantTable *qpool) {
   DG_LAUNCH(k_idct, nwg, st, imgs, list, qpool);

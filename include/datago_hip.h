@@ -270,7 +270,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "png_chunked" 0 = inflate every PNG with the serial kernel (test switch; default 1)
  *   "uf_units"    1 or 2 (default 2): PNG unfilter filter units per lane per diagonal step (1: half the LDS)
  *   "inf_decode"  0..5: chunk-parallel inflate lookup bits (literal/length, distance) per lane in LDS:
- *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (default, 24 KiB), 3 7/5, 4 6/5, 5 6/4
+ *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (default, 24 KiB), 3 7/5, 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
+ *                 the compressed stream prefetched two 16-byte quads ahead per lane
  *   "copy_threads" host threads copying a host-out batch's outputs to the caller's buffers (default 8)
  *   "hv_fused"     1 = fuse the first H and V passes of colour JPEGs where they fit (default 0; slower)
  *   "h_mfma"       1 = band H passes on the matrix cores (k_resize_hm, i8 MFMA; default 0: measured slower); 0 = VALU kernel

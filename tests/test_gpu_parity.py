@@ -217,7 +217,7 @@ def test_band_and_slot_options_validated():
     L = _lib()
     ctx = L.Context(0)
     for k, v in (("hb_bands", 0), ("hb_bands", 65), ("slots", 0), ("slots", 7), ("inf_decode", -1),
-                 ("inf_decode", 6), ("uf_units", 0), ("uf_units", 3)):
+                 ("inf_decode", 8), ("uf_units", 0), ("uf_units", 3)):
         with pytest.raises(Exception):
             ctx.set_option(k, v)
 

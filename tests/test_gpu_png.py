@@ -196,7 +196,7 @@ def test_png_large_full_size_properties(ctx512):
     assert st == 0 and (arr.shape[1], arr.shape[0]) == t.target_size(1800, 1200)
 
 
-@pytest.mark.parametrize("inf_decode", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("inf_decode", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_chunked_inflate_matches_serial_and_oracle(inf_decode):
     """Large streams take the chunk-parallel inflate (block-header search,
     one lane per chunk, window markers); it must equal the oracle and the

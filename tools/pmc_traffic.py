@@ -42,8 +42,10 @@ def stage_sequence(rows):
             phase = "h2"
         elif name.startswith("k_resize_h"):
             st = "resize_h1" if phase in (None, "h1") else "resize_h2"
+        elif name.startswith("k_idct"):
+            st = "idct"  # k_idct, k_idct_t (one lane per block)
         else:
-            st = name[2:]  # idct, color, coeffs, copy
+            st = name[2:]  # color, coeffs, copy
         out.append((int(r["Dispatch_Id"]), st))
     return out
 
