@@ -47,6 +47,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_T = 256 * 4 * 2.4e9 / 2 / 1e12  # VALU wave-instructions/s: 256 CUs x 4 SIMDs, one per 2 cycles, 2.4 GHz
 
 
+# dg_submit* host phases (stats "host_us_<phase>"; the last is the wait for a free slot)
+HOST_PHASES = ("plan", "pools", "layout", "lists", "upload", "h2d", "launch", "slotwait")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -789,13 +793,13 @@ def main() -> int:
     ctx.set_option("timing", 0)
     # host planning phases of the timed steps only (read before the untimed legs add to them)
     host_phases = {q: round(ctx.stat("host_us_" + q) / 1e3 / a.steps, 3)
-                   for q in ("plan", "pools", "layout", "lists", "upload", "launch", "slotwait")}
+                   for q in HOST_PHASES}
     host_phases_cpu = {q: round(ctx.stat("host_cpu_us_" + q) / 1e3 / a.steps, 3)
-                       for q in ("plan", "pools", "layout", "lists", "upload", "launch")}
+                       for q in HOST_PHASES[:-1]}
     ph_all = sum_over_ranks([host_phases[q] if r == rank else 0.0 for r in range(world)
-                             for q in ("plan", "pools", "layout", "lists", "upload", "launch", "slotwait")] +
+                             for q in HOST_PHASES] +
                             [host_phases_cpu[q] if r == rank else 0.0 for r in range(world)
-                             for q in ("plan", "pools", "layout", "lists", "upload", "launch")], world)
+                             for q in HOST_PHASES[:-1]], world)
     # max over ranks; totals over ranks
     (dt_max,) = max_over_ranks([dt], world)
     per_rank_s = sum_over_ranks([dt if r == rank else 0.0 for r in range(world)], world)
@@ -1089,13 +1093,14 @@ def main() -> int:
             "host_submit_ms_per_step": round(1e3 * host_s["submit"] / a.steps, 3),  # Python + dg_submit_device planning
             "host_submit_ms_per_step_per_rank": [round(1e3 * h_ / a.steps, 3) for h_ in per_rank_host],
             "host_submit_phases_ms_per_step": host_phases,
+            "meta_bytes_per_batch": ctx.stat("meta_bytes"),
             # per rank: wall ms per step in each dg_submit_device phase, the thread's CPU ms in the same
             # phases (wall >> cpu = blocking: allocation, driver locks, copies), and the slot wait
             "host_submit_phases_per_rank": [
-                {"wall": {q: round(ph_all[r * 7 + j], 3) for j, q in
-                          enumerate(("plan", "pools", "layout", "lists", "upload", "launch", "slotwait"))},
-                 "cpu": {q: round(ph_all[7 * world + r * 6 + j], 3) for j, q in
-                         enumerate(("plan", "pools", "layout", "lists", "upload", "launch"))}}
+                {"wall": {q: round(ph_all[r * len(HOST_PHASES) + j], 3) for j, q in
+                          enumerate(HOST_PHASES)},
+                 "cpu": {q: round(ph_all[len(HOST_PHASES) * world + r * (len(HOST_PHASES) - 1) + j], 3) for j, q in
+                         enumerate(HOST_PHASES[:-1])}}
                 for r in range(world)],
             "rank_cpus": (f"{len(pinned)} CPUs per rank, disjoint contiguous shares of the job's affinity set"
                           if pinned else "unpinned"),

@@ -347,6 +347,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     sub_bits_ = (uint32_t)v;
     return DG_OK;
   }
+  if (k == "sub_auto") {
+    if (v < 1024 || v > 65536 || (v & (v - 1))) return DG_ERR_INVALID;
+    sub_auto_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "lead_bits") {
     if (v < -1 || v > (1 << 20)) return DG_ERR_INVALID;
     lead_bits_ = v;
@@ -502,8 +507,8 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     idct_thread_ = v != 0;
     return DG_OK;
   }
-  if (k == "h_pairs") {
-    h_pairs_ = v != 0;
+  if (k == "h_prefetch") {
+    h_prefetch_ = v != 0;
     return DG_OK;
   }
   if (k == "destuff_one") {
@@ -606,15 +611,17 @@ int64_t Context::get_stat(const std::string &k) {
         if (k == std::string("wg_") + kn[a] + "_" + sn[q]) return (int64_t)(wgstat_[a][q] * 1000.0);
   }
   if (k == "sub_bits") return last_sub_bits_;
+  if (k == "sub_auto") return sub_auto_;
+  if (k == "meta_bytes") return (int64_t)last_meta_bytes_;
   if (k == "png_serial_fallbacks") return stat_png_serial_;
   if (k == "band_dec_images") return stat_band_dec_;
   if (k == "direct_d2h") return stat_direct_d2h_;
   if (k == "png_chunks") return stat_png_chunks_;
   {  // host microseconds spent in dg_submit* since the last reset, per phase: wall and thread CPU
-    static const char *pn[7] = {"plan", "pools", "layout", "lists", "upload", "launch", "slotwait"};
-    for (int q = 0; q < 7; q++) {
+    static const char *pn[8] = {"plan", "pools", "layout", "lists", "upload", "h2d", "launch", "slotwait"};
+    for (int q = 0; q < 8; q++) {
       if (k == std::string("host_us_") + pn[q]) return (int64_t)host_us_[q];
-      if (q < 6 && k == std::string("host_cpu_us_") + pn[q]) return (int64_t)host_cpu_us_[q];
+      if (q < 7 && k == std::string("host_cpu_us_") + pn[q]) return (int64_t)host_cpu_us_[q];
     }
   }
   if (k == "hpool") return (int64_t)hpool_.size();
@@ -663,6 +670,20 @@ void Context::free_retired() {
   retired_dev_bytes_ = retired_pin_bytes_ = 0;
 }
 
+size_t Context::grow_cap(size_t bytes, bool headroom) {
+  return align_up(std::max(bytes, (size_t)1 << 20) + (headroom ? bytes / 2 : 0), 1 << 20);
+}
+
+// An allocation failed: free the retired buffers (after a sync of every
+// stream; the failed call is about to fail the submit anyway) so the retry
+// sees them.  True = worth retrying.
+bool Context::reclaim() {
+  (void)hipGetLastError();
+  if (sync_all() != DG_OK) return false;
+  free_retired();
+  return true;
+}
+
 // mu_ held.  hipFree synchronises the device, so only when nothing is in flight.
 void Context::free_retired_if_idle() {
   if (retired_dev_.empty() && retired_pinned_.empty()) return;
@@ -674,13 +695,23 @@ void Context::free_retired_if_idle() {
 dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
   (void)user;
   if (b.cap >= bytes) return DG_OK;
+  const bool regrow = b.p != nullptr;
   if (b.p) {
     retire(b.p, b.cap, false);
     b.p = nullptr;
     b.cap = 0;
   }
-  size_t cap = align_up(std::max(bytes, (size_t)1 << 20) + bytes / 4, 1 << 20);
+  // 50% headroom on re-growth: an allocation blocks on the driver (8 ranks
+  // sharing one GPU measured 36-209 ms of wall time per step in the layout
+  // phase against 0.3 ms of CPU while batches kept setting new size maxima,
+  // profiles/r04/ranks), so growth must stay rare.  Under memory pressure the
+  // retired buffers go first, then the headroom.
+  size_t cap = grow_cap(bytes, regrow);
   hipError_t e = hipMalloc(&b.p, cap);
+  if (e != hipSuccess && reclaim()) {
+    cap = grow_cap(bytes, false);
+    e = hipMalloc(&b.p, cap);
+  }
   if (e != hipSuccess) {
     set_error("device allocation failed");
     b.p = nullptr;
@@ -693,13 +724,19 @@ dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
 dg_status Context::ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user) {
   (void)user;
   if (b.cap >= bytes) return DG_OK;
+  const bool regrow = b.p != nullptr;
   if (b.p) {
     retire(b.p, b.cap, true);
     b.p = nullptr;
     b.cap = 0;
   }
-  size_t cap = align_up(std::max(bytes, (size_t)1 << 20) + bytes / 4, 1 << 20);
-  if (hipHostMalloc(&b.p, cap, hipHostMallocDefault) != hipSuccess) {
+  size_t cap = grow_cap(bytes, regrow);
+  hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
+  if (e != hipSuccess && reclaim()) {
+    cap = grow_cap(bytes, false);
+    e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
+  }
+  if (e != hipSuccess) {
     set_error("pinned host allocation failed");
     b.p = nullptr;
     return DG_ERR_OOM;
@@ -938,7 +975,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     if (st) return st;
   }
   // context lock + the slot's previous batch (stat "host_us_slotwait")
-  host_us_[6] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - wait_t0).count();
+  host_us_[7] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - wait_t0).count();
   std::unique_ptr<Batch> bp(new Batch());
   Batch &b = *bp;
   b.ticket = next_ticket_++;
@@ -1050,14 +1087,17 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   // Subsequence size: the entropy kernels are latency-bound, so they want as
   // many lanes as the chip can keep resident, but every subsequence costs a
   // sync re-decode.  Measured on MI355X (profiles/r01/sweep_v4): 2048 bits is
-  // best up to ~64 MiB of coded data per batch, 4096 above.
+  // best up to ~64 MiB of coded data per batch; above, option "sub_auto"
+  // (round 4: 8192, profiles/r04/ab -- the chip stays full with half the
+  // lanes once the write pass no longer decodes, and the 6 kbit lead-in of a
+  // 4:2:0 range costs 75% instead of 150% of its bits).
   uint32_t sub_bits = sub_bits_;
   if (!sub_bits) {
     uint64_t coded = 0;
     for (int i = 0; i < n; i++)
       if (!b.plans[i].status && b.plans[i].fmt == kFmtJpeg && !b.plans[i].hdr.progressive)
         coded += b.plans[i].hdr.scan_end - b.plans[i].hdr.scan_off;
-    sub_bits = coded >= (64ull << 20) ? 4096 : 2048;
+    sub_bits = coded >= (64ull << 20) ? sub_auto_ : 2048;
   }
   last_sub_bits_ = sub_bits;
   Layout L;        // scratch arena
@@ -1710,7 +1750,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     uint32_t items = 0;
     for (uint32_t c = 0; c < d.ncomp; c++) items += d.cbh[c] * ((d.cbw[c] + 63) / 64);  // kIdctBlocks
     if (!d.idct_fused && !(d.pass[0].mode & kHDecode))  // fused: k_huff_write (+ k_idct_list) / k_band_dec
-      for (uint32_t it = 0; it < items; it++) b.lists[L_IDCT].push_back({I, it});
+      for (uint32_t it = 0; it < items; it += idct_thread_ ? kIdctItemStride : 1u) b.lists[L_IDCT].push_back({I, it});
     if (d.ncomp == 3 && !d.color_fused) {
       uint32_t q = (d.width + 7) / 8 * d.height;
       for (uint32_t it = 0; it < q; it += 256) b.lists[L_COLOR].push_back({I, it});
@@ -1745,11 +1785,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         // k_resize_hb<K> reads taps in even-aligned pairs: a window starting
         // at an odd segment position spans ksize + 1 positions
         const uint32_t kk = ps.ksize + 1;
-        int cls = kk <= 8 ? 0 : kk <= 16 ? 1 : kk <= 32 ? 2 : 3;
+        const int cls = kk <= 8 ? 0 : kk <= 16 ? 1 : kk <= 32 ? 2 : 3;
         const int fused = (ps.mode & kHFused) ? 1 : 0;
-        // the pair layout's 8- and 16-tap kernels hold narrower segments (hseg_px in kernels.hip)
-        if (fused && h_pairs_)
-          while (cls < 2 && h_pass_span(ps) > (cls == 0 ? 192.0 : 384.0)) cls++;
         const uint32_t ks = h_mfma_ ? h_mfma_steps(ps) : 0u;
         if (ks)
           for (uint32_t it = 0; it < cnt; it++) hm[s / 2][fused][ks - 1].push_back({I, it});
@@ -1757,7 +1794,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
           for (uint32_t it = 0; it < cnt; it++) hb[s / 2][fused][cls].push_back({I, it});
       } else {
         uint32_t cnt = (ps.width * ps.C + 15) / 16 * ps.rows;
-        for (uint32_t it = 0; it < cnt; it += 256) b.lists[L_RH0 + s].push_back({I, it});
+        for (uint32_t it = 0; it < cnt; it += 256 * kVItemUnits) b.lists[L_RH0 + s].push_back({I, it});
       }
     }
     if (d.copy_needed) {
@@ -1906,6 +1943,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       if (b.desc_of[i] >= 0) ins.push_back({P + b.meta_bytes + in_off[i], h_srcs[i], lens[i]});
     parallel_copy(ins, copy_threads_);
   }
+  last_meta_bytes_ = b.meta_bytes;
+  phase(4);
   if (timing_) HIPCHK(hipEventRecord(sl.ev[0], sl.st));
   HIPCHK(hipMemcpyAsync(sl.meta.p, P, b.meta_bytes, hipMemcpyHostToDevice, sl.st));
   if (host_io && IN.off) HIPCHK(hipMemcpyAsync(sl.input.p, P + b.meta_bytes, IN.off, hipMemcpyHostToDevice, sl.st));
@@ -1922,10 +1961,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         b.out_direct[i] = 1;
   }
   sl.batch = std::move(bp);
-  phase(4);
+  phase(5);
   st = launch_all(sl, false);
   if (st) return st;
-  phase(5);
+  phase(6);
   stat_batches_++;
   *ticket = sl.batch->ticket;
   return DG_OK;
@@ -2223,7 +2262,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
   launch_band_dec(sl.st, dd, lst(L_DEC), b.decclass, qp, dec_strips_ | (dec_dbg_ << 16));
   launch_resize_hm(sl.st, dd, lst(L_RM0), b.hmclass[0], 0);
-  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0, h_pairs_);
+  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0, h_prefetch_);
   launch_resize_hv(sl.st, dd, lst(L_RHV), b.hvclass);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
@@ -2231,7 +2270,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_hm(sl.st, dd, lst(L_RM2), b.hmclass[1], 2);
-  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2, h_pairs_);
+  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2, h_prefetch_);
   launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3);

@@ -214,6 +214,8 @@ class Context {
   dg_status ensure(DevBuf &b, size_t bytes, hipStream_t user = nullptr);
   void retire(void *p, size_t bytes, bool pinned);
   void free_retired();
+  static size_t grow_cap(size_t bytes, bool headroom);
+  bool reclaim();
   void free_retired_if_idle();
   std::vector<void *> retired_dev_, retired_pinned_;  // grown-out buffers, freed later (ensure)
   size_t retired_dev_bytes_ = 0, retired_pin_bytes_ = 0;
@@ -320,6 +322,7 @@ class Context {
   uint64_t next_ticket_ = 1;
 
   uint32_t sub_bits_ = 0;  // 0 = auto per batch (see submit)
+  uint32_t sub_auto_ = 8192;  // the auto size of large batches
   int64_t lead_bits_ = -1;  // -1 = auto per image (see submit)
   uint32_t last_sub_bits_ = kDefaultSubBits;
   bool timing_ = false;
@@ -330,12 +333,13 @@ class Context {
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
   int decode_sem_ = 0;                  // option "decode_semantics"
   bool ckpt_ = true;                    // option "ckpt"
-  double host_us_[7] = {0, 0, 0, 0, 0, 0, 0};  // submit phases + slot wait (stats "host_us_*"; option "reset_host_us")
-  double host_cpu_us_[6] = {0, 0, 0, 0, 0, 0};  // the same phases' thread CPU time (stats "host_cpu_us_*")
+  double host_us_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // submit phases + slot wait (stats "host_us_*"; option "reset_host_us")
+  double host_cpu_us_[7] = {0, 0, 0, 0, 0, 0, 0};
+  size_t last_meta_bytes_ = 0;  // stat "meta_bytes": the last batch's descriptor/list upload  // the same phases' thread CPU time (stats "host_cpu_us_*")
   int copy_threads_ = 8;                // option "copy_threads": host threads for a host-out batch's output copies
   bool hv_fused_ = false;               // option "hv_fused": first H + V pass fused (k_resize_hv) when it fits
   bool idct_thread_ = true;             // option "idct_thread": one lane per block (k_idct_t) instead of 8 (k_idct)
-  bool h_pairs_ = false;                // option "h_pairs": fused band H kernels with the i16-pair LDS layout (measured neutral: off)
+  bool h_prefetch_ = true;              // option "h_prefetch": specialised fused fills load the next band before the convolution
   bool destuff_one_ = false;            // option "destuff_one": single-pass destuff with decoupled look-back
                                         // (configs[1] 0.66 vs 0.43 ms three-pass: off)
   bool chroma_rec_ = true;              // option "chroma_rec": half-rate chroma planes as 8-byte records (dg_plane.h)

@@ -955,17 +955,29 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
 // take their neighbour blocks' edge samples from the adjacent lanes
 // (ds_bpermute); only lanes 0 and 63 hand their edges to the neighbouring
 // waves by the byte-store protocol of dg_plane.h.
+// A workgroup (one wave) takes kIdctItemStride consecutive L_IDCT items in
+// turn (the host lists every kIdctItemStride-th item: a quarter of the list
+// k_idct needs).  Four waves per workgroup instead measured no better and
+// cost 15 VGPRs (109: 4 waves per SIMD).
+__device__ __forceinline__ void idct_t_item(const ImageDesc &im, uint32_t item, const QuantTable *__restrict__ qpool);
+
 __global__ __launch_bounds__(64) void k_idct_t(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
                                               const QuantTable *__restrict__ qpool) {
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
-  uint32_t item = it.item0, c = 0;
+#pragma nounroll
+  for (uint32_t k = 0; k < kIdctItemStride; k++) idct_t_item(im, it.item0 + k, qpool);
+}
+
+__device__ __forceinline__ void idct_t_item(const ImageDesc &im, uint32_t item0, const QuantTable *__restrict__ qpool) {
+  uint32_t item = item0, c = 0;
   for (; c < im.ncomp; c++) {
     const uint32_t ck = (im.cbw[c] + kIdctBlocks - 1) / kIdctBlocks;
     const uint32_t n = im.cbh[c] * ck;
     if (item < n) break;
     item -= n;
   }
+  if (c >= im.ncomp) return;  // past the image's last item (wave-uniform)
   const uint32_t ck = (im.cbw[c] + kIdctBlocks - 1) / kIdctBlocks;
   const uint32_t by = item / ck, chunk = item - by * ck;
   const uint32_t lane = threadIdx.x, cbw = im.cbw[c];
@@ -1618,41 +1630,79 @@ __device__ __forceinline__ int fill_class(const ImageDesc &im) {
   return FC_GENERIC;
 }
 
+// The raw plane words one octet of a specialised fill reads: luma, and the
+// chroma (records, or plain samples for 4:4:4) of the near (0) and far (1)
+// chroma rows.  Loading them is split from the arithmetic (hcolor_fc8) so
+// the band kernel can issue the next band's loads before the convolution.
+struct FillRaw {
+  u32x2 y, b0, r0, b1, r1;
+};
+
 template <int FC>
-__device__ __forceinline__ void hcolor_fc8(const ImageDesc &im, uint32_t y, uint32_t x0, uint32_t v[8]) {
+__device__ __forceinline__ FillRaw hload_fc8(const ImageDesc &im, uint32_t y, uint32_t x0) {
   constexpr bool Z = FC == FC_420_Z || FC == FC_422_Z || FC == FC_444_Z;
   constexpr int SS = (FC == FC_420 || FC == FC_420_Z) ? 2 : (FC == FC_422 || FC == FC_422_Z) ? 1 : 0;
   const DG_GLOBAL uint8_t *pY = gp<const uint8_t>(im.plane[0]);
   const DG_GLOBAL uint8_t *pB = gp<const uint8_t>(im.plane[1]);
   const DG_GLOBAL uint8_t *pR = gp<const uint8_t>(im.plane[2]);
-  const uint32_t sY = im.cbw[0] * 8;
+  const uint32_t sY = im.cbw[0] * 8, sC = im.cbw[1] * 8;
+  FillRaw f;
+  f.y = *(const DG_GLOBAL u32x2 *)(pY + (size_t)__umul24(y, sY) + x0);
+  if (SS == 0) {
+    f.b0 = *(const DG_GLOBAL u32x2 *)(pB + (size_t)__umul24(y, sC) + x0);
+    f.r0 = *(const DG_GLOBAL u32x2 *)(pR + (size_t)__umul24(y, sC) + x0);
+    f.b1 = f.r1 = u32x2{0, 0};
+  } else {
+    const uint32_t c0 = x0 >> 1;
+    uint32_t rr = y, rn = y;
+    if (SS == 2) {
+      rr = y >> 1;
+      const uint32_t last = Z ? im.cbh[1] * 8 - 1 : im.cdsh[1] - 1;
+      rn = (y & 1) ? (rr + 1 <= last ? rr + 1 : last) : (rr > 0 ? rr - 1 : 0);
+    }
+    f.b0 = *(const DG_GLOBAL u32x2 *)(pB + (size_t)__umul24(rr, 2 * sC) + 2 * c0);
+    f.r0 = *(const DG_GLOBAL u32x2 *)(pR + (size_t)__umul24(rr, 2 * sC) + 2 * c0);
+    if (SS == 2) {
+      f.b1 = *(const DG_GLOBAL u32x2 *)(pB + (size_t)__umul24(rn, 2 * sC) + 2 * c0);
+      f.r1 = *(const DG_GLOBAL u32x2 *)(pR + (size_t)__umul24(rn, 2 * sC) + 2 * c0);
+    } else {
+      f.b1 = f.r1 = u32x2{0, 0};
+    }
+  }
+  return f;
+}
+
+template <int FC>
+__device__ __forceinline__ void hcolor_fc8(const ImageDesc &im, const FillRaw &f, uint32_t x0, uint32_t v[8]) {
+  constexpr bool Z = FC == FC_420_Z || FC == FC_422_Z || FC == FC_444_Z;
+  constexpr int SS = (FC == FC_420 || FC == FC_420_Z) ? 2 : (FC == FC_422 || FC == FC_422_Z) ? 1 : 0;
   int32_t Yv[8], Cb[8], Cr[8];
-  auto unpack8 = [](u32x2 v, int32_t o[8]) {
+  auto unpack8 = [](u32x2 w, int32_t o[8]) {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      o[k] = (v.x >> (8 * k)) & 0xFF;
-      o[k + 4] = (v.y >> (8 * k)) & 0xFF;
+      o[k] = (w.x >> (8 * k)) & 0xFF;
+      o[k + 4] = (w.y >> (8 * k)) & 0xFF;
     }
   };
-  unpack8(*(const DG_GLOBAL u32x2 *)(pY + (size_t)__umul24(y, sY) + x0), Yv);
+  auto rec6 = [](u32x2 w, int32_t cs[6]) {  // load_crec6's unpacking (dg_plane.h)
+    cs[0] = (int32_t)(w.y & 0xFF);
+#pragma unroll
+    for (int k = 0; k < 4; k++) cs[k + 1] = (int32_t)((w.x >> (8 * k)) & 0xFF);
+    cs[5] = (int32_t)((w.y >> 8) & 0xFF);
+  };
+  unpack8(f.y, Yv);
   if (SS == 0) {
-    const uint32_t sC = im.cbw[1] * 8;
-    unpack8(*(const DG_GLOBAL u32x2 *)(pB + (size_t)__umul24(y, sC) + x0), Cb);
-    unpack8(*(const DG_GLOBAL u32x2 *)(pR + (size_t)__umul24(y, sC) + x0), Cr);
+    unpack8(f.b0, Cb);
+    unpack8(f.r0, Cr);
   } else {
     const uint32_t sC = im.cbw[1] * 8, c0 = x0 >> 1;
     int32_t b[6], r[6];
-    if (SS == 1) {
-      load_crec6(pB, sC, y, c0, b);
-      load_crec6(pR, sC, y, c0, r);
-    } else {
-      const uint32_t rr = y >> 1, last = Z ? im.cbh[1] * 8 - 1 : im.cdsh[1] - 1;
-      const uint32_t rn = (y & 1) ? (rr + 1 <= last ? rr + 1 : last) : (rr > 0 ? rr - 1 : 0);
+    rec6(f.b0, b);
+    rec6(f.r0, r);
+    if (SS == 2) {
       int32_t b1[6], r1[6];
-      load_crec6(pB, sC, rr, c0, b);
-      load_crec6(pR, sC, rr, c0, r);
-      load_crec6(pB, sC, rn, c0, b1);
-      load_crec6(pR, sC, rn, c0, r1);
+      rec6(f.b1, b1);
+      rec6(f.r1, r1);
 #pragma unroll
       for (int k = 0; k < 6; k++) {
         b[k] = Z ? (3 * b[k] + 2 + b1[k]) >> 2 : 3 * b[k] + b1[k];
@@ -1698,31 +1748,14 @@ __device__ __forceinline__ void hcolor_fc8(const ImageDesc &im, uint32_t y, uint
   }
 }
 
-// 8 fused-fill pixels (RGB in bytes 0..2 of v[k]) of segment pixels 8q..8q+7
-// into the band's LDS: one dword per pixel (seg), or, with the pair layout
-// (PAIRS), per pixel pair (2k, 2k+1) the R and G pairs as i16 x 2 in one
-// 8-byte word (segrg) and the B pair in one dword (segb), the operands
-// v_dot2_i32_i16 takes as they are: no byte selects in the convolution.
-template <bool PAIRS>
-__device__ __forceinline__ void hput8(const uint32_t v[8], uint32_t *seg, u32x2 *segrg, uint32_t *segb) {
-  if (!PAIRS) {
-    u32x4 *d4 = (u32x4 *)seg;
-    d4[0] = u32x4{v[0], v[1], v[2], v[3]};
-    d4[1] = u32x4{v[4], v[5], v[6], v[7]};
-    return;
-  }
-  uint32_t rg[8], bq[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const uint32_t a = v[2 * k], b = v[2 * k + 1];
-    rg[2 * k] = __builtin_amdgcn_perm(b, a, 0x0c040c00u);      // [a.R, 0, b.R, 0]
-    rg[2 * k + 1] = __builtin_amdgcn_perm(b, a, 0x0c050c01u);  // [a.G, 0, b.G, 0]
-    bq[k] = __builtin_amdgcn_perm(b, a, 0x0c060c02u);          // [a.B, 0, b.B, 0]
-  }
-  u32x4 *r4 = (u32x4 *)segrg;
-  r4[0] = u32x4{rg[0], rg[1], rg[2], rg[3]};
-  r4[1] = u32x4{rg[4], rg[5], rg[6], rg[7]};
-  *(u32x4 *)segb = u32x4{bq[0], bq[1], bq[2], bq[3]};
+// 8 fused-fill pixels (RGB in bytes 0..2 of v[k]) into the band's LDS
+// segment, one dword per pixel.  (A layout of i16 pixel pairs per channel,
+// the dot2 operands as they are, measured neutral in round 4 and was
+// dropped: the convolution is not issue-bound.)
+__device__ __forceinline__ void hput8(const uint32_t v[8], uint32_t *seg) {
+  u32x4 *d4 = (u32x4 *)seg;
+  d4[0] = u32x4{v[0], v[1], v[2], v[3]};
+  d4[1] = u32x4{v[4], v[5], v[6], v[7]};
 }
 
 // 4 source pixels at p (p % 4 == 0) of an interleaved C-byte row of `in_size`
@@ -1831,61 +1864,14 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
     }
 }
 
-// The convolution of hconv_rows for C = 3 over the pair layout (hput8): per
-// tap pair and row one 8-byte and one 4-byte LDS read give the R, G and B
-// operands of the three v_dot2_i32_i16 as they are.
-template <int KMAX>
-__device__ __forceinline__ void hconv_pairs(const u32x2 *segrg, const uint32_t *segb, uint32_t sp, uint32_t off,
-                                            const uint32_t *kw2, uint32_t ksize, uint32_t r0, uint32_t nrows,
-                                            int32_t prec, uint8_t *ob, uint32_t col) {
-  constexpr uint32_t R = kHBandRows / 2;
-  const int32_t bias = 1 << (prec - 1);
-  int32_t a[R][3];
-#pragma unroll
-  for (uint32_t r = 0; r < R; r++) a[r][0] = a[r][1] = a[r][2] = bias;
-  const uint32_t pe0 = off >> 1;
-#pragma unroll
-  for (int j = 0; j < (KMAX + 1) / 2; j++) {
-    if ((uint32_t)(2 * j) >= ksize + 1) break;
-    const s16x2 w = __builtin_bit_cast(s16x2, kw2[j]);
-#pragma unroll
-    for (uint32_t r = 0; r < R; r++) {
-      const uint32_t i = (r0 + 2 * r) * sp + pe0 + j;
-      const u32x2 rg = *(const u32x2 *)((const uint32_t *)segrg + 2 * i);
-      const uint32_t bq = segb[i];
-      const uint32_t rv = rg.x, gv = rg.y;
-      a[r][0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, rv), w, a[r][0], false);
-      a[r][1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, gv), w, a[r][1], false);
-      a[r][2] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, bq), w, a[r][2], false);
-    }
-  }
-#pragma unroll
-  for (uint32_t r = 0; r < R; r++)
-    if (r0 + 2 * r < nrows) {
-      uint8_t *o = ob + (r0 + 2 * r) * (kHBandCols * 4) + col * 3;
-#pragma unroll
-      for (int c = 0; c < 3; c++) o[c] = clip_shift(a[r][c], prec);
-    }
-}
-
-// LDS source segment (pixels per row) of a band H kernel.  The pair layout
-// (6 bytes per pixel) is sized per weight class: a window of <= 8 taps means
-// a downscale of at most 1x, <= 16 taps at most 7/3 x, so 128 output columns
-// read at most ~160 / ~344 source pixels (h_pass_span); the byte layout and
-// the wider classes keep kHSegPx.
-constexpr uint32_t hseg_px(int kmax, bool pairs) {
-  return !pairs ? kHSegPx : kmax == 8 ? 192u : kmax == 16 ? 384u : kHSegPx;
-}
-
 // FUSED: the first pass of a colour JPEG (fill = upsample + colour
 // conversion from the planes, C = 3); otherwise the fill copies interleaved
 // bytes of C = 1..4 channels.  Separate kernels so each allocates registers
 // for its own path only.
-template <int KMAX, bool FUSED, int FC = FC_GENERIC, bool PAIRS = false>
+template <int KMAX, bool FUSED, int FC = FC_GENERIC, bool PF = false>
 __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps, uint32_t item, uint32_t *seg,
-                                      uint8_t *ob, uint32_t *ext, u32x2 *segrg = nullptr, uint32_t *segb = nullptr) {
-  constexpr uint32_t SEGPX = hseg_px(KMAX, PAIRS);
-  constexpr uint32_t SP = SEGPX / 2 + 4;  // pair layout: pairs per row (even: 16-byte aligned octets)
+                                      uint8_t *ob, uint32_t *ext) {
+  constexpr uint32_t SEGPX = kHSegPx;
   // one workgroup: a tile of kHBandCols output columns x ps.bands bands of
   // kHBandRows rows; the column tile's weights, source extent and descriptor
   // reads are set up once and reused for every band
@@ -1948,6 +1934,16 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
   const int32_t prec = ps.precision;
   const uint32_t rb = (x1 - x0) * C;  // <= kHBandCols * 4 = 512 bytes: 32 chunks of 16
   const uint32_t ybeg = group * kHBandRows * ps.bands;
+  // specialised fused fills prefetch (option "h_prefetch", ImageDesc... pass mode kHPrefetch)
+  constexpr bool PREFETCH = FUSED && FC != FC_GENERIC && PF;
+  FillRaw pre;
+  if (PREFETCH && ybeg < ps.rows) {  // band 0's first job
+    const uint32_t nr0 = ps.rows - ybeg < kHBandRows ? ps.rows - ybeg : kHBandRows;
+    if (t < nr0 * njob_row) {
+      const uint32_t r = __umul24(t, inv_row) >> 20, q = t - r * njob_row;
+      pre = hload_fc8<FC>(im, ps.row0 + ybeg + r, p0 + 8 * q);
+    }
+  }
   for (uint32_t bi = 0; bi < ps.bands; bi++) {
     const uint32_t y0 = ybeg + bi * kHBandRows;
     if (y0 >= ps.rows) break;
@@ -1958,23 +1954,34 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
       const uint32_t r = __umul24(j, inv_row) >> 20, q = j - r * njob_row;
       if (FUSED) {
         uint32_t v[8];
-        if (FC == FC_GENERIC)
+        if (FC == FC_GENERIC) {
           hcolor8(im, ps.row0 + y0 + r, p0 + 8 * q, v);
-        else
-          hcolor_fc8<FC>(im, ps.row0 + y0 + r, p0 + 8 * q, v);
-        hput8<PAIRS>(v, seg + r * kHSegStride + 8 * q, PAIRS ? segrg + r * SP + 4 * q : nullptr,
-                     PAIRS ? segb + r * SP + 4 * q : nullptr);
+        } else {
+          // a thread's first job of the band was loaded before the previous
+          // band's convolution (pre); later ones load here
+          const FillRaw f = (PREFETCH && j == t) ? pre : hload_fc8<FC>(im, ps.row0 + y0 + r, p0 + 8 * q);
+          hcolor_fc8<FC>(im, f, p0 + 8 * q, v);
+        }
+        hput8(v, seg + r * kHSegStride + 8 * q);
       } else {
         const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0 + r) * ps.src_stride;
         hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * q, seg + r * kHSegStride + 4 * q);
       }
     }
     __syncthreads();
+    if (PREFETCH) {  // the next band's first fill job: its loads overlap this band's convolution
+      const uint32_t y1 = y0 + kHBandRows;
+      if (bi + 1 < ps.bands && y1 < ps.rows) {
+        const uint32_t nr1 = ps.rows - y1 < kHBandRows ? ps.rows - y1 : kHBandRows;
+        if (t < nr1 * njob_row) {
+          const uint32_t r = __umul24(t, inv_row) >> 20, q = t - r * njob_row;
+          pre = hload_fc8<FC>(im, ps.row0 + y1 + r, p0 + 8 * q);
+        }
+      }
+    }
     // phase 2: convolve (thread: column col, rows r0, r0 + 2, ...)
     if (valid) {
-      if (PAIRS)
-        hconv_pairs<KMAX>(segrg, segb, SP, off, kw2, ksize, r0, nrows, prec, ob, col);
-      else if (FUSED || C == 3)
+      if (FUSED || C == 3)
         hconv_rows<KMAX, 3>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
       else if (C == 1)
         hconv_rows<KMAX, 1>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
@@ -2005,14 +2012,10 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
 // Register budget for 5 waves per SIMD (<= 96 VGPRs; every variant fits
 // without scratch: 66-95 VGPRs).  A 4-wave budget measured slower
 // (resize_h1 2.81-2.90 vs 2.69-2.74 ms) and is no longer built.
-template <int KMAX, bool FUSED, bool PAIRS = false>
+template <int KMAX, bool FUSED, bool PF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_resize_hb(
     const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list, int stage) {
-  static_assert(!PAIRS || (FUSED && KMAX > 0), "the pair layout is for fused fills with register weights");
-  constexpr uint32_t SP = hseg_px(KMAX, PAIRS) / 2 + 4;
-  __shared__ __attribute__((aligned(16))) uint32_t seg[PAIRS ? 4 : kHBandRows * kHSegStride];
-  __shared__ __attribute__((aligned(16))) u32x2 segrg[PAIRS ? kHBandRows * SP : 2];
-  __shared__ __attribute__((aligned(16))) uint32_t segb[PAIRS ? kHBandRows * SP : 4];
+  __shared__ __attribute__((aligned(16))) uint32_t seg[kHBandRows * kHSegStride];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kHBandRows * kHBandCols * 4];
   __shared__ uint32_t ext[2];
   const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
@@ -2020,16 +2023,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const ResizePass &ps = im.pass[stage];
   if (FUSED) {  // a fused fill reads the planes: specialised per layout (uniform per workgroup)
     switch (fill_class(im)) {
-      case FC_420: hband<KMAX, FUSED, FC_420, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
-      case FC_420_Z: hband<KMAX, FUSED, FC_420_Z, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
-      case FC_422: hband<KMAX, FUSED, FC_422, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
-      case FC_422_Z: hband<KMAX, FUSED, FC_422_Z, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
-      case FC_444: hband<KMAX, FUSED, FC_444, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
-      case FC_444_Z: hband<KMAX, FUSED, FC_444_Z, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb); return;
+      case FC_420: hband<KMAX, FUSED, FC_420, PF>(im, ps, it.item0, seg, ob, ext); return;
+      case FC_420_Z: hband<KMAX, FUSED, FC_420_Z, PF>(im, ps, it.item0, seg, ob, ext); return;
+      case FC_422: hband<KMAX, FUSED, FC_422, PF>(im, ps, it.item0, seg, ob, ext); return;
+      case FC_422_Z: hband<KMAX, FUSED, FC_422_Z, PF>(im, ps, it.item0, seg, ob, ext); return;
+      case FC_444: hband<KMAX, FUSED, FC_444, PF>(im, ps, it.item0, seg, ob, ext); return;
+      case FC_444_Z: hband<KMAX, FUSED, FC_444_Z, PF>(im, ps, it.item0, seg, ob, ext); return;
       default: break;
     }
   }
-  hband<KMAX, FUSED, FC_GENERIC, PAIRS>(im, ps, it.item0, seg, ob, ext, segrg, segb);
+  hband<KMAX, FUSED, FC_GENERIC, false>(im, ps, it.item0, seg, ob, ext);
 }
 
 // ---- band H pass on the matrix cores (k_resize_hm)
@@ -2403,6 +2406,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   }
 }
 
+constexpr uint32_t kVUnitsPerThread = kVItemUnits;
+
 // Vertical pass: each thread produces 16 consecutive bytes of one output row
 // (channel-agnostic), one 16-byte load per tap: a wave streams 1 KiB of a
 // source row per tap.
@@ -2412,7 +2417,10 @@ __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ 
   const ResizePass &ps = imgs[it.image].pass[stage];
   const uint32_t rowbytes = ps.width * ps.C;
   const uint32_t units = (rowbytes + 15) / 16;
-  const uint32_t idx = it.item0 + threadIdx.x;
+  // kVUnitsPerThread consecutive 256-unit strides per workgroup item (the
+  // host lists one item per kVUnitsPerThread * 256 units)
+  for (uint32_t kv = 0; kv < kVUnitsPerThread; kv++) {
+  const uint32_t idx = it.item0 + kv * 256 + threadIdx.x;
   if (idx >= units * ps.rows) return;
   const uint32_t y = idx / units, u = idx - y * units;
   const uint32_t b0 = u * 16;
@@ -2481,6 +2489,7 @@ __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ 
     d[3] = o[3];
   } else {
     for (uint32_t j = 0; j < nb; j++) dst[j] = (uint8_t)(o[j >> 2] >> (8 * (j & 3)));
+  }
   }
 }
 
@@ -2622,25 +2631,25 @@ void launch_coeffs(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t
 void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
   DG_LAUNCH(k_resize_h, nwg, st, imgs, list, stage);
 }
-template <bool FUSED, bool PAIRS>
+template <bool FUSED, bool PF = false>
 static void launch_hb_classes(hipStream_t st, const ImageDesc *imgs, const WgItem *&list, const uint32_t ncls[4],
                               int stage) {
-  DG_LAUNCH((k_resize_hb<8, FUSED, PAIRS>), ncls[0], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<8, FUSED, PF>), ncls[0], st, imgs, list, stage);
   list += ncls[0];
-  DG_LAUNCH((k_resize_hb<16, FUSED, PAIRS>), ncls[1], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hb<16, FUSED, PF>), ncls[1], st, imgs, list, stage);
   list += ncls[1];
-  DG_LAUNCH((k_resize_hb<32, FUSED>), ncls[2], st, imgs, list, stage);  // pairs: 35 KiB of LDS, 4 waves/SIMD
+  DG_LAUNCH((k_resize_hb<32, FUSED, PF>), ncls[2], st, imgs, list, stage);
   list += ncls[2];
   DG_LAUNCH((k_resize_hb<0, FUSED>), ncls[3], st, imgs, list, stage);
   list += ncls[3];
 }
 void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][4],
-                      int stage, bool pairs) {
-  if (pairs)
+                      int stage, bool prefetch) {
+  if (prefetch)
     launch_hb_classes<true, true>(st, imgs, list, ncls[1], stage);
   else
     launch_hb_classes<true, false>(st, imgs, list, ncls[1], stage);
-  launch_hb_classes<false, false>(st, imgs, list, ncls[0], stage);
+  launch_hb_classes<false>(st, imgs, list, ncls[0], stage);
 }
 void launch_resize_hm(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][2],
                       int stage) {

@@ -279,12 +279,15 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *                 MFMA convolution; default 0: measured slower); 0 = IDCT to planes + the band H kernel
  *   "dec_strips"   k_band_dec: 16-row strips per workgroup (default 8)
  *   "reset_host_us" clears the host submit phase timers (stats "host_us_*")
+ *   "sub_auto"    subsequence size of batches over 64 MiB of coded data when "sub_bits" is 0 (default 8192)
  * Stats: "batches", "coalesced_batches", "coalesced_images", "resync_rounds", "fix_workgroups", "write_mismatch",
  * "unsettled_batches", "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool" (tables pooled now),
  * "pool_flushes" (times the table pools were started over), "png_chunks", "png_serial_fallbacks",
  * "band_dec_images" (images whose first H pass ran in k_band_dec), "prog_items", "prog_chains" (work items / chains
- * of the pipelined progressive launches), "prog_aggregates", "prog_aggregate_images";
- * -1 if unknown.
+ * of the pipelined progressive launches), "prog_aggregates", "prog_aggregate_images",
+ * "meta_bytes" (the last batch's descriptor/list upload), "host_us_<phase>" / "host_cpu_us_<phase>" (wall / thread
+ * CPU microseconds in dg_submit* per phase: plan, pools, layout, lists, upload (staging copy), h2d, launch;
+ * "host_us_slotwait": waiting for a free slot); -1 if unknown.
  *
  * Entropy-decode self-checks: an image whose write pass disagrees with the sync pass, or every sequential JPEG of
  * a batch whose boundary repair did not settle, is returned DG_ERR_UNSUPPORTED (the caller's CPU decoder takes

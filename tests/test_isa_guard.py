@@ -31,21 +31,3 @@ def test_no_v_ashr_pk_u8_i32(tmp_path):
             bad = [l for l in asm.splitlines() if "v_ashr_pk_u8_i32" in l or "v_lshr_pk_u8" in l]
             assert not bad, (src, bad[:3])
 
-
-def _kernel_body(asm, name):
-    i = asm.index(name + ":")
-    return asm[i:asm.index(".Lfunc_end", i)]
-
-
-@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
-def test_pair_layout_convolution_keeps_every_channel(tmp_path):
-    """hipcc 7.2 dropped the second element of a u32x2 loaded from an LDS array
-    of u32x2 in the pair-layout convolution (hconv_pairs): the G channel's
-    dot2 chain vanished and the G bytes were wrong (caught by the GPU parity
-    tests).  The pair kernels must issue as many v_dot2 as the byte-layout
-    kernels of the same class: 3 channels x taps/2 x 4 rows per fill class."""
-    _, asm = _asm("kernels.hip", str(tmp_path))
-    for k in (8, 16):
-        pairs = _kernel_body(asm, f"_ZN2dg11k_resize_hbILi{k}ELb1ELb1EEEvPKNS_9ImageDescEPKNS_6WgItemEi").count("v_dot2")
-        bytes_ = _kernel_body(asm, f"_ZN2dg11k_resize_hbILi{k}ELb1ELb0EEEvPKNS_9ImageDescEPKNS_6WgItemEi").count("v_dot2")
-        assert pairs == bytes_ > 0, (k, pairs, bytes_)
