@@ -244,10 +244,32 @@ def wds_key_hash(key: str) -> int:
 # ------------------------------------------------------------------ context
 
 def _as_ptr_array(ptrs: Sequence[int]):
-    arr = (ctypes.c_void_p * max(1, len(ptrs)))()
-    for i, p in enumerate(ptrs):
-        arr[i] = p
-    return arr
+    """Pointer array argument: a uint64 numpy array is passed in place, a
+    sequence of ints is converted in one call (no per-element assignment)."""
+    if isinstance(ptrs, np.ndarray):
+        a = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        if a.size == 0:
+            a = np.zeros(1, np.uint64)
+        return (ctypes.c_void_p * a.size).from_buffer(a)
+    return (ctypes.c_void_p * max(1, len(ptrs)))(*ptrs)
+
+
+def _as_array(ctype, npdtype, vals, n: int):
+    """Typed array argument (numpy arrays in place, like _as_ptr_array)."""
+    if isinstance(vals, np.ndarray):
+        a = np.ascontiguousarray(vals, dtype=npdtype)
+        if a.size == 0:
+            a = np.zeros(1, npdtype)
+        return (ctype * a.size).from_buffer(a)
+    return (ctype * max(1, n))(*vals)
+
+
+def meta_status(metas) -> np.ndarray:
+    """The status field of every PayloadMeta in a metas array, as int32s (a
+    view, no per-element attribute access)."""
+    raw = np.frombuffer(metas, dtype=np.uint8).reshape(len(metas), ctypes.sizeof(PayloadMeta))
+    off = PayloadMeta.status.offset
+    return raw[:, off:off + 4].copy().view(np.int32).reshape(-1)
 
 
 class Context:
@@ -412,10 +434,10 @@ class Context:
         n = len(d_ptrs)
         hp = _as_ptr_array(h_ptrs)
         dp = _as_ptr_array(d_ptrs)
-        la = (ctypes.c_size_t * max(1, n))(*lens)
-        fb = (ctypes.c_int32 * max(1, n))(*(forced if forced is not None else [-1] * n))
+        la = _as_array(ctypes.c_size_t, np.uint64, lens, n)
+        fb = _as_array(ctypes.c_int32, np.int32, forced if forced is not None else np.full(n, -1, np.int32), n)
         op = _as_ptr_array(d_outs)
-        ca = (ctypes.c_uint64 * max(1, n))(*caps)
+        ca = _as_array(ctypes.c_uint64, np.uint64, caps, n)
         metas = (PayloadMeta * max(1, n))()
         ticket = ctypes.c_uint64()
         _check(load().dg_submit_device(self._h, n, hp, dp, la, fb, op, ca, metas, ctypes.byref(ticket)))

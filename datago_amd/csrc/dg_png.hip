@@ -657,8 +657,8 @@ __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ i
   const ImageDesc &im = imgs[c.image];
   const DG_GLOBAL uint32_t *z = gp<const uint32_t>(im.png.zs);
   const uint32_t zlen = im.png.zlen, zwords = (zlen + 3) / 4;
-  const uint32_t b0 = c.idx * kInfChunk * 8u;
-  const uint32_t b1 = min((c.idx + 1) * kInfChunk * 8u, zlen * 8u);
+  const uint32_t b0 = c.idx * c.span * 8u;
+  const uint32_t b1 = min((c.idx + 1) * c.span * 8u, zlen * 8u);
   const uint32_t lane = threadIdx.x, hl = lane >> 5, sh = lane & 31u;
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t found = kInfNone, qn = 0;

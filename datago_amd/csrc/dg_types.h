@@ -191,7 +191,7 @@ DG_HD A7Pass png_adam7(uint32_t W, uint32_t H, uint32_t bitspp, uint32_t p) {
 }
 
 // Chunk-parallel inflate.  The zlib stream of a large PNG is cut into
-// kInfChunk-byte chunks.  k_inf_find looks in each chunk (but the first) for
+// chunks of `span` bytes (option "inf_chunk", default kInfChunk).  k_inf_find looks in each chunk (but the first) for
 // the first bit position that parses as a dynamic-Huffman block header with
 // complete codes; k_inf_decode decodes, one lane per chunk, from there until
 // it reaches a block boundary that another chunk starts at (or the end).  A
@@ -213,7 +213,7 @@ struct InfChunk {
   uint32_t len;       // entries produced
   uint32_t stop;      // chunk index whose start the decode reached (nchunks: end of stream)
   uint32_t status;    // 0 ok, 1 decode error, 2 overflow
-  uint32_t pad;
+  uint32_t span;      // compressed bytes per chunk of this image
 };
 constexpr uint32_t kInfTabBytes = 4096;        // per-chunk table scratch (see k_inf_decode)
 // A gather job: copy `len` bytes (one IDAT payload) from src to dst.

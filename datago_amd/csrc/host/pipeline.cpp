@@ -542,6 +542,20 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     decode_sem_ = (int)v;
     return DG_OK;
   }
+  if (k == "meta_pull") {  // 1: the GPU reads the descriptor upload from page-locked memory (0: hipMemcpyAsync)
+    meta_pull_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "plan_threads") {  // host threads parsing a submission's headers (1 = the caller only)
+    if (v < 1 || v > 64) return DG_ERR_INVALID;
+    plan_threads_ = (int)v;
+    return DG_OK;
+  }
+  if (k == "inf_chunk") {  // compressed bytes per chunk of the chunk-parallel inflate
+    if (v < 4096 || v > 65536 || (v & (v - 1))) return DG_ERR_INVALID;
+    inf_chunk_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "png_chunked") {  // 0: every PNG inflates serially (test switch)
     chunked_off_ = v == 0;
     return DG_OK;
@@ -613,6 +627,10 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "sub_bits") return last_sub_bits_;
   if (k == "sub_auto") return sub_auto_;
   if (k == "meta_bytes") return (int64_t)last_meta_bytes_;
+  if (k == "allocs") return stat_allocs_;
+  if (k == "alloc_mb") return stat_alloc_mb_;
+  if (k == "alloc_us") return (int64_t)stat_alloc_us_;
+  if (k == "reclaims") return stat_reclaims_;
   if (k == "png_serial_fallbacks") return stat_png_serial_;
   if (k == "band_dec_images") return stat_band_dec_;
   if (k == "direct_d2h") return stat_direct_d2h_;
@@ -670,6 +688,12 @@ void Context::free_retired() {
   retired_dev_bytes_ = retired_pin_bytes_ = 0;
 }
 
+void Context::note_alloc(std::chrono::steady_clock::time_point t0, size_t bytes) {
+  stat_allocs_++;
+  stat_alloc_mb_ += (int64_t)(bytes >> 20);
+  stat_alloc_us_ += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+}
+
 size_t Context::grow_cap(size_t bytes, bool headroom) {
   return align_up(std::max(bytes, (size_t)1 << 20) + (headroom ? bytes / 2 : 0), 1 << 20);
 }
@@ -679,6 +703,7 @@ size_t Context::grow_cap(size_t bytes, bool headroom) {
 // sees them.  True = worth retrying.
 bool Context::reclaim() {
   (void)hipGetLastError();
+  stat_reclaims_++;
   if (sync_all() != DG_OK) return false;
   free_retired();
   return true;
@@ -707,11 +732,13 @@ dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
   // profiles/r04/ranks), so growth must stay rare.  Under memory pressure the
   // retired buffers go first, then the headroom.
   size_t cap = grow_cap(bytes, regrow);
+  const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipMalloc(&b.p, cap);
   if (e != hipSuccess && reclaim()) {
     cap = grow_cap(bytes, false);
     e = hipMalloc(&b.p, cap);
   }
+  note_alloc(t0, cap);
   if (e != hipSuccess) {
     set_error("device allocation failed");
     b.p = nullptr;
@@ -731,11 +758,13 @@ dg_status Context::ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user) {
     b.cap = 0;
   }
   size_t cap = grow_cap(bytes, regrow);
+  const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
   if (e != hipSuccess && reclaim()) {
     cap = grow_cap(bytes, false);
     e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
   }
+  note_alloc(t0, cap);
   if (e != hipSuccess) {
     set_error("pinned host allocation failed");
     b.p = nullptr;
@@ -1009,10 +1038,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     phase_t0 = now;
     cpu_t0 = c;
   };
-  // ---- 1. plan every image (host, header only)
-  for (int i = 0; i < n; i++) plan_image(h_srcs[i], lens[i], forced ? forced[i] : -1, b.plans[i]);
-  for (int i = 0; i < n; i++) {
+  // ---- 1. plan every image (host, header only; on the planning workers)
+  auto plan_one = [&](int i) {
     ImagePlan &p = b.plans[i];
+    plan_image(h_srcs[i], lens[i], forced ? forced[i] : -1, p);
     dg_payload_meta &m = *b.mptr[i];
     memset(&m, 0, sizeof(m));
     m.status = p.status;
@@ -1038,6 +1067,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       p.status = DG_ERR_INVALID;
       m.status = DG_ERR_INVALID;
     }
+  };
+  if (plan_threads_ > 1 && n >= 2 * kPlanGrain) {
+    if (!plan_pool_ || plan_pool_->threads() != plan_threads_) plan_pool_.reset(new HostPool(plan_threads_));
+    plan_pool_->run(n, kPlanGrain, plan_one);
+  } else {
+    for (int i = 0; i < n; i++) plan_one(i);
   }
   phase(0);
   // ---- 2. table pools
@@ -1157,19 +1192,21 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       // e.g. masks, inflate serially in one wave)
       {
         const uint64_t want = g.rawlen;
-        const uint32_t nch = (uint32_t)((g.zlen + kInfChunk - 1) / kInfChunk);
+        const uint32_t span = inf_chunk_;
+        const uint32_t nch = (uint32_t)((g.zlen + span - 1) / span);
         if (nch >= 2 && !chunked_off_) {
           pd.chunk0 = (uint32_t)b.ichunks.size();
           pd.nchunks = nch;
           // entries per chunk: 3x the image's average expansion (+64 Ki), at most the whole image;
           // a chunk that needs more sends the image to the serial kernel
           const double ratio = (double)want / (double)g.zlen;
-          const uint64_t cap = std::min<uint64_t>(want, (uint64_t)(3.0 * ratio * kInfChunk) + 65536);
+          const uint64_t cap = std::min<uint64_t>(want, (uint64_t)(3.0 * ratio * span) + 65536);
           for (uint32_t k = 0; k < nch; k++) {
             InfChunk c;
             memset(&c, 0, sizeof(c));
             c.image = (uint32_t)b.descs.size();
             c.idx = k;
+            c.span = span;
             c.cap = (uint32_t)cap;
             c.start = k == 0 ? 16u : kInfNone;  // chunk 0: first block after the 2-byte zlib header
             c.out = L.take(cap * 2, 256);       // offsets: made absolute below
@@ -1902,7 +1939,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.ichunk_off = M.take(b.ichunks.size() * sizeof(InfChunk));
   b.pscan_off = M.take(b.pscans.size() * sizeof(ProgScan));
   b.blob_off = M.take(b.blob.size());
-  b.meta_bytes = M.off;
+  b.meta_bytes = align_up(M.off, 256);  // the host inputs follow, 16-byte aligned for k_meta_pull
   st = ensure(sl.meta, b.meta_bytes + 256, sl.st);
   if (st) return st;
   for (ImageDesc &d : b.descs) {
@@ -1946,8 +1983,20 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   last_meta_bytes_ = b.meta_bytes;
   phase(4);
   if (timing_) HIPCHK(hipEventRecord(sl.ev[0], sl.st));
-  HIPCHK(hipMemcpyAsync(sl.meta.p, P, b.meta_bytes, hipMemcpyHostToDevice, sl.st));
-  if (host_io && IN.off) HIPCHK(hipMemcpyAsync(sl.input.p, P + b.meta_bytes, IN.off, hipMemcpyHostToDevice, sl.st));
+  if (meta_pull_) {
+    launch_meta_pull(sl.st, P, sl.meta.p, b.meta_bytes);
+    HIPCHK(hipGetLastError());
+  } else {
+    HIPCHK(hipMemcpyAsync(sl.meta.p, P, b.meta_bytes, hipMemcpyHostToDevice, sl.st));
+  }
+  if (host_io && IN.off) {  // the coded inputs (dg_submit / dg_decode_one)
+    if (meta_pull_) {
+      launch_meta_pull(sl.st, P + b.meta_bytes, sl.input.p, IN.off);
+      HIPCHK(hipGetLastError());
+    } else {
+      HIPCHK(hipMemcpyAsync(sl.input.p, P + b.meta_bytes, IN.off, hipMemcpyHostToDevice, sl.st));
+    }
+  }
   b.stage_ms.clear();
   sl.subs_off = subs_off;  // SubStates and checkpoints live in the scratch arena
   sl.ckpt_off = ckpt_off;

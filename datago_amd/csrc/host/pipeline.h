@@ -16,6 +16,7 @@
 #include "jpeg_header.h"
 #include "png_header.h"
 #include "jpeg_enc.h"
+#include "host_pool.h"
 
 namespace dg {
 
@@ -215,6 +216,9 @@ class Context {
   void retire(void *p, size_t bytes, bool pinned);
   void free_retired();
   static size_t grow_cap(size_t bytes, bool headroom);
+  void note_alloc(std::chrono::steady_clock::time_point t0, size_t bytes);
+  int64_t stat_allocs_ = 0, stat_alloc_mb_ = 0, stat_reclaims_ = 0;  // stats "allocs", "alloc_mb", "reclaims"
+  double stat_alloc_us_ = 0;                                          // stat "alloc_us"
   bool reclaim();
   void free_retired_if_idle();
   std::vector<void *> retired_dev_, retired_pinned_;  // grown-out buffers, freed later (ensure)
@@ -330,6 +334,11 @@ class Context {
   int debug_flags_ = 0;
   bool wg_timing_ = false;
   bool chunked_off_ = false;  // option "png_chunked" = 0
+  uint32_t inf_chunk_ = kInfChunk;  // option "inf_chunk"
+  int plan_threads_ = 4;            // option "plan_threads"
+  bool meta_pull_ = true;           // option "meta_pull"
+  static constexpr int kPlanGrain = 32;  // images per planning work piece
+  std::unique_ptr<HostPool> plan_pool_;
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"
   int decode_sem_ = 0;                  // option "decode_semantics"
   bool ckpt_ = true;                    // option "ckpt"

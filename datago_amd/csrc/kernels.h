@@ -64,6 +64,8 @@ void launch_band_dec(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
                      const QuantTable *qpool, uint32_t strips_per_wg);
 // final copy / gray->RGB expansion: 256 output pixels per workgroup
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
+// bytes (rounded up to 16) from page-locked host memory to device memory, read by the GPU
+void launch_meta_pull(hipStream_t st, const void *src, void *dst, size_t bytes);
 // progressive JPEG (dg_prog.hip): zero coefficients (kProgZeroBytes per
 // workgroup), then one wave per work item (a scan, or a chain of scans linked
 // by ProgScan::next): pipelined launches with pflags (progress words, zeroed,

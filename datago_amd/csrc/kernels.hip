@@ -2556,6 +2556,16 @@ __global__ __launch_bounds__(256) void k_copy(const ImageDesc *__restrict__ imgs
 
 // ------------------------------------------------------------ launchers
 
+// Descriptor/list upload pulled by the GPU: 16-byte loads from the slot's
+// page-locked staging buffer (mapped into the device's address space) into
+// HBM.  hipMemcpyAsync of the ~2 MB meta region cost ~0.8 ms of the submitting
+// thread's CPU per configs[1] batch (profiles/r04: host phase "h2d"), for a
+// copy the GPU finishes in tens of microseconds.
+__global__ __launch_bounds__(256) void k_meta_pull(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst,
+                                                   uint32_t n16) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
+}
+
 #define DG_LAUNCH(kern, nwg, st, ...)                                              \
   do {                                                                            \
     if (nwg) hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), 0, st, __VA_ARGS__); \
@@ -2670,6 +2680,12 @@ void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
 }
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   DG_LAUNCH(k_copy, nwg, st, imgs, list);
+}
+
+void launch_meta_pull(hipStream_t st, const void *src, void *dst, size_t bytes) {
+  const uint32_t n16 = (uint32_t)((bytes + 15) / 16);
+  const uint32_t nwg = (n16 + 255) / 256 < 1024u ? (n16 + 255) / 256 : 1024u;
+  DG_LAUNCH(k_meta_pull, nwg, st, (const u32x4 *)src, (u32x4 *)dst, n16);
 }
 
 }  // namespace dg

@@ -268,11 +268,15 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "entropy_lpt" 1 = dispatch the slowest entropy workgroups first (default 1)
  *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)
  *   "png_chunked" 0 = inflate every PNG with the serial kernel (test switch; default 1)
+ *   "inf_chunk"   chunk-parallel inflate: compressed bytes per chunk (power of two, 4096..65536; default 32768)
  *   "uf_units"    1 or 2 (default 2): PNG unfilter filter units per lane per diagonal step (1: half the LDS)
  *   "inf_decode"  0..5: chunk-parallel inflate lookup bits (literal/length, distance) per lane in LDS:
  *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (default, 24 KiB), 3 7/5, 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
  *                 the compressed stream prefetched two 16-byte quads ahead per lane
  *   "copy_threads" host threads copying a host-out batch's outputs to the caller's buffers (default 8)
+ *   "meta_pull"   1 = the GPU reads each batch's descriptors and work lists from page-locked staging (default);
+ *                 0 = hipMemcpyAsync
+ *   "plan_threads" host threads parsing a submission's headers (default 4; 1 = the submitting thread only)
  *   "hv_fused"     1 = fuse the first H and V passes of colour JPEGs where they fit (default 0; slower)
  *   "h_mfma"       1 = band H passes on the matrix cores (k_resize_hm, i8 MFMA; default 0: measured slower); 0 = VALU kernel
  *   "band_dec"     1 = IDCT + upsampling + colour + the first H pass of a JPEG in one kernel (k_band_dec,
@@ -285,7 +289,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  * "pool_flushes" (times the table pools were started over), "png_chunks", "png_serial_fallbacks",
  * "band_dec_images" (images whose first H pass ran in k_band_dec), "prog_items", "prog_chains" (work items / chains
  * of the pipelined progressive launches), "prog_aggregates", "prog_aggregate_images",
- * "meta_bytes" (the last batch's descriptor/list upload), "host_us_<phase>" / "host_cpu_us_<phase>" (wall / thread
+ * "meta_bytes" (the last batch's descriptor/list upload), "allocs", "alloc_mb", "alloc_us", "reclaims"
+ * (device / page-locked buffer growth: count, MiB, wall microseconds; OOM reclaims), "host_us_<phase>" / "host_cpu_us_<phase>" (wall / thread
  * CPU microseconds in dg_submit* per phase: plan, pools, layout, lists, upload (staging copy), h2d, launch;
  * "host_us_slotwait": waiting for a free slot); -1 if unknown.
  *

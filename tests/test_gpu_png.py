@@ -196,12 +196,14 @@ def test_png_large_full_size_properties(ctx512):
     assert st == 0 and (arr.shape[1], arr.shape[0]) == t.target_size(1800, 1200)
 
 
-@pytest.mark.parametrize("inf_decode", [0, 1, 2, 3, 4, 5, 6, 7])
-def test_chunked_inflate_matches_serial_and_oracle(inf_decode):
+@pytest.mark.parametrize("inf_decode,inf_chunk", [(d, 32768) for d in range(8)] + [(2, 4096), (2, 8192), (2, 16384),
+                                                                                    (3, 65536)])
+def test_chunked_inflate_matches_serial_and_oracle(inf_decode, inf_chunk):
     """Large streams take the chunk-parallel inflate (block-header search,
     one lane per chunk, window markers); it must equal the oracle and the
     serial kernel (option png_chunked=0) byte for byte, for every
-    k_inf_decode shape (option inf_decode: lanes per workgroup, lookup bits)."""
+    k_inf_decode shape (option inf_decode: lanes per workgroup, lookup bits)
+    and chunk size (option inf_chunk: compressed bytes per chunk)."""
     L = _lib()
     rng = np.random.default_rng(31)
     datas = []
@@ -214,6 +216,7 @@ def test_chunked_inflate_matches_serial_and_oracle(inf_decode):
     datas.append(synth.make_png(78, 1600, 1000, "L", level=6, filters="random"))
     a = L.Context(0)
     a.set_option("inf_decode", inf_decode)
+    a.set_option("inf_chunk", inf_chunk)
     b = L.Context(0)
     b.set_option("png_chunked", 0)
     ra, rb = a.decode_batch(datas), b.decode_batch(datas)

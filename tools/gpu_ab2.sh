@@ -27,6 +27,6 @@ for r in $(seq 1 $REPS); do
     timeout -k 10 400 python bench.py --steps $STEPS --warmup 3 --e2e-steps 0 --one-threads 0 --no-cpu-baseline \
       $EXTRA $cfg --out $OUT/$tag.json > $OUT/$tag.log 2>&1
     rc=$?; echo "=== $tag [$cfg] exit $rc"; [ $rc -eq 0 ] || { tail -20 $OUT/$tag.log; exit $rc; }
-    python -c "import json;d=json.load(open('$OUT/$tag.json'));s=d['roofline_isolated']['stages_ms'];print(d['value'],d['ms_per_step'],{k:round(v,3) for k,v in s.items() if v>0.05})"
+    python -c "import json;d=json.load(open('$OUT/$tag.json'));s=d['roofline_isolated']['stages_ms'];print(d['value'],d['ms_per_step'],{k:round(v,3) for k,v in s.items() if v>0.05});print('  host',d['host_submit_ms_per_step'],d['host_submit_phases_per_rank'][0]['cpu'],d.get('allocations'))"
   done
 done
