@@ -1114,7 +1114,7 @@ def main() -> int:
             "host_submit_ms_per_step_per_rank": [round(1e3 * h_ / a.steps, 3) for h_ in per_rank_host],
             "host_submit_phases_ms_per_step": host_phases,
             "meta_bytes_per_batch": ctx.stat("meta_bytes"),
-            "allocations": {k_: ctx.stat(k_) for k_ in ("allocs", "alloc_mb", "alloc_us", "reclaims")},
+            "allocations": {k_: ctx.stat(k_) for k_ in ("allocs", "alloc_mb", "alloc_us", "reclaims", "retire_syncs")},
             # per rank: wall ms per step in each dg_submit_device phase, the thread's CPU ms in the same
             # phases (wall >> cpu = blocking: allocation, driver locks, copies), and the slot wait
             "host_submit_phases_per_rank": [

@@ -475,7 +475,9 @@ DG_HD void stage_finish(StageCtx &c) {
 // stops and completes its totals with the stored tail.  This cuts a re-decode
 // from a full range to about the self-synchronisation distance.
 constexpr uint32_t kCkptBits = 256;
-constexpr uint32_t kMaxCkpt = 15;  // enough for sub_bits <= 4096
+// enough for sub_bits <= 4096, and for the half-way checkpoint of an
+// 8192-bit range (index 15), where k_huff_write splits a range (write_split)
+constexpr uint32_t kMaxCkpt = 16;
 struct Ckpt {
   uint32_t st;   // packed state (rel past the checkpoint position, r, z)
   uint32_t m, n; // tail (segmented: m > 0 means the tail contains a reset)
@@ -587,10 +589,14 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
                         const DG_GLOBAL uint32_t *mk,
                         uint32_t s, uint32_t in, RangeAcc &acc, WriteCtx *w, DG_GLOBAL Ckpt *ck = nullptr,
                         bool merge = false, uint32_t old_out = 0, StageCtx *stg = nullptr,
-                        const uint16_t *mt = nullptr, uint32_t acm = 0xFFu, uint32_t pair = 0) {
+                        const uint16_t *mt = nullptr, uint32_t acm = 0xFFu, uint32_t pair = 0,
+                        uint32_t a0o = kInf, uint32_t a1o = kInf) {
+  // [a0o, a1o): a part of the range (k_huff_write's split halves); `in` is
+  // then the state at the first symbol boundary at/after a0o
   const uint32_t S = im.sub_bits, total = im.ds_bits;
-  const uint32_t a0 = s * S;
-  const uint32_t a1 = (a0 + S < total) ? a0 + S : total;
+  const uint32_t r0 = s * S;
+  const uint32_t a0 = a0o != kInf ? a0o : r0;
+  const uint32_t a1 = a1o != kInf ? a1o : ((r0 + S < total) ? r0 + S : total);
   uint32_t r = st_r(in), z = st_z(in);
   uint32_t pos = a0 + st_rel(in);
   acc.m = 0;

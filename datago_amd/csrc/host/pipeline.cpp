@@ -542,8 +542,13 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     decode_sem_ = (int)v;
     return DG_OK;
   }
-  if (k == "meta_pull") {  // 1: the GPU reads the descriptor upload from page-locked memory (0: hipMemcpyAsync)
-    meta_pull_ = v != 0;
+  if (k == "write_split") {  // 1: k_huff_write decodes each range as two halves (see k_huff_write)
+    write_split_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "meta_pull") {  // the GPU reads from page-locked staging: 1 the descriptors, 2 also host inputs
+    if (v < 0 || v > 2) return DG_ERR_INVALID;
+    meta_pull_ = (int)v;
     return DG_OK;
   }
   if (k == "plan_threads") {  // host threads parsing a submission's headers (1 = the caller only)
@@ -631,6 +636,7 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "alloc_mb") return stat_alloc_mb_;
   if (k == "alloc_us") return (int64_t)stat_alloc_us_;
   if (k == "reclaims") return stat_reclaims_;
+  if (k == "retire_syncs") return stat_retire_syncs_;
   if (k == "png_serial_fallbacks") return stat_png_serial_;
   if (k == "band_dec_images") return stat_band_dec_;
   if (k == "direct_d2h") return stat_direct_d2h_;
@@ -670,14 +676,16 @@ int Context::timings(const char **names, float *ms, int cap) {
 // per host each keeping GiBs of grown-out buffers page-locked would pin a lot
 // of the host's memory.  Retired buffers are also freed at the first idle
 // moment (a wait that leaves no batch in flight, free_retired_if_idle).
-static constexpr size_t kRetiredDevMax = (size_t)4 << 30;
+static constexpr size_t kRetiredDevMax = (size_t)32 << 30;  // 4 GiB synced every few batches of growth (round 4)
 static constexpr size_t kRetiredPinMax = (size_t)512 << 20;
 
 void Context::retire(void *p, size_t bytes, bool pinned) {
   (pinned ? retired_pinned_ : retired_dev_).push_back(p);
   (pinned ? retired_pin_bytes_ : retired_dev_bytes_) += bytes;
-  if ((retired_dev_bytes_ > kRetiredDevMax || retired_pin_bytes_ > kRetiredPinMax) && sync_all() == DG_OK)
+  if ((retired_dev_bytes_ > kRetiredDevMax || retired_pin_bytes_ > kRetiredPinMax) && sync_all() == DG_OK) {
+    stat_retire_syncs_++;
     free_retired();
+  }
 }
 
 void Context::free_retired() {
@@ -720,18 +728,19 @@ void Context::free_retired_if_idle() {
 dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
   (void)user;
   if (b.cap >= bytes) return DG_OK;
-  const bool regrow = b.p != nullptr;
   if (b.p) {
     retire(b.p, b.cap, false);
     b.p = nullptr;
     b.cap = 0;
   }
-  // 50% headroom on re-growth: an allocation blocks on the driver (8 ranks
-  // sharing one GPU measured 36-209 ms of wall time per step in the layout
-  // phase against 0.3 ms of CPU while batches kept setting new size maxima,
-  // profiles/r04/ranks), so growth must stay rare.  Under memory pressure the
+  // 50% headroom: an allocation blocks on the driver (8 ranks sharing one
+  // GPU measured 36-209 ms of wall time per step in the layout phase against
+  // 0.3 ms of CPU while batches kept setting new size maxima,
+  // profiles/r04/ranks), so growth must stay rare.  (Headroom on re-growth
+  // only cost configs[1] 1.4 ms of submit time per batch: the extra growths
+  // retired enough to trigger device-wide syncs.)  Under memory pressure the
   // retired buffers go first, then the headroom.
-  size_t cap = grow_cap(bytes, regrow);
+  size_t cap = grow_cap(bytes, true);
   const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipMalloc(&b.p, cap);
   if (e != hipSuccess && reclaim()) {
@@ -751,13 +760,12 @@ dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
 dg_status Context::ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user) {
   (void)user;
   if (b.cap >= bytes) return DG_OK;
-  const bool regrow = b.p != nullptr;
   if (b.p) {
     retire(b.p, b.cap, true);
     b.p = nullptr;
     b.cap = 0;
   }
-  size_t cap = grow_cap(bytes, regrow);
+  size_t cap = grow_cap(bytes, true);
   const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipHostMalloc(&b.p, cap, hipHostMallocDefault);
   if (e != hipSuccess && reclaim()) {
@@ -801,36 +809,70 @@ dg_status Context::flush_pools() {
   hpool_idx_.clear();
   qpool_.clear();
   qpool_idx_.clear();
+  for (RecentTab &r : hrecent_) r.idx = -1;
+  for (RecentTab &r : qrecent_) r.idx = -1;
   hpool_uploaded_ = qpool_uploaded_ = 0;
   pool_gen_ = next;
   stat_pool_flush_++;
   return DG_OK;
 }
 
+// Table de-duplication.  Loaders mostly see a handful of distinct tables
+// (the encoder's standard ones), so a few recently pooled tables are compared
+// byte for byte first; only a miss builds the key string and hashes it (the
+// per-table string and hash were 0.65 ms of a 1,024-image WebDataset submit).
+static int recent_find(RecentTab *r, int n, const uint8_t *key, uint32_t len) {
+  for (int i = 0; i < n; i++)
+    if (r[i].idx >= 0 && r[i].len == len && memcmp(r[i].key, key, len) == 0) return r[i].idx;
+  return -1;
+}
+
+static void recent_put(RecentTab *r, int n, uint32_t &next, const uint8_t *key, uint32_t len, int idx) {
+  RecentTab &e = r[next++ % (uint32_t)n];
+  e.len = len;
+  memcpy(e.key, key, len);
+  e.idx = idx;
+}
+
 int Context::pool_huff(const HuffSpec &s) {
-  std::string key((const char *)s.bits, 17);
-  key.append((const char *)s.vals, (size_t)s.nvals);
+  uint8_t raw[17 + 256];
+  memcpy(raw, s.bits, 17);
+  const uint32_t len = 17 + (uint32_t)std::max(0, std::min(256, s.nvals));
+  memcpy(raw + 17, s.vals, len - 17);
+  int idx = recent_find(hrecent_, kRecentTabs, raw, len);
+  if (idx >= 0) return idx;
+  std::string key((const char *)raw, len);
   auto it = hpool_idx_.find(key);
-  if (it != hpool_idx_.end()) return it->second;
-  HuffTable t;
-  if (!build_huff_table(s, t)) return -1;
-  if (hpool_.size() >= kPoolMax) return -2;
-  hpool_.push_back(t);
-  int idx = (int)hpool_.size() - 1;
-  hpool_idx_[key] = idx;
+  if (it != hpool_idx_.end()) {
+    idx = it->second;
+  } else {
+    HuffTable t;
+    if (!build_huff_table(s, t)) return -1;
+    if (hpool_.size() >= kPoolMax) return -2;
+    hpool_.push_back(t);
+    idx = (int)hpool_.size() - 1;
+    hpool_idx_[key] = idx;
+  }
+  recent_put(hrecent_, kRecentTabs, hrecent_next_, raw, len, idx);
   return idx;
 }
 
 int Context::pool_quant(const uint16_t *q) {
+  int idx = recent_find(qrecent_, kRecentTabs, (const uint8_t *)q, 128);
+  if (idx >= 0) return idx;
   std::string key((const char *)q, 128);
   auto it = qpool_idx_.find(key);
-  if (it != qpool_idx_.end()) return it->second;
-  QuantTable t;
-  memcpy(t.q, q, 128);
-  if (qpool_.size() >= kPoolMax) return -2;
-  qpool_.push_back(t);
-  int idx = (int)qpool_.size() - 1;
-  qpool_idx_[key] = idx;
+  if (it != qpool_idx_.end()) {
+    idx = it->second;
+  } else {
+    QuantTable t;
+    memcpy(t.q, q, 128);
+    if (qpool_.size() >= kPoolMax) return -2;
+    qpool_.push_back(t);
+    idx = (int)qpool_.size() - 1;
+    qpool_idx_[key] = idx;
+  }
+  recent_put(qrecent_, kRecentTabs, qrecent_next_, (const uint8_t *)q, 128, idx);
   return idx;
 }
 
@@ -1121,8 +1163,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   // ---- 3. layout
   // Subsequence size: the entropy kernels are latency-bound, so they want as
   // many lanes as the chip can keep resident, but every subsequence costs a
-  // sync re-decode.  Measured on MI355X (profiles/r01/sweep_v4): 2048 bits is
-  // best up to ~64 MiB of coded data per batch; above, option "sub_auto"
+  // sync re-decode.  Measured on MI355X (profiles/r01/sweep_v4): 2048 bits
+  // below 64 MiB of coded data (configs[2]'s 1,024 WebDataset members, ~25
+  // MiB: 39.9 vs 38.5 Gpx/s with 4096, profiles/r04/wds_sub2); from 64 MiB
+  // option "sub_auto"
   // (round 4: 8192, profiles/r04/ab -- the chip stays full with half the
   // lanes once the write pass no longer decodes, and the 6 kbit lead-in of a
   // 4:2:0 range costs 75% instead of 150% of its bits).
@@ -1132,7 +1176,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     for (int i = 0; i < n; i++)
       if (!b.plans[i].status && b.plans[i].fmt == kFmtJpeg && !b.plans[i].hdr.progressive)
         coded += b.plans[i].hdr.scan_end - b.plans[i].hdr.scan_off;
-    sub_bits = coded >= (64ull << 20) ? sub_auto_ : 2048;
+    sub_bits = coded >= (64ull << 20) ? sub_auto_ : 2048u;
   }
   last_sub_bits_ = sub_bits;
   Layout L;        // scratch arena
@@ -1318,6 +1362,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     // completed blocks go straight to plane pixels inside k_huff_write (not
     // with decode-once staging, whose k_huff_scatter writes coefficients)
     d.idct_fused = (idct_fused_ && !entropy_once_) ? 1u : 0u;
+    // k_huff_write splits each range at the sync pass's half-way checkpoint
+    // (option "write_split"): needs that checkpoint, no restart markers and
+    // the plain write path
+    if (write_split_ && d.ckpt && !d.idct_fused && !entropy_once_ && h.restart == 0 && d.sub_bits >= 1024 &&
+        d.sub_bits / 2 / kCkptBits - 1 < num_ckpt(d.sub_bits))
+      d.ckpt |= 2u;
     if (d.idct_fused) b.any_fused = true;
     // lead-in before each subsequence (lead_in in dg_entropy.h): covers the
     // self-synchronisation distance, which is longest for 6-block MCUs
@@ -1778,7 +1828,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       const uint64_t bytes = (uint64_t)d.total_blocks * 128;
       for (uint32_t c = 0; (uint64_t)c * kProgZeroBytes < bytes; c++) b.lists[L_PROG_ZERO].push_back({I, c});
     } else {
-    for (uint32_t w = 0; w < d.nsub; w += kSubPerWg) b.lists[L_HUFF].push_back({I, w});
+    // split ranges (write_split): 128 ranges per k_huff_write workgroup, two lanes each
+    const uint32_t wstep = (d.ckpt & 2u) ? kSubPerWg / 2 : kSubPerWg;
+    for (uint32_t w = 0; w < d.nsub; w += wstep) b.lists[L_HUFF].push_back({I, w});
     for (uint32_t w = 0; w < d.nsub; w += kSubPerWg - 1) b.lists[L_SYNC].push_back({I, w});
     b.descs[di].ds_state0 = (uint32_t)b.lists[L_DESTUFF].size();  // k_destuff_one's state words, list order
     for (uint32_t c = 0; c < d.nchunk; c++) b.lists[L_DESTUFF].push_back({I, c});
@@ -1983,14 +2035,14 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   last_meta_bytes_ = b.meta_bytes;
   phase(4);
   if (timing_) HIPCHK(hipEventRecord(sl.ev[0], sl.st));
-  if (meta_pull_) {
+  if (meta_pull_ >= 1) {
     launch_meta_pull(sl.st, P, sl.meta.p, b.meta_bytes);
     HIPCHK(hipGetLastError());
   } else {
     HIPCHK(hipMemcpyAsync(sl.meta.p, P, b.meta_bytes, hipMemcpyHostToDevice, sl.st));
   }
   if (host_io && IN.off) {  // the coded inputs (dg_submit / dg_decode_one)
-    if (meta_pull_) {
+    if (meta_pull_ >= 2) {  // off by default: dg_decode_one 18.1 -> 16.6 Gpx/s with it (profiles/r04/one_r4i)
       launch_meta_pull(sl.st, P + b.meta_bytes, sl.input.p, IN.off);
       HIPCHK(hipGetLastError());
     } else {
@@ -2295,7 +2347,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   if (b.stage_on)
     launch_huff_scatter(sl.st, dd, lst(L_HUFF), cnt(L_HUFF), subs);
   else
-    launch_huff_write(sl.st, dm, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots, qp, (uint32_t)write_pair_);
+    launch_huff_write(sl.st, dm, lst(L_HUFF), cnt(L_HUFF), hp, subs, fl, b.max_slots, qp, (uint32_t)write_pair_, ck);
   if (next()) return DG_ERR_DEVICE;
   if (next()) return DG_ERR_DEVICE;  // coeffs (side stream)
   if (pside || dc_side) HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_prog, 0));  // progressive coefficients

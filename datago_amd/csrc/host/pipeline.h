@@ -166,6 +166,13 @@ enum ListId {
 };
 static_assert((int)L_COUNT <= 40, "Batch::lists");
 
+// A recently pooled table (pool_huff / pool_quant): its key bytes and slot.
+struct RecentTab {
+  uint8_t key[17 + 256];
+  uint32_t len = 0;
+  int idx = -1;
+};
+
 class Context {
  public:
   Context(int device, const dg_image_config *cfg);
@@ -218,6 +225,7 @@ class Context {
   static size_t grow_cap(size_t bytes, bool headroom);
   void note_alloc(std::chrono::steady_clock::time_point t0, size_t bytes);
   int64_t stat_allocs_ = 0, stat_alloc_mb_ = 0, stat_reclaims_ = 0;  // stats "allocs", "alloc_mb", "reclaims"
+  int64_t stat_retire_syncs_ = 0;  // stat "retire_syncs": device-wide syncs to free retired buffers
   double stat_alloc_us_ = 0;                                          // stat "alloc_us"
   bool reclaim();
   void free_retired_if_idle();
@@ -308,6 +316,9 @@ class Context {
 
   std::vector<HuffTable> hpool_;
   std::unordered_map<std::string, int> hpool_idx_;
+  static constexpr int kRecentTabs = 8;  // recently pooled tables, compared before the hash map
+  RecentTab hrecent_[kRecentTabs], qrecent_[kRecentTabs];
+  uint32_t hrecent_next_ = 0, qrecent_next_ = 0;
   std::vector<QuantTable> qpool_;
   std::unordered_map<std::string, int> qpool_idx_;
   size_t hpool_uploaded_ = 0, qpool_uploaded_ = 0;
@@ -336,7 +347,8 @@ class Context {
   bool chunked_off_ = false;  // option "png_chunked" = 0
   uint32_t inf_chunk_ = kInfChunk;  // option "inf_chunk"
   int plan_threads_ = 4;            // option "plan_threads"
-  bool meta_pull_ = true;           // option "meta_pull"
+  int meta_pull_ = 1;               // option "meta_pull"
+  bool write_split_ = false;        // option "write_split"
   static constexpr int kPlanGrain = 32;  // images per planning work piece
   std::unique_ptr<HostPool> plan_pool_;
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"

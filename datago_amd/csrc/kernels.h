@@ -27,7 +27,7 @@ void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
 void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, SubState *subs);
 void launch_huff_write(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                        const HuffTable *pool, const SubState *subs, BatchFlags *flags, uint32_t max_slots,
-                       const QuantTable *qpool, uint32_t pair);
+                       const QuantTable *qpool, uint32_t pair, const Ckpt *ckpt);
 // fused IDCT leftovers (BatchFlags::idct_list), grid-strided over the device-side count
 void launch_idct_list(hipStream_t st, const ImageDesc *imgs, const QuantTable *qpool, const BatchFlags *flags,
                       uint32_t nwg);

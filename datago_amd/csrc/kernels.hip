@@ -649,7 +649,8 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
                                                     const WgItem *__restrict__ list,
                                                     const HuffTable *__restrict__ pool,
                                                     const SubState *__restrict__ subs, BatchFlags *flags,
-                                                    const QuantTable *__restrict__ qpool, uint32_t pair) {
+                                                    const QuantTable *__restrict__ qpool, uint32_t pair,
+                                                    const Ckpt *__restrict__ ckpt) {
   extern __shared__ __attribute__((aligned(16))) uint8_t huff_dyn[];  // im.nslots tables (launch: batch max)
   HuffTable *tabs = (HuffTable *)huff_dyn;
   __shared__ __attribute__((aligned(16))) int16_t blk[kSubPerWg][kBlkStride];
@@ -671,9 +672,43 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
   }
   __syncthreads();
   const int t = threadIdx.x;
-  const uint32_t s = it.item0 + t;
-  if (s < im.nsub) {
-    const SubState ss = subs[im.sub_base + s];
+  // Split ranges (ImageDesc.ckpt bit 1, option "write_split"): 128 ranges per
+  // workgroup, each decoded as two halves by lanes t and t + 64 of a wave
+  // pair -- the first half up to the sync pass's half-way checkpoint, the
+  // second from the state recorded there, with the blocks and DC sums before
+  // it taken from the checkpoint's tail.  Twice the lanes at half the chain:
+  // the long 8192-bit ranges that make the sync pass's lead-ins cheap no
+  // longer lengthen the write pass.
+  const bool split = (im.ckpt & 2u) != 0;
+  const uint32_t s = split ? it.item0 + (uint32_t)(t & 63) + ((uint32_t)(t >> 7) << 6) : it.item0 + (uint32_t)t;
+  const uint32_t half = split ? ((uint32_t)t >> 6) & 1u : 0u;
+  bool run = s < im.nsub;
+  uint32_t in = 0, want = 0, a0o = kInf, a1o = kInf;
+  SubState ss = {};
+  if (run) {
+    ss = subs[im.sub_base + s];
+    in = ss.in;
+    want = ss.out;
+    if (split) {
+      const uint32_t S = im.sub_bits, mid = s * S + S / 2, kmid = S / 2 / kCkptBits - 1;
+      const Ckpt c = ckpt[im.ckpt_base + (size_t)s * num_ckpt(S) + kmid];
+      const bool ok = mid < im.ds_bits && im.nmk == 0 && ss.m == 0 && c.m == 0 && st_rel(c.st) < 255u;
+      if (!ok) {
+        run = half == 0;  // the first lane takes the whole range
+      } else if (half == 0) {
+        a1o = mid;
+        want = c.st;
+      } else {
+        a0o = mid;
+        in = c.st;
+        ss.nin += ss.n - c.n;  // blocks started before the checkpoint (tails: checkpoint -> range end)
+        ss.dcin[0] += ss.dc[0] - c.dc[0];
+        ss.dcin[1] += ss.dc[1] - c.dc[1];
+        ss.dcin[2] += ss.dc[2] - c.dc[2];
+      }
+    }
+  }
+  if (run) {
     WriteCtx w;
     w.blk = blk[t];
     w.coef = gp<int16_t>(im.coef);
@@ -701,9 +736,9 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
       for (int i = 0; i < 8; i++) p[i] = zero;
     }
     RangeAcc acc;
-    decode_range<true, HuffTable, true>(im, tabs, gp<const uint8_t>(im.ds), gp<const uint32_t>(im.mk), s, ss.in,
-                                        acc, &w, nullptr, false, 0, nullptr, nullptr, 0xFFu, pair);
-    if (acc.out != ss.out || (s == 0 && (flags->debug & kDbgForceWriteMismatch))) {
+    decode_range<true, HuffTable, true>(im, tabs, gp<const uint8_t>(im.ds), gp<const uint32_t>(im.mk), s, in,
+                                        acc, &w, nullptr, false, 0, nullptr, nullptr, 0xFFu, pair, a0o, a1o);
+    if (acc.out != want || (s == 0 && (flags->debug & kDbgForceWriteMismatch))) {
       // the write pass left this range in another state than the sync pass
       // proved: the blocks after it are not trustworthy.  The image goes back
       // to the caller's CPU decoder (DG_ERR_UNSUPPORTED) unless it is already
@@ -2612,10 +2647,10 @@ void launch_huff_scan(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint3
 }
 void launch_huff_write(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                        const HuffTable *pool, const SubState *subs, BatchFlags *flags, uint32_t max_slots,
-                       const QuantTable *qpool, uint32_t pair) {
+                       const QuantTable *qpool, uint32_t pair, const Ckpt *ckpt) {
   if (!nwg) return;
   hipLaunchKernelGGL(k_huff_write, dim3(nwg), dim3(256), (size_t)max_slots * sizeof(HuffTable), st, imgs, list,
-                     pool, subs, flags, qpool, pair);
+                     pool, subs, flags, qpool, pair, ckpt);
 }
 void launch_idct_list(hipStream_t st, const ImageDesc *imgs, const QuantTable *qpool, const BatchFlags *flags,
                       uint32_t nwg) {

@@ -274,8 +274,10 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (default, 24 KiB), 3 7/5, 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
  *                 the compressed stream prefetched two 16-byte quads ahead per lane
  *   "copy_threads" host threads copying a host-out batch's outputs to the caller's buffers (default 8)
+ *   "write_split" 1 = k_huff_write decodes each entropy range as two halves split at the sync pass's
+ *                 half-way checkpoint (images without restart markers)
  *   "meta_pull"   1 = the GPU reads each batch's descriptors and work lists from page-locked staging (default);
- *                 0 = hipMemcpyAsync
+ *                 2 = also a host batch's coded inputs; 0 = hipMemcpyAsync for both
  *   "plan_threads" host threads parsing a submission's headers (default 4; 1 = the submitting thread only)
  *   "hv_fused"     1 = fuse the first H and V passes of colour JPEGs where they fit (default 0; slower)
  *   "h_mfma"       1 = band H passes on the matrix cores (k_resize_hm, i8 MFMA; default 0: measured slower); 0 = VALU kernel
@@ -289,8 +291,9 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  * "pool_flushes" (times the table pools were started over), "png_chunks", "png_serial_fallbacks",
  * "band_dec_images" (images whose first H pass ran in k_band_dec), "prog_items", "prog_chains" (work items / chains
  * of the pipelined progressive launches), "prog_aggregates", "prog_aggregate_images",
- * "meta_bytes" (the last batch's descriptor/list upload), "allocs", "alloc_mb", "alloc_us", "reclaims"
- * (device / page-locked buffer growth: count, MiB, wall microseconds; OOM reclaims), "host_us_<phase>" / "host_cpu_us_<phase>" (wall / thread
+ * "meta_bytes" (the last batch's descriptor/list upload), "allocs", "alloc_mb", "alloc_us", "reclaims",
+ * "retire_syncs" (device / page-locked buffer growth: count, MiB, wall microseconds; OOM reclaims; device-wide
+ * syncs that freed grown-out buffers), "host_us_<phase>" / "host_cpu_us_<phase>" (wall / thread
  * CPU microseconds in dg_submit* per phase: plan, pools, layout, lists, upload (staging copy), h2d, launch;
  * "host_us_slotwait": waiting for a free slot); -1 if unknown.
  *

@@ -213,11 +213,54 @@ def test_entropy_decode_once_matches(sub_bits):
         assert np.array_equal(arr.reshape(ref.shape), ref), (i, sub_bits)
 
 
+@pytest.mark.parametrize("meta_pull,plan_threads", [(0, 1), (1, 1), (2, 4), (0, 7)])
+def test_upload_and_planning_options_bit_exact(meta_pull, plan_threads):
+    """The descriptor/input upload (meta_pull: GPU-pulled from page-locked
+    staging, or hipMemcpyAsync) and the planning workers (plan_threads) move
+    no pixel: host-in batches (inputs pulled too) and device-resident batches
+    both equal the oracle."""
+    L = _lib()
+    ctx = L.Context(0, crop_and_resize=True, default_image_size=512, downsampling_ratio=16,
+                    min_aspect_ratio=0.5, max_aspect_ratio=2.0, decode_semantics=1)
+    ctx.set_option("meta_pull", meta_pull)
+    ctx.set_option("plan_threads", plan_threads)
+    datas = _rand_jpegs(41, 80, maxdim=500)  # > 2 x 32 images: the workers take part
+    t = B.ARAwareTransform(512, 16, 0.5, 2.0)
+    refs = [_oracle_resized(d, *t.target_size(*O.jpeg_info(d)[1:3]), 1) for d in datas]
+    for _ in range(2):
+        for ref, (st, arr, meta) in zip(refs, ctx.decode_batch(datas)):
+            assert st == 0
+            assert np.array_equal(arr, ref), (meta_pull, plan_threads)
+    assert ctx.stat("meta_bytes") > 0
+
+
+@pytest.mark.parametrize("sub_bits", [1024, 4096, 8192])
+def test_write_split_bit_exact(sub_bits):
+    """Option write_split: k_huff_write decodes each range as two halves, the
+    second from the sync pass's half-way checkpoint with the blocks and DC
+    sums before it taken from the checkpoint's tail.  Bit-exact against the
+    oracle, with restart markers (no split), gray, 4:2:2 and 4:4:4, ranges
+    shorter than half a subsequence, and no write mismatch."""
+    L = _lib()
+    datas = _rand_jpegs(12, 12, maxdim=1400) + _rand_jpegs(13, 4, maxdim=900, rst=True)
+    datas.append(synth.make_jpeg(89, 2400, 1600, 92, "4:2:0", False))
+    datas.append(synth.make_jpeg(90, 1800, 1200, 60, "4:4:4", False))
+    ctx = L.Context(0)
+    ctx.set_option("write_split", 1)
+    ctx.set_option("sub_bits", sub_bits)
+    for i, (d, (st, arr, _)) in enumerate(zip(datas, ctx.decode_batch(datas))):
+        assert st == 0, i
+        ost, ref = O.jpeg_decode(d)
+        assert np.array_equal(arr.reshape(ref.shape), ref), (i, sub_bits)
+    assert ctx.stat("write_mismatch") == 0
+
+
 def test_band_and_slot_options_validated():
     L = _lib()
     ctx = L.Context(0)
     for k, v in (("hb_bands", 0), ("hb_bands", 65), ("slots", 0), ("slots", 7), ("inf_decode", -1),
-                 ("inf_decode", 8), ("uf_units", 0), ("uf_units", 3)):
+                 ("inf_decode", 8), ("uf_units", 0), ("uf_units", 3), ("plan_threads", 0), ("inf_chunk", 1000),
+                 ("inf_chunk", 2048), ("sub_auto", 3000), ("meta_pull", 3)):
         with pytest.raises(Exception):
             ctx.set_option(k, v)
 

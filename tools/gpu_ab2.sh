@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU tests (FILES / K subset, TESTS=0 to skip), then the headline bench
 # alternating the default and variants (AB="k=v k2=v2;k3=v3": ';'-separated
-# variants of space-separated context options), REPS rounds.
+# variants of space-separated context options, or bench arguments written
+# --flag=value), REPS rounds.
 #   OUT=gpurun_out/x AB="chroma_rec=0;destuff_one=0" FILES="tests/test_gpu_parity.py" tools/gpu_ab2.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -23,7 +24,8 @@ IFS=';' read -ra ABS <<< "$AB"
 for r in $(seq 1 $REPS); do
   for k in $(seq 0 ${#ABS[@]}); do
     if [ $k -eq 0 ]; then cfg=""; tag=base_$r; else
-      cfg=""; for o in ${ABS[$((k-1))]}; do cfg="$cfg --ctx-opt $o"; done; tag=ab${k}_$r; fi
+      cfg=""; for o in ${ABS[$((k-1))]}; do case $o in --*) cfg="$cfg ${o/=/ }";; *) cfg="$cfg --ctx-opt $o";; esac; done
+      tag=ab${k}_$r; fi
     timeout -k 10 400 python bench.py --steps $STEPS --warmup 3 --e2e-steps 0 --one-threads 0 --no-cpu-baseline \
       $EXTRA $cfg --out $OUT/$tag.json > $OUT/$tag.log 2>&1
     rc=$?; echo "=== $tag [$cfg] exit $rc"; [ $rc -eq 0 ] || { tail -20 $OUT/$tag.log; exit $rc; }

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc
+OUT=${OUT:-gpurun_out/pmc}
 mkdir -p $OUT
 ARGS="--steps ${STEPS:-2} --warmup 1 --batch ${BATCH:-256} --pool ${POOL:-4096} --no-cpu-baseline --e2e-steps 0 --one-threads 0 --serial-steps 0"
 run() {  # name counters...
