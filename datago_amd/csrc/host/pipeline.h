@@ -348,7 +348,7 @@ class Context {
   uint32_t inf_chunk_ = kInfChunk;  // option "inf_chunk"
   int plan_threads_ = 4;            // option "plan_threads"
   int meta_pull_ = 1;               // option "meta_pull"
-  bool write_split_ = false;        // option "write_split"
+  bool write_split_ = true;         // option "write_split"
   static constexpr int kPlanGrain = 32;  // images per planning work piece
   std::unique_ptr<HostPool> plan_pool_;
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"

@@ -275,7 +275,7 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *                 the compressed stream prefetched two 16-byte quads ahead per lane
  *   "copy_threads" host threads copying a host-out batch's outputs to the caller's buffers (default 8)
  *   "write_split" 1 = k_huff_write decodes each entropy range as two halves split at the sync pass's
- *                 half-way checkpoint (images without restart markers)
+ *                 half-way checkpoint (images without restart markers; default); 0 = one lane per range
  *   "meta_pull"   1 = the GPU reads each batch's descriptors and work lists from page-locked staging (default);
  *                 2 = also a host batch's coded inputs; 0 = hipMemcpyAsync for both
  *   "plan_threads" host threads parsing a submission's headers (default 4; 1 = the submitting thread only)

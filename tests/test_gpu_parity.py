@@ -234,8 +234,8 @@ def test_upload_and_planning_options_bit_exact(meta_pull, plan_threads):
     assert ctx.stat("meta_bytes") > 0
 
 
-@pytest.mark.parametrize("sub_bits", [1024, 4096, 8192])
-def test_write_split_bit_exact(sub_bits):
+@pytest.mark.parametrize("sub_bits,split", [(1024, 1), (4096, 1), (8192, 1), (8192, 0)])
+def test_write_split_bit_exact(sub_bits, split):
     """Option write_split: k_huff_write decodes each range as two halves, the
     second from the sync pass's half-way checkpoint with the blocks and DC
     sums before it taken from the checkpoint's tail.  Bit-exact against the
@@ -246,7 +246,7 @@ def test_write_split_bit_exact(sub_bits):
     datas.append(synth.make_jpeg(89, 2400, 1600, 92, "4:2:0", False))
     datas.append(synth.make_jpeg(90, 1800, 1200, 60, "4:4:4", False))
     ctx = L.Context(0)
-    ctx.set_option("write_split", 1)
+    ctx.set_option("write_split", split)
     ctx.set_option("sub_bits", sub_bits)
     for i, (d, (st, arr, _)) in enumerate(zip(datas, ctx.decode_batch(datas))):
         assert st == 0, i
