@@ -965,6 +965,28 @@ def main() -> int:
                "coalesce_max": 64, "coalesce_us": 500, "prog_lanes": a.prog_lanes,
                "note": "host JPEG bytes in -> host RGB out per call (PCIe both ways) into a reused page-locked "
                        "buffer per thread (dg_host_register), like e2e_host_mpix_s"}
+        # the same calls from native threads (tools/one_bench, linked to the library): the Rust glue's
+        # tokio workers are native; Python threads also contend for the interpreter lock between calls
+        native = os.path.join(ROOT, "tools", "one_bench")
+        if os.path.exists(native) and all(forced_pool[i] < 0 for i in order):
+            import struct
+            import subprocess
+            import tempfile
+            with tempfile.NamedTemporaryFile(prefix="one_pool_", suffix=".bin", delete=False) as tf:
+                tf.write(struct.pack("<I", len(order)))
+                for i in order:
+                    tf.write(struct.pack("<Q", len(pool[i])))
+                    tf.write(pool[i])
+            try:
+                r = subprocess.run([native, tf.name, str(a.one_threads), str(len(order)), str(a.size), str(a.ratio),
+                                    str(a.decode_semantics)] + list(a.ctx_opt),
+                                   capture_output=True, text=True, timeout=300)
+                one["native_threads"] = (json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else
+                                         {"error": r.returncode, "stderr": r.stderr[-300:]})
+            except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+                one["native_threads"] = {"error": str(e)[:200]}
+            finally:
+                os.unlink(tf.name)
 
     result = None
     if rank == 0:

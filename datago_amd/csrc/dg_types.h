@@ -120,7 +120,7 @@ constexpr uint32_t kHVRows = 64;      // k_resize_hv: V output rows per workgrou
 constexpr uint32_t kHBandRows = 8;    // rows per workgroup of the band H kernel
 constexpr uint32_t kHBandCols = 128;  // output columns per workgroup
 constexpr uint32_t kIdctItemStride = 4;  // k_idct_t: L_IDCT items per workgroup (one per wave)
-constexpr uint32_t kVItemUnits = 4;      // k_resize_v: 256-unit strides per workgroup item
+
 constexpr uint32_t kHSegPx = 640;     // LDS source segment (pixels) per row
 constexpr uint32_t kHBandsDefault = 16;  // default ResizePass::bands (8 -> 16: +1.5% overlapped, profiles/r02/bands)
 

@@ -542,6 +542,16 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     decode_sem_ = (int)v;
     return DG_OK;
   }
+  if (k == "v_units") {  // k_resize_v: 256-unit strides per workgroup item
+    if (v < 1 || v > 8) return DG_ERR_INVALID;
+    v_units_ = (uint32_t)v;
+    return DG_OK;
+  }
+  if (k == "lead_big") {  // auto lead-in of images with >= 4-block MCUs (4:2:0), bits
+    if (v < 0 || v > (1 << 16)) return DG_ERR_INVALID;
+    lead_big_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "write_split") {  // 1: k_huff_write decodes each range as two halves (see k_huff_write)
     write_split_ = v != 0;
     return DG_OK;
@@ -1372,7 +1382,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     // lead-in before each subsequence (lead_in in dg_entropy.h): covers the
     // self-synchronisation distance, which is longest for 6-block MCUs
     // (4:2:0; p99.9 ~7 kbit on the bench corpus, tools/sync_stats.cpp)
-    d.lead_bits = lead_bits_ >= 0 ? (uint32_t)lead_bits_ : (bpm >= 4 ? 6144u : 2048u);
+    d.lead_bits = lead_bits_ >= 0 ? (uint32_t)lead_bits_ : (bpm >= 4 ? lead_big_ : 2048u);
     // shorter ranges of symbol-dense images get a proportionally shorter lead-in (option
     // "lead_density"): their codes are short, so the decoder self-synchronises in fewer bits
     if (lead_density_ && lead_bits_ < 0 && d.sub_bits < sub_bits)
@@ -1883,7 +1893,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
           for (uint32_t it = 0; it < cnt; it++) hb[s / 2][fused][cls].push_back({I, it});
       } else {
         uint32_t cnt = (ps.width * ps.C + 15) / 16 * ps.rows;
-        for (uint32_t it = 0; it < cnt; it += 256 * kVItemUnits) b.lists[L_RH0 + s].push_back({I, it});
+        for (uint32_t it = 0; it < cnt; it += 256 * v_units_) b.lists[L_RH0 + s].push_back({I, it});
       }
     }
     if (d.copy_needed) {
@@ -2367,14 +2377,14 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_resize_hv(sl.st, dd, lst(L_RHV), b.hvclass);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
-  launch_resize_v(sl.st, dd, lst(L_RV1), cnt(L_RV1), 1);
+  launch_resize_v(sl.st, dd, lst(L_RV1), cnt(L_RV1), 1, v_units_);
   launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_hm(sl.st, dd, lst(L_RM2), b.hmclass[1], 2);
   launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2, h_prefetch_);
   launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
-  launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3);
+  launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3, v_units_);
   launch_alpha(sl.st, dd, lst(L_ALPHA2), cnt(L_ALPHA2), 2 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_copy(sl.st, dd, lst(L_COPY), cnt(L_COPY));

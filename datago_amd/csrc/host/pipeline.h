@@ -349,6 +349,8 @@ class Context {
   int plan_threads_ = 4;            // option "plan_threads"
   int meta_pull_ = 1;               // option "meta_pull"
   bool write_split_ = true;         // option "write_split"
+  uint32_t lead_big_ = 4096;        // option "lead_big" (6144 -> 4096 with 8192-bit ranges: +1.3%, profiles/r04/lead_big)
+  uint32_t v_units_ = 4;            // option "v_units"
   static constexpr int kPlanGrain = 32;  // images per planning work piece
   std::unique_ptr<HostPool> plan_pool_;
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"

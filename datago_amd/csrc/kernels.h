@@ -57,7 +57,8 @@ void launch_resize_hm(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
                       int stage);
 // fused first H + V pass (pass[0].mode & kHVFused): lists of H weight classes <= 8, <= 16 taps
 void launch_resize_hv(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2]);
-void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage);
+void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage,
+                     uint32_t vunits);
 // k_band_dec (dg_band.hip): IDCT + upsampling + colour + the first H pass of images with pass[0].mode &
 // kHDecode; list = ncls[0] items of the 320-pixel class, then ncls[1] of the 640-pixel class
 void launch_band_dec(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2],

@@ -2441,7 +2441,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   }
 }
 
-constexpr uint32_t kVUnitsPerThread = kVItemUnits;
 
 // Vertical pass: each thread produces 16 consecutive bytes of one output row
 // (channel-agnostic), one 16-byte load per tap: a wave streams 1 KiB of a
@@ -2449,12 +2448,13 @@ constexpr uint32_t kVUnitsPerThread = kVItemUnits;
 __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ imgs,
                                                   const WgItem *__restrict__ list, int stage) {
   const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
-  const ResizePass &ps = imgs[it.image].pass[stage];
+  // stage in bits 0-7; bits 8+: consecutive 256-unit strides per workgroup
+  // item (option "v_units"; the host lists one item per v_units * 256 units)
+  const uint32_t vunits = (uint32_t)stage >> 8;
+  const ResizePass &ps = imgs[it.image].pass[stage & 0xFF];
   const uint32_t rowbytes = ps.width * ps.C;
   const uint32_t units = (rowbytes + 15) / 16;
-  // kVUnitsPerThread consecutive 256-unit strides per workgroup item (the
-  // host lists one item per kVUnitsPerThread * 256 units)
-  for (uint32_t kv = 0; kv < kVUnitsPerThread; kv++) {
+  for (uint32_t kv = 0; kv < vunits; kv++) {
   const uint32_t idx = it.item0 + kv * 256 + threadIdx.x;
   if (idx >= units * ps.rows) return;
   const uint32_t y = idx / units, u = idx - y * units;
@@ -2710,8 +2710,9 @@ void launch_resize_hv(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
   DG_LAUNCH(k_resize_hv<8>, ncls[0], st, imgs, list);
   DG_LAUNCH(k_resize_hv<16>, ncls[1], st, imgs, list + ncls[0]);
 }
-void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage) {
-  DG_LAUNCH(k_resize_v, nwg, st, imgs, list, stage);
+void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage,
+                     uint32_t vunits) {
+  DG_LAUNCH(k_resize_v, nwg, st, imgs, list, stage | (int)(vunits << 8));
 }
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   DG_LAUNCH(k_copy, nwg, st, imgs, list);

@@ -15,6 +15,6 @@ for t in ${THREADS:-32}; do
     cfg=""; for x in $o; do cfg="$cfg --ctx-opt $x"; done
     name=t${t}_$k
     timeout -k 10 400 python bench.py $B ${ONE_EXTRA:-} --one-threads $t $cfg --out $OUT/$name.json > $OUT/$name.log 2>&1 || exit $?
-    python -c "import json;d=json.load(open('$OUT/$name.json'));o=d['e2e_decode_one'];print('$name [$o]',o['mpix_s'],o['images_per_s'],o['mean_images_per_batch'])"
+    python -c "import json;d=json.load(open('$OUT/$name.json'));o=d['e2e_decode_one'];print('$name [$o]',o['mpix_s'],o['images_per_s'],o['mean_images_per_batch'],'native',o.get('native_threads'))"
   done
 done

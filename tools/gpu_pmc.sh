@@ -1,5 +1,6 @@
 #!/bin/bash
-# Hardware-counter passes over a short bench run (one rocprofv3 --pmc pass per
+# Hardware-counter passes over a short bench run, one batch in flight so that
+# dispatch order maps kernels to stages exactly (one rocprofv3 --pmc pass per
 # counter group; never combined with runtime/sys traces).  Output under
 # gpurun_out/pmc/<pass>/; summarise with tools/pmc_summary.py.
 set -u
@@ -7,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc}
 mkdir -p $OUT
-ARGS="--steps ${STEPS:-2} --warmup 1 --batch ${BATCH:-256} --pool ${POOL:-4096} --no-cpu-baseline --e2e-steps 0 --one-threads 0 --serial-steps 0"
+ARGS="--steps ${STEPS:-2} --warmup 1 --batch ${BATCH:-256} --pool ${POOL:-4096} --inflight ${INFLIGHT:-1} ${PMC_EXTRA:-} --no-cpu-baseline --e2e-steps 0 --one-threads 0 --serial-steps 0"
 run() {  # name counters...
   local name=$1; shift
   echo "=== pmc $name: $*"
