@@ -350,7 +350,7 @@ class Context {
   int meta_pull_ = 1;               // option "meta_pull"
   bool write_split_ = true;         // option "write_split"
   uint32_t lead_big_ = 4096;        // option "lead_big" (6144 -> 4096 with 8192-bit ranges: +1.3%, profiles/r04/lead_big)
-  uint32_t v_units_ = 4;            // option "v_units"
+  uint32_t v_units_ = 2;            // option "v_units" (profiles/r04/v_units: 1 / 2 / 4 -> V traffic 1.95 / ? / 3.91 GB per batch)
   static constexpr int kPlanGrain = 32;  // images per planning work piece
   std::unique_ptr<HostPool> plan_pool_;
   uint32_t hb_bands_ = kHBandsDefault;  // option "hb_bands"

@@ -228,7 +228,7 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "sub_bits"    entropy-decoder subsequence size in bits (multiple of 32,
  *                 64..65536; 0 = auto per batch, the default)
  *   "lead_bits"   entropy lead-in before each subsequence (-1 = auto per image)
- *   "v_units"     k_resize_v: 256-unit (4 KiB) strides per workgroup item, 1..8 (default 4)
+ *   "v_units"     k_resize_v: 256-unit (4 KiB) strides per workgroup item, 1..8 (default 2)
  *   "lead_big"    the auto lead-in of images with 4- or 6-block MCUs (default 4096; others 2048)
  *   "coalesce_max" dg_decode_one: most images merged into one GPU batch (1 = off; default 64)
  *   "coalesce_us" dg_decode_one: longest wait for other callers (default 500)
