@@ -73,10 +73,11 @@ int main(int argc, char **argv) {
         fails++;
     }
   };
-  // warm-up: one pass over a few images per thread (allocations, table pools)
+  // warm-up: one untimed pass over every image (buffer growth, table pools;
+  // bench.py's Python leg runs on a context the whole bench has warmed)
   {
     std::vector<std::thread> ts;
-    for (int t = 0; t < threads; t++) ts.emplace_back(work, t, std::min<int>(2 * threads, images));
+    for (int t = 0; t < threads; t++) ts.emplace_back(work, t, images);
     for (auto &t : ts) t.join();
   }
   next = 0;
