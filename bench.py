@@ -962,7 +962,8 @@ def main() -> int:
         one = {"threads": a.one_threads, "images": n_one, "failed": sum(fails),
                "mpix_s": round(sum(done_px) / dt1 / 1e6, 2), "images_per_s": round(n_one / dt1, 1),
                "gpu_batches": nb_, "mean_images_per_batch": round((ctx.stat("coalesced_images") - i0) / max(nb_, 1), 1),
-               "coalesce_max": 64, "coalesce_us": 500, "prog_lanes": a.prog_lanes,
+               "coalesce_max": 64, "coalesce_us": 500, "coalesce_inflight": ctx.stat("coalesce_inflight"),
+               "prog_lanes": a.prog_lanes,
                "note": "host JPEG bytes in -> host RGB out per call (PCIe both ways) into a reused page-locked "
                        "buffer per thread (dg_host_register), like e2e_host_mpix_s"}
         # the same calls from native threads (tools/one_bench, linked to the library): the Rust glue's

@@ -641,6 +641,7 @@ int64_t Context::get_stat(const std::string &k) {
   }
   if (k == "sub_bits") return last_sub_bits_;
   if (k == "sub_auto") return sub_auto_;
+  if (k == "coalesce_inflight") return coalesce_inflight_;
   if (k == "meta_bytes") return (int64_t)last_meta_bytes_;
   if (k == "allocs") return stat_allocs_;
   if (k == "alloc_mb") return stat_alloc_mb_;

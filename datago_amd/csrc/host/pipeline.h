@@ -310,7 +310,9 @@ class Context {
   bool sync_pair_ = false;   // option "sync_pair": the same in k_huff_sync (measured slower beside multi_lead: off)
   bool prog_side_ = false;  // option "prog_side": progressive scans on the side stream (measured slower: off)
   int coalesce_max_ = 64, coalesce_us_ = 500;
-  int coalesce_inflight_ = 0;  // option "coalesce_inflight": coalesced batches in flight (0 = nslots_)
+  // option "coalesce_inflight": coalesced batches in flight (0 = nslots_); 3 fills the batches better
+  // (7.6 vs 5.4 images) and measured 5-20% faster than 4 from 32 callers (profiles/r04/one_r4*)
+  int coalesce_inflight_ = 3;
   int64_t stat_coalesced_batches_ = 0, stat_coalesced_images_ = 0;
   dg_status flush_batch(std::vector<OneReq *> &batch, bool prog);
 

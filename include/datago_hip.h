@@ -232,6 +232,7 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "lead_big"    the auto lead-in of images with 4- or 6-block MCUs (default 4096; others 2048)
  *   "coalesce_max" dg_decode_one: most images merged into one GPU batch (1 = off; default 64)
  *   "coalesce_us" dg_decode_one: longest wait for other callers (default 500)
+ *   "coalesce_inflight" dg_decode_one: coalesced batches in flight (0 = "slots"; default 3)
  *   "wg_timing"   debug: per-workgroup timestamps of the entropy kernels
  *   "timing"      1 = record per-kernel HIP events (dg_last_batch_timings)
  *   "side_stream" 1 = Lanczos tables on a second stream (default 1)
