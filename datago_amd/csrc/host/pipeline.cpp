@@ -751,7 +751,12 @@ dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
   // only cost configs[1] 1.4 ms of submit time per batch: the extra growths
   // retired enough to trigger device-wide syncs.)  Under memory pressure the
   // retired buffers go first, then the headroom.
-  size_t cap = grow_cap(bytes, true);
+  // no headroom once the device is three quarters full (several ranks or
+  // contexts sharing one device: 8 ranks x 4 slots x 1.5 ran a 288 GB device
+  // out of memory, profiles/r04/ranks_r4f)
+  size_t dfree = 0, dtotal = 0;
+  const bool roomy = hipMemGetInfo(&dfree, &dtotal) != hipSuccess || dfree > dtotal / 4 + bytes;
+  size_t cap = grow_cap(bytes, roomy);
   const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipMalloc(&b.p, cap);
   if (e != hipSuccess && reclaim()) {
