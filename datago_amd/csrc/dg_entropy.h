@@ -475,10 +475,11 @@ DG_HD void stage_finish(StageCtx &c) {
 // stops and completes its totals with the stored tail.  This cuts a re-decode
 // from a full range to about the self-synchronisation distance.
 constexpr uint32_t kCkptBits = 256;
-// enough for sub_bits <= 4096, and for the half-way checkpoint of an 8192-
-// or 16384-bit range (index 15 / 31), where k_huff_write splits a range
-// (write_split)
-constexpr uint32_t kMaxCkpt = 32;
+// enough for sub_bits <= 4096, and for the half-way checkpoint of an
+// 8192-bit range (index 15), where k_huff_write splits a range (write_split).
+// (32, for split 16384-bit ranges: sub_auto 16384 measured no faster,
+// profiles/r04/sub16k)
+constexpr uint32_t kMaxCkpt = 16;
 struct Ckpt {
   uint32_t st;   // packed state (rel past the checkpoint position, r, z)
   uint32_t m, n; // tail (segmented: m > 0 means the tail contains a reset)
