@@ -54,6 +54,8 @@ HOST_PHASES = ("plan", "pools", "layout", "lists", "upload", "h2d", "launch", "s
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process and its ranks (0: leave the runtime's default; <= 32)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0, help="images per step (0: 256, or 1024 for wds's ImageNet-size JPEGs)")
@@ -542,6 +544,8 @@ def pin_rank_cores(local: int, local_world: int):
 
 def main() -> int:
     a = parse()
+    if a.hw_queues > 0:  # before anything initialises HIP (ranks inherit it)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(a.hw_queues, 32))
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         return launch_ranks(a.gpus)
     rank = int(os.environ.get("RANK", "0"))
