@@ -1818,7 +1818,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   phase(2);
   // ---- 5. workgroup lists
-  for (auto &l : b.lists) l.clear();
+  for (int l = 0; l < L_COUNT; l++) {  // sized from the previous batch: no regrowth copies
+    b.lists[l].clear();
+    b.lists[l].reserve(list_hint_[l] + list_hint_[l] / 4);
+  }
   std::vector<WgItem> hb[2][2][4];  // band H items per (stage, fused fill, weight-count class)
   std::vector<WgItem> hvl[2];       // k_resize_hv items per H weight class
   std::vector<WgItem> decl[2];      // k_band_dec items per segment class
@@ -1919,6 +1922,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       b.lists[L_ENC_IMG].push_back({I, 0});
     }
   }
+  for (int l = 0; l < L_COUNT; l++) list_hint_[l] = b.lists[l].size();
   if (entropy_lpt_) {
     // Entropy workgroups decode a fixed number of bits, but their time follows
     // the symbol count: images with few coded bits per block (low quality,

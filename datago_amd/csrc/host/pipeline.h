@@ -350,6 +350,7 @@ class Context {
   uint32_t inf_chunk_ = kInfChunk;  // option "inf_chunk"
   int plan_threads_ = 4;            // option "plan_threads"
   int meta_pull_ = 1;               // option "meta_pull"
+  size_t list_hint_[L_COUNT] = {};  // work-list sizes of the previous batch (reserve)
   bool write_split_ = true;         // option "write_split"
   uint32_t lead_big_ = 4096;        // option "lead_big" (6144 -> 4096 with 8192-bit ranges: +1.3%, profiles/r04/lead_big)
   uint32_t v_units_ = 2;            // option "v_units" (profiles/r04/v_units: 1 / 2 / 4 -> V traffic 1.95 / ? / 3.91 GB per batch)
