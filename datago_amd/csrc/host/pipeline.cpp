@@ -1387,7 +1387,10 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     if (d.idct_fused) b.any_fused = true;
     // lead-in before each subsequence (lead_in in dg_entropy.h): covers the
     // self-synchronisation distance, which is longest for 6-block MCUs
-    // (4:2:0; p99.9 ~7 kbit on the bench corpus, tools/sync_stats.cpp)
+    // (4:2:0; p99.9 ~7 kbit on the bench corpus, tools/sync_stats.cpp).
+    // Option "lead_big" (4096): shorter than that tail, but a wrong entry
+    // guess only costs a re-decode up to the first checkpoint where it merges
+    // (6144 -> 4096: +1.3% on configs[1]; 2048 / 1024 slower on configs[2])
     d.lead_bits = lead_bits_ >= 0 ? (uint32_t)lead_bits_ : (bpm >= 4 ? lead_big_ : 2048u);
     // shorter ranges of symbol-dense images get a proportionally shorter lead-in (option
     // "lead_density"): their codes are short, so the decoder self-synchronises in fewer bits
