@@ -1896,7 +1896,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         // k_resize_hb<K> reads taps in even-aligned pairs: a window starting
         // at an odd segment position spans ksize + 1 positions
         const uint32_t kk = ps.ksize + 1;
-        const int cls = kk <= 8 ? 0 : kk <= 16 ? 1 : kk <= 32 ? 2 : 3;
+        int cls = kk <= 8 ? 0 : kk <= 16 ? 1 : kk <= 32 ? 2 : 3;
+        // the 8- and 16-tap kernels stage narrower segments (hseg_px in kernels.hip)
+        while (cls < 2 && h_pass_span(ps) > (cls == 0 ? 192.0 : 384.0)) cls++;
         const int fused = (ps.mode & kHFused) ? 1 : 0;
         const uint32_t ks = h_mfma_ ? h_mfma_steps(ps) : 0u;
         if (ks)

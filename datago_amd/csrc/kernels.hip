@@ -1899,6 +1899,13 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
     }
 }
 
+// LDS source segment (pixels per row) of a band H kernel, per weight class:
+// a window of <= 8 taps means a downscale of at most ~1.2x, <= 16 taps at most
+// ~2.5x, so 128 output columns read at most 192 / 384 source pixels (the host
+// promotes a pass to the next class when h_pass_span says otherwise).  The
+// smaller segments let 8 workgroups share a CU instead of 6 (LDS-bound).
+constexpr uint32_t hseg_px(int kmax) { return kmax == 8 ? 192u : kmax == 16 ? 384u : kHSegPx; }
+
 // FUSED: the first pass of a colour JPEG (fill = upsample + colour
 // conversion from the planes, C = 3); otherwise the fill copies interleaved
 // bytes of C = 1..4 channels.  Separate kernels so each allocates registers
@@ -1906,7 +1913,7 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
 template <int KMAX, bool FUSED, int FC = FC_GENERIC, bool PF = false>
 __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps, uint32_t item, uint32_t *seg,
                                       uint8_t *ob, uint32_t *ext) {
-  constexpr uint32_t SEGPX = kHSegPx;
+  constexpr uint32_t SEGPX = hseg_px(KMAX), SS = SEGPX + 8;  // pixels per row; row stride (dwords)
   // one workgroup: a tile of kHBandCols output columns x ps.bands bands of
   // kHBandRows rows; the column tile's weights, source extent and descriptor
   // reads are set up once and reused for every band
@@ -1997,10 +2004,10 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
           const FillRaw f = (PREFETCH && j == t) ? pre : hload_fc8<FC>(im, ps.row0 + y0 + r, p0 + 8 * q);
           hcolor_fc8<FC>(im, f, p0 + 8 * q, v);
         }
-        hput8(v, seg + r * kHSegStride + 8 * q);
+        hput8(v, seg + r * SS + 8 * q);
       } else {
         const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(ps.row0 + y0 + r) * ps.src_stride;
-        hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * q, seg + r * kHSegStride + 4 * q);
+        hfill_bytes4(src, C, ps.src_stride, ps.in_size, p0 + 4 * q, seg + r * SS + 4 * q);
       }
     }
     __syncthreads();
@@ -2017,13 +2024,13 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
     // phase 2: convolve (thread: column col, rows r0, r0 + 2, ...)
     if (valid) {
       if (FUSED || C == 3)
-        hconv_rows<KMAX, 3>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
+        hconv_rows<KMAX, 3, SS>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
       else if (C == 1)
-        hconv_rows<KMAX, 1>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
+        hconv_rows<KMAX, 1, SS>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
       else if (C == 4)
-        hconv_rows<KMAX, 4>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
+        hconv_rows<KMAX, 4, SS>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
       else
-        hconv_rows<KMAX, 2>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
+        hconv_rows<KMAX, 2, SS>(seg, off, kw2, kp, ksize, n, r0, nrows, prec, ob, col);
     }
     __syncthreads();
     // phase 3: store the band's rows, 16 bytes per thread per step (the next
@@ -2045,12 +2052,14 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
 }
 
 // Register budget for 5 waves per SIMD (<= 96 VGPRs; every variant fits
-// without scratch: 66-95 VGPRs).  A 4-wave budget measured slower
-// (resize_h1 2.81-2.90 vs 2.69-2.74 ms) and is no longer built.
+// without scratch: 64-95 VGPRs).  A 4-wave budget measured slower
+// (resize_h1 2.81-2.90 vs 2.69-2.74 ms) and is no longer built.  The 8-tap
+// kernels fit 6 waves (80 VGPRs, no scratch; their 10 KiB of LDS allows it);
+// the 16-tap ones would spill at 6.
 template <int KMAX, bool FUSED, bool PF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_resize_hb(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX == 8 ? 6 : 5))) void k_resize_hb(
     const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list, int stage) {
-  __shared__ __attribute__((aligned(16))) uint32_t seg[kHBandRows * kHSegStride];
+  __shared__ __attribute__((aligned(16))) uint32_t seg[kHBandRows * (hseg_px(KMAX) + 8)];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kHBandRows * kHBandCols * 4];
   __shared__ uint32_t ext[2];
   const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
