@@ -542,6 +542,21 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     decode_sem_ = (int)v;
     return DG_OK;
   }
+  if (k == "small_coded") {  // batches under this many coded bytes take sub_small / lead_small (0 = off)
+    if (v < 0) return DG_ERR_INVALID;
+    small_coded_ = (uint64_t)v;
+    return DG_OK;
+  }
+  if (k == "sub_small") {
+    if (v < 64 || v > 65536 || (v & (v - 1))) return DG_ERR_INVALID;
+    sub_small_ = (uint32_t)v;
+    return DG_OK;
+  }
+  if (k == "lead_small") {
+    if (v < 0 || v > (1 << 16)) return DG_ERR_INVALID;
+    lead_small_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "v_units") {  // k_resize_v: 256-unit strides per workgroup item
     if (v < 1 || v > 8) return DG_ERR_INVALID;
     v_units_ = (uint32_t)v;
@@ -1186,13 +1201,20 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   // (round 4: 8192, profiles/r04/ab -- the chip stays full with half the
   // lanes once the write pass no longer decodes, and the 6 kbit lead-in of a
   // 4:2:0 range costs 75% instead of 150% of its bits).
+  // Small batches (dg_decode_one's few images, option "small_coded" bytes of
+  // coded data) are latency-bound: a lane's chain of lead-in + range bits is
+  // the batch's k_huff_sync time (0.87 ms of a ~3 ms coalesced batch in the
+  // decode_one trace, profiles/r04/one_trace), so they take short ranges and
+  // lead-ins ("sub_small", "lead_small") at the cost of more total decode.
   uint32_t sub_bits = sub_bits_;
+  bool small = false;
   if (!sub_bits) {
     uint64_t coded = 0;
     for (int i = 0; i < n; i++)
       if (!b.plans[i].status && b.plans[i].fmt == kFmtJpeg && !b.plans[i].hdr.progressive)
         coded += b.plans[i].hdr.scan_end - b.plans[i].hdr.scan_off;
-    sub_bits = coded >= (64ull << 20) ? sub_auto_ : 2048u;
+    small = coded < small_coded_;
+    sub_bits = coded >= (64ull << 20) ? sub_auto_ : small ? sub_small_ : 2048u;
   }
   last_sub_bits_ = sub_bits;
   Layout L;        // scratch arena
@@ -1391,7 +1413,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     // Option "lead_big" (4096): shorter than that tail, but a wrong entry
     // guess only costs a re-decode up to the first checkpoint where it merges
     // (6144 -> 4096: +1.3% on configs[1]; 2048 / 1024 slower on configs[2])
-    d.lead_bits = lead_bits_ >= 0 ? (uint32_t)lead_bits_ : (bpm >= 4 ? lead_big_ : 2048u);
+    d.lead_bits = lead_bits_ >= 0 ? (uint32_t)lead_bits_ : small ? lead_small_ : (bpm >= 4 ? lead_big_ : 2048u);
     // shorter ranges of symbol-dense images get a proportionally shorter lead-in (option
     // "lead_density"): their codes are short, so the decoder self-synchronises in fewer bits
     if (lead_density_ && lead_bits_ < 0 && d.sub_bits < sub_bits)

@@ -353,6 +353,8 @@ class Context {
   size_t list_hint_[L_COUNT] = {};  // work-list sizes of the previous batch (reserve)
   bool write_split_ = true;         // option "write_split"
   uint32_t lead_big_ = 4096;        // option "lead_big" (6144 -> 4096 with 8192-bit ranges: +1.3%, profiles/r04/lead_big)
+  uint64_t small_coded_ = 0;        // option "small_coded" (0: off)
+  uint32_t sub_small_ = 512, lead_small_ = 1024;  // options "sub_small", "lead_small"
   uint32_t v_units_ = 2;            // option "v_units" (profiles/r04/v_units: 1 / 2 / 4 -> V traffic 1.95 / ? / 3.91 GB per batch)
   static constexpr int kPlanGrain = 32;  // images per planning work piece
   std::unique_ptr<HostPool> plan_pool_;

@@ -228,6 +228,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "sub_bits"    entropy-decoder subsequence size in bits (multiple of 32,
  *                 64..65536; 0 = auto per batch, the default)
  *   "lead_bits"   entropy lead-in before each subsequence (-1 = auto per image)
+ *   "small_coded" batches under this many bytes of coded data take "sub_small" (512) bit ranges and
+ *                 "lead_small" (1024) bit lead-ins (default 0 = off; measured slower for dg_decode_one)
  *   "v_units"     k_resize_v: 256-unit (4 KiB) strides per workgroup item, 1..8 (default 2)
  *   "lead_big"    the auto lead-in of images with 4- or 6-block MCUs (default 4096; others 2048)
  *   "coalesce_max" dg_decode_one: most images merged into one GPU batch (1 = off; default 64)
