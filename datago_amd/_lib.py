@@ -10,8 +10,10 @@ loads it via DT_NEEDED "libamdhip64.so"; our library's DT_NEEDED
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
+import weakref
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -247,17 +249,16 @@ def _as_ptr_array(ptrs: Sequence[int]):
     """Pointer array argument: a uint64 numpy array is passed in place, a
     sequence of ints is converted in one call (no per-element assignment)."""
     if isinstance(ptrs, np.ndarray):
-        a = np.ascontiguousarray(ptrs, dtype=np.uint64)
-        if a.size == 0:
-            a = np.zeros(1, np.uint64)
-        return (ctypes.c_void_p * a.size).from_buffer(a)
+        return _as_array(ctypes.c_void_p, np.uint64, ptrs, ptrs.size)
     return (ctypes.c_void_p * max(1, len(ptrs)))(*ptrs)
 
 
 def _as_array(ctype, npdtype, vals, n: int):
-    """Typed array argument (numpy arrays in place, like _as_ptr_array)."""
+    """Typed array argument (numpy arrays in place, like _as_ptr_array; a
+    read-only or non-contiguous array is copied: from_buffer needs a
+    writable buffer)."""
     if isinstance(vals, np.ndarray):
-        a = np.ascontiguousarray(vals, dtype=npdtype)
+        a = np.require(vals, dtype=npdtype, requirements=["C", "W"])
         if a.size == 0:
             a = np.zeros(1, npdtype)
         return (ctype * a.size).from_buffer(a)
@@ -272,6 +273,31 @@ def meta_status(metas) -> np.ndarray:
     return raw[:, off:off + 4].copy().view(np.int32).reshape(-1)
 
 
+# Contexts still open at interpreter exit are closed in creation order's
+# reverse by an atexit hook, while the HIP runtime and every thread's buffers
+# still exist (a context may sit in a reference cycle, or in a module global
+# whose __del__ never runs).  DG_NO_ATEXIT_CLOSE=1 leaves them to the
+# library's own exit hook (the path a non-Python host takes).
+_live: "weakref.WeakValueDictionary[int, Context]" = weakref.WeakValueDictionary()
+_live_seq = [0]
+
+
+def close_all() -> None:
+    """Close every context still open, newest first."""
+    for k in sorted(_live.keys(), reverse=True):
+        c = _live.get(k)
+        if c is not None:
+            c.close()
+
+
+def _close_all_at_exit() -> None:
+    if os.environ.get("DG_NO_ATEXIT_CLOSE") != "1":
+        close_all()
+
+
+atexit.register(_close_all_at_exit)
+
+
 class Context:
     """dg_ctx: one HIP stream + device arenas on one device (rank -> device)."""
 
@@ -284,17 +310,20 @@ class Context:
                           max_aspect_ratio, int(pre_encode_images), int(image_to_rgb8), encode_format,
                           jpeg_quality, decode_semantics)
         h = ctypes.c_void_p()
+        self._h = None
         _check(L.dg_ctx_create(device, ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
+        _live_seq[0] += 1
+        _live[_live_seq[0]] = self
         self.device = device
         self.cfg = cfg
         bt = L.dg_ctx_buckets(h)
         self.buckets = BucketTable(0, 0, 0, 0, _borrowed=bt) if bt else None
 
     def close(self) -> None:
-        if self._h and _lib is not None:
-            _lib.dg_ctx_destroy(self._h)
-            self._h = None
+        h, self._h = getattr(self, "_h", None), None
+        if h and _lib is not None:
+            _lib.dg_ctx_destroy(h)
 
     def __del__(self):
         self.close()

@@ -216,15 +216,26 @@ struct RangeAcc {
 
 // Write-side context: coefficient block buffer of this thread (64 int16,
 // zigzag order), global coefficient base, prefix values.
+// k_huff_write's block buffers are 128 bytes apart with their 16-byte parts
+// XOR-swizzled by the owner lane: coefficient zz sits at blk[zz ^ sw], sw =
+// ((lane >> 1) & 7) << 3, so the 16-byte accesses of 16 consecutive lanes
+// cover all 64 banks (the unswizzled 128-byte stride put them on two groups
+// of four).  72-int16 buffers did the same with 12% more LDS; at 64 the
+// kernel fits three workgroups per CU instead of two.
 struct WriteCtx {
   int16_t *blk;
+  uint32_t sw = 0;  // swizzle of this thread's buffer (int16 units; 0 on the host)
   DG_GLOBAL int16_t *coef;
   uint32_t seg, nin;
   int32_t pred[3];
   uint32_t blocks_per_seg, total_blocks;
   int32_t cur;   // global index of the block being filled (-1 = none / dropped)
   uint32_t zs;   // first zigzag index this thread owns in the current block
+  uint32_t hi = 0;  // zigzag index of the last coefficient written into the current block
 #if defined(DG_DEVICE)
+  // sparse blocks (ImageDesc::ccnt): per-block count of the 16-byte parts
+  // stored, nullptr = dense (all 8 parts)
+  DG_GLOBAL uint8_t *cnt = nullptr;
   // wave-cooperative flush (k_huff_write): this wave's lane-0 block, block
   // stride (int16), and a 128-dword LDS table of the wave
   int16_t *wave_blk;
@@ -266,13 +277,18 @@ DG_HD void wc_flush(WriteCtx &w, uint32_t ze) {
     const u32x4 *s4 = (const u32x4 *)w.blk;
     DG_GLOBAL u32x4 *d4 = (DG_GLOBAL u32x4 *)dst;
 #pragma unroll
-    for (int i = 0; i < 8; i++) d4[i] = s4[i];
+    for (int i = 0; i < 8; i++) d4[i] = s4[i ^ (w.sw >> 3)];
 #else
-    for (int i = 0; i < 64; i++) dst[i] = w.blk[i];
+    for (int i = 0; i < 64; i++) dst[i] = w.blk[i ^ w.sw];
 #endif
   } else {
-    for (uint32_t i = w.zs; i < ze; i++) dst[i] = w.blk[i];
+    for (uint32_t i = w.zs; i < ze; i++) dst[i] = w.blk[i ^ w.sw];
   }
+#if defined(DG_DEVICE)
+  // a block shared by two ranges (or cut at the range end) is stored dense:
+  // each owner writes its zigzag span and both announce all 8 parts
+  if (w.cnt) w.cnt[w.cur] = 8;
+#endif
   w.cur = -1;
 }
 
@@ -303,7 +319,9 @@ __device__ __forceinline__ void wc_coop_flush(WriteCtx &w, bool pending) {
   const uint64_t am = __ballot(1);
   if (pending) {
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
-    w.tab[rank] = __lane_id();
+    // lane | parts to store << 8 (sparse: through the last nonzero coefficient)
+    const uint32_t np = w.cnt ? (w.hi >> 3) + 1u : 8u;
+    w.tab[rank] = __lane_id() | (np << 8);
     w.tab[64 + rank] = (uint32_t)w.cur;
   }
   __builtin_amdgcn_wave_barrier();
@@ -325,7 +343,9 @@ __device__ __forceinline__ void wc_coop_flush(WriteCtx &w, bool pending) {
       const uint32_t k = k0 + g;
       const bool act = g < groups && k < nb;
       const int32_t idx = act ? (int32_t)w.tab[64 + k] : -1;
-      int16_t *b = w.wave_blk + (act ? w.tab[k] : 0u) * w.stride;
+      const uint32_t own = act ? w.tab[k] & 255u : 0u;
+      int16_t *b = w.wave_blk + own * w.stride;
+      const uint32_t osw = w.stride == 64u ? ((own >> 1) & 7u) << 3 : 0u;  // the owner's swizzle
       const bool live = act && idx >= 0;
       uint32_t c = 0, by = 0, bx = 0;
       if (live) block_pos(im, (uint32_t)idx, c, by, bx);
@@ -333,7 +353,7 @@ __device__ __forceinline__ void wc_coop_flush(WriteCtx &w, bool pending) {
       if (live) {
         int32_t v[8];
 #pragma unroll
-        for (int r = 0; r < 8; r++) v[r] = (int32_t)b[w.n2z[r * 8 + part]] * w.qt[c * 64 + r * 8 + part];
+        for (int r = 0; r < 8; r++) v[r] = (int32_t)b[w.n2z[r * 8 + part] ^ osw] * w.qt[c * 64 + r * 8 + part];
         idct_col(zune, v, ws);
       }
       __builtin_amdgcn_wave_barrier();
@@ -364,10 +384,19 @@ __device__ __forceinline__ void wc_coop_flush(WriteCtx &w, bool pending) {
   for (uint32_t c = wr; c < nc; c += na) {
     const uint32_t k = c >> 3, part = c & 7u;
     const int32_t idx = (int32_t)w.tab[64 + k];
-    u32x4 *src = (u32x4 *)(w.wave_blk + w.tab[k] * w.stride) + part;
-    if (idx >= 0) *(DG_GLOBAL u32x4 *)(w.coef + (size_t)idx * 64 + part * 8) = *src;
-    if (part == 0) wc_list_late(w, idx);  // fused IDCT with < 8 active lanes: k_idct_list takes it
-    *src = zero;
+    const uint32_t tk = w.tab[k], np = tk >> 8;
+    const uint32_t own = tk & 255u;
+    u32x4 *src = (u32x4 *)(w.wave_blk + own * w.stride) + (w.stride == 64u ? part ^ ((own >> 1) & 7u) : part);
+    // parts past the last nonzero coefficient are zero in LDS already and
+    // are not stored (sparse blocks; np = 8 otherwise)
+    if (part < np) {
+      if (idx >= 0) *(DG_GLOBAL u32x4 *)(w.coef + (size_t)idx * 64 + part * 8) = *src;
+      *src = zero;
+    }
+    if (part == 0) {
+      if (w.cnt && idx >= 0) w.cnt[idx] = (uint8_t)np;
+      wc_list_late(w, idx);  // fused IDCT with < 8 active lanes: k_idct_list takes it
+    }
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -755,7 +784,10 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
         w->nin++;
       }
       const uint32_t zz = z + run;
-      if (isdc || (size && zz < 64u)) w->blk[zz] = (int16_t)(isdc ? sel3(w->pred, comp) : v);
+      if (isdc || (size && zz < 64u)) {
+        w->blk[zz ^ w->sw] = (int16_t)(isdc ? sel3(w->pred, comp) : v);
+        w->hi = zz;
+      }
     }
     uint32_t zn = take_m ? zm : huff_next_z(z, sym);
     if (pair && !stage && (WRITE || !take_m)) {
@@ -776,7 +808,10 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
         if (tk) {
           if (WRITE) {
             const uint32_t zz2 = zn + (sx >> 4);
-            if (zx && zz2 < 64u) w->blk[zz2] = (int16_t)huff_value(bx, lx, zx);
+            if (zx && zz2 < 64u) {
+              w->blk[zz2 ^ w->sw] = (int16_t)huff_value(bx, lx, zx);
+              w->hi = zz2;
+            }
           }
           pos += lx + zx;
           used += lx + zx;

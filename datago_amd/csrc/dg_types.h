@@ -295,6 +295,11 @@ struct ImageDesc {
   uint16_t sem;             // decode semantics: 0 libjpeg-turbo, 1 zune-jpeg (option "decode_semantics")
   uint64_t coef;            // device address of block 0 (int16 zigzag[64] per block, decode order)
   uint64_t stage;           // decode-once staging (dg_entropy.h StageCtx), 0 = off
+  // Sparse coefficient blocks (option "sparse_coef"): one byte per block, the
+  // number of 16-byte zigzag parts k_huff_write stored (1..8, through the
+  // block's last nonzero coefficient); k_idct_t loads only those parts and
+  // takes the rest as zero.  0 = dense blocks (every part written and read).
+  uint64_t ccnt;
   // ---- geometry
   uint32_t width, height;
   uint32_t mcux, mcuy;

@@ -1,8 +1,14 @@
 // capi.cpp — extern "C" entry points declared in include/datago_hip.h.
 #include <string.h>
 
+#include <stdlib.h>
+
+#include <mutex>
 #include <new>
+#include <set>
+#include <shared_mutex>
 #include <string>
+#include <vector>
 
 #include "../../../include/datago_hip.h"
 #include "buckets.h"
@@ -20,11 +26,19 @@ struct dg_bucket_table {
   dg_bucket_table(uint32_t a, uint32_t b, double c, double d) : t(a, b, c, d) {}
 };
 
+// A context behind the C ABI.  Entry points hold `gate` shared while they
+// use the context; dg_ctx_destroy (and the exit hook) take it exclusively.
+// The exit hook tears down the contexts a process leaves alive -- before
+// the HIP runtime's own static destructors run -- when no thread is inside
+// one of their calls; a context it ran down stays `dead` (later calls
+// return DG_ERR_INVALID) instead of being freed under a caller.
 struct dg_ctx {
-  dg::Context c;
+  std::shared_mutex gate;
+  bool dead = false;
+  dg::Context *c;
   dg_bucket_table view;
   dg_ctx(int dev, const dg_image_config *cfg)
-      : c(dev, cfg),
+      : c(new dg::Context(dev, cfg)),
         view(cfg && cfg->crop_and_resize && cfg->default_image_size && cfg->downsampling_ratio
                  ? cfg->default_image_size
                  : 224,
@@ -33,7 +47,72 @@ struct dg_ctx {
                  : 16,
              cfg && cfg->crop_and_resize ? cfg->min_aspect_ratio : 0.5,
              cfg && cfg->crop_and_resize ? cfg->max_aspect_ratio : 2.0) {}
+  ~dg_ctx() { delete c; }
 };
+
+namespace {
+
+// Live contexts (never destroyed itself: the exit hook may run after other
+// static destructors of this library).
+std::mutex &reg_mu() {
+  static std::mutex *m = new std::mutex;
+  return *m;
+}
+std::set<dg_ctx *> &registry() {
+  static std::set<dg_ctx *> *r = new std::set<dg_ctx *>;
+  return *r;
+}
+
+// Registered with atexit at the first dg_ctx_create, i.e. after the HIP
+// runtime (loaded with this library) registered its destructors, so it runs
+// before them.  DG_NO_EXIT_HOOK=1 leaves everything to the runtime.
+void exit_hook() {
+  std::vector<dg_ctx *> live;
+  {
+    std::lock_guard<std::mutex> lk(reg_mu());
+    live.assign(registry().begin(), registry().end());
+  }
+  for (dg_ctx *x : live) {
+    if (!x->gate.try_lock()) continue;  // a thread is still inside a call: leave it to the runtime
+    if (!x->dead) {
+      delete x->c;
+      x->c = nullptr;
+      x->dead = true;
+    }
+    x->gate.unlock();
+  }
+}
+
+void install_exit_hook() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char *e = getenv("DG_NO_EXIT_HOOK");
+    if (!(e && e[0] == '1')) atexit(exit_hook);
+  });
+}
+
+// Shared use of a live context for one entry point.
+struct CtxUse {
+  dg_ctx *x;
+  bool ok = false;
+  explicit CtxUse(dg_ctx *c) : x(c) {
+    if (!c) return;
+    c->gate.lock_shared();
+    ok = !c->dead;
+    if (!ok) c->gate.unlock_shared();
+  }
+  ~CtxUse() {
+    if (ok) x->gate.unlock_shared();
+  }
+  CtxUse(const CtxUse &) = delete;
+  CtxUse &operator=(const CtxUse &) = delete;
+};
+
+}  // namespace
+
+#define DG_USE(ctx, fail)  \
+  CtxUse use_(ctx);        \
+  if (!use_.ok) return fail
 
 extern "C" {
 
@@ -143,19 +222,32 @@ dg_status dg_ctx_create(int32_t device, const dg_image_config *cfg, dg_ctx **out
   *out = nullptr;
   dg_ctx *c = new (std::nothrow) dg_ctx(device, cfg);
   if (!c) return DG_ERR_OOM;
-  dg_status st = c->c.init();
+  dg_status st = c->c->init();
   if (st) {
     delete c;
     return st;
+  }
+  install_exit_hook();
+  {
+    std::lock_guard<std::mutex> lk(reg_mu());
+    registry().insert(c);
   }
   *out = c;
   return DG_OK;
 }
 
-void dg_ctx_destroy(dg_ctx *ctx) { delete ctx; }
+void dg_ctx_destroy(dg_ctx *ctx) {
+  if (!ctx) return;
+  {
+    std::lock_guard<std::mutex> lk(reg_mu());
+    registry().erase(ctx);
+  }
+  { std::unique_lock<std::shared_mutex> lk(ctx->gate); }  // every call on it has returned
+  delete ctx;
+}
 
 const dg_bucket_table *dg_ctx_buckets(const dg_ctx *ctx) {
-  if (!ctx || !ctx->c.buckets()) return nullptr;
+  if (!ctx || ctx->dead || !ctx->c->buckets()) return nullptr;
   return &ctx->view;
 }
 
@@ -190,79 +282,99 @@ dg_status dg_sample_align(const dg_bucket_table *t, int32_t n, const uint8_t *co
 }
 
 dg_status dg_output_size(dg_ctx *ctx, const uint8_t *bytes, size_t len, int32_t forced, uint64_t *nbytes) {
-  if (!ctx || !nbytes) return DG_ERR_INVALID;
-  return ctx->c.output_size(bytes, len, forced, nbytes);
+  if (!nbytes) return DG_ERR_INVALID;
+  DG_USE(ctx, DG_ERR_INVALID);
+  return ctx->c->output_size(bytes, len, forced, nbytes);
 }
 
 dg_status dg_submit(dg_ctx *ctx, int32_t n, const uint8_t *const *srcs, const size_t *lens, const int32_t *forced,
                     uint8_t *const *outs, const uint64_t *caps, dg_payload_meta *metas, uint64_t *ticket) {
-  if (!ctx || !ticket) return DG_ERR_INVALID;
-  return ctx->c.submit_user(n, srcs, nullptr, lens, forced, outs, caps, metas, true, ticket);
+  if (!ticket) return DG_ERR_INVALID;
+  DG_USE(ctx, DG_ERR_INVALID);
+  return ctx->c->submit_user(n, srcs, nullptr, lens, forced, outs, caps, metas, true, ticket);
 }
 
 dg_status dg_submit_device(dg_ctx *ctx, int32_t n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs,
                            const size_t *lens, const int32_t *forced, uint8_t *const *d_outs,
                            const uint64_t *caps, dg_payload_meta *metas, uint64_t *ticket) {
-  if (!ctx || !ticket || (n > 0 && !d_srcs)) return DG_ERR_INVALID;
-  return ctx->c.submit_user(n, h_srcs, d_srcs, lens, forced, d_outs, caps, metas, false, ticket);
+  if (!ticket || (n > 0 && !d_srcs)) return DG_ERR_INVALID;
+  DG_USE(ctx, DG_ERR_INVALID);
+  return ctx->c->submit_user(n, h_srcs, d_srcs, lens, forced, d_outs, caps, metas, false, ticket);
 }
 
-dg_status dg_wait(dg_ctx *ctx, uint64_t ticket) { return ctx ? ctx->c.wait_user(ticket) : DG_ERR_INVALID; }
-dg_status dg_poll(dg_ctx *ctx, uint64_t ticket) { return ctx ? ctx->c.poll_user(ticket) : DG_ERR_INVALID; }
+dg_status dg_wait(dg_ctx *ctx, uint64_t ticket) {
+  DG_USE(ctx, DG_ERR_INVALID);
+  return ctx->c->wait_user(ticket);
+}
+dg_status dg_poll(dg_ctx *ctx, uint64_t ticket) {
+  DG_USE(ctx, DG_ERR_INVALID);
+  return ctx->c->poll_user(ticket);
+}
 dg_status dg_wait_ready(dg_ctx *ctx, uint64_t ticket, int32_t *pending) {
-  return ctx ? ctx->c.wait_ready(ticket, pending) : DG_ERR_INVALID;
+  DG_USE(ctx, DG_ERR_INVALID);
+  return ctx->c->wait_ready(ticket, pending);
 }
 
 dg_status dg_decode_one(dg_ctx *ctx, const uint8_t *src, size_t len, int32_t forced, uint8_t *out, uint64_t cap,
                         dg_payload_meta *meta) {
-  if (!ctx || !meta) return DG_ERR_INVALID;
-  return ctx->c.decode_one(src, len, forced, out, cap, meta);
+  if (!meta) return DG_ERR_INVALID;
+  DG_USE(ctx, DG_ERR_INVALID);
+  return ctx->c->decode_one(src, len, forced, out, cap, meta);
 }
 
 dg_status dg_device_alloc(dg_ctx *ctx, size_t bytes, void **dptr) {
-  if (!ctx || !dptr) return DG_ERR_INVALID;
-  hipSetDevice(ctx->c.device());
+  if (!dptr) return DG_ERR_INVALID;
+  DG_USE(ctx, DG_ERR_INVALID);
+  hipSetDevice(ctx->c->device());
   if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess) return DG_ERR_OOM;
   return DG_OK;
 }
 dg_status dg_device_free(dg_ctx *ctx, void *dptr) {
-  if (!ctx) return DG_ERR_INVALID;
-  hipSetDevice(ctx->c.device());
+  DG_USE(ctx, DG_ERR_INVALID);
+  hipSetDevice(ctx->c->device());
   return hipFree(dptr) == hipSuccess ? DG_OK : DG_ERR_DEVICE;
 }
 dg_status dg_memcpy_h2d(dg_ctx *ctx, void *dst, const void *src, size_t bytes) {
-  if (!ctx) return DG_ERR_INVALID;
-  hipSetDevice(ctx->c.device());
+  DG_USE(ctx, DG_ERR_INVALID);
+  hipSetDevice(ctx->c->device());
   return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? DG_OK : DG_ERR_DEVICE;
 }
 dg_status dg_memcpy_d2h(dg_ctx *ctx, void *dst, const void *src, size_t bytes) {
-  if (!ctx) return DG_ERR_INVALID;
-  hipSetDevice(ctx->c.device());
+  DG_USE(ctx, DG_ERR_INVALID);
+  hipSetDevice(ctx->c->device());
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? DG_OK : DG_ERR_DEVICE;
 }
 dg_status dg_host_register(dg_ctx *ctx, void *ptr, size_t bytes) {
-  if (!ctx || !ptr || !bytes) return DG_ERR_INVALID;
-  return ctx->c.host_register(ptr, bytes);
+  if (!ptr || !bytes) return DG_ERR_INVALID;
+  DG_USE(ctx, DG_ERR_INVALID);
+  return ctx->c->host_register(ptr, bytes);
 }
 dg_status dg_host_unregister(dg_ctx *ctx, void *ptr) {
-  if (!ctx || !ptr) return DG_ERR_INVALID;
-  return ctx->c.host_unregister(ptr);
+  if (!ptr) return DG_ERR_INVALID;
+  DG_USE(ctx, DG_ERR_INVALID);
+  return ctx->c->host_unregister(ptr);
 }
 dg_status dg_synchronize(dg_ctx *ctx) {
-  if (!ctx) return DG_ERR_INVALID;
-  hipSetDevice(ctx->c.device());
-  return ctx->c.sync_all();
+  DG_USE(ctx, DG_ERR_INVALID);
+  hipSetDevice(ctx->c->device());
+  return ctx->c->sync_all();
 }
 
 int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_t cap) {
-  return ctx ? ctx->c.timings(names, ms, cap) : 0;
+  DG_USE(ctx, 0);
+  return ctx->c->timings(names, ms, cap);
 }
 
 dg_status dg_ctx_set_option(dg_ctx *ctx, const char *key, int64_t value) {
-  if (!ctx || !key) return DG_ERR_INVALID;
-  return ctx->c.set_option(key, value);
+  if (!key) return DG_ERR_INVALID;
+  DG_USE(ctx, DG_ERR_INVALID);
+  return ctx->c->set_option(key, value);
 }
 
-int64_t dg_ctx_get_stat(dg_ctx *ctx, const char *key) { return ctx && key ? ctx->c.get_stat(key) : -1; }
+int64_t dg_ctx_get_stat(dg_ctx *ctx, const char *key) {
+  if (!key) return -1;
+  DG_USE(ctx, -1);
+  return ctx->c->get_stat(key);
+}
 
 }  // extern "C"

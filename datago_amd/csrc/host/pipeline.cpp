@@ -45,6 +45,9 @@ static double thread_cpu_us() {
 
 // Boundary-repair rounds (finish()) before a batch is declared unsettled.
 static constexpr int kMaxResyncRounds = 64;
+// submit(): the batch does not fit the device (budget or allocation); the
+// caller splits it (submit_split).  Never returned through the C ABI.
+static constexpr dg_status kNeedSplit = (dg_status)15;  // (inside the enum's value range)
 
 // 64-row unfilter bands of pass p of a PNG (the image itself when not
 // interlaced); k_png_unfilter numbers its progress flags the same way.
@@ -110,6 +113,7 @@ Context::Context(int device, const dg_image_config *cfg) : device_(device) {
 }
 
 Context::~Context() {
+  plan_pool_.reset();  // join the planning workers before any HIP object goes
   hipSetDevice(device_);
   sync_all();
   for (int g = 0; g < kPoolGens; g++)
@@ -387,6 +391,25 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     side_stream_ = v != 0;
     return DG_OK;
   }
+  if (k == "coef_cache_mb") {  // Lanczos table cache arena (0: off); takes effect at the next reset
+    if (v < 0 || v > 65536) return DG_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const Slot &o : slots_)
+      if (o.batch && !o.batch->done && o.batch->uses_ccache) return DG_ERR_INVALID;  // not while tables are in use
+    ccache_cap_ = (size_t)v << 20;
+    ccache_idx_.clear();
+    ccache_.clear();
+    ccache_off_ = 0;
+    if (d_ccache_.p) hipFree(d_ccache_.p);
+    d_ccache_.p = nullptr;
+    d_ccache_.cap = 0;
+    return DG_OK;
+  }
+  if (k == "max_device_mb") {  // device memory budget of the context (0: none)
+    if (v < 0) return DG_ERR_INVALID;
+    max_dev_bytes_ = (size_t)v << 20;
+    return DG_OK;
+  }
   if (k == "slots") {
     if (v < 1 || v > (int64_t)kMaxInflight) return DG_ERR_INVALID;
     nslots_ = (int)v;
@@ -505,6 +528,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
   }
   if (k == "idct_thread") {
     idct_thread_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "sparse_coef") {
+    sparse_coef_ = v != 0;
     return DG_OK;
   }
   if (k == "h_prefetch") {
@@ -662,6 +689,19 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "alloc_mb") return stat_alloc_mb_;
   if (k == "alloc_us") return (int64_t)stat_alloc_us_;
   if (k == "reclaims") return stat_reclaims_;
+  if (k == "peak_device_mb") return stat_peak_dev_ >> 20;
+  if (k == "device_mb") {
+    std::lock_guard<std::mutex> lk(mu_);
+    return (int64_t)(dev_footprint() >> 20);
+  }
+  if (k == "max_device_mb") return (int64_t)(max_dev_bytes_ >> 20);
+  if (k == "budget_splits") return stat_budget_splits_;
+  if (k == "coef_cache_hits") return stat_ccache_hits_;
+  if (k == "coef_cache_new") return stat_ccache_new_;
+  if (k == "coef_cache_resets") return stat_ccache_resets_;
+  if (k == "coef_cache_mb") return (int64_t)(ccache_off_ >> 20);
+  if (k == "budget_frees") return stat_budget_frees_;
+  if (k == "budget_oom") return stat_budget_oom_;
   if (k == "retire_syncs") return stat_retire_syncs_;
   if (k == "png_serial_fallbacks") return stat_png_serial_;
   if (k == "band_dec_images") return stat_band_dec_;
@@ -702,7 +742,12 @@ int Context::timings(const char **names, float *ms, int cap) {
 // per host each keeping GiBs of grown-out buffers page-locked would pin a lot
 // of the host's memory.  Retired buffers are also freed at the first idle
 // moment (a wait that leaves no batch in flight, free_retired_if_idle).
-static constexpr size_t kRetiredDevMax = (size_t)32 << 30;  // 4 GiB synced every few batches of growth (round 4)
+// 32 GiB of retired device buffers at most before a device-wide sync frees
+// them (growth happens while a workload sets new size maxima, i.e. in its
+// first batches; a lower limit made those batches sync every few growths).
+// Ranks sharing one device should set a budget (option "max_device_mb"):
+// under a budget nothing is retired -- a grown-out buffer is freed at once.
+static constexpr size_t kRetiredDevMax = (size_t)32 << 30;
 static constexpr size_t kRetiredPinMax = (size_t)512 << 20;
 
 void Context::retire(void *p, size_t bytes, bool pinned) {
@@ -755,7 +800,11 @@ dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
   (void)user;
   if (b.cap >= bytes) return DG_OK;
   if (b.p) {
-    retire(b.p, b.cap, false);
+    if (max_dev_bytes_) {  // under a budget the old buffer is gone now (budget_fit counted it so)
+      hipFree(b.p);
+    } else {
+      retire(b.p, b.cap, false);
+    }
     b.p = nullptr;
     b.cap = 0;
   }
@@ -768,10 +817,16 @@ dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
   // retired buffers go first, then the headroom.
   // no headroom once the device is three quarters full (several ranks or
   // contexts sharing one device: 8 ranks x 4 slots x 1.5 ran a 288 GB device
-  // out of memory, profiles/r04/ranks_r4f)
+  // out of memory, profiles/r04/ranks_r4f); under a budget, only the room
+  // budget_fit left.
   size_t dfree = 0, dtotal = 0;
   const bool roomy = hipMemGetInfo(&dfree, &dtotal) != hipSuccess || dfree > dtotal / 4 + bytes;
   size_t cap = grow_cap(bytes, roomy);
+  if (max_dev_bytes_) {
+    const size_t lim = align_up(bytes, 1 << 20) + (budget_room_ / 3 & ~(((size_t)1 << 20) - 1));
+    cap = std::min(cap, std::max(lim, align_up(bytes, 1 << 20)));
+    budget_room_ -= std::min(budget_room_, cap - std::min(cap, bytes));
+  }
   const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipMalloc(&b.p, cap);
   if (e != hipSuccess && reclaim()) {
@@ -785,7 +840,124 @@ dg_status Context::ensure(DevBuf &b, size_t bytes, hipStream_t user) {
     return DG_ERR_OOM;
   }
   b.cap = cap;
+  stat_peak_dev_ = std::max<int64_t>(stat_peak_dev_, (int64_t)dev_footprint());
   return DG_OK;
+}
+
+// Device bytes the context holds: every slot's buffers, the table pools and
+// the retired buffers not yet freed (`except`'s buffers left out).
+size_t Context::dev_footprint(const Slot *except) const {
+  size_t t = retired_dev_bytes_;
+  for (const Slot &o : slots_) {
+    if (&o == except) continue;
+    for (const DevBuf *b : {&o.scratch, &o.meta, &o.input, &o.coef, &o.wgt}) t += b->cap;
+  }
+  for (int g = 0; g < kPoolGens; g++) t += d_hpool_[g].cap + d_qpool_[g].cap;
+  return t + d_ccache_.cap;
+}
+
+// The arena is nearly full: start it over once no batch in flight reads or
+// writes it (finishing them first, as a pool flush does).  Runs before a
+// batch's lookups, so a batch never mixes entries of two arena lifetimes.
+void Context::ccache_maybe_reset(Slot &self) {
+  if (!ccache_cap_ || ccache_off_ <= ccache_cap_ / 8 * 7) return;
+  for (Slot &o : slots_) {
+    if (&o == &self || !o.batch || o.batch->done || !o.batch->uses_ccache) continue;
+    if (finish(o)) return;  // keep the arena as it is; the next batch tries again
+  }
+  ccache_idx_.clear();
+  ccache_.clear();
+  ccache_off_ = 0;
+  stat_ccache_resets_++;
+}
+
+void Context::ccache_rollback(size_t n0, size_t off0) {
+  while (ccache_.size() > n0) {
+    ccache_idx_.erase(ccache_.back().key);
+    ccache_.pop_back();
+  }
+  ccache_off_ = std::min(ccache_off_, off0);
+}
+
+int Context::ccache_lookup(const ResizePass &ps, Batch &b, bool &hit) {
+  hit = false;
+  if (!ccache_cap_ || max_dev_bytes_ && ccache_cap_ > max_dev_bytes_ / 8) return -1;
+  CKey k;
+  memcpy(&k.in0, &ps.in0, 8);
+  memcpy(&k.in1, &ps.in1, 8);
+  k.in_size = ps.in_size;
+  k.out_size = ps.out_size;
+  k.ksize = ps.ksize;
+  auto it = ccache_idx_.find(k);
+  if (it != ccache_idx_.end()) {
+    if (!ccache_[it->second].ready) return -1;  // a batch in flight is writing it: compute our own copy
+    hit = true;
+    b.uses_ccache = true;
+    stat_ccache_hits_++;
+    return it->second;
+  }
+  const size_t bytes = align_up((size_t)ps.out_size * 8 + (size_t)ps.out_size * ps.ksize * 2, 256);
+  if (ccache_off_ + bytes > ccache_cap_) return -1;
+  if (!d_ccache_.p) {
+    if (hipMalloc(&d_ccache_.p, ccache_cap_) != hipSuccess) {
+      (void)hipGetLastError();
+      d_ccache_.p = nullptr;
+      ccache_cap_ = 0;  // no cache on this device
+      return -1;
+    }
+    d_ccache_.cap = ccache_cap_;
+  }
+  const int idx = (int)ccache_.size();
+  ccache_.push_back(CEntry{k, ccache_off_, 0, false});
+  ccache_idx_.emplace(k, idx);
+  ccache_off_ += bytes;
+  b.uses_ccache = true;
+  stat_ccache_new_++;
+  return idx;
+}
+
+// An idle slot's device buffers (no batch, or its batch finished).
+void Context::free_slot_buffers(Slot &o) {
+  for (DevBuf *b : {&o.scratch, &o.meta, &o.input, &o.coef}) {
+    if (!b->p) continue;
+    hipFree(b->p);
+    b->p = nullptr;
+    b->cap = 0;
+    stat_budget_frees_++;
+  }
+}
+
+// mu_ held.  The device budget (option "max_device_mb"): make room for a
+// batch of `self` whose scratch / coefficient / input arenas need rs / rc /
+// ri bytes.  In order: keep self's buffers if they already fit; free the
+// retired buffers; then, slot by slot, finish the other slots' batches
+// (waiting for their GPU work, as a dg_wait would) and free their buffers;
+// finally drop self's own oversized buffers (idle: the slot's previous batch
+// is finished) for exact-size ones.  False: the batch alone does not fit --
+// the caller splits it (submit_split).  budget_room_: what growth may add on
+// top.  (The descriptor buffer, a few MB, grows after this check.)
+bool Context::budget_fit(Slot &self, size_t rs, size_t rc, size_t ri) {
+  budget_room_ = 0;
+  if (!max_dev_bytes_) return true;
+  const size_t fixed = self.meta.cap + self.wgt.cap;
+  const size_t keep = std::max(self.scratch.cap, rs) + std::max(self.coef.cap, rc) + std::max(self.input.cap, ri) + fixed;
+  const size_t tight = rs + rc + ri + fixed;
+  auto others = [&] { return dev_footprint(&self); };
+  if (others() + keep > max_dev_bytes_ && !retired_dev_.empty() && sync_all() == DG_OK) free_retired();
+  for (int k = 0; k < kAllSlots && others() + keep > max_dev_bytes_; k++) {
+    Slot &o = slots_[(&self - slots_ + 1 + k) % kAllSlots];  // the slots after self first: the oldest batches
+    if (&o == &self) continue;
+    if (o.batch && !o.batch->done && finish(o)) continue;
+    free_slot_buffers(o);
+  }
+  if (others() + keep <= max_dev_bytes_) {
+    budget_room_ = max_dev_bytes_ - others() - keep;
+    return true;
+  }
+  if (others() + tight > max_dev_bytes_) return false;
+  free_slot_buffers(self);
+  budget_room_ = max_dev_bytes_ - others() - tight;
+  return true;
 }
 
 dg_status Context::ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user) {
@@ -1191,6 +1363,17 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.qp = (const QuantTable *)d_qpool_[pool_gen_].p;
 
   phase(1);
+  // Lanczos table cache: entries this submit creates are dropped again if it
+  // returns before its batch is installed (budget split, allocation failure)
+  ccache_maybe_reset(sl);
+  struct CacheRoll {
+    Context *c;
+    size_t n0, off0;
+    bool armed = true;
+    ~CacheRoll() {
+      if (armed) c->ccache_rollback(n0, off0);
+    }
+  } croll{this, ccache_.size(), ccache_off_};
   // ---- 3. layout
   // Subsequence size: the entropy kernels are latency-bound, so they want as
   // many lanes as the chip can keep resident, but every subsequence costs a
@@ -1229,7 +1412,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   b.descs.reserve(n);
   // first pass: sizes only (pointers are patched after allocation)
   struct Offs {
-    size_t coef, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], pass_srcoff[kStages];
+    size_t coef, ccnt, plane[3], pix, pass_dst[kStages], pass_coef[kStages], pass_bounds[kStages], pass_srcoff[kStages];
+    int pass_cache[kStages];    // Lanczos table cache entry of the pass (-1: tables in the scratch arena)
+    bool pass_hit[kStages];     // ... already computed (no k_coeffs item)
     size_t final_off, tmp, out, ds, mk, chunk, stage;
     size_t zs, raw, unf, pal;
     size_t tout, ecoef, ebits, ewords, hdr, eaux;  // JPEG / PNG re-encode
@@ -1245,6 +1430,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     memset(&d, 0, sizeof(d));
     Offs o;
     memset(&o, 0, sizeof(o));
+    for (int s_ = 0; s_ < kStages; s_++) o.pass_cache[s_] = -1;
     uint32_t W, H, C;
     size_t cur_stride;
     bool colour = false;  // the source is the YCbCr planes of a colour JPEG
@@ -1440,6 +1626,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     }  // sequential
     // buffers
     o.coef = CO.take((size_t)d.total_blocks * 128);
+    // sparse blocks: k_huff_write's cooperative flush + k_idct_t only (not the
+    // fused / decode-once writers, k_idct or k_band_dec; progressive scans
+    // write whole blocks)
+    o.ccnt = (sparse_coef_ && idct_thread_ && !d.prog && !d.idct_fused && !entropy_once_)
+                 ? CO.take((size_t)d.total_blocks, 64) + 1
+                 : 0;
     for (int c = 0; c < 3; c++) o.plane[c] = (size_t)-1;  // allocated after the pass plan (not for k_band_dec)
     C = d.dec_c;
     colour = h.ncomp == 3;
@@ -1484,8 +1676,11 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       ps.dst_stride = (uint32_t)align_up((size_t)width * C, 16);
       o.pass_srcoff[stage] = (size_t)xoff * C;  // column window of the source (V passes)
       o.pass_dst[stage] = L.take((size_t)ps.dst_stride * ps.rows);
-      o.pass_coef[stage] = L.take((size_t)out_size * ps.ksize * 2);
-      o.pass_bounds[stage] = L.take((size_t)out_size * 8);
+      o.pass_cache[stage] = ccache_lookup(ps, b, o.pass_hit[stage]);
+      if (o.pass_cache[stage] < 0) {
+        o.pass_coef[stage] = L.take((size_t)out_size * ps.ksize * 2);
+        o.pass_bounds[stage] = L.take((size_t)out_size * 8);
+      }
       cur_stride = ps.dst_stride;
       last_stage = stage;
       return ps;
@@ -1709,15 +1904,26 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     if (dd.idct_fused) fused_blocks += dd.total_blocks;
   b.idct_cap = b.any_fused ? (uint32_t)std::min<uint64_t>(2 * b.total_subs + fused_blocks + 4096, 0xFFFFFFF0u) : 0u;
   const size_t idct_list_off = L.take((size_t)b.idct_cap * 8 + 16);
-  st = ensure(sl.scratch, L.off + 256, sl.st);
-  if (st) return st;
-  st = ensure(sl.coef, CO.off + 256, sl.st);
+  // Device memory: under the budget (option "max_device_mb") a batch that
+  // does not fit even with the other slots drained goes back to the caller
+  // to be split (submit_split); without one, a failed allocation first
+  // finishes the other slots' batches and frees their buffers, then splits.
+  const size_t rs = L.off + 256, rc = CO.off + 256, ri = host_io ? IN.off + 64 : 0;
+  if (!budget_fit(sl, rs, rc, ri)) return kNeedSplit;
+  for (int attempt = 0;; attempt++) {
+    st = ensure(sl.scratch, rs, sl.st);
+    if (!st) st = ensure(sl.coef, rc, sl.st);
+    if (!st && host_io) st = ensure(sl.input, ri, sl.st);
+    if (st != DG_ERR_OOM) break;
+    if (attempt > 0) return kNeedSplit;
+    for (Slot &o : slots_) {
+      if (&o == &sl) continue;
+      if (o.batch && !o.batch->done && finish(o)) continue;
+      free_slot_buffers(o);
+    }
+  }
   if (st) return st;
   sl.coef_bytes = CO.off;
-  if (host_io) {
-    st = ensure(sl.input, IN.off + 64, sl.st);
-    if (st) return st;
-  }
   // ---- 4. patch device addresses
   char *S = (char *)sl.scratch.p;
   for (InfChunk &c : b.ichunks) {
@@ -1765,6 +1971,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     } else {
     d.scan = (uint64_t)(uintptr_t)(src + h.scan_off);
     d.coef = (uint64_t)(uintptr_t)((char *)sl.coef.p + o.coef);
+    d.ccnt = (o.ccnt && !(d.pass[0].mode & kHDecode)) ? (uint64_t)(uintptr_t)((char *)sl.coef.p + o.ccnt - 1) : 0;
     if (d.prog) {
       // one record per scan; level = 1 + the highest level of an earlier scan
       // sharing a component and an overlapping coefficient band
@@ -1822,8 +2029,21 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       if (!ps.kind) continue;
       ps.src = cur + o.pass_srcoff[s];
       ps.dst = o.pass_dst[s] == (size_t)-1 ? out : (uint64_t)(uintptr_t)(S + o.pass_dst[s]);
-      ps.coef = (uint64_t)(uintptr_t)(S + o.pass_coef[s]);
-      ps.bounds = (uint64_t)(uintptr_t)(S + o.pass_bounds[s]);
+      if (o.pass_cache[s] >= 0) {  // cached tables: bounds, then the weights
+        const CEntry &e = ccache_[o.pass_cache[s]];
+        char *cb = (char *)d_ccache_.p + e.off;
+        ps.bounds = (uint64_t)(uintptr_t)cb;
+        ps.coef = (uint64_t)(uintptr_t)(cb + (size_t)ps.out_size * 8);
+        if (o.pass_hit[s]) {
+          ps.precision = e.precision;
+          b.coef_hit.resize(b.descs.size(), 0);
+          b.coef_hit[b.desc_of[i]] |= (uint8_t)(1u << s);
+        } else
+          b.ccache_prod.push_back({b.desc_of[i], s, o.pass_cache[s]});
+      } else {
+        ps.coef = (uint64_t)(uintptr_t)(S + o.pass_coef[s]);
+        ps.bounds = (uint64_t)(uintptr_t)(S + o.pass_bounds[s]);
+      }
       cur = ps.dst;
     }
     d.final_src = cur + (d.copy_needed ? o.final_off : 0);
@@ -1906,7 +2126,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     for (int s = 0; s < kStages; s++) {
       const ResizePass &ps = d.pass[s];
       if (!ps.kind) continue;
-      b.lists[L_COEF].push_back({I, (uint32_t)s});
+      if (!(di < (int)b.coef_hit.size() && (b.coef_hit[di] >> s) & 1u)) b.lists[L_COEF].push_back({I, (uint32_t)s});
       if (hv && s < 2) continue;  // k_resize_hv runs both
       if (s == 0 && (ps.mode & kHDecode)) continue;  // k_band_dec runs it
       if (ps.kind == 1 && (ps.mode & kHDirect)) {  // one workgroup per (row, 512-column tile)
@@ -2109,9 +2329,13 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         b.out_direct[i] = 1;
   }
   sl.batch = std::move(bp);
+  croll.armed = false;
   phase(5);
   st = launch_all(sl, false);
-  if (st) return st;
+  if (st) {
+    fail_batch(sl, st);
+    return st;
+  }
   phase(6);
   stat_batches_++;
   *ticket = sl.batch->ticket;
@@ -2469,7 +2693,30 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   return DG_OK;
 }
 
+// A batch that cannot complete (a launch, resync or copy-back failure): no
+// kernel of it is left running, every image not already failed reads `st`,
+// deferred metas are published, and the batch counts as done -- a later
+// submit on the slot must not finish() it again and publish planning-time
+// metas over the error.
+void Context::fail_batch(Slot &sl, dg_status st) {
+  if (!sl.batch || sl.batch->done) return;
+  for (hipStream_t q : {sl.st, sl.side})
+    if (q) (void)hipStreamSynchronize(q);
+  (void)hipGetLastError();
+  Batch &b = *sl.batch;
+  for (int i = 0; i < b.n && i < (int)b.mptr.size(); i++)
+    if (b.mptr[i] && b.mptr[i]->status == DG_OK) b.mptr[i]->status = st;
+  for (size_t i = 0; i < b.pub.size(); i++) *b.pub[i] = b.local_meta[i];
+  b.done = true;
+}
+
 dg_status Context::finish(Slot &sl) {
+  const dg_status st = finish_body(sl);
+  if (st) fail_batch(sl, st);
+  return st;
+}
+
+dg_status Context::finish_body(Slot &sl) {
   Batch &b = *sl.batch;
   for (;;) {
     HIPCHK(hipEventSynchronize(sl.done));
@@ -2599,6 +2846,12 @@ dg_status Context::finish(Slot &sl) {
       HIPCHK(hipStreamSynchronize(sl.st));
     }
   }
+  for (const Batch::CProd &pr : b.ccache_prod) {  // tables this batch wrote into the cache: hits from now on
+    if (pr.entry >= (int)ccache_.size()) continue;
+    CEntry &e = ccache_[pr.entry];
+    e.precision = back[pr.desc].pass[pr.stage].precision;
+    e.ready = e.precision > 0;
+  }
   std::vector<CopyJob> copies;
   for (int i = 0; i < b.n; i++) {
     if (b.desc_of[i] < 0) continue;
@@ -2673,15 +2926,15 @@ dg_status Context::flush_batch(std::vector<OneReq *> &batch, bool prog) {
     outs[i] = batch[i]->out;
     caps[i] = batch[i]->cap;
   }
-  uint64_t t = 0;
-  int slot = -1;
-  if (prog) {
-    std::lock_guard<std::mutex> lk(mu_);
-    slot = pick_prog_slot();
+  std::vector<dg_payload_meta *> mp(n);
+  for (int i = 0; i < n; i++) mp[i] = &metas[i];
+  std::vector<uint64_t> ts;
+  dg_status st = submit_split(n, srcs.data(), nullptr, lens.data(), forced.data(), outs.data(), caps.data(), mp.data(),
+                              true, ts, prog, false);
+  for (uint64_t t : ts) {
+    const dg_status s1 = wait(t);
+    if (!st) st = s1;
   }
-  dg_status st = submit(n, srcs.data(), nullptr, lens.data(), forced.data(), outs.data(), caps.data(), metas.data(),
-                        true, &t, nullptr, slot);
-  if (!st) st = wait(t);
   for (int i = 0; i < n; i++) {
     *batch[i]->meta = metas[i];
     batch[i]->st = st ? st : (dg_status)metas[i].status;
@@ -2784,6 +3037,39 @@ bool Context::pagg_stale_locked() {
   return false;
 }
 
+dg_status Context::submit_split(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs,
+                                const size_t *lens, const int32_t *forced, uint8_t *const *outs,
+                                const uint64_t *caps, dg_payload_meta *const *mptrs, bool host_io,
+                                std::vector<uint64_t> &tickets, bool prog, bool defer_meta) {
+  if (n <= 0) return DG_OK;
+  int slot = -1;
+  if (prog) {
+    std::lock_guard<std::mutex> lk(mu_);
+    slot = pick_prog_slot();
+  }
+  uint64_t t = 0;
+  dg_status st = submit(n, h_srcs, d_srcs, lens, forced, outs, caps, nullptr, host_io, &t, mptrs, slot, defer_meta);
+  if (st != kNeedSplit) {
+    if (!st) tickets.push_back(t);
+    return st;
+  }
+  if (n == 1) {  // one image larger than the device budget: that sample fails, not the worker
+    dg_payload_meta &m = *mptrs[0];
+    memset(&m, 0, sizeof(m));
+    m.status = DG_ERR_OOM;
+    m.bucket = -1;
+    stat_budget_oom_++;
+    set_error("image does not fit the device memory budget (max_device_mb)");
+    return DG_OK;
+  }
+  stat_budget_splits_++;
+  const int h = n / 2;
+  st = submit_split(h, h_srcs, d_srcs, lens, forced, outs, caps, mptrs, host_io, tickets, prog, defer_meta);
+  if (st) return st;
+  return submit_split(n - h, h_srcs + h, d_srcs ? d_srcs + h : nullptr, lens + h, forced ? forced + h : nullptr,
+                      outs + h, caps + h, mptrs + h, host_io, tickets, prog, defer_meta);
+}
+
 dg_status Context::flush_pagg_locked() {
   if (pagg_.empty()) return DG_OK;
   const int n = (int)pagg_.size();
@@ -2803,21 +3089,16 @@ dg_status Context::flush_pagg_locked() {
     caps[i] = e.cap;
     mp[i] = e.meta;
   }
-  int slot;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    slot = pick_prog_slot();
-  }
-  uint64_t t = 0;
-  dg_status st = submit(n, h.data(), pagg_host_ ? nullptr : d.data(), lens.data(), forced.data(), outs.data(),
-                        caps.data(), nullptr, pagg_host_, &t, mp.data(), slot, true);
-  if (st) {  // no batch: the members fail now, and dg_wait on any of their tickets returns st
-    for (PEntry &e : pagg_) e.meta->status = st;
-    t = 0;
+  std::vector<uint64_t> ts;
+  dg_status st = submit_split(n, h.data(), pagg_host_ ? nullptr : d.data(), lens.data(), forced.data(), outs.data(),
+                              caps.data(), mp.data(), pagg_host_, ts, true, true);
+  if (st) {  // the members of parts that did not launch fail now; dg_wait on their tickets returns st
+    for (PEntry &e : pagg_)
+      if (e.meta->status == DG_ERR_NOT_READY) e.meta->status = st;
   }
   stat_prog_aggs_++;
   stat_prog_agg_images_ += n;
-  pgen_[pagg_gen_] = PGen{t, pagg_refs_, st};
+  pgen_[pagg_gen_] = PGen{ts, pagg_refs_, st};
   pagg_refs_ = 0;
   pagg_gen_++;
   pagg_.clear();
@@ -2837,6 +3118,20 @@ dg_status Context::submit_user(int n, const uint8_t *const *h_srcs, const uint8_
     }
   if (!np) {
     dg_status st = submit(n, h_srcs, d_srcs, lens, forced, outs, caps, metas, host_io, ticket);
+    if (st == kNeedSplit) {  // over the device budget: parts under one user ticket
+      std::vector<dg_payload_meta *> mp(n);
+      for (int i = 0; i < n; i++) mp[i] = &metas[i];
+      SplitRec rec;
+      st = submit_split(n, h_srcs, d_srcs, lens, forced, outs, caps, mp.data(), host_io, rec.tbs, false, false);
+      if (st) return st;
+      std::lock_guard<std::mutex> lk(pmu_);
+      {
+        std::lock_guard<std::mutex> lk2(mu_);
+        *ticket = next_ticket_++;
+      }
+      split_[*ticket] = rec;
+      return DG_OK;
+    }
     // a stale aggregate is launched by whoever comes by, but a baseline
     // submitter never queues behind a thread that holds the aggregate (its
     // launch may wait for a busy progressive slot)
@@ -2862,8 +3157,8 @@ dg_status Context::submit_user(int n, const uint8_t *const *h_srcs, const uint8_
       cp.push_back(caps[i]);
       mp.push_back(&metas[i]);
     }
-    dg_status st = submit((int)h.size(), h.data(), host_io ? nullptr : d.data(), ln.data(), fb.data(), ou.data(),
-                          cp.data(), nullptr, host_io, &rec.tb, mp.data());
+    dg_status st = submit_split((int)h.size(), h.data(), host_io ? nullptr : d.data(), ln.data(), fb.data(),
+                                ou.data(), cp.data(), mp.data(), host_io, rec.tbs, false, false);
     if (st) return st;
   }
   std::lock_guard<std::mutex> lk(pmu_);
@@ -2901,24 +3196,37 @@ dg_status Context::submit_user(int n, const uint8_t *const *h_srcs, const uint8_
   return DG_OK;
 }
 
+// A user ticket of a split submission: its baseline part(s) (several when
+// the device budget split them) and, when gen != 0, the progressive
+// aggregate holding its progressive members.
 dg_status Context::wait_user(uint64_t ticket) {
   SplitRec rec;
-  uint64_t tp = 0;
+  std::vector<uint64_t> tps;
   dg_status agg_st = DG_OK;
   {
     std::lock_guard<std::mutex> lk(pmu_);
     auto it = split_.find(ticket);
     if (it == split_.end()) return wait(ticket);
     rec = it->second;
-    if (rec.gen == pagg_gen_) flush_pagg_locked();  // someone blocks on the open aggregate: launch it now
-    const PGen &g = pgen_[rec.gen];
-    tp = g.ticket;
-    agg_st = g.st;
+    if (rec.gen && rec.gen == pagg_gen_) flush_pagg_locked();  // someone blocks on the open aggregate: launch it now
+    if (rec.gen) {
+      const PGen &g = pgen_[rec.gen];
+      tps = g.tickets;
+      agg_st = g.st;
+    }
   }
-  dg_status st = rec.tb ? wait(rec.tb) : DG_OK;
-  dg_status st2 = tp ? wait(tp) : agg_st;
+  dg_status st = DG_OK;
+  for (uint64_t t : rec.tbs) {
+    const dg_status s1 = wait(t);
+    if (!st) st = s1;
+  }
+  dg_status st2 = agg_st;
+  for (uint64_t t : tps) {
+    const dg_status s1 = wait(t);
+    if (!st2) st2 = s1;
+  }
   std::lock_guard<std::mutex> lk(pmu_);
-  if (split_.erase(ticket)) {
+  if (split_.erase(ticket) && rec.gen) {
     auto g = pgen_.find(rec.gen);
     if (g != pgen_.end() && --g->second.refs <= 0) pgen_.erase(g);
   }
@@ -2937,39 +3245,61 @@ dg_status Context::wait_ready(uint64_t ticket, int32_t *pending) {
     }
     rec = it->second;
   }
-  dg_status st = rec.tb ? wait(rec.tb) : DG_OK;
+  dg_status st = DG_OK;
+  for (uint64_t t : rec.tbs) {
+    const dg_status s1 = wait(t);
+    if (!st) st = s1;
+  }
   if (pending) {  // progressive members not complete yet (their metas read DG_ERR_NOT_READY)
-    std::lock_guard<std::mutex> lk(pmu_);
-    uint64_t tp = 0;
-    if (rec.gen != pagg_gen_) {
-      auto g = pgen_.find(rec.gen);
-      tp = g != pgen_.end() ? g->second.ticket : 0;
+    std::vector<uint64_t> tps;
+    bool busy = false;
+    dg_status agg_st = DG_OK;
+    if (rec.gen) {
+      std::lock_guard<std::mutex> lk(pmu_);
+      if (rec.gen != pagg_gen_) {
+        auto g = pgen_.find(rec.gen);
+        if (g != pgen_.end()) {
+          tps = g->second.tickets;
+          agg_st = g->second.st;
+        }
+      }
+      busy = rec.gen == pagg_gen_;
+      for (uint64_t t : tps) busy = busy || poll(t) == DG_ERR_NOT_READY;
     }
-    bool busy = rec.gen == pagg_gen_ || (tp && poll(tp) == DG_ERR_NOT_READY);
     // The aggregate's kernels are done: complete it (outputs copied to host
     // buffers, statuses written, metas published) before reporting 0 pending,
     // so pending == 0 means the progressive members are ready to read.  The
-    // event has completed, so this does not block (bar a rare entropy resync).
-    if (!busy && tp) wait(tp);
+    // events have completed, so this does not block (bar a rare entropy
+    // resync); it runs outside pmu_, like wait_user's, so polls and waits on
+    // other tickets do not queue behind the aggregate's output copies.
+    dg_status st2 = agg_st;
+    if (!busy)
+      for (uint64_t t : tps) {
+        const dg_status s1 = wait(t);
+        if (!st2) st2 = s1;
+      }
     *pending = busy ? rec.nprog : 0;
+    if (!st) st = st2;
   }
   return st;
 }
 
 dg_status Context::poll_user(uint64_t ticket) {
   SplitRec rec;
-  uint64_t tp = 0;
+  std::vector<uint64_t> tps;
   {
     std::lock_guard<std::mutex> lk(pmu_);
     if (pagg_stale_locked()) flush_pagg_locked();
     auto it = split_.find(ticket);
     if (it == split_.end()) return poll(ticket);
     rec = it->second;
-    if (rec.gen == pagg_gen_) return DG_ERR_NOT_READY;
-    tp = pgen_[rec.gen].ticket;
+    if (rec.gen && rec.gen == pagg_gen_) return DG_ERR_NOT_READY;
+    if (rec.gen) tps = pgen_[rec.gen].tickets;
   }
-  if (rec.tb && poll(rec.tb) == DG_ERR_NOT_READY) return DG_ERR_NOT_READY;
-  if (tp && poll(tp) == DG_ERR_NOT_READY) return DG_ERR_NOT_READY;
+  for (uint64_t t : rec.tbs)
+    if (poll(t) == DG_ERR_NOT_READY) return DG_ERR_NOT_READY;
+  for (uint64_t t : tps)
+    if (poll(t) == DG_ERR_NOT_READY) return DG_ERR_NOT_READY;
   return DG_OK;
 }
 

@@ -119,6 +119,14 @@ struct Batch {
   std::vector<size_t> enc_host_off;  // host_io + encode: offset of image i's payload in the pinned read-back
   BatchFlags flags = {0, 0, 0, 0};
   std::vector<float> stage_ms;
+  // Lanczos table cache (Context::ccache_*): this batch reads cached tables
+  // or writes new ones (desc, stage, entry) that become hits once it finishes
+  bool uses_ccache = false;
+  std::vector<uint8_t> coef_hit;  // per descriptor: bit s = pass s reads cached tables (no k_coeffs item)
+  struct CProd {
+    int desc, stage, entry;
+  };
+  std::vector<CProd> ccache_prod;
 };
 
 // One in-flight batch's device/pinned buffers.  Three (option "slots", 1 to
@@ -237,7 +245,57 @@ class Context {
   void plan_prog_items(Batch &b);
   dg_status flush_pagg_locked();  // pmu_ held
   bool pagg_stale_locked();       // the open aggregate is older than prog_flush_us
-  dg_status finish(Slot &sl);
+  // submit(), split into halves while a part's plan exceeds the device
+  // budget (option "max_device_mb"); tickets of the parts that run are
+  // appended.  prog: the parts go to progressive slots.
+  dg_status submit_split(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
+                         const int32_t *forced, uint8_t *const *outs, const uint64_t *caps,
+                         dg_payload_meta *const *mptrs, bool host_io, std::vector<uint64_t> &tickets, bool prog,
+                         bool defer_meta);
+  size_t dev_footprint(const Slot *except = nullptr) const;  // device bytes this context holds
+  bool budget_fit(Slot &self, size_t rs, size_t rc, size_t ri);  // mu_ held: room for self's next batch
+  void free_slot_buffers(Slot &o);
+  // Lanczos tables cached across batches (option "coef_cache_mb"): a pass's
+  // i16 weights and bounds depend only on (box, in/out size, taps), and
+  // sources of one size recur (ImageNet-like shards, a cycled pool), so
+  // k_coeffs computes each once into a device arena; later batches point
+  // their passes at it.  An entry turns into a hit once the batch that wrote
+  // it has finished (its precision read back with the descriptors).
+  struct CKey {
+    uint64_t in0, in1;
+    uint32_t in_size, out_size, ksize;
+    bool operator==(const CKey &o) const {
+      return in0 == o.in0 && in1 == o.in1 && in_size == o.in_size && out_size == o.out_size && ksize == o.ksize;
+    }
+  };
+  struct CKeyHash {
+    size_t operator()(const CKey &k) const {
+      uint64_t h = k.in0 * 0x9E3779B97F4A7C15ull ^ (k.in1 + 0x632BE59BD9B4E019ull);
+      h ^= ((uint64_t)k.in_size << 40) ^ ((uint64_t)k.out_size << 20) ^ k.ksize;
+      h *= 0xBF58476D1CE4E5B9ull;
+      return (size_t)(h ^ (h >> 31));
+    }
+  };
+  struct CEntry {
+    CKey key;
+    size_t off;         // bounds at off, weights at off + out_size * 8 (arena offsets)
+    int32_t precision;  // read back from the producing batch
+    bool ready;
+  };
+  std::unordered_map<CKey, int, CKeyHash> ccache_idx_;
+  std::vector<CEntry> ccache_;
+  DevBuf d_ccache_;
+  size_t ccache_off_ = 0, ccache_cap_ = (size_t)256 << 20;
+  int64_t stat_ccache_hits_ = 0, stat_ccache_new_ = 0, stat_ccache_resets_ = 0;
+  int ccache_lookup(const ResizePass &ps, Batch &b, bool &hit);  // mu_ held; -1 = not cached
+  void ccache_maybe_reset(Slot &self);                            // mu_ held, before a batch's lookups
+  void ccache_rollback(size_t n0, size_t off0);                   // a submit that installs no batch
+  size_t max_dev_bytes_ = 0;        // option "max_device_mb" (0: no budget)
+  size_t budget_room_ = 0;          // headroom the current submit's growth may take under the budget
+  int64_t stat_peak_dev_ = 0, stat_budget_splits_ = 0, stat_budget_frees_ = 0, stat_budget_oom_ = 0;
+  dg_status finish(Slot &sl);       // finish_body, or fail_batch on its error
+  dg_status finish_body(Slot &sl);
+  void fail_batch(Slot &sl, dg_status st);
   Slot *find(uint64_t ticket);
   int pick_slot();
   int pick_prog_slot();
@@ -280,7 +338,7 @@ class Context {
     dg_payload_meta *meta;
   };
   struct SplitRec {
-    uint64_t tb = 0;   // internal ticket of the non-progressive members (0: none)
+    std::vector<uint64_t> tbs;  // internal tickets of the non-progressive members (a device-budget split: several)
     uint64_t gen = 0;  // aggregate generation holding the progressive members
     int32_t nprog = 0;
   };
@@ -290,7 +348,7 @@ class Context {
   uint64_t pagg_gen_ = 1;
   std::chrono::steady_clock::time_point pagg_t0_;
   struct PGen {
-    uint64_t ticket = 0;  // the aggregate's batch (0: its launch failed)
+    std::vector<uint64_t> tickets;  // the aggregate's batches (several after a device-budget split; none: launch failed)
     int refs = 0;         // split records still referring to it
     dg_status st = DG_OK; // launch status, returned by dg_wait of its members
   };
@@ -367,6 +425,8 @@ class Context {
   int copy_threads_ = 8;                // option "copy_threads": host threads for a host-out batch's output copies
   bool hv_fused_ = false;               // option "hv_fused": first H + V pass fused (k_resize_hv) when it fits
   bool idct_thread_ = true;             // option "idct_thread": one lane per block (k_idct_t) instead of 8 (k_idct)
+  bool sparse_coef_ = true;             // option "sparse_coef": k_huff_write stores, k_idct_t loads, only the
+                                        // 16-byte parts through each block's last nonzero (ImageDesc::ccnt)
   bool h_prefetch_ = true;              // option "h_prefetch": specialised fused fills load the next band before the convolution
   bool destuff_one_ = false;            // option "destuff_one": single-pass destuff with decoupled look-back
                                         // (configs[1] 0.66 vs 0.43 ms three-pass: off)

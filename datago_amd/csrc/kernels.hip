@@ -639,11 +639,11 @@ __global__ __launch_bounds__(256) void k_huff_scan(ImageDesc *__restrict__ imgs,
   }
 }
 
-// Per-thread coefficient blocks in LDS, 72 int16 (36 dwords) apart: the
-// 16-byte zeroing stores and flush loads of consecutive lanes then cover
-// distinct banks (a 64-coefficient stride put all lanes of a group on the same
-// four banks), and single-coefficient stores spread over banks by lane.
-constexpr int kBlkStride = 72;
+// Per-thread coefficient blocks in LDS, 64 int16 apart with their parts
+// swizzled by lane (WriteCtx::sw): the 16-byte zeroing stores and flush loads
+// of consecutive lanes cover distinct banks, as the 72-int16 stride of rounds
+// 1-4 did, in 32 instead of 36 KiB per workgroup (three workgroups per CU).
+constexpr int kBlkStride = 64;
 
 __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs,
                                                     const WgItem *__restrict__ list,
@@ -711,6 +711,7 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
   if (run) {
     WriteCtx w;
     w.blk = blk[t];
+    w.sw = (((uint32_t)t >> 1) & 7u) << 3;
     w.coef = gp<int16_t>(im.coef);
     w.seg = ss.seg;
     w.nin = ss.nin;
@@ -721,6 +722,8 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
     w.total_blocks = im.total_blocks;
     w.cur = -1;
     w.zs = 0;
+    w.hi = 0;
+    w.cnt = (im.ccnt && !fused) ? gp<uint8_t>(im.ccnt) : nullptr;
     w.wave_blk = blk[t & ~63];
     w.stride = kBlkStride;
     w.tab = wtab[t >> 6];
@@ -781,6 +784,8 @@ __global__ __launch_bounds__(256) void k_huff_scatter(const ImageDesc *__restric
   w.total_blocks = im.total_blocks;
   w.cur = -1;
   w.zs = 0;
+  w.hi = 0;
+  w.cnt = nullptr;  // dense blocks (decode-once images never get ImageDesc::ccnt)
   if (s * im.sub_bits >= im.ds_bits) return;  // empty trailing range: decodes nothing
   const uint32_t bpm = im.bpm, cbits = im.comp_bits;
   const uint32_t zin = st_z(ss.in);
@@ -994,35 +999,26 @@ __global__ __launch_bounds__(256) void k_idct(const ImageDesc *__restrict__ imgs
 // turn (the host lists every kIdctItemStride-th item: a quarter of the list
 // k_idct needs).  Four waves per workgroup instead measured no better and
 // cost 15 VGPRs (109: 4 waves per SIMD).
-__device__ __forceinline__ void idct_t_item(const ImageDesc &im, uint32_t item, const QuantTable *__restrict__ qpool);
-
-__global__ __launch_bounds__(64) void k_idct_t(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
-                                              const QuantTable *__restrict__ qpool) {
-  const WgItem it = list[blockIdx.x];
-  const ImageDesc &im = imgs[it.image];
-#pragma nounroll
-  for (uint32_t k = 0; k < kIdctItemStride; k++) idct_t_item(im, it.item0 + k, qpool);
-}
-
-__device__ __forceinline__ void idct_t_item(const ImageDesc &im, uint32_t item0, const QuantTable *__restrict__ qpool) {
-  uint32_t item = item0, c = 0;
+// Where item `item` of an image puts this lane: component, block row, block
+// column, MCU-interleaved block index; false past the image's last item
+// (wave-uniform).
+struct IdctLoc {
+  uint32_t c, by, bx, bidx;
+  bool v;  // the lane has a block (bx inside the plane)
+};
+__device__ __forceinline__ bool idct_t_locate(const ImageDesc &im, uint32_t item, IdctLoc &L) {
+  uint32_t c = 0;
   for (; c < im.ncomp; c++) {
     const uint32_t ck = (im.cbw[c] + kIdctBlocks - 1) / kIdctBlocks;
     const uint32_t n = im.cbh[c] * ck;
     if (item < n) break;
     item -= n;
   }
-  if (c >= im.ncomp) return;  // past the image's last item (wave-uniform)
+  if (c >= im.ncomp) return false;
   const uint32_t ck = (im.cbw[c] + kIdctBlocks - 1) / kIdctBlocks;
   const uint32_t by = item / ck, chunk = item - by * ck;
-  const uint32_t lane = threadIdx.x, cbw = im.cbw[c];
-  const uint32_t bx = chunk * kIdctBlocks + lane;
-  const bool v = bx < cbw;
-  // Decode semantics as a runtime flag: with it as a template constant the
-  // whole block's transforms become one straight-line region and the
-  // scheduler interleaves all eight columns (185 VGPRs, 2 waves per SIMD);
-  // the per-transform branch keeps it at 94.
-  const bool zune = im.sem != 0;
+  const uint32_t cbw = im.cbw[c];
+  const uint32_t bx = chunk * kIdctBlocks + threadIdx.x;
   const uint32_t chc = im.ch[c];
   uint32_t bidx;
   if (im.ncomp == 1) {
@@ -1032,13 +1028,65 @@ __device__ __forceinline__ void idct_t_item(const ImageDesc &im, uint32_t item0,
     const uint32_t mx = chc == 1 ? bx : chc == 2 ? bx >> 1 : bx / chc, hx = bx - mx * chc;
     bidx = (my * im.mcux + mx) * im.bpm + im.cfirst[c] + vy * chc + hx;
   }
+  L.c = c;
+  L.by = by;
+  L.bx = bx;
+  L.v = bx < cbw;
+  L.bidx = L.v ? bidx : 0u;
+  return true;
+}
+
+// 16-byte parts of the lane's block to load: all 8 for dense blocks, the
+// count k_huff_write stored for sparse ones (ImageDesc::ccnt), 0 without a block
+__device__ __forceinline__ uint32_t idct_t_parts(const ImageDesc &im, const IdctLoc &L) {
+  if (!L.v) return 0u;
+  if (!im.ccnt) return 8u;
+  const uint32_t n = gp<const uint8_t>(im.ccnt)[L.bidx];
+  return n < 8u ? n : 8u;
+}
+
+__device__ __forceinline__ void idct_t_item(const ImageDesc &im, const IdctLoc &L, const u32x4 w[8],
+                                            const QuantTable *__restrict__ qpool);
+
+__global__ __launch_bounds__(64) void k_idct_t(const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
+                                              const QuantTable *__restrict__ qpool) {
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  // Sparse blocks: the part count of the next item's block is loaded while
+  // this item transforms, so the count -> parts dependency costs one memory
+  // round trip per workgroup, not one per item.
+  IdctLoc L;
+  bool ok = idct_t_locate(im, it.item0, L);
+  uint32_t np = ok ? idct_t_parts(im, L) : 0u;
+#pragma nounroll
+  for (uint32_t k = 0; k < kIdctItemStride && ok; k++) {
+    u32x4 w[8];
+    const DG_GLOBAL u32x4 *src = (const DG_GLOBAL u32x4 *)(gp<const int16_t>(im.coef) + (size_t)L.bidx * 64);
+#pragma unroll
+    for (uint32_t i = 0; i < 8; i++) w[i] = i < np ? src[i] : u32x4{0, 0, 0, 0};
+    IdctLoc N;
+    const bool nok = k + 1 < kIdctItemStride && idct_t_locate(im, it.item0 + k + 1, N);
+    const uint32_t nnp = nok ? idct_t_parts(im, N) : 0u;
+    idct_t_item(im, L, w, qpool);
+    L = N;
+    ok = nok;
+    np = nnp;
+  }
+}
+
+__device__ __forceinline__ void idct_t_item(const ImageDesc &im, const IdctLoc &L, const u32x4 w[8],
+                                            const QuantTable *__restrict__ qpool) {
+  const uint32_t c = L.c, by = L.by, bx = L.bx;
+  const bool v = L.v;
+  const uint32_t lane = threadIdx.x, cbw = im.cbw[c];
+  // Decode semantics as a runtime flag: with it as a template constant the
+  // whole block's transforms become one straight-line region and the
+  // scheduler interleaves all eight columns (185 VGPRs, 2 waves per SIMD);
+  // the per-transform branch keeps it at 94.
+  const bool zune = im.sem != 0;
   const DG_GLOBAL uint16_t *q = gp<const uint16_t>((uint64_t)(uintptr_t)qpool[im.qpool[c]].q);
   int32_t x[64];
   {
-    u32x4 w[8];
-    const DG_GLOBAL u32x4 *src = (const DG_GLOBAL u32x4 *)(gp<const int16_t>(im.coef) + (size_t)(v ? bidx : 0) * 64);
-#pragma unroll
-    for (int i = 0; i < 8; i++) w[i] = v ? src[i] : u32x4{0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 64; k++) {
       const uint32_t word = w[k >> 3][(k >> 1) & 3];

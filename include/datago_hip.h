@@ -124,6 +124,12 @@ typedef struct dg_ctx dg_ctx;
 /* device: HIP device ordinal (rank -> device).  cfg may be NULL (no resize:
  * image_config absent -> decode only, like img_tfm = None). */
 dg_status dg_ctx_create(int32_t device, const dg_image_config *cfg, dg_ctx **out);
+/* Waits for every call on ctx to return, then for its GPU work, and frees it.
+ * A process may also exit with contexts alive: an exit hook of the library
+ * (registered at the first dg_ctx_create, so it runs before the HIP
+ * runtime's own teardown) runs them down when no thread is inside one of
+ * their calls; calls made afterwards return DG_ERR_INVALID.
+ * DG_NO_EXIT_HOOK=1 disables it. */
 void dg_ctx_destroy(dg_ctx *ctx);
 const dg_bucket_table *dg_ctx_buckets(const dg_ctx *ctx);
 
@@ -291,6 +297,13 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "dec_strips"   k_band_dec: 16-row strips per workgroup (default 8)
  *   "reset_host_us" clears the host submit phase timers (stats "host_us_*")
  *   "sub_auto"    subsequence size of batches over 64 MiB of coded data when "sub_bits" is 0 (default 8192)
+ *   "sparse_coef" 1 = k_huff_write stores, and k_idct_t loads, only the 16-byte zigzag parts of each
+ *                 coefficient block up to its last nonzero coefficient (default 1); 0 = whole 128-byte blocks
+ *   "max_device_mb" device memory budget of the context in MiB (default 0 = none).  A submission whose
+ *                 plan does not fit -- after the retired buffers and the other slots' buffers are freed,
+ *                 waiting for their batches -- is split into sub-batches under the caller's one ticket; an
+ *                 image that alone exceeds it comes back DG_ERR_OOM.  Without a budget a failed device
+ *                 allocation takes the same path (drain the other slots, then split)
  * Stats: "batches", "coalesced_batches", "coalesced_images", "resync_rounds", "fix_workgroups", "write_mismatch",
  * "unsettled_batches", "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool" (tables pooled now),
  * "pool_flushes" (times the table pools were started over), "png_chunks", "png_serial_fallbacks",
@@ -298,7 +311,9 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  * of the pipelined progressive launches), "prog_aggregates", "prog_aggregate_images",
  * "meta_bytes" (the last batch's descriptor/list upload), "allocs", "alloc_mb", "alloc_us", "reclaims",
  * "retire_syncs" (device / page-locked buffer growth: count, MiB, wall microseconds; OOM reclaims; device-wide
- * syncs that freed grown-out buffers), "host_us_<phase>" / "host_cpu_us_<phase>" (wall / thread
+ * syncs that freed grown-out buffers), "device_mb" / "peak_device_mb" (device memory the context holds now /
+ * at most), "budget_splits", "budget_frees", "budget_oom" (sub-batch splits, slot buffers freed, images
+ * failed with DG_ERR_OOM under the budget or after a failed allocation), "host_us_<phase>" / "host_cpu_us_<phase>" (wall / thread
  * CPU microseconds in dg_submit* per phase: plan, pools, layout, lists, upload (staging copy), h2d, launch;
  * "host_us_slotwait": waiting for a free slot); -1 if unknown.
  *

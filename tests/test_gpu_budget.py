@@ -1,0 +1,100 @@
+"""Device memory budget (context option max_device_mb).
+
+A submission whose plan does not fit the budget is split into sub-batches
+under the caller's one ticket; the outputs stay bit-exact (equal to an
+unbudgeted context's, which the parity suites pin to the oracle).  An image
+that alone exceeds the budget fails with DG_ERR_OOM and nothing else does
+(worker_files.rs:63-70: a failed sample is dropped, never the worker)."""
+import numpy as np
+import pytest
+
+from datago_amd import _lib as L
+from datago_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(crop_and_resize=True, default_image_size=512, downsampling_ratio=16, min_aspect_ratio=0.5,
+          max_aspect_ratio=2.0, decode_semantics=1)
+
+
+def _ctx():
+    """A context without the Lanczos table cache (its arena would not count
+    the same with and without a budget)."""
+    c = L.Context(0, **KW)
+    c.set_option("coef_cache_mb", 0)
+    return c
+
+
+def _base_mb():
+    """Device MB of a context after one tiny image: table pools + tiny arenas."""
+    c = _ctx()
+    st, _, _ = c.decode_batch([synth.make_jpeg(1, 32, 32, 90)])[0]
+    assert st == 0
+    mb = c.stat("device_mb")
+    c.close()
+    return mb
+
+
+def test_budget_splits_stay_bit_exact():
+    datas = synth.mixed_corpus(77, 40, 256, 1200)
+    ref = _ctx()
+    want = ref.decode_batch(datas)
+    peak = ref.stat("peak_device_mb")
+    ref.close()
+    base = _base_mb()
+    assert peak > base
+    budget = base + max(8, (peak - base) // 3)
+    c = _ctx()
+    c.set_option("max_device_mb", budget)
+    got = c.decode_batch(datas)
+    assert c.stat("budget_splits") > 0, (peak, base, budget)
+    for (s0, a0, _), (s1, a1, _) in zip(want, got):
+        assert s0 == s1 == 0
+        assert a0.shape == a1.shape and np.array_equal(a0, a1)
+    # the descriptor buffer grows after the budget check: a few MB of slack at most
+    assert c.stat("peak_device_mb") <= budget + 16, (c.stat("peak_device_mb"), budget)
+    # device-resident submissions under the same budget: one ticket, several parts
+    tk, metas, keep = c.submit_host(datas[:12], [np.empty(max(c.output_size(d)[1], 1), np.uint8)
+                                                 for d in datas[:12]])
+    c.wait(tk)
+    assert all(metas[i].status == 0 for i in range(12))
+    c.close()
+
+
+def test_image_over_budget_fails_alone():
+    base = _base_mb()
+    c = _ctx()
+    c.set_option("max_device_mb", base + 6)
+    small = [synth.make_jpeg(10 + i, 96, 64, 90) for i in range(3)]
+    big = synth.make_jpeg(20, 2400, 1800, 92)
+    res = c.decode_batch(small[:2] + [big] + small[2:])
+    assert [r[0] for r in res] == [0, 0, L.DG_ERR_OOM, 0]
+    assert c.stat("budget_oom") == 1
+    ok = _ctx()
+    for (s, a, _), (s2, a2, _) in zip([res[0], res[1], res[3]], ok.decode_batch(small)):
+        assert s == s2 == 0 and np.array_equal(a, a2)
+    ok.close()
+    c.close()
+
+
+def test_budget_with_progressive_members():
+    """A split submission with progressive members: the baseline part splits,
+    the aggregate too; dg_wait_ready then dg_wait complete every member."""
+    base = _base_mb()
+    datas = synth.mixed_corpus(78, 16, 256, 900)
+    datas[3] = synth.make_jpeg(31, 700, 500, 90, "4:2:0", progressive=True)
+    datas[9] = synth.make_jpeg(32, 500, 700, 90, "4:4:4", progressive=True)
+    ref = _ctx()
+    want = ref.decode_batch(datas)
+    peak = ref.stat("peak_device_mb")
+    ref.close()
+    c = _ctx()
+    c.set_option("max_device_mb", base + max(8, (peak - base) // 3))
+    outs = [np.zeros(max(c.output_size(d)[1], 1), np.uint8) for d in datas]
+    tk, metas, keep = c.submit_host(datas, outs)
+    c.wait_ready(tk)
+    c.wait(tk)
+    for i, (s0, a0, _) in enumerate(want):
+        assert s0 == 0 and metas[i].status == 0
+        assert np.array_equal(outs[i][: a0.size], a0.reshape(-1))
+    c.close()
