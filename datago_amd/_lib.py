@@ -500,7 +500,8 @@ class Context:
         metas = (PayloadMeta * max(1, n))()
         ticket = ctypes.c_uint64()
         _check(load().dg_submit(self._h, n, srcs, lens, fb, optrs, capa, metas, ctypes.byref(ticket)))
-        return ticket.value, metas, (bufs, srcs, lens, fb, optrs, capa)
+        # keepalive: the output arrays too -- the batch writes them until wait(ticket)
+        return ticket.value, metas, (bufs, srcs, lens, fb, optrs, capa, list(outs))
 
     def host_register(self, arr: np.ndarray) -> None:
         """dg_host_register: page-lock a reused output array (or arena)."""

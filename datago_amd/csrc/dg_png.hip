@@ -21,6 +21,7 @@
 // stream, which goes through a 64 KiB LDS ring (the 32 KiB DEFLATE window plus
 // one flush unit) to HBM in 32 KiB coalesced bursts.  Parallelism across the
 // batch comes from one wave per image.
+#include <type_traits>
 #include <hip/hip_runtime.h>
 
 #include "dg_types.h"
@@ -723,16 +724,16 @@ __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ i
 // counts held in registers, the symbol read from `sym` (sorted by length).
 // k_inf_decode keeps the literal/length and distance lookups in LDS.
 #define DG_LDS __attribute__((address_space(3)))
-template <uint32_t B, typename LutPtr>
+template <uint32_t B, typename LutPtr, typename SymPtr = DG_GLOBAL uint16_t *>
 struct LaneTab {
   LutPtr lut;
-  DG_GLOBAL uint16_t *sym;  // [n], by (length, symbol)
+  SymPtr sym;  // [n], by (length, symbol)
   uint32_t first1, index1;  // canonical walk state at length B + 1
   uint32_t cpk[3];          // counts of lengths B+1..15, 10 bits each, 3 per word
 };
 
-template <uint32_t B, typename LutPtr>
-__device__ bool lane_build(const DG_GLOBAL uint8_t *lens, uint32_t n, LaneTab<B, LutPtr> &t) {
+template <uint32_t B, typename LutPtr, typename SymPtr>
+__device__ bool lane_build(const DG_GLOBAL uint8_t *lens, uint32_t n, LaneTab<B, LutPtr, SymPtr> &t) {
   uint32_t cnt[16];
 #pragma unroll
   for (uint32_t k = 0; k < 16; k++) cnt[k] = 0;
@@ -848,8 +849,8 @@ __device__ __forceinline__ uint32_t lb_get(LaneBits &r, uint32_t k) {
 // consumed bit position: wp counts the word held in w1
 __device__ __forceinline__ uint32_t lb_pos(const LaneBits &r) { return r.wp * 32u - r.nb; }
 
-template <uint32_t B, typename LutPtr>
-__device__ __forceinline__ uint32_t lane_sym(LaneBits &r, const LaneTab<B, LutPtr> &t) {
+template <uint32_t B, typename LutPtr, typename SymPtr>
+__device__ __forceinline__ uint32_t lane_sym(LaneBits &r, const LaneTab<B, LutPtr, SymPtr> &t) {
   const uint32_t peek = (uint32_t)r.bb;
   const uint32_t e = t.lut[peek & ((1u << B) - 1u)];
   if (e & 15u) {
@@ -875,10 +876,16 @@ __device__ __forceinline__ uint32_t lane_sym(LaneBits &r, const LaneTab<B, LutPt
   return 0xFFFFu;
 }
 
-// LDS bytes per lane: an LB-bit literal/length and a DB-bit distance lookup
-template <uint32_t LB, uint32_t DB>
+// LDS bytes per lane: an LB-bit literal/length and a DB-bit distance lookup,
+// and with SL the two symbol tables (288 + 32 entries) the canonical walk of
+// longer codes reads.  Without SL those live in global memory: every code
+// longer than the lookup costs the lane a dependent L2 round trip, and a
+// noisy RGB stream's literal codes are mostly 8-9 bits (round 5: the
+// configs[4] pool's images are literal-only deflate, ~22 KiB blocks).
+// (SL: + 4 bytes, so the lanes' tables start on different banks.)
+template <uint32_t LB, uint32_t DB, bool SL = false>
 constexpr uint32_t inf_lds_per_lane() {
-  return ((1u << LB) + (1u << DB)) * 2u;
+  return ((1u << LB) + (1u << DB) + (SL ? 288u + 32u + 2u : 0u)) * 2u;
 }
 
 // One lane per chunk: decode from the chunk's candidate block start until a
@@ -887,10 +894,10 @@ constexpr uint32_t inf_lds_per_lane() {
 // lie before the chunk (resolved by k_inf_resolve). WG lanes per workgroup;
 // the lookups take WG * inf_lds_per_lane<LB, DB>() bytes of LDS (64 lanes,
 // 9/7 bits: 80 KiB, two workgroups per CU).
-template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false>
+template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false, bool SL = false>
 __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
                                                    uint32_t nch) {
-  constexpr uint32_t kInfLdsPerLane = inf_lds_per_lane<LB, DB>();
+  constexpr uint32_t kInfLdsPerLane = inf_lds_per_lane<LB, DB, SL>();
   const uint32_t gi = blockIdx.x * WG + threadIdx.x;
   if (gi >= nch) return;
   InfChunk &c = ch[gi];
@@ -909,8 +916,17 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
   // LDS: per lane a 9-bit literal/length and a 7-bit distance lookup
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   DG_LDS uint16_t *lds = (DG_LDS uint16_t *)(DG_LDS uint8_t *)smem_raw + threadIdx.x * kInfLdsPerLane / 2;
-  LaneTab<LB, DG_LDS uint16_t *> tl{lds, (DG_GLOBAL uint16_t *)(tb + 2624), 0, 0, {0, 0, 0}};
-  LaneTab<DB, DG_LDS uint16_t *> td{lds + (1u << LB), (DG_GLOBAL uint16_t *)(tb + 3264), 0, 0, {0, 0, 0}};
+  using SymP = typename std::conditional<SL, DG_LDS uint16_t *, DG_GLOBAL uint16_t *>::type;
+  SymP lsym, dsym;
+  if constexpr (SL) {
+    lsym = lds + (1u << LB) + (1u << DB);
+    dsym = lsym + 288;
+  } else {
+    lsym = (DG_GLOBAL uint16_t *)(tb + 2624);
+    dsym = (DG_GLOBAL uint16_t *)(tb + 3264);
+  }
+  LaneTab<LB, DG_LDS uint16_t *, SymP> tl{lds, lsym, 0, 0, {0, 0, 0}};
+  LaneTab<DB, DG_LDS uint16_t *, SymP> td{lds + (1u << LB), dsym, 0, 0, {0, 0, 0}};
   LaneTab<6, DG_GLOBAL uint16_t *> tc{(DG_GLOBAL uint16_t *)(tb + 3328), (DG_GLOBAL uint16_t *)(tb + 3520), 0, 0,
                                       {0, 0, 0}};
   const uint32_t zbits_total = pd.zlen * 8u;
@@ -1570,17 +1586,18 @@ void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
 void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_inf_find, dim3(nwg), dim3(64), 0, st, imgs, ch, list);
 }
-template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false>
+template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false, bool SL = false>
 static void launch_inf_decode_t(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch) {
-  constexpr uint32_t lds = WG * inf_lds_per_lane<LB, DB>();
+  constexpr uint32_t lds = WG * inf_lds_per_lane<LB, DB, SL>();
   static bool attr = false;  // > 64 KiB of dynamic LDS
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_inf_decode<WG, LB, DB, Q>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+    (void)hipFuncSetAttribute((const void *)k_inf_decode<WG, LB, DB, Q, SL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   if (nch)
-    hipLaunchKernelGGL((k_inf_decode<WG, LB, DB, Q>), dim3((nch + WG - 1) / WG), dim3(WG), lds, st, imgs, ch, nch);
+    hipLaunchKernelGGL((k_inf_decode<WG, LB, DB, Q, SL>), dim3((nch + WG - 1) / WG), dim3(WG), lds, st, imgs, ch,
+                       nch);
 }
 // variant: 64-lane workgroups with 0 = 9/7-bit lookups (80 KiB, 2 per CU);
 // 1 = 8/6 bits (40 KiB, 4 per CU); 2 = 7/6 bits (24 KiB, 6 per CU);
@@ -1597,6 +1614,11 @@ void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint
     case 5: launch_inf_decode_t<64, 6, 4>(st, imgs, ch, nch); break;
     case 6: launch_inf_decode_t<64, 7, 6, true>(st, imgs, ch, nch); break;   // 2 + quad prefetch
     case 7: launch_inf_decode_t<64, 8, 6, true>(st, imgs, ch, nch); break;   // 1 + quad prefetch
+    // symbol tables in LDS (SL): 7/6 bits 64 KiB per wave, 6/5 52 KiB, 5/4 46 KiB, 8/6 96 KiB
+    case 8: launch_inf_decode_t<64, 7, 6, false, true>(st, imgs, ch, nch); break;
+    case 9: launch_inf_decode_t<64, 6, 5, false, true>(st, imgs, ch, nch); break;
+    case 10: launch_inf_decode_t<64, 5, 4, false, true>(st, imgs, ch, nch); break;
+    case 11: launch_inf_decode_t<64, 8, 6, false, true>(st, imgs, ch, nch); break;
     default: launch_inf_decode_t<64, 9, 7>(st, imgs, ch, nch); break;
   }
 }

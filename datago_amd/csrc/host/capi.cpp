@@ -1,7 +1,10 @@
 // capi.cpp — extern "C" entry points declared in include/datago_hip.h.
 #include <string.h>
 
+#include <execinfo.h>
+#include <signal.h>
 #include <stdlib.h>
+#include <unistd.h>
 
 #include <mutex>
 #include <new>
@@ -83,11 +86,28 @@ void exit_hook() {
   }
 }
 
+// Debug (DG_SEGV_TRACE=1): a host fault prints the native stack to stderr
+// (symbolised from the dynamic symbol tables) before the default action.
+void segv_trace(int sig) {
+  void *fr[64];
+  const int n = backtrace(fr, 64);
+  static const char msg[] = "datago_amd: fatal signal, native stack:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 void install_exit_hook() {
   static std::once_flag once;
   std::call_once(once, [] {
     const char *e = getenv("DG_NO_EXIT_HOOK");
     if (!(e && e[0] == '1')) atexit(exit_hook);
+    const char *t = getenv("DG_SEGV_TRACE");
+    if (t && t[0] == '1') {
+      signal(SIGSEGV, segv_trace);
+      signal(SIGABRT, segv_trace);
+    }
   });
 }
 

@@ -400,6 +400,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     ccache_idx_.clear();
     ccache_.clear();
     ccache_off_ = 0;
+    ccache_full_ = false;
     if (d_ccache_.p) hipFree(d_ccache_.p);
     d_ccache_.p = nullptr;
     d_ccache_.cap = 0;
@@ -632,8 +633,9 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "inf_decode") {  // k_inf_decode lookup bits (literal/length, distance): 0 9/7, 1 8/6, 2 7/6, 3 7/5, 4 6/5,
-                            // 5 6/4; 6, 7 = 2, 1 with the stream prefetched two quads ahead
-    if (v < 0 || v > 7) return DG_ERR_INVALID;
+                            // 5 6/4; 6, 7 = 2, 1 with the stream prefetched two quads ahead; 8 / 9 / 10 / 11 =
+                            // 7/6, 6/5, 5/4, 8/6 with the canonical walk's symbol tables in LDS
+    if (v < 0 || v > 11) return DG_ERR_INVALID;
     inf_decode_ = (uint32_t)v;
     return DG_OK;
   }
@@ -860,7 +862,7 @@ size_t Context::dev_footprint(const Slot *except) const {
 // writes it (finishing them first, as a pool flush does).  Runs before a
 // batch's lookups, so a batch never mixes entries of two arena lifetimes.
 void Context::ccache_maybe_reset(Slot &self) {
-  if (!ccache_cap_ || ccache_off_ <= ccache_cap_ / 8 * 7) return;
+  if (!ccache_cap_ || (!ccache_full_ && ccache_off_ <= ccache_cap_ / 8 * 7)) return;
   for (Slot &o : slots_) {
     if (&o == &self || !o.batch || o.batch->done || !o.batch->uses_ccache) continue;
     if (finish(o)) return;  // keep the arena as it is; the next batch tries again
@@ -868,6 +870,7 @@ void Context::ccache_maybe_reset(Slot &self) {
   ccache_idx_.clear();
   ccache_.clear();
   ccache_off_ = 0;
+  ccache_full_ = false;
   stat_ccache_resets_++;
 }
 
@@ -897,7 +900,10 @@ int Context::ccache_lookup(const ResizePass &ps, Batch &b, bool &hit) {
     return it->second;
   }
   const size_t bytes = align_up((size_t)ps.out_size * 8 + (size_t)ps.out_size * ps.ksize * 2, 256);
-  if (ccache_off_ + bytes > ccache_cap_) return -1;
+  if (ccache_off_ + bytes > ccache_cap_) {  // full: the next submit starts the arena over
+    ccache_full_ = true;
+    return -1;
+  }
   if (!d_ccache_.p) {
     if (hipMalloc(&d_ccache_.p, ccache_cap_) != hipSuccess) {
       (void)hipGetLastError();

@@ -286,6 +286,7 @@ class Context {
   std::vector<CEntry> ccache_;
   DevBuf d_ccache_;
   size_t ccache_off_ = 0, ccache_cap_ = (size_t)256 << 20;
+  bool ccache_full_ = false;  // an entry did not fit: start over at the next submit
   int64_t stat_ccache_hits_ = 0, stat_ccache_new_ = 0, stat_ccache_resets_ = 0;
   int ccache_lookup(const ResizePass &ps, Batch &b, bool &hit);  // mu_ held; -1 = not cached
   void ccache_maybe_reset(Slot &self);                            // mu_ held, before a batch's lookups

@@ -283,7 +283,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "uf_units"    1 or 2 (default 2): PNG unfilter filter units per lane per diagonal step (1: half the LDS)
  *   "inf_decode"  0..5: chunk-parallel inflate lookup bits (literal/length, distance) per lane in LDS:
  *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (default, 24 KiB), 3 7/5, 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
- *                 the compressed stream prefetched two 16-byte quads ahead per lane
+ *                 the compressed stream prefetched two 16-byte quads ahead per lane; 8 / 9 / 10 / 11 = 7/6, 6/5,
+ *                 5/4, 8/6 bits with the symbol tables of longer codes in LDS too (64 / 52 / 46 / 96 KiB per wave)
  *   "copy_threads" host threads copying a host-out batch's outputs to the caller's buffers (default 8)
  *   "write_split" 1 = k_huff_write decodes each entropy range as two halves split at the sync pass's
  *                 half-way checkpoint (images without restart markers; default); 0 = one lane per range

@@ -26,8 +26,10 @@ def _ctx():
 
 
 def _base_mb():
-    """Device MB of a context after one tiny image: table pools + tiny arenas."""
+    """Device MB of a context after one tiny image: table pools + tiny arenas
+    (allocated as a budgeted context does: exact sizes, no growth headroom)."""
     c = _ctx()
+    c.set_option("max_device_mb", 1 << 20)
     st, _, _ = c.decode_batch([synth.make_jpeg(1, 32, 32, 90)])[0]
     assert st == 0
     mb = c.stat("device_mb")

@@ -56,8 +56,8 @@ def test_cache_arena_resets():
     c.set_option("coef_cache_mb", 1)
     ref = L.Context(0, **KW)
     ref.set_option("coef_cache_mb", 0)
-    for k in range(6):
-        datas = synth.mixed_corpus(200 + k % 3, 16, 300, 1400)
+    for seed in (200, 201, 200, 202, 203, 204, 203, 205, 206, 205):  # repeats hit, new corpora fill the arena
+        datas = synth.mixed_corpus(seed, 10, 300, 1400)
         tk = [c.submit_host(datas, [np.zeros(max(c.output_size(d)[1], 1), np.uint8) for d in datas])]
         got = c.decode_batch(datas)
         want = ref.decode_batch(datas)
