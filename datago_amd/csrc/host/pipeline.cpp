@@ -397,7 +397,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     for (const Slot &o : slots_)
       if (o.batch && !o.batch->done && o.batch->uses_ccache) return DG_ERR_INVALID;  // not while tables are in use
     ccache_cap_ = (size_t)v << 20;
-    ccache_idx_.clear();
+    ccache_index_clear();
     ccache_.clear();
     ccache_off_ = 0;
     ccache_full_ = false;
@@ -867,17 +867,34 @@ void Context::ccache_maybe_reset(Slot &self) {
     if (&o == &self || !o.batch || o.batch->done || !o.batch->uses_ccache) continue;
     if (finish(o)) return;  // keep the arena as it is; the next batch tries again
   }
-  ccache_idx_.clear();
+  ccache_index_clear();
   ccache_.clear();
   ccache_off_ = 0;
   ccache_full_ = false;
   stat_ccache_resets_++;
 }
 
+void Context::ccache_index_clear() { ccache_slot_.assign((size_t)1 << kCIdxBits, -1); }
+
+int Context::ccache_find(const CKey &k, uint32_t &slot) const {
+  const uint32_t mask = (1u << kCIdxBits) - 1u;
+  slot = (uint32_t)CKeyHash()(k) & mask;
+  for (uint32_t probe = 0; probe <= mask; probe++, slot = (slot + 1) & mask) {
+    const int32_t e = ccache_slot_[slot];
+    if (e < 0) return -1;
+    if (ccache_[e].key == k) return e;
+  }
+  return -1;
+}
+
 void Context::ccache_rollback(size_t n0, size_t off0) {
-  while (ccache_.size() > n0) {
-    ccache_idx_.erase(ccache_.back().key);
-    ccache_.pop_back();
+  if (ccache_.size() <= n0) return;
+  ccache_.resize(n0);  // (rare: a submit that installed no batch) rebuild the index
+  ccache_index_clear();
+  for (size_t i = 0; i < ccache_.size(); i++) {
+    uint32_t slot;
+    ccache_find(ccache_[i].key, slot);
+    ccache_slot_[slot] = (int32_t)i;
   }
   ccache_off_ = std::min(ccache_off_, off0);
 }
@@ -891,16 +908,19 @@ int Context::ccache_lookup(const ResizePass &ps, Batch &b, bool &hit) {
   k.in_size = ps.in_size;
   k.out_size = ps.out_size;
   k.ksize = ps.ksize;
-  auto it = ccache_idx_.find(k);
-  if (it != ccache_idx_.end()) {
-    if (!ccache_[it->second].ready) return -1;  // a batch in flight is writing it: compute our own copy
+  if (ccache_slot_.empty()) ccache_index_clear();
+  uint32_t slot;
+  const int found = ccache_find(k, slot);
+  if (found >= 0) {
+    if (!ccache_[found].ready) return -1;  // a batch in flight is writing it: compute our own copy
     hit = true;
     b.uses_ccache = true;
     stat_ccache_hits_++;
-    return it->second;
+    return found;
   }
   const size_t bytes = align_up((size_t)ps.out_size * 8 + (size_t)ps.out_size * ps.ksize * 2, 256);
-  if (ccache_off_ + bytes > ccache_cap_) {  // full: the next submit starts the arena over
+  // full (arena, or the index at 3/4 load): the next submit starts the arena over
+  if (ccache_off_ + bytes > ccache_cap_ || ccache_.size() >= ((size_t)3 << kCIdxBits) / 4) {
     ccache_full_ = true;
     return -1;
   }
@@ -915,7 +935,7 @@ int Context::ccache_lookup(const ResizePass &ps, Batch &b, bool &hit) {
   }
   const int idx = (int)ccache_.size();
   ccache_.push_back(CEntry{k, ccache_off_, 0, false});
-  ccache_idx_.emplace(k, idx);
+  ccache_slot_[slot] = idx;
   ccache_off_ += bytes;
   b.uses_ccache = true;
   stat_ccache_new_++;

@@ -282,7 +282,13 @@ class Context {
     int32_t precision;  // read back from the producing batch
     bool ready;
   };
-  std::unordered_map<CKey, int, CKeyHash> ccache_idx_;
+  // open-addressed index over ccache_ (linear probing, -1 = empty): a
+  // node-based map cost ~0.8 us per lookup, 0.5 ms of planning per
+  // configs[1] batch (profiles/r05/ab5); this one is a few cache lines
+  static constexpr uint32_t kCIdxBits = 16;
+  std::vector<int32_t> ccache_slot_;  // 1 << kCIdxBits slots
+  int ccache_find(const CKey &k, uint32_t &slot) const;  // entry index or -1; slot: where it is / would go
+  void ccache_index_clear();
   std::vector<CEntry> ccache_;
   DevBuf d_ccache_;
   size_t ccache_off_ = 0, ccache_cap_ = (size_t)256 << 20;
