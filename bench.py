@@ -1195,7 +1195,9 @@ def main() -> int:
             "corpus_generated_here": n_made if seq is not None else None,
             "stats": {"resync_rounds": ctx.stat("resync_rounds"), "fix_workgroups": ctx.stat("fix_workgroups"),
                       "write_mismatch": ctx.stat("write_mismatch"), "sync_iters_max": ctx.stat("sync_iters_max"),
-                      "sub_bits": ctx.stat("sub_bits"), "lead_bits": a.lead_bits},
+                      "sub_bits": ctx.stat("sub_bits"), "lead_bits": a.lead_bits,
+                      "png_chunks": ctx.stat("png_chunks"), "png_serial_fallbacks": ctx.stat("png_serial_fallbacks"),
+                      "png_small_streams": ctx.stat("png_small_streams")},
             "wg_timing_us": ({f"{k}_{q}": ctx.stat(f"wg_{k}_{q}") / 1000 for k in ("sync", "write")
                               for q in ("span", "mean", "p90", "max")} if a.wg_timing else None),
         }

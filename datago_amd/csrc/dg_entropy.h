@@ -231,10 +231,9 @@ struct WriteCtx {
   uint32_t blocks_per_seg, total_blocks;
   int32_t cur;   // global index of the block being filled (-1 = none / dropped)
   uint32_t zs;   // first zigzag index this thread owns in the current block
-  uint32_t hi = 0;  // zigzag index of the last coefficient written into the current block
 #if defined(DG_DEVICE)
-  // sparse blocks (ImageDesc::ccnt): per-block count of the 16-byte parts
-  // stored, nullptr = dense (all 8 parts)
+  // sparse blocks (ImageDesc::ccnt): per block, the mask of the 16-byte
+  // parts stored (the nonzero ones); nullptr = dense (all 8 parts)
   DG_GLOBAL uint8_t *cnt = nullptr;
   // wave-cooperative flush (k_huff_write): this wave's lane-0 block, block
   // stride (int16), and a 128-dword LDS table of the wave
@@ -287,7 +286,7 @@ DG_HD void wc_flush(WriteCtx &w, uint32_t ze) {
 #if defined(DG_DEVICE)
   // a block shared by two ranges (or cut at the range end) is stored dense:
   // each owner writes its zigzag span and both announce all 8 parts
-  if (w.cnt) w.cnt[w.cur] = 8;
+  if (w.cnt) w.cnt[w.cur] = 0xFFu;
 #endif
   w.cur = -1;
 }
@@ -319,9 +318,7 @@ __device__ __forceinline__ void wc_coop_flush(WriteCtx &w, bool pending) {
   const uint64_t am = __ballot(1);
   if (pending) {
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
-    // lane | parts to store << 8 (sparse: through the last nonzero coefficient)
-    const uint32_t np = w.cnt ? (w.hi >> 3) + 1u : 8u;
-    w.tab[rank] = __lane_id() | (np << 8);
+    w.tab[rank] = __lane_id();  // bits 8..15: the nonzero parts (sparse flushes OR them in)
     w.tab[64 + rank] = (uint32_t)w.cur;
   }
   __builtin_amdgcn_wave_barrier();
@@ -384,19 +381,21 @@ __device__ __forceinline__ void wc_coop_flush(WriteCtx &w, bool pending) {
   for (uint32_t c = wr; c < nc; c += na) {
     const uint32_t k = c >> 3, part = c & 7u;
     const int32_t idx = (int32_t)w.tab[64 + k];
-    const uint32_t tk = w.tab[k], np = tk >> 8;
-    const uint32_t own = tk & 255u;
+    const uint32_t own = w.tab[k] & 255u;
     u32x4 *src = (u32x4 *)(w.wave_blk + own * w.stride) + (w.stride == 64u ? part ^ ((own >> 1) & 7u) : part);
-    // parts past the last nonzero coefficient are zero in LDS already and
-    // are not stored (sparse blocks; np = 8 otherwise)
-    if (part < np) {
-      if (idx >= 0) *(DG_GLOBAL u32x4 *)(w.coef + (size_t)idx * 64 + part * 8) = *src;
-      *src = zero;
-    }
-    if (part == 0) {
-      if (w.cnt && idx >= 0) w.cnt[idx] = (uint8_t)np;
-      wc_list_late(w, idx);  // fused IDCT with < 8 active lanes: k_idct_list takes it
-    }
+    const u32x4 v = *src;
+    // sparse blocks: an all-zero part is not stored; the parts that are go
+    // into the block's mask (k_idct_t loads those, the rest read as zero)
+    const bool nz = (v.x | v.y | v.z | v.w) != 0u;
+    if (idx >= 0 && (nz || !w.cnt)) *(DG_GLOBAL u32x4 *)(w.coef + (size_t)idx * 64 + part * 8) = v;
+    if (w.cnt && nz) atomicOr(&w.tab[k], 256u << part);
+    *src = zero;
+    if (part == 0) wc_list_late(w, idx);  // fused IDCT with < 8 active lanes: k_idct_list takes it
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (w.cnt && wr < nb) {  // one lane per flushed block: its mask
+    const int32_t idx = (int32_t)w.tab[64 + wr];
+    if (idx >= 0) w.cnt[idx] = (uint8_t)(w.tab[wr] >> 8);
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -784,10 +783,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
         w->nin++;
       }
       const uint32_t zz = z + run;
-      if (isdc || (size && zz < 64u)) {
-        w->blk[zz ^ w->sw] = (int16_t)(isdc ? sel3(w->pred, comp) : v);
-        w->hi = zz;
-      }
+      if (isdc || (size && zz < 64u)) w->blk[zz ^ w->sw] = (int16_t)(isdc ? sel3(w->pred, comp) : v);
     }
     uint32_t zn = take_m ? zm : huff_next_z(z, sym);
     if (pair && !stage && (WRITE || !take_m)) {
@@ -808,10 +804,7 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
         if (tk) {
           if (WRITE) {
             const uint32_t zz2 = zn + (sx >> 4);
-            if (zx && zz2 < 64u) {
-              w->blk[zz2 ^ w->sw] = (int16_t)huff_value(bx, lx, zx);
-              w->hi = zz2;
-            }
+            if (zx && zz2 < 64u) w->blk[zz2 ^ w->sw] = (int16_t)huff_value(bx, lx, zx);
           }
           pos += lx + zx;
           used += lx + zx;

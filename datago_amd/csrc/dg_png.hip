@@ -52,13 +52,19 @@ constexpr uint32_t kFlush = 32768;     // ring -> HBM burst
 constexpr uint32_t kWin = 1024;        // input window (32-bit words) in LDS
 constexpr uint32_t kLitBits = 10, kDistBits = 8, kClBits = 7;
 
-__constant__ uint16_t c_lbase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                     31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t c_dbase[30] = {1,    2,    3,    4,    5,    7,     9,     13,    17,  25,
-                                     33,   49,   65,   97,   129,  193,   257,   385,   513, 769,
-                                     1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+// base | extra bits << 16 of each length / distance symbol: one dword, so a
+// wave-uniform index reads it with a scalar load
+__constant__ uint32_t c_lenx[29] = {
+    3,  4,  5,  6,  7,  8,  9,  10, 11 | 1u << 16,  13 | 1u << 16,  15 | 1u << 16,  17 | 1u << 16,  19 | 2u << 16,
+    23 | 2u << 16,  27 | 2u << 16,  31 | 2u << 16,  35 | 3u << 16,  43 | 3u << 16,  51 | 3u << 16,  59 | 3u << 16,
+    67 | 4u << 16,  83 | 4u << 16,  99 | 4u << 16,  115 | 4u << 16, 131 | 5u << 16, 163 | 5u << 16, 195 | 5u << 16,
+    227 | 5u << 16, 258};
+__constant__ uint32_t c_distx[30] = {
+    1,  2,  3,  4,  5 | 1u << 16,  7 | 1u << 16,  9 | 2u << 16,  13 | 2u << 16,  17 | 3u << 16,  25 | 3u << 16,
+    33 | 4u << 16,  49 | 4u << 16,  65 | 5u << 16,  97 | 5u << 16,  129 | 6u << 16,  193 | 6u << 16,
+    257 | 7u << 16,  385 | 7u << 16,  513 | 8u << 16,  769 | 8u << 16,  1025 | 9u << 16,  1537 | 9u << 16,
+    2049 | 10u << 16,  3073 | 10u << 16,  4097 | 11u << 16,  6145 | 11u << 16,  8193 | 12u << 16,
+    12289 | 12u << 16,  16385 | 13u << 16,  24577 | 13u << 16};
 __constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // Canonical Huffman table in LDS.  lut[prefix] = (symbol << 4) | length for
@@ -179,6 +185,16 @@ __device__ __forceinline__ void refill(InflateSmem &sm, BitReader &br, const DG_
   br.wnext++;
 }
 
+// The reader state is wave-uniform by construction; re-asserting it keeps the
+// compiler from carrying it in VGPRs after the lane-dependent stores (it then
+// branches on SCC and reads the symbol tables with scalar loads).
+__device__ __forceinline__ void br_uni(BitReader &br) {
+  br.bb = ((uint64_t)uni((uint32_t)(br.bb >> 32)) << 32) | uni((uint32_t)br.bb);
+  br.nb = uni(br.nb);
+  br.wnext = uni(br.wnext);
+  br.wbase = uni(br.wbase);
+}
+
 __device__ __forceinline__ uint32_t getbits(BitReader &br, uint32_t k) {
   const uint32_t v = (uint32_t)br.bb & ((1u << k) - 1u);
   br.bb >>= k;
@@ -277,6 +293,9 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
   }
   bool last = false;
   while (!status && !last && op < want) {
+    br_uni(br);
+    op = uni(op);
+    fp = uni(fp);
     refill(sm, br, z);
     last = getbits(br, 1) != 0;
     const uint32_t type = getbits(br, 2);
@@ -411,6 +430,10 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
     }
     // symbols
     for (;;) {
+      br_uni(br);
+      op = uni(op);
+      fp = uni(fp);
+      nlit = uni(nlit);
       refill(sm, br, z);
       const uint32_t s = decode_sym(br, tl);
       if (s < 256) {
@@ -427,7 +450,8 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
         status = 2;
         break;
       }
-      const uint32_t len = c_lbase[s - 257] + getbits(br, c_lext[s - 257]);
+      const uint32_t lx = c_lenx[s - 257];
+      const uint32_t len = (lx & 0xFFFFu) + getbits(br, lx >> 16);
       refill(sm, br, z);
       const uint32_t ds = decode_sym(br, td);
       if (ds >= 30) {
@@ -435,33 +459,39 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
         break;
       }
       refill(sm, br, z);
-      const uint32_t dist = c_dbase[ds] + getbits(br, c_dext[ds]);
+      const uint32_t dx = c_distx[ds];
+      const uint32_t dist = (dx & 0xFFFFu) + getbits(br, dx >> 16);
       if (dist > op) {
         status = 2;
         break;
       }
       stash_flush();
       // every source byte lies before `op` (an overlapping copy repeats the
-      // first `dist` bytes), so all <= 5 reads per lane go out before the
-      // writes: one LDS round trip per match
-      const uint32_t q = op, src0 = op - dist;
-      const float rcp = 1.0f / (float)dist;
-      uint32_t v[5];
-#pragma unroll
-      for (uint32_t i = 0; i < 5; i++) {  // len <= 258
-        const uint32_t j = lane + 64 * i;
-        uint32_t k = j;
-        if (dist < len) {
-          uint32_t qt = (uint32_t)((float)j * rcp);
-          k = j - qt * dist;
-          if (k >= dist) k -= dist;
+      // first `dist` bytes), so no read sees a byte this match writes: each
+      // 64-byte round reads then writes.  Branches are wave-uniform.
+      const uint32_t q = op, src0 = op - dist, rounds = (len + 63u) >> 6;
+      if (dist == 1u) {  // run of one byte (masks, flat rows): one broadcast read
+        const uint32_t b = sm.ring[src0 & kRingMask];
+        for (uint32_t r = 0; r < rounds; r++) {
+          const uint32_t j = lane + 64u * r;
+          if (j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)b;
         }
-        v[i] = j < len ? sm.ring[(src0 + k) & kRingMask] : 0u;
-      }
-#pragma unroll
-      for (uint32_t i = 0; i < 5; i++) {
-        const uint32_t j = lane + 64 * i;
-        if (j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)v[i];
+      } else if (dist >= len) {  // no overlap: straight copy
+        for (uint32_t r = 0; r < rounds; r++) {
+          const uint32_t j = lane + 64u * r;
+          const uint32_t v = j < len ? sm.ring[(src0 + j) & kRingMask] : 0u;
+          if (j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)v;
+        }
+      } else {  // overlapping period-`dist` copy
+        const float rcp = 1.0f / (float)dist;
+        for (uint32_t r = 0; r < rounds; r++) {
+          const uint32_t j = lane + 64u * r;
+          const uint32_t qt = (uint32_t)((float)j * rcp);  // j / dist or one less (j < 320)
+          uint32_t k = j - qt * dist;
+          if (k >= dist) k -= dist;
+          const uint32_t v = j < len ? sm.ring[(src0 + k) & kRingMask] : 0u;
+          if (j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)v;
+        }
       }
       op += len;
       if (op >= want) break;
@@ -646,13 +676,24 @@ __device__ __forceinline__ bool inf_candidate(const DG_GLOBAL uint32_t *z, uint3
 }
 
 // One wave per chunk (but chunk 0): the first candidate block start in the
-// chunk's bit range.  64 consecutive bit positions per step through the fast
-// stage (the 5 words they span are wave-uniform loads); the survivors queue
-// up in LDS in position order and go through the full stage 64 at a time, one
-// per lane, so the wave does not serialise on one lane's check per step.
+// chunk's bit range, through three filters of rising cost, each applied to
+// the survivors of the last, 64 positions per lane-parallel round:
+//  1. header fields (BTYPE = 2, HLIT <= 29, HDIST <= 29), ~10 instructions per
+//     position over 64 consecutive positions per step; ~22% of random
+//     positions pass (round 5: this stage alone replaced inf_header_fast on
+//     every position -- the finder issued ~380 K VALU per wave and kept the
+//     GPU busy while the other batches' kernels waited);
+//  2. inf_header_fast (the code-length code's Kraft sum) on 64 queued
+//     survivors at a time, their stream words read from a 32-word LDS ring of
+//     the recent steps; ~2% of those pass;
+//  3. inf_header_full, 64 at a time as before.
+// Every stage keeps position order, so the first position passing stage 3 is
+// the first candidate of the chunk.
 __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
                                                  const WgItem *__restrict__ list) {
-  __shared__ uint32_t qpos[128];
+  __shared__ uint32_t qpos[128];   // stage-3 queue (Kraft survivors)
+  __shared__ uint32_t q1pos[128];  // stage-2 queue (header-field survivors)
+  __shared__ uint32_t ring[32];    // stream words W - 27 .. W + 4 of the current step
   const WgItem it = list[blockIdx.x];
   InfChunk &c = ch[it.image];
   const ImageDesc &im = imgs[c.image];
@@ -662,7 +703,7 @@ __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ i
   const uint32_t b1 = min((c.idx + 1) * c.span * 8u, zlen * 8u);
   const uint32_t lane = threadIdx.x, hl = lane >> 5, sh = lane & 31u;
   const uint64_t below = (1ull << lane) - 1ull;
-  uint32_t found = kInfNone, qn = 0;
+  uint32_t found = kInfNone, qn = 0, q1n = 0, age = 0;
   // words W..W+4 of the current step (W = p / 32) and W+5, W+6 (the next
   // step's new ones), loaded a step ahead
   auto word = [&](uint32_t w) { return uni(w < zwords ? z[w] : 0u); };
@@ -677,39 +718,69 @@ __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ i
   for (uint32_t p = b0;; p += 64) {  // b0 and p are multiples of 64
     const bool more = p < b1;
     if (more) {
-      uint32_t q[4];
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++) q[k] = hl ? u[k + 1] : u[k];
-      uint64_t lo, hi;
-      inf_bits96(q, sh, lo, hi);
-      const bool pass = p + lane < b1 && inf_header_fast(lo, hi) != 0;
+      const uint32_t W = p >> 5;
+      if (lane < 5) ring[(W + lane) & 31u] = lane == 0 ? u[0] : lane == 1 ? u[1] : lane == 2 ? u[2] : lane == 3 ? u[3] : u[4];
+      // stage 1: BFINAL any, BTYPE = 2 (bits 1-2), HLIT and HDIST <= 29 (bits 3-12)
+      const uint64_t a = (uint64_t)(hl ? u[1] : u[0]) | ((uint64_t)(hl ? u[2] : u[1]) << 32);
+      const uint32_t h = (uint32_t)(a >> sh) & 0x1FFFu;
+      const bool pass = p + lane < b1 && ((h >> 1) & 3u) == 2u && ((h >> 3) & 31u) <= 29u && ((h >> 8) & 31u) <= 29u;
       const uint64_t m = __ballot(pass);
-      if (pass) qpos[qn + (uint32_t)__popcll(m & below)] = p + lane;
-      qn += (uint32_t)__popcll(m);
+      if (pass) q1pos[q1n + (uint32_t)__popcll(m & below)] = p + lane;
+      q1n += (uint32_t)__popcll(m);
+      age++;
       u[0] = u[2];
       u[1] = u[3];
       u[2] = u[4];
       u[3] = n5;
       u[4] = n6;
-      n5 = word((p >> 5) + 7);
-      n6 = word((p >> 5) + 8);
+      n5 = word(W + 7);
+      n6 = word(W + 8);
     }
-    // full checks, oldest 64 survivors first (all remaining ones at the end)
-    while (qn >= 64 || (!more && qn > 0)) {
-      __syncthreads();
-      const uint32_t nb = qn < 64 ? qn : 64u;
-      const uint32_t pos = qpos[lane < nb ? lane : 0];
-      const bool ok = lane < nb && inf_candidate(z, zwords, pos);
-      const uint64_t mo = __ballot(ok);
-      if (mo) {
-        found = uni(qpos[__ffsll((long long)mo) - 1]);
-        break;
+    // stage 2: the Kraft test on queued survivors (all of them at the end, or
+    // once they are 8 steps old: the ring holds 13 steps back); stage 3: full
+    // checks, oldest 64 Kraft survivors first (all remaining ones at the end).
+    // A stage-2 round runs only while the stage-3 queue has room for it.
+    for (;;) {
+      bool did = false;
+      if (qn < 64 && (q1n >= 64 || (q1n > 0 && (!more || age >= 8)))) {
+        __syncthreads();
+        const uint32_t nb = q1n < 64 ? q1n : 64u;
+        const uint32_t pos = q1pos[lane < nb ? lane : 0];
+        uint32_t q[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) q[k] = ring[((pos >> 5) + k) & 31u];
+        uint64_t lo, hi;
+        inf_bits96(q, pos & 31u, lo, hi);
+        const bool pass = lane < nb && inf_header_fast(lo, hi) != 0;
+        const uint64_t m = __ballot(pass);
+        if (pass) qpos[qn + (uint32_t)__popcll(m & below)] = pos;
+        qn += (uint32_t)__popcll(m);
+        const uint32_t rest = q1n - nb;  // < 64
+        const uint32_t keep = lane < rest ? q1pos[64 + lane] : 0u;
+        __syncthreads();
+        if (lane < rest) q1pos[lane] = keep;
+        q1n = rest;
+        age = 0;
+        did = true;
       }
-      const uint32_t rest = qn - nb;  // < 64
-      const uint32_t keep = lane < rest ? qpos[64 + lane] : 0u;
-      __syncthreads();
-      if (lane < rest) qpos[lane] = keep;
-      qn = rest;
+      if (qn >= 64 || (!more && qn > 0)) {
+        __syncthreads();
+        const uint32_t nb = qn < 64 ? qn : 64u;
+        const uint32_t pos = qpos[lane < nb ? lane : 0];
+        const bool ok = lane < nb && inf_candidate(z, zwords, pos);
+        const uint64_t mo = __ballot(ok);
+        if (mo) {
+          found = uni(qpos[__ffsll((long long)mo) - 1]);
+          break;
+        }
+        const uint32_t rest = qn - nb;  // < 64
+        const uint32_t keep = lane < rest ? qpos[64 + lane] : 0u;
+        __syncthreads();
+        if (lane < rest) qpos[lane] = keep;
+        qn = rest;
+        did = true;
+      }
+      if (!did) break;
     }
     if (found != kInfNone || !more) break;
     __syncthreads();
@@ -786,52 +857,69 @@ __device__ bool lane_build(const DG_GLOBAL uint8_t *lens, uint32_t n, LaneTab<B,
   return true;
 }
 
+constexpr uint32_t kLbBuf = 8;  // Q: stream words buffered in registers per lane
+
 struct LaneBits {
   uint64_t bb;
   uint32_t nb, wp, zwords;  // wp: index of the next stream word to shift into bb
   uint32_t w1;              // Q = false: that word, loaded one refill ahead
-  u32x4 cur, nxt;           // Q = true: the aligned quad holding word wp, and the quad after it
+  uint32_t nbuf;            // Q = true: words wp .. wp + nbuf - 1 held in buf
+  uint32_t buf[kLbBuf];
 };
 
-// 16-byte aligned quad of stream words at word index i (i % 4 == 0); words
-// past the stream read as zero
-__device__ __forceinline__ u32x4 lb_quad(const DG_GLOBAL uint32_t *z, uint32_t zwords, uint32_t i) {
-  if (i + 4 <= zwords) return *(const DG_GLOBAL u32x4 *)(z + i);
-  u32x4 q = {0u, 0u, 0u, 0u};
+// Q: the next kLbBuf stream words of every lane sit in registers, refilled
+// for the whole wave at once (lb_top) when any lane runs low.  A per-lane
+// load one word ahead (Q = false) sits in a lane-divergent branch, so the
+// compiler waits for it where the branches join: every fourth symbol of a
+// literal-heavy stream paid a full memory latency.
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ void lb_fill(LaneBits &r, const DG_GLOBAL uint32_t *z) {
+  const uint32_t i = r.wp;
+  if (i + kLbBuf <= r.zwords) {
 #pragma unroll
-  for (uint32_t k = 0; k < 4; k++)
-    if (i + k < zwords) q[k] = z[i + k];
-  return q;
+    for (uint32_t k = 0; k < kLbBuf; k += 4) {
+      const u32x4a q = *(const DG_GLOBAL u32x4a *)(z + i + k);
+      r.buf[k] = q.x;
+      r.buf[k + 1] = q.y;
+      r.buf[k + 2] = q.z;
+      r.buf[k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kLbBuf; k++) r.buf[k] = i + k < r.zwords ? z[i + k] : 0u;
+  }
+  r.nbuf = kLbBuf;
 }
 
-// Q: prefetch 4 to 8 words (16 to 32 symbols of a literal-heavy stream) ahead
-// in two aligned 16-byte quads instead of one word (about 4 symbols): the
-// per-lane decode is a dependent chain, and one word ahead left each refill
-// waiting out most of a global load's latency.
 template <bool Q>
 __device__ __forceinline__ void lb_seek(LaneBits &r, const DG_GLOBAL uint32_t *z, uint32_t wp) {
   r.wp = wp;
   if (Q) {
-    r.cur = lb_quad(z, r.zwords, wp & ~3u);
-    r.nxt = lb_quad(z, r.zwords, (wp & ~3u) + 4u);
+    lb_fill(r, z);
   } else {
     r.w1 = wp < r.zwords ? z[wp] : 0u;
   }
+}
+
+// Q: at a point every lane of the wave reaches: refill all lanes' buffers
+// together once any lane holds fewer words than a symbol step can take (a
+// length/distance pair is at most 48 bits: two words)
+template <bool Q>
+__device__ __forceinline__ void lb_top(LaneBits &r, const DG_GLOBAL uint32_t *z) {
+  if (Q && __ballot(r.nbuf < 3u)) lb_fill(r, z);
 }
 
 template <bool Q = false>
 __device__ __forceinline__ void lb_refill(LaneBits &r, const DG_GLOBAL uint32_t *z) {
   if (r.nb < 32) {
     if (Q) {
-      const uint32_t k = r.wp & 3u;
-      const uint32_t w = k == 0 ? r.cur.x : k == 1 ? r.cur.y : k == 2 ? r.cur.z : r.cur.w;
-      r.bb |= (uint64_t)w << r.nb;
+      if (r.nbuf == 0) lb_fill(r, z);  // off the symbol loop (headers, stored blocks)
+      r.bb |= (uint64_t)r.buf[0] << r.nb;
       r.nb += 32;
       r.wp++;
-      if ((r.wp & 3u) == 0) {
-        r.cur = r.nxt;
-        r.nxt = lb_quad(z, r.zwords, r.wp + 4u);
-      }
+      r.nbuf--;
+#pragma unroll
+      for (uint32_t k = 0; k + 1 < kLbBuf; k++) r.buf[k] = r.buf[k + 1];
     } else {
       r.bb |= (uint64_t)r.w1 << r.nb;
       r.nb += 32;
@@ -1044,6 +1132,7 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
     }
     // symbols of the block
     for (;;) {
+      lb_top<Q>(r, z);
       lb_refill<Q>(r, z);
       const uint32_t s = lane_sym(r, tl);
       if (s < 256) {
@@ -1059,7 +1148,8 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
         status = 1;
         break;
       }
-      const uint32_t len = c_lbase[s - 257] + lb_get(r, c_lext[s - 257]);
+      const uint32_t lx = c_lenx[s - 257];
+      const uint32_t len = (lx & 0xFFFFu) + lb_get(r, lx >> 16);
       lb_refill<Q>(r, z);
       const uint32_t ds = lane_sym(r, td);
       if (ds >= 30) {
@@ -1067,7 +1157,8 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
         break;
       }
       lb_refill<Q>(r, z);
-      const uint32_t dist = c_dbase[ds] + lb_get(r, c_dext[ds]);
+      const uint32_t dx = c_distx[ds];
+      const uint32_t dist = (dx & 0xFFFFu) + lb_get(r, dx >> 16);
       if (q + len > cap) {
         status = 2;
         break;
@@ -1602,8 +1693,8 @@ static void launch_inf_decode_t(hipStream_t st, const ImageDesc *imgs, InfChunk 
 // variant: 64-lane workgroups with 0 = 9/7-bit lookups (80 KiB, 2 per CU);
 // 1 = 8/6 bits (40 KiB, 4 per CU); 2 = 7/6 bits (24 KiB, 6 per CU);
 // 3 = 7/5 bits (20 KiB, 8 per CU); 4 = 6/5 bits (12 KiB); 5 = 6/4 bits
-// (10 KiB); 6 / 7 = 2 / 1 with the stream prefetched two 16-byte quads
-// ahead (lb_refill<true>). 32-lane workgroups measured no faster
+// (10 KiB); 6 / 7 = 2 / 1 with the wave-batched register stream buffer
+// (lb_top / lb_refill<true>). 32-lane workgroups measured no faster
 // than 64-lane ones of the same LDS (profiles/r03/infdec)
 void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch, uint32_t variant) {
   switch (variant) {
@@ -1612,13 +1703,17 @@ void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint
     case 3: launch_inf_decode_t<64, 7, 5>(st, imgs, ch, nch); break;
     case 4: launch_inf_decode_t<64, 6, 5>(st, imgs, ch, nch); break;
     case 5: launch_inf_decode_t<64, 6, 4>(st, imgs, ch, nch); break;
-    case 6: launch_inf_decode_t<64, 7, 6, true>(st, imgs, ch, nch); break;   // 2 + quad prefetch
-    case 7: launch_inf_decode_t<64, 8, 6, true>(st, imgs, ch, nch); break;   // 1 + quad prefetch
-    // symbol tables in LDS (SL): 7/6 bits 64 KiB per wave, 6/5 52 KiB, 5/4 46 KiB, 8/6 96 KiB
+    case 6: launch_inf_decode_t<64, 7, 6, true>(st, imgs, ch, nch); break;   // 2 + register buffer
+    case 7: launch_inf_decode_t<64, 8, 6, true>(st, imgs, ch, nch); break;   // 1 + register buffer
+    // symbol tables in LDS (SL): 7/6 bits 64 KiB per wave, 6/5 52 KiB, 8/6 96 KiB; 12 / 13 = 8 / 9 with the
+    // register buffer (neither the walk's symbol read nor a stream load on a lane's per-symbol path)
     case 8: launch_inf_decode_t<64, 7, 6, false, true>(st, imgs, ch, nch); break;
     case 9: launch_inf_decode_t<64, 6, 5, false, true>(st, imgs, ch, nch); break;
-    case 10: launch_inf_decode_t<64, 5, 4, false, true>(st, imgs, ch, nch); break;
     case 11: launch_inf_decode_t<64, 8, 6, false, true>(st, imgs, ch, nch); break;
+    case 12: launch_inf_decode_t<64, 7, 6, true, true>(st, imgs, ch, nch); break;
+    case 13: launch_inf_decode_t<64, 6, 5, true, true>(st, imgs, ch, nch); break;
+    case 14: launch_inf_decode_t<64, 9, 7, true>(st, imgs, ch, nch); break;
+    case 15: launch_inf_decode_t<64, 8, 6, true, true>(st, imgs, ch, nch); break;
     default: launch_inf_decode_t<64, 9, 7>(st, imgs, ch, nch); break;
   }
 }

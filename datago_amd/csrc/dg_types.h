@@ -296,8 +296,8 @@ struct ImageDesc {
   uint64_t coef;            // device address of block 0 (int16 zigzag[64] per block, decode order)
   uint64_t stage;           // decode-once staging (dg_entropy.h StageCtx), 0 = off
   // Sparse coefficient blocks (option "sparse_coef"): one byte per block, the
-  // number of 16-byte zigzag parts k_huff_write stored (1..8, through the
-  // block's last nonzero coefficient); k_idct_t loads only those parts and
+  // mask of the 16-byte zigzag parts k_huff_write stored (its nonzero ones;
+  // 0xFF for a block two ranges share); k_idct_t loads only those parts and
   // takes the rest as zero.  0 = dense blocks (every part written and read).
   uint64_t ccnt;
   // ---- geometry

@@ -184,7 +184,7 @@ dg_status Context::init() {
     HIPCHK(hipEventCreateWithFlags(&sl.ev_png0, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_png1, hipEventDisableTiming));
   }
-  if (dg_status st = make_streams(0, kMaxInflight, slot_queue_, 0)) return st;
+  if (dg_status st = make_streams(0, kMaxInflight, slot_queue_, 0, side_queue_)) return st;
   return make_prog_streams();
 }
 
@@ -196,13 +196,16 @@ dg_status Context::init() {
 // lowest priority; 3: a CU mask over every CU (a masked stream gets a
 // hardware queue of its own).
 dg_status Context::make_prog_streams() {
-  return make_streams(kMaxInflight, kProgSlots, prog_queue_, prog_cus_);
+  return make_streams(kMaxInflight, kProgSlots, prog_queue_, prog_cus_, -1);
 }
 
 // (Re)create the main and side streams of slots [first, first + count):
 // mode 0 plain, 1 / 2 highest / lowest priority, 3 a CU mask over `cus` CUs
-// (0 = all).  Modes 1-3 get hardware queues of their own.
-dg_status Context::make_streams(int first, int count, int mode, int cus) {
+// (0 = all).  Modes 1-3 get hardware queues of their own.  HIP hands a new
+// stream the least-used queue of its pool, so the main streams are made
+// first: the slots in use then start on distinct queues, and a side stream
+// (side_mode, -1 = mode) shares a queue with at most one other slot's stream.
+dg_status Context::make_streams(int first, int count, int mode, int cus, int side_mode) {
   HIPCHK(hipSetDevice(device_));
   int least = 0, greatest = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -214,9 +217,15 @@ dg_status Context::make_streams(int first, int count, int mode, int cus) {
         HIPCHK(hipStreamDestroy(*q));
         *q = nullptr;
       }
-      if (mode == 1 || mode == 2) {
-        HIPCHK(hipStreamCreateWithPriority(q, hipStreamNonBlocking, mode == 1 ? greatest : least));
-      } else if (mode == 3) {  // cus of the CUs, spread evenly (every ncu/cus-th)
+    }
+  }
+  for (int pass = 0; pass < 2; pass++) {
+    const int m = pass == 1 && side_mode >= 0 ? side_mode : mode;
+    for (int j = first; j < first + count; j++) {
+      hipStream_t *q = pass == 0 ? &slots_[j].st : &slots_[j].side;
+      if (m == 1 || m == 2) {
+        HIPCHK(hipStreamCreateWithPriority(q, hipStreamNonBlocking, m == 1 ? greatest : least));
+      } else if (m == 3) {  // cus of the CUs, spread evenly (every ncu/cus-th)
         std::vector<uint32_t> mask((ncu_ + 31) / 32, 0u);
         const uint32_t want = cus > 0 && (uint32_t)cus < ncu_ ? (uint32_t)cus : ncu_;
         for (uint32_t k = 0; k < want; k++) {
@@ -459,7 +468,20 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
       }
     }
     slot_queue_ = (int)v;
-    return make_streams(0, kMaxInflight, slot_queue_, 0);
+    return make_streams(0, kMaxInflight, slot_queue_, 0, side_queue_);
+  }
+  if (k == "side_queue") {  // the baseline slots' side streams: -1 as slot_queue, else a slot_queue mode
+    if (v < -1 || v > 3) return DG_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int j = 0; j < kMaxInflight; j++) {
+      Slot &sl = slots_[j];
+      if (sl.batch && !sl.batch->done) {
+        dg_status st = finish(sl);
+        if (st) return st;
+      }
+    }
+    side_queue_ = (int)v;
+    return make_streams(0, kMaxInflight, slot_queue_, 0, side_queue_);
   }
   if (k == "prog_cus") {  // prog_queue 3: CUs the progressive streams may use (0 = all); set before prog_queue
     if (v < 0 || v > 4096) return DG_ERR_INVALID;
@@ -633,9 +655,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "inf_decode") {  // k_inf_decode lookup bits (literal/length, distance): 0 9/7, 1 8/6, 2 7/6, 3 7/5, 4 6/5,
-                            // 5 6/4; 6, 7 = 2, 1 with the stream prefetched two quads ahead; 8 / 9 / 10 / 11 =
-                            // 7/6, 6/5, 5/4, 8/6 with the canonical walk's symbol tables in LDS
-    if (v < 0 || v > 11) return DG_ERR_INVALID;
+                            // 5 6/4; 6, 7 = 2, 1 with the wave-batched register stream buffer; 8 / 9 / 11 =
+                            // 7/6, 6/5, 8/6 with the canonical walk's symbol tables in LDS; 12 / 13 = 8 / 9
+                            // with the register buffer; 14 = 0 with it, 15 = 11 with it
+    if (v < 0 || v > 15 || v == 10) return DG_ERR_INVALID;
     inf_decode_ = (uint32_t)v;
     return DG_OK;
   }
@@ -709,6 +732,7 @@ int64_t Context::get_stat(const std::string &k) {
   if (k == "band_dec_images") return stat_band_dec_;
   if (k == "direct_d2h") return stat_direct_d2h_;
   if (k == "png_chunks") return stat_png_chunks_;
+  if (k == "png_small_streams") return stat_png_small_;
   {  // host microseconds spent in dg_submit* since the last reset, per phase: wall and thread CPU
     static const char *pn[8] = {"plan", "pools", "layout", "lists", "upload", "h2d", "launch", "slotwait"};
     for (int q = 0; q < 8; q++) {
@@ -2885,6 +2909,8 @@ dg_status Context::finish_body(Slot &sl) {
     if (back[b.desc_of[i]].fmt == kFmtPng && back[b.desc_of[i]].png.nchunks) {
       stat_png_chunks_ += back[b.desc_of[i]].png.nchunks;
       stat_png_serial_ += back[b.desc_of[i]].png.serial ? 1 : 0;
+    } else if (back[b.desc_of[i]].fmt == kFmtPng) {
+      stat_png_small_++;
     }
     if (!status && b.unsettled && b.plans[i].fmt == kFmtJpeg && !b.plans[i].hdr.progressive)
       status = DG_ERR_UNSUPPORTED;

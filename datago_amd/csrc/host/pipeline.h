@@ -307,7 +307,7 @@ class Context {
   int pick_slot();
   int pick_prog_slot();
   dg_status make_prog_streams();
-  dg_status make_streams(int first, int count, int mode, int cus);
+  dg_status make_streams(int first, int count, int mode, int cus, int side_mode);
 
   int device_;
   bool has_cfg_ = false;
@@ -367,6 +367,7 @@ class Context {
   int prog_batch_ = 2048;
   int prog_flush_us_ = 20000;
   int slot_queue_ = 1;      // option "slot_queue" (make_streams for the baseline slots): high priority
+  int side_queue_ = 3;      // option "side_queue": the baseline slots' side streams (-1: as slot_queue; 3: own queues)
   int prog_cus_ = 0;        // option "prog_cus" (prog_queue 3: CU mask width, 0 = all)
   int prog_queue_ = 2;      // option "prog_queue" (make_prog_streams): low priority, a queue of its own
   int64_t stat_prog_aggs_ = 0, stat_prog_agg_images_ = 0;
@@ -453,7 +454,7 @@ class Context {
   int prog_chain_ = 100;                // option "prog_chain": chain dependency groups costing <= this % of the longest scan
   bool entropy_lpt_ = true;             // option "entropy_lpt": slow entropy workgroups first
   bool entropy_once_ = false;           // option "entropy_once": decode-once staging + k_huff_scatter
-  int64_t stat_png_serial_ = 0, stat_png_chunks_ = 0;
+  int64_t stat_png_serial_ = 0, stat_png_chunks_ = 0, stat_png_small_ = 0;
   int64_t stat_band_dec_ = 0;  // images whose first H pass ran in k_band_dec (stat "band_dec_images")
   // "wg_timing" summaries of the last batch (microseconds): per kernel {span, mean, p90, max}
   double wgstat_[2][4] = {{0}};

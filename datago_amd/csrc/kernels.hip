@@ -722,7 +722,6 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
     w.total_blocks = im.total_blocks;
     w.cur = -1;
     w.zs = 0;
-    w.hi = 0;
     w.cnt = (im.ccnt && !fused) ? gp<uint8_t>(im.ccnt) : nullptr;
     w.wave_blk = blk[t & ~63];
     w.stride = kBlkStride;
@@ -784,7 +783,6 @@ __global__ __launch_bounds__(256) void k_huff_scatter(const ImageDesc *__restric
   w.total_blocks = im.total_blocks;
   w.cur = -1;
   w.zs = 0;
-  w.hi = 0;
   w.cnt = nullptr;  // dense blocks (decode-once images never get ImageDesc::ccnt)
   if (s * im.sub_bits >= im.ds_bits) return;  // empty trailing range: decodes nothing
   const uint32_t bpm = im.bpm, cbits = im.comp_bits;
@@ -1036,13 +1034,13 @@ __device__ __forceinline__ bool idct_t_locate(const ImageDesc &im, uint32_t item
   return true;
 }
 
-// 16-byte parts of the lane's block to load: all 8 for dense blocks, the
-// count k_huff_write stored for sparse ones (ImageDesc::ccnt), 0 without a block
+// 16-byte parts of the lane's block to load, as a mask: all 8 for dense
+// blocks, the nonzero ones k_huff_write stored for sparse ones
+// (ImageDesc::ccnt), none without a block
 __device__ __forceinline__ uint32_t idct_t_parts(const ImageDesc &im, const IdctLoc &L) {
   if (!L.v) return 0u;
-  if (!im.ccnt) return 8u;
-  const uint32_t n = gp<const uint8_t>(im.ccnt)[L.bidx];
-  return n < 8u ? n : 8u;
+  if (!im.ccnt) return 0xFFu;
+  return gp<const uint8_t>(im.ccnt)[L.bidx];
 }
 
 __device__ __forceinline__ void idct_t_item(const ImageDesc &im, const IdctLoc &L, const u32x4 w[8],
@@ -1063,7 +1061,7 @@ __global__ __launch_bounds__(64) void k_idct_t(const ImageDesc *__restrict__ img
     u32x4 w[8];
     const DG_GLOBAL u32x4 *src = (const DG_GLOBAL u32x4 *)(gp<const int16_t>(im.coef) + (size_t)L.bidx * 64);
 #pragma unroll
-    for (uint32_t i = 0; i < 8; i++) w[i] = i < np ? src[i] : u32x4{0, 0, 0, 0};
+    for (uint32_t i = 0; i < 8; i++) w[i] = (np >> i) & 1u ? src[i] : u32x4{0, 0, 0, 0};
     IdctLoc N;
     const bool nok = k + 1 < kIdctItemStride && idct_t_locate(im, it.item0 + k + 1, N);
     const uint32_t nnp = nok ? idct_t_parts(im, N) : 0u;

@@ -264,6 +264,11 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *                 3 CU-masked.  1-3 take hardware queues apart from the process's shared ones, so one slot's
  *                 long kernels (PNG inflate) stop serialising another's: PNG pairs 9.4 -> 11.2 (1) / 12.6 (3)
  *                 Gpx/s, JPEG 95 (0, 1) / 90 (3) Gpx/s
+ *   "side_queue"  the baseline slots' side streams (serial PNG mask inflate, progressive DC items): -1 as
+ *                 slot_queue, else a slot_queue mode; default 3 (CU-masked over every CU: a queue of its own,
+ *                 so a slot's serial mask inflate never holds back another slot's main stream: PNG pairs
+ *                 14.5 -> 17.1 Gpx/s, JPEG unchanged).  Main streams are created first, so the slots in use
+ *                 start on distinct hardware queues
  *   "prog_chain"  progressive work items: dependency groups costing <= this % of the batch's longest scan
  *                 run back to back in one wave (default 100; 0 = one wave per scan)
  *   "prog_pipe"   1 = all scans of a batch in one pipelined launch (default); 0 = one launch per level
@@ -282,9 +287,10 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "inf_chunk"   chunk-parallel inflate: compressed bytes per chunk (power of two, 4096..65536; default 32768)
  *   "uf_units"    1 or 2 (default 2): PNG unfilter filter units per lane per diagonal step (1: half the LDS)
  *   "inf_decode"  0..5: chunk-parallel inflate lookup bits (literal/length, distance) per lane in LDS:
- *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (default, 24 KiB), 3 7/5, 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
- *                 the compressed stream prefetched two 16-byte quads ahead per lane; 8 / 9 / 10 / 11 = 7/6, 6/5,
- *                 5/4, 8/6 bits with the symbol tables of longer codes in LDS too (64 / 52 / 46 / 96 KiB per wave)
+ *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (24 KiB), 3 7/5, 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
+ *                 the next 8 stream words of every lane in registers, refilled wave-wide; 8 / 9 / 11 = 7/6, 6/5,
+ *                 8/6 bits with the symbol tables of longer codes in LDS too (64 / 52 / 96 KiB per wave); 12 / 13 =
+ *                 8 / 9 with the register buffer; 14 = 0 with it; 15 = 11 with it
  *   "copy_threads" host threads copying a host-out batch's outputs to the caller's buffers (default 8)
  *   "write_split" 1 = k_huff_write decodes each entropy range as two halves split at the sync pass's
  *                 half-way checkpoint (images without restart markers; default); 0 = one lane per range
@@ -308,6 +314,7 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  * Stats: "batches", "coalesced_batches", "coalesced_images", "resync_rounds", "fix_workgroups", "write_mismatch",
  * "unsettled_batches", "sync_iters_max", "sub_bits" (last batch), "hpool", "qpool" (tables pooled now),
  * "pool_flushes" (times the table pools were started over), "png_chunks", "png_serial_fallbacks",
+ * "png_small_streams" (PNG streams below two chunks, inflated serially by one wave),
  * "band_dec_images" (images whose first H pass ran in k_band_dec), "prog_items", "prog_chains" (work items / chains
  * of the pipelined progressive launches), "prog_aggregates", "prog_aggregate_images",
  * "meta_bytes" (the last batch's descriptor/list upload), "allocs", "alloc_mb", "alloc_us", "reclaims",

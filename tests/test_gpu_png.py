@@ -196,7 +196,7 @@ def test_png_large_full_size_properties(ctx512):
     assert st == 0 and (arr.shape[1], arr.shape[0]) == t.target_size(1800, 1200)
 
 
-@pytest.mark.parametrize("inf_decode,inf_chunk", [(d, 32768) for d in range(12)] + [(2, 4096), (2, 8192), (2, 16384),
+@pytest.mark.parametrize("inf_decode,inf_chunk", [(d, 32768) for d in range(16) if d != 10] + [(2, 4096), (2, 8192), (2, 16384),
                                                                                      (3, 65536), (9, 16384)])
 def test_chunked_inflate_matches_serial_and_oracle(inf_decode, inf_chunk):
     """Large streams take the chunk-parallel inflate (block-header search,
@@ -226,6 +226,8 @@ def test_chunked_inflate_matches_serial_and_oracle(inf_decode, inf_chunk):
         assert np.array_equal(xa, ref) and np.array_equal(xb, ref)
     assert a.stat("png_chunks") > 0
     print("chunks", a.stat("png_chunks"), "serial fallbacks", a.stat("png_serial_fallbacks"))
+    if inf_chunk >= 32768:  # the finder found every chunk's block start (a miss would only cost speed)
+        assert a.stat("png_serial_fallbacks") == 0
 
 
 A7_CASES = [(k, w, h) for k in synth.PNG_KINDS for (w, h) in [(1, 1), (2, 3), (5, 9), (8, 8), (33, 17), (257, 130)]]
