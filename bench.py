@@ -1169,7 +1169,7 @@ def main() -> int:
             "host_submit_phases_ms_per_step": host_phases,
             "meta_bytes_per_batch": ctx.stat("meta_bytes"),
             "allocations": {k_: ctx.stat(k_) for k_ in ("allocs", "alloc_mb", "alloc_us", "reclaims", "retire_syncs",
-                                                        "peak_device_mb", "max_device_mb", "budget_splits",
+                                                        "peak_device_mb", "max_device_mb", "budget_slots", "budget_splits",
                                                         "budget_frees", "budget_oom")},
             # per rank: wall ms per step in each dg_submit_device phase, the thread's CPU ms in the same
             # phases (wall >> cpu = blocking: allocation, driver locks, copies), and the slot wait

@@ -467,8 +467,8 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
       }
       stash_flush();
       // every source byte lies before `op` (an overlapping copy repeats the
-      // first `dist` bytes), so no read sees a byte this match writes: each
-      // 64-byte round reads then writes.  Branches are wave-uniform.
+      // first `dist` bytes), so no read sees a byte this match writes.
+      // Branches are wave-uniform.
       const uint32_t q = op, src0 = op - dist, rounds = (len + 63u) >> 6;
       if (dist == 1u) {  // run of one byte (masks, flat rows): one broadcast read
         const uint32_t b = sm.ring[src0 & kRingMask];
@@ -476,21 +476,25 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
           const uint32_t j = lane + 64u * r;
           if (j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)b;
         }
-      } else if (dist >= len) {  // no overlap: straight copy
-        for (uint32_t r = 0; r < rounds; r++) {
-          const uint32_t j = lane + 64u * r;
-          const uint32_t v = j < len ? sm.ring[(src0 + j) & kRingMask] : 0u;
-          if (j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)v;
-        }
-      } else {  // overlapping period-`dist` copy
+      } else {  // every read before the writes: one LDS round trip (len <= 258)
         const float rcp = 1.0f / (float)dist;
-        for (uint32_t r = 0; r < rounds; r++) {
+        const bool wrap = dist < len;
+        uint32_t v[5];
+#pragma unroll
+        for (uint32_t r = 0; r < 5; r++) {
           const uint32_t j = lane + 64u * r;
-          const uint32_t qt = (uint32_t)((float)j * rcp);  // j / dist or one less (j < 320)
-          uint32_t k = j - qt * dist;
-          if (k >= dist) k -= dist;
-          const uint32_t v = j < len ? sm.ring[(src0 + k) & kRingMask] : 0u;
-          if (j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)v;
+          uint32_t k = j;
+          if (wrap) {  // overlapping period-`dist` copy
+            const uint32_t qt = (uint32_t)((float)j * rcp);  // j / dist or one less (j < 320)
+            k = j - qt * dist;
+            if (k >= dist) k -= dist;
+          }
+          v[r] = r < rounds && j < len ? sm.ring[(src0 + k) & kRingMask] : 0u;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < 5; r++) {
+          const uint32_t j = lane + 64u * r;
+          if (r < rounds && j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)v[r];
         }
       }
       op += len;

@@ -184,8 +184,7 @@ dg_status Context::init() {
     HIPCHK(hipEventCreateWithFlags(&sl.ev_png0, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&sl.ev_png1, hipEventDisableTiming));
   }
-  if (dg_status st = make_streams(0, kMaxInflight, slot_queue_, 0, side_queue_)) return st;
-  return make_prog_streams();
+  return make_streams(0, kMaxInflight, slot_queue_, 0, side_queue_);  // the progressive slots' on first use
 }
 
 // Streams of the progressive slots (option "prog_queue").  A progressive
@@ -199,13 +198,27 @@ dg_status Context::make_prog_streams() {
   return make_streams(kMaxInflight, kProgSlots, prog_queue_, prog_cus_, -1);
 }
 
+// A slot's streams on first use: the baseline slots past "slots" and the
+// progressive slots have none until a batch goes to them -- every stream
+// with a queue of its own is a hardware queue, and eight processes sharing
+// one device run out of them (each rank would hold 16).
+dg_status Context::slot_streams(Slot &sl) {
+  if (sl.st) return DG_OK;
+  const int j = (int)(&sl - slots_);
+  return j < kMaxInflight ? make_streams(j, 1, slot_queue_, 0, side_queue_)
+                          : make_streams(j, 1, prog_queue_, prog_cus_, -1, kAllSlots);
+}
+
 // (Re)create the main and side streams of slots [first, first + count):
 // mode 0 plain, 1 / 2 highest / lowest priority, 3 a CU mask over `cus` CUs
 // (0 = all).  Modes 1-3 get hardware queues of their own.  HIP hands a new
 // stream the least-used queue of its pool, so the main streams are made
 // first: the slots in use then start on distinct queues, and a side stream
 // (side_mode, -1 = mode) shares a queue with at most one other slot's stream.
-dg_status Context::make_streams(int first, int count, int mode, int cus, int side_mode) {
+// Only slots below `limit` (-1: "slots") get streams now; the others on
+// first use (slot_streams).
+dg_status Context::make_streams(int first, int count, int mode, int cus, int side_mode, int limit) {
+  if (limit < 0) limit = nslots_;
   HIPCHK(hipSetDevice(device_));
   int least = 0, greatest = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -221,7 +234,7 @@ dg_status Context::make_streams(int first, int count, int mode, int cus, int sid
   }
   for (int pass = 0; pass < 2; pass++) {
     const int m = pass == 1 && side_mode >= 0 ? side_mode : mode;
-    for (int j = first; j < first + count; j++) {
+    for (int j = first; j < first + count && (j < limit || count == 1); j++) {
       hipStream_t *q = pass == 0 ? &slots_[j].st : &slots_[j].side;
       if (m == 1 || m == 2) {
         HIPCHK(hipStreamCreateWithPriority(q, hipStreamNonBlocking, m == 1 ? greatest : least));
@@ -418,6 +431,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
   if (k == "max_device_mb") {  // device memory budget of the context (0: none)
     if (v < 0) return DG_ERR_INVALID;
     max_dev_bytes_ = (size_t)v << 20;
+    budget_slots_ = kMaxInflight;
     return DG_OK;
   }
   if (k == "slots") {
@@ -721,6 +735,7 @@ int64_t Context::get_stat(const std::string &k) {
   }
   if (k == "max_device_mb") return (int64_t)(max_dev_bytes_ >> 20);
   if (k == "budget_splits") return stat_budget_splits_;
+  if (k == "budget_slots") return max_dev_bytes_ ? std::min<int64_t>(nslots_, stat_budget_slots_min_) : nslots_;
   if (k == "coef_cache_hits") return stat_ccache_hits_;
   if (k == "coef_cache_new") return stat_ccache_new_;
   if (k == "coef_cache_resets") return stat_ccache_resets_;
@@ -980,26 +995,45 @@ void Context::free_slot_buffers(Slot &o) {
 // mu_ held.  The device budget (option "max_device_mb"): make room for a
 // batch of `self` whose scratch / coefficient / input arenas need rs / rc /
 // ri bytes.  In order: keep self's buffers if they already fit; free the
-// retired buffers; then, slot by slot, finish the other slots' batches
-// (waiting for their GPU work, as a dg_wait would) and free their buffers;
-// finally drop self's own oversized buffers (idle: the slot's previous batch
-// is finished) for exact-size ones.  False: the batch alone does not fit --
-// the caller splits it (submit_split).  budget_room_: what growth may add on
-// top.  (The descriptor buffer, a few MB, grows after this check.)
+// retired buffers; give back the buffers of baseline slots the budget took
+// out of turn; then take the highest other baseline slot out of turn
+// (budget_slots_: pick_slot cycles over fewer slots from now on), finishing
+// its batch (waiting for its GPU work, as a dg_wait would) and freeing its
+// buffers, and likewise the progressive slots; finally drop self's own
+// oversized buffers (idle: the slot's previous batch is finished) for
+// exact-size ones.  So a budget below what "slots" batches need settles on
+// fewer batches in flight instead of trading buffers between slots batch
+// after batch (each trade a hipFree + hipMalloc).  False: the batch alone
+// does not fit -- the caller splits it (submit_split).  budget_room_: what
+// growth may add on top.  (The descriptor buffer, a few MB, grows after this
+// check.)
 bool Context::budget_fit(Slot &self, size_t rs, size_t rc, size_t ri) {
   budget_room_ = 0;
   if (!max_dev_bytes_) return true;
   const size_t fixed = self.meta.cap + self.wgt.cap;
   const size_t keep = std::max(self.scratch.cap, rs) + std::max(self.coef.cap, rc) + std::max(self.input.cap, ri) + fixed;
   const size_t tight = rs + rc + ri + fixed;
+  const int si = (int)(&self - slots_);
   auto others = [&] { return dev_footprint(&self); };
-  if (others() + keep > max_dev_bytes_ && !retired_dev_.empty() && sync_all() == DG_OK) free_retired();
-  for (int k = 0; k < kAllSlots && others() + keep > max_dev_bytes_; k++) {
-    Slot &o = slots_[(&self - slots_ + 1 + k) % kAllSlots];  // the slots after self first: the oldest batches
-    if (&o == &self) continue;
-    if (o.batch && !o.batch->done && finish(o)) continue;
+  auto give_back = [&](Slot &o) {
+    if (o.batch && !o.batch->done && finish(o)) return;
     free_slot_buffers(o);
+  };
+  auto has_buffers = [](const Slot &o) { return o.scratch.p || o.coef.p || o.input.p; };
+  if (others() + keep > max_dev_bytes_ && !retired_dev_.empty() && sync_all() == DG_OK) free_retired();
+  for (int j = std::max(1, budget_slots_); j < kMaxInflight && others() + keep > max_dev_bytes_; j++)
+    if (j != si && has_buffers(slots_[j])) give_back(slots_[j]);
+  while (others() + keep > max_dev_bytes_) {
+    int j = kMaxInflight - 1;
+    while (j >= 0 && (j == si || !has_buffers(slots_[j]))) j--;
+    if (j < 0) break;
+    give_back(slots_[j]);
+    if (has_buffers(slots_[j])) break;  // its batch failed to finish: nothing more to take
+    budget_slots_ = std::max(1, std::min(budget_slots_, std::max(j, si + 1)));
+    stat_budget_slots_min_ = std::min<int64_t>(stat_budget_slots_min_, budget_slots_);
   }
+  for (int j = kMaxInflight; j < kAllSlots && others() + keep > max_dev_bytes_; j++)
+    if (j != si) give_back(slots_[j]);
   if (others() + keep <= max_dev_bytes_) {
     budget_room_ = max_dev_bytes_ - others() - keep;
     return true;
@@ -1278,6 +1312,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   }
   HIPCHK(hipSetDevice(device_));
   Slot &sl = slots_[force_slot >= 0 ? force_slot : pick_slot()];
+  if (dg_status st = slot_streams(sl)) return st;
   // This slot's previous batch must complete first.  Its GPU work is waited
   // for without the context lock: a progressive slot's batch can run ~1 s,
   // and every other dg_submit / dg_wait / dg_poll of the context would stall
@@ -2396,8 +2431,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
 // finishes first.  Progressive batches have slots of their own
 // (pick_prog_slot), so every baseline slot cycles at the baseline pace.
 int Context::pick_slot() {
-  const int i = next_slot_ % nslots_;
-  next_slot_ = (i + 1) % nslots_;
+  const int ns = max_dev_bytes_ ? std::max(1, std::min(nslots_, budget_slots_)) : nslots_;
+  const int i = next_slot_ % ns;
+  next_slot_ = (i + 1) % ns;
   return i;
 }
 

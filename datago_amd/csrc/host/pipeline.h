@@ -299,6 +299,8 @@ class Context {
   void ccache_rollback(size_t n0, size_t off0);                   // a submit that installs no batch
   size_t max_dev_bytes_ = 0;        // option "max_device_mb" (0: no budget)
   size_t budget_room_ = 0;          // headroom the current submit's growth may take under the budget
+  int budget_slots_ = kMaxInflight;  // baseline slots in turn under the budget (budget_fit lowers it)
+  int64_t stat_budget_slots_min_ = kMaxInflight;
   int64_t stat_peak_dev_ = 0, stat_budget_splits_ = 0, stat_budget_frees_ = 0, stat_budget_oom_ = 0;
   dg_status finish(Slot &sl);       // finish_body, or fail_batch on its error
   dg_status finish_body(Slot &sl);
@@ -307,7 +309,8 @@ class Context {
   int pick_slot();
   int pick_prog_slot();
   dg_status make_prog_streams();
-  dg_status make_streams(int first, int count, int mode, int cus, int side_mode);
+  dg_status make_streams(int first, int count, int mode, int cus, int side_mode, int limit = -1);
+  dg_status slot_streams(Slot &sl);
 
   int device_;
   bool has_cfg_ = false;

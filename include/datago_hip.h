@@ -306,9 +306,11 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "sub_auto"    subsequence size of batches over 64 MiB of coded data when "sub_bits" is 0 (default 8192)
  *   "sparse_coef" 1 = k_huff_write stores, and k_idct_t loads, only the 16-byte zigzag parts of each
  *                 coefficient block up to its last nonzero coefficient (default 1); 0 = whole 128-byte blocks
- *   "max_device_mb" device memory budget of the context in MiB (default 0 = none).  A submission whose
- *                 plan does not fit -- after the retired buffers and the other slots' buffers are freed,
- *                 waiting for their batches -- is split into sub-batches under the caller's one ticket; an
+ *   "max_device_mb" device memory budget of the context in MiB (default 0 = none).  A batch that does
+ *                 not fit beside the other slots' buffers takes the highest other slot out of turn (its
+ *                 batch finished, its buffers freed): the context settles on fewer batches in flight (stat
+ *                 "budget_slots").  A submission whose plan does not fit -- after the retired buffers and
+ *                 the other slots' buffers are freed -- is split into sub-batches under the caller's one ticket; an
  *                 image that alone exceeds it comes back DG_ERR_OOM.  Without a budget a failed device
  *                 allocation takes the same path (drain the other slots, then split)
  * Stats: "batches", "coalesced_batches", "coalesced_images", "resync_rounds", "fix_workgroups", "write_mismatch",
@@ -320,7 +322,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  * "meta_bytes" (the last batch's descriptor/list upload), "allocs", "alloc_mb", "alloc_us", "reclaims",
  * "retire_syncs" (device / page-locked buffer growth: count, MiB, wall microseconds; OOM reclaims; device-wide
  * syncs that freed grown-out buffers), "device_mb" / "peak_device_mb" (device memory the context holds now /
- * at most), "budget_splits", "budget_frees", "budget_oom" (sub-batch splits, slot buffers freed, images
+ * at most), "budget_slots" (baseline slots in turn under the budget), "budget_splits", "budget_frees",
+ * "budget_oom" (sub-batch splits, slot buffers freed, images
  * failed with DG_ERR_OOM under the budget or after a failed allocation), "host_us_<phase>" / "host_cpu_us_<phase>" (wall / thread
  * CPU microseconds in dg_submit* per phase: plan, pools, layout, lists, upload (staging copy), h2d, launch;
  * "host_us_slotwait": waiting for a free slot); -1 if unknown.

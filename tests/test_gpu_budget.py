@@ -100,3 +100,37 @@ def test_budget_with_progressive_members():
         assert s0 == 0 and metas[i].status == 0
         assert np.array_equal(outs[i][: a0.size], a0.reshape(-1))
     c.close()
+
+
+def test_budget_settles_on_fewer_slots():
+    """A budget that holds ~2.5 slots' buffers: the context takes slots out of
+    turn (stat budget_slots) instead of trading buffers between slots batch
+    after batch; 12 batches in flight stay bit-exact."""
+    datas = synth.mixed_corpus(79, 12, 256, 900)
+    ref = _ctx()
+    want = ref.decode_batch(datas)
+    ref.close()
+    base = _base_mb()
+    one = _ctx()
+    one.set_option("max_device_mb", 1 << 20)  # exact sizes, as under a budget
+    one.decode_batch(datas)
+    per_slot = one.stat("device_mb") - base
+    one.close()
+    assert per_slot > 0
+    budget = base + (5 * per_slot) // 2
+    c = _ctx()
+    c.set_option("max_device_mb", budget)
+    runs = []
+    for _ in range(12):
+        outs = [np.zeros(max(c.output_size(d)[1], 1), np.uint8) for d in datas]
+        runs.append((c.submit_host(datas, outs), outs))
+    for (tk, metas, keep), outs in runs:
+        c.wait(tk)
+        for i, (s0, a0, _) in enumerate(want):
+            assert s0 == 0 and metas[i].status == 0
+            assert np.array_equal(outs[i][: a0.size], a0.reshape(-1))
+    assert c.stat("budget_slots") <= 3, c.stat("budget_slots")
+    assert c.stat("budget_frees") <= 8, c.stat("budget_frees")  # a few slots given back once, not per batch
+    assert c.stat("budget_oom") == 0
+    assert c.stat("peak_device_mb") <= budget + 16, (c.stat("peak_device_mb"), budget)
+    c.close()
