@@ -13,6 +13,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--batches", type=int, default=200)
+    ap.add_argument("--timeline", type=float, default=0.0, help="print every kernel within this many us of a mid batch")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = [(r[0].split("(")[0].replace("void ", "").replace("dg::", ""), r[1], r[2], r[3], r[4])
@@ -20,12 +21,15 @@ def main():
     # batches: a stream's kernels from one k_destuff_count to the next
     per_stream = collections.defaultdict(list)
     for n, s, e, g, st in rows:
-        per_stream[st].append((n, s, e, g))
+        per_stream[st].append((n, s, e, g, st))
     batches = []
     for st, ks in per_stream.items():
         cur = None
         for k in ks:
-            if k[0].startswith("k_destuff_count"):
+            # a batch starts at its descriptor pull (or, without one, its first destuff)
+            starts = k[0].startswith("k_meta_pull") or (k[0].startswith("k_destuff_count") and not (
+                cur and cur[-1][0].startswith("k_meta_pull")))
+            if starts:
                 if cur:
                     batches.append(cur)
                 cur = [k]
@@ -34,7 +38,7 @@ def main():
         if cur:
             batches.append(cur)
     batches.sort(key=lambda b: b[0][1])
-    batches = [b for b in batches if b[0][3] < 2_000_000][-a.batches:]  # small (coalesced) batches
+    batches = [b for b in batches if max(k[3] for k in b) < 2_000_000][-a.batches:]  # small (coalesced) batches
     spans = sorted((b[-1][2] - b[0][1]) / 1e3 for b in batches)
     if not spans:
         print("no batches")
@@ -43,7 +47,7 @@ def main():
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
     for b in batches:
         t0 = b[0][1]
-        for n, s, e, g in b:
+        for n, s, e, g, _ in b:
             x = agg[n.split("<")[0]]
             x[0] += 1
             x[1] += (e - s) / 1e3
@@ -51,6 +55,12 @@ def main():
     print("kernel,launches_per_batch,avg_us,avg_start_offset_us")
     for n, (k, d, o) in sorted(agg.items(), key=lambda kv: kv[1][2] / kv[1][0]):
         print(f"{n},{k / len(batches):.2f},{d / k:.1f},{o / k:.0f}")
+    if a.timeline:
+        t_sel = batches[len(batches) // 2][0][1]
+        print(f"timeline around t={t_sel} (all streams, {a.timeline} us):")
+        for n, s, e, g, st in rows:
+            if t_sel <= s <= t_sel + a.timeline * 1e3:
+                print(f"  {(s - t_sel) / 1e3:8.1f} {(e - t_sel) / 1e3:8.1f} s{st} {n[:40]} grid={g}")
 
 
 if __name__ == "__main__":
