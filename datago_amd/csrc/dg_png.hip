@@ -35,6 +35,14 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 
 // ------------------------------------------------------------ gather
 
+// An IDAT chunk's bytes into the image's contiguous zlib stream.  Both ends
+// sit at arbitrary byte offsets (chunk headers in the file, cumulative IDAT
+// lengths in the stream), so a thread stores 16-byte-aligned destination
+// chunks built from five aligned source dwords (v_alignbyte); only the
+// misaligned head and the tail go byte by byte.  (Byte loads and stores for
+// every byte kept ~190 K waves resident per configs[4] batch.)  The source
+// dword reads end at most 4 bytes past the chunk: inside the PNG file, whose
+// IEND chunk follows the last IDAT.
 __global__ __launch_bounds__(256) void k_png_gather(const GatherJob *__restrict__ jobs, const WgItem *__restrict__ list) {
   const WgItem it = list[blockIdx.x];
   const GatherJob j = jobs[it.image];
@@ -42,7 +50,26 @@ __global__ __launch_bounds__(256) void k_png_gather(const GatherJob *__restrict_
   const uint32_t e = j.len - b0 < kGatherPiece ? j.len : b0 + kGatherPiece;
   const DG_GLOBAL uint8_t *s = gp<const uint8_t>(j.src);
   DG_GLOBAL uint8_t *d = gp<uint8_t>(j.dst);
-  for (uint32_t i = b0 + threadIdx.x; i < e; i += 256) d[i] = s[i];
+  const uint32_t t = threadIdx.x;
+  const uint32_t lead = (16u - (uint32_t)((j.dst + b0) & 15u)) & 15u;
+  const uint32_t a0 = b0 + lead < e ? b0 + lead : e;  // first 16-byte-aligned destination offset
+  const uint32_t nb = (e - a0) >> 4;                 // whole 16-byte chunks
+  if (t < a0 - b0) d[b0 + t] = s[b0 + t];
+  const uint32_t a1 = a0 + nb * 16u;
+  if (t < e - a1) d[a1 + t] = s[a1 + t];
+  for (uint32_t k = t; k < nb; k += 256) {
+    const uint32_t o = a0 + 16u * k;
+    const uint64_t sa = j.src + o;
+    const uint32_t r = (uint32_t)sa & 3u;
+    const DG_GLOBAL uint32_t *w = gp<const uint32_t>(sa - r);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbyte(w1, w0, r);
+    v.y = __builtin_amdgcn_alignbyte(w2, w1, r);
+    v.z = __builtin_amdgcn_alignbyte(w3, w2, r);
+    v.w = __builtin_amdgcn_alignbyte(w4, w3, r);
+    *(DG_GLOBAL u32x4 *)(d + o) = v;
+  }
 }
 
 // ------------------------------------------------------------ inflate
@@ -681,113 +708,110 @@ __device__ __forceinline__ bool inf_candidate(const DG_GLOBAL uint32_t *z, uint3
 
 // One wave per chunk (but chunk 0): the first candidate block start in the
 // chunk's bit range, through three filters of rising cost, each applied to
-// the survivors of the last, 64 positions per lane-parallel round:
-//  1. header fields (BTYPE = 2, HLIT <= 29, HDIST <= 29), ~10 instructions per
-//     position over 64 consecutive positions per step; ~22% of random
-//     positions pass (round 5: this stage alone replaced inf_header_fast on
-//     every position -- the finder issued ~380 K VALU per wave and kept the
-//     GPU busy while the other batches' kernels waited);
-//  2. inf_header_fast (the code-length code's Kraft sum) on 64 queued
-//     survivors at a time, their stream words read from a 32-word LDS ring of
-//     the recent steps; ~2% of those pass;
-//  3. inf_header_full, 64 at a time as before.
+// the survivors of the last:
+//  1. header fields (BFINAL = 0 -- or 1 in a second pass over a chunk the
+//     first found nothing in --, BTYPE = 2, HLIT <= 29, HDIST <= 29),
+//     bit-parallel: a lane tests 32 consecutive positions with a dozen 64-bit
+//     shift / and operations on its two stream words, so a step covers 2048
+//     positions; ~11% of random positions pass.  (Round 5: one position per
+//     lane per step, ~20 instructions for 64 positions, made the finder ~60%
+//     of a configs[4] batch's VALU work -- more than the decode it feeds.)
+//  2. inf_header_fast (the code-length code's Kraft sum) on the step's
+//     survivors, 64 at a time, their stream words read from the step's words
+//     in LDS; ~0.4% of those pass;
+//  3. inf_header_full on the Kraft survivors, once kInfStage3 of them have
+//     queued (a round costs its longest lane's decode: batching more
+//     positions per round scans further past the first real header).
 // Every stage keeps position order, so the first position passing stage 3 is
 // the first candidate of the chunk.
+constexpr uint32_t kInfStage3 = 32;
+
 __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
                                                  const WgItem *__restrict__ list) {
-  __shared__ uint32_t qpos[128];   // stage-3 queue (Kraft survivors)
-  __shared__ uint32_t q1pos[128];  // stage-2 queue (header-field survivors)
-  __shared__ uint32_t ring[32];    // stream words W - 27 .. W + 4 of the current step
+  __shared__ uint32_t q1pos[2048];  // stage-2 queue: the step's header-field survivors, in order
+  __shared__ uint32_t qpos[128];    // stage-3 queue (Kraft survivors)
+  __shared__ uint32_t win[72];      // the step's stream words W .. W + 67
   const WgItem it = list[blockIdx.x];
   InfChunk &c = ch[it.image];
   const ImageDesc &im = imgs[c.image];
   const DG_GLOBAL uint32_t *z = gp<const uint32_t>(im.png.zs);
   const uint32_t zlen = im.png.zlen, zwords = (zlen + 3) / 4;
-  const uint32_t b0 = c.idx * c.span * 8u;
+  const uint32_t b0 = c.idx * c.span * 8u;  // a multiple of 2048 (span: a power of two >= 4096)
   const uint32_t b1 = min((c.idx + 1) * c.span * 8u, zlen * 8u);
-  const uint32_t lane = threadIdx.x, hl = lane >> 5, sh = lane & 31u;
+  const uint32_t lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1ull;
-  uint32_t found = kInfNone, qn = 0, q1n = 0, age = 0;
-  // words W..W+4 of the current step (W = p / 32) and W+5, W+6 (the next
-  // step's new ones), loaded a step ahead
-  auto word = [&](uint32_t w) { return uni(w < zwords ? z[w] : 0u); };
-  uint32_t u[5], n5 = 0, n6 = 0;
-  {
-    const uint32_t W = b0 >> 5;
-#pragma unroll
-    for (uint32_t k = 0; k < 5; k++) u[k] = word(W + k);
-    n5 = word(W + 5);
-    n6 = word(W + 6);
-  }
-  for (uint32_t p = b0;; p += 64) {  // b0 and p are multiples of 64
-    const bool more = p < b1;
-    if (more) {
-      const uint32_t W = p >> 5;
-      if (lane < 5) ring[(W + lane) & 31u] = lane == 0 ? u[0] : lane == 1 ? u[1] : lane == 2 ? u[2] : lane == 3 ? u[3] : u[4];
-      // stage 1: BFINAL any, BTYPE = 2 (bits 1-2), HLIT and HDIST <= 29 (bits 3-12)
-      const uint64_t a = (uint64_t)(hl ? u[1] : u[0]) | ((uint64_t)(hl ? u[2] : u[1]) << 32);
-      const uint32_t h = (uint32_t)(a >> sh) & 0x1FFFu;
-      const bool pass = p + lane < b1 && ((h >> 1) & 3u) == 2u && ((h >> 3) & 31u) <= 29u && ((h >> 8) & 31u) <= 29u;
-      const uint64_t m = __ballot(pass);
-      if (pass) q1pos[q1n + (uint32_t)__popcll(m & below)] = p + lane;
-      q1n += (uint32_t)__popcll(m);
-      age++;
-      u[0] = u[2];
-      u[1] = u[3];
-      u[2] = u[4];
-      u[3] = n5;
-      u[4] = n6;
-      n5 = word(W + 7);
-      n6 = word(W + 8);
-    }
-    // stage 2: the Kraft test on queued survivors (all of them at the end, or
-    // once they are 8 steps old: the ring holds 13 steps back); stage 3: full
-    // checks, oldest 64 Kraft survivors first (all remaining ones at the end).
-    // A stage-2 round runs only while the stage-3 queue has room for it.
-    for (;;) {
-      bool did = false;
-      if (qn < 64 && (q1n >= 64 || (q1n > 0 && (!more || age >= 8)))) {
-        __syncthreads();
-        const uint32_t nb = q1n < 64 ? q1n : 64u;
-        const uint32_t pos = q1pos[lane < nb ? lane : 0];
-        uint32_t q[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) q[k] = ring[((pos >> 5) + k) & 31u];
-        uint64_t lo, hi;
-        inf_bits96(q, pos & 31u, lo, hi);
-        const bool pass = lane < nb && inf_header_fast(lo, hi) != 0;
-        const uint64_t m = __ballot(pass);
-        if (pass) qpos[qn + (uint32_t)__popcll(m & below)] = pos;
-        qn += (uint32_t)__popcll(m);
-        const uint32_t rest = q1n - nb;  // < 64
-        const uint32_t keep = lane < rest ? q1pos[64 + lane] : 0u;
-        __syncthreads();
-        if (lane < rest) q1pos[lane] = keep;
-        q1n = rest;
-        age = 0;
-        did = true;
-      }
-      if (qn >= 64 || (!more && qn > 0)) {
-        __syncthreads();
-        const uint32_t nb = qn < 64 ? qn : 64u;
-        const uint32_t pos = qpos[lane < nb ? lane : 0];
-        const bool ok = lane < nb && inf_candidate(z, zwords, pos);
-        const uint64_t mo = __ballot(ok);
-        if (mo) {
-          found = uni(qpos[__ffsll((long long)mo) - 1]);
-          break;
-        }
-        const uint32_t rest = qn - nb;  // < 64
-        const uint32_t keep = lane < rest ? qpos[64 + lane] : 0u;
-        __syncthreads();
-        if (lane < rest) qpos[lane] = keep;
-        qn = rest;
-        did = true;
-      }
-      if (!did) break;
-    }
-    if (found != kInfNone || !more) break;
+  auto word = [&](uint32_t w) { return w < zwords ? z[w] : 0u; };
+  uint32_t found = kInfNone;
+  // stage 3 on the oldest min(qn, 64) queued positions; true when one passes
+  auto stage3 = [&](uint32_t &qn) {
     __syncthreads();
+    const uint32_t nb = qn < 64 ? qn : 64u;
+    const uint32_t pos = qpos[lane < nb ? lane : 0];
+    const bool ok = lane < nb && inf_candidate(z, zwords, pos);
+    const uint64_t mo = __ballot(ok);
+    if (mo) {
+      found = uni(qpos[__ffsll((long long)mo) - 1]);
+      return true;
+    }
+    const uint32_t rest = qn - nb;  // < 64
+    const uint32_t keep = lane < rest ? qpos[64 + lane] : 0u;
+    __syncthreads();
+    if (lane < rest) qpos[lane] = keep;
+    qn = rest;
+    return false;
+  };
+  for (uint32_t bfinal = 0; bfinal < 2 && found == kInfNone; bfinal++) {
+    uint32_t qn = 0;
+    uint32_t nw = word((b0 >> 5) + lane), ne = lane < 4 ? word((b0 >> 5) + 64 + lane) : 0u;  // a step ahead
+    for (uint32_t p = b0; p < b1 && found == kInfNone; p += 2048) {
+      const uint32_t W = p >> 5;
+      __syncthreads();
+      win[lane] = nw;
+      if (lane < 4) win[64 + lane] = ne;
+      nw = word(W + 64 + lane);
+      ne = lane < 4 ? word(W + 128 + lane) : 0u;
+      __syncthreads();
+      // stage 1: lane `lane` tests positions q .. q + 31, q = p + 32 lane
+      const uint64_t A = (uint64_t)win[lane] | ((uint64_t)win[lane + 1] << 32);
+      const uint32_t b1s = (uint32_t)(A >> 1), b2s = (uint32_t)(A >> 2);
+      const uint32_t lit = (uint32_t)(A >> 4) & (uint32_t)(A >> 5) & (uint32_t)(A >> 6) & (uint32_t)(A >> 7);
+      const uint32_t dst = (uint32_t)(A >> 9) & (uint32_t)(A >> 10) & (uint32_t)(A >> 11) & (uint32_t)(A >> 12);
+      uint32_t m = (bfinal ? (uint32_t)A : ~(uint32_t)A) & ~b1s & b2s & ~lit & ~dst;
+      const uint32_t q = p + 32u * lane;
+      m = q >= b1 ? 0u : (b1 - q >= 32u ? m : m & ((1u << (b1 - q)) - 1u));
+      // survivors into q1pos in position order: exclusive scan of the lanes' counts
+      const uint32_t cnt = (uint32_t)__popc(m);
+      uint32_t incl = cnt;
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+      }
+      const uint32_t tot = uni(__shfl(incl, 63));
+      uint32_t k = incl - cnt;
+      while (m) {
+        q1pos[k++] = q + (uint32_t)__ffs(m) - 1u;
+        m &= m - 1u;
+      }
+      __syncthreads();
+      // stage 2, 64 survivors at a time; stage 3 once kInfStage3 queue up
+      for (uint32_t r0 = 0; r0 < tot; r0 += 64) {
+        const uint32_t nb = tot - r0 < 64 ? tot - r0 : 64u;
+        const uint32_t pos = q1pos[r0 + (lane < nb ? lane : 0u)];
+        uint32_t qw[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) qw[j] = win[(pos >> 5) - W + j];
+        uint64_t lo, hi;
+        inf_bits96(qw, pos & 31u, lo, hi);
+        const bool pass = lane < nb && inf_header_fast(lo, hi) != 0;
+        const uint64_t mp = __ballot(pass);
+        if (pass) qpos[qn + (uint32_t)__popcll(mp & below)] = pos;
+        qn += (uint32_t)__popcll(mp);
+        if (qn >= kInfStage3 && stage3(qn)) break;
+      }
+    }
+    while (found == kInfNone && qn > 0)  // the chunk's last Kraft survivors
+      if (stage3(qn)) break;
   }
   if (lane == 0) c.start = found;
 }
