@@ -227,7 +227,8 @@ class Context {
   int pool_huff(const HuffSpec &s);
   dg_status flush_pools();
   int pool_quant(const uint16_t *q);
-  dg_status ensure(DevBuf &b, size_t bytes, hipStream_t user = nullptr);
+  dg_status ensure(DevBuf &b, size_t bytes, hipStream_t user = nullptr, bool exact = false);
+  void prewarm_slots(const Slot &self);
   void retire(void *p, size_t bytes, bool pinned);
   void free_retired();
   static size_t grow_cap(size_t bytes, bool headroom);
@@ -239,7 +240,7 @@ class Context {
   void free_retired_if_idle();
   std::vector<void *> retired_dev_, retired_pinned_;  // grown-out buffers, freed later (ensure)
   size_t retired_dev_bytes_ = 0, retired_pin_bytes_ = 0;
-  dg_status ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user = nullptr);
+  dg_status ensure_pinned(PinBuf &b, size_t bytes, hipStream_t user = nullptr, bool exact = false);
   dg_status upload_pools();
   dg_status launch_all(Slot &sl, bool from_fix);
   void plan_prog_items(Batch &b);

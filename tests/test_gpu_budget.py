@@ -37,9 +37,17 @@ def _base_mb():
     return mb
 
 
+def _ref_ctx():
+    """Unbudgeted outputs, footprint as one slot's exact-size buffers (a huge
+    budget: no growth headroom, no prewarmed idle slots)."""
+    c = _ctx()
+    c.set_option("max_device_mb", 1 << 20)
+    return c
+
+
 def test_budget_splits_stay_bit_exact():
     datas = synth.mixed_corpus(77, 40, 256, 1200)
-    ref = _ctx()
+    ref = _ref_ctx()
     want = ref.decode_batch(datas)
     peak = ref.stat("peak_device_mb")
     ref.close()
@@ -86,7 +94,7 @@ def test_budget_with_progressive_members():
     datas = synth.mixed_corpus(78, 16, 256, 900)
     datas[3] = synth.make_jpeg(31, 700, 500, 90, "4:2:0", progressive=True)
     datas[9] = synth.make_jpeg(32, 500, 700, 90, "4:4:4", progressive=True)
-    ref = _ctx()
+    ref = _ref_ctx()
     want = ref.decode_batch(datas)
     peak = ref.stat("peak_device_mb")
     ref.close()
