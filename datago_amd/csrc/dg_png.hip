@@ -74,8 +74,12 @@ __global__ __launch_bounds__(256) void k_png_gather(const GatherJob *__restrict_
 
 // ------------------------------------------------------------ inflate
 
-constexpr uint32_t kRing = 65536, kRingMask = kRing - 1;
-constexpr uint32_t kFlush = 32768;     // ring -> HBM burst
+// The serial inflate writes every output byte through to HBM as it makes it
+// (a wave's 64 consecutive bytes: one coalesced store) and keeps only the
+// 32 KiB deflate window in LDS (round 5: a 64 KiB ring flushed in 32 KiB
+// bursts held 74 KiB of LDS per workgroup, and the masks' workgroups waited
+// to be dispatched behind the chunk decode and the unfilter).
+constexpr uint32_t kRing = 32768, kRingMask = kRing - 1;
 constexpr uint32_t kWin = 1024;        // input window (32-bit words) in LDS
 constexpr uint32_t kLitBits = 10, kDistBits = 8, kClBits = 7;
 
@@ -252,32 +256,37 @@ __device__ __forceinline__ uint32_t decode_sym(BitReader &br, const HTab &t) {
   return 0xFFFFu;
 }
 
-// ring[fp .. fp+n) -> out[fp .. fp+n), clamped to `want`
-__device__ __forceinline__ void flush_ring(InflateSmem &sm, DG_GLOBAL uint8_t *out, uint32_t fp, uint32_t n,
-                                           uint32_t want) {
-  if (fp + n > want) n = want > fp ? want - fp : 0u;
-  const uint32_t lane = threadIdx.x;
-  if ((fp & 15u) == 0 && n == kFlush) {
-    for (uint32_t i = lane * 16; i < n; i += 64 * 16) {
-      const uint32_t r = (fp + i) & kRingMask;
-      *(DG_GLOBAL u32x4 *)(out + fp + i) = *(const u32x4 *)(sm.ring + r);
-    }
-  } else {
-    for (uint32_t i = lane; i < n; i += 64) out[fp + i] = sm.ring[(fp + i) & kRingMask];
-  }
-}
-
 // mode 0: streams too small to chunk (launched beside the chunked kernels);
 // 1: images the chunked path gave up on (pd.serial, after k_inf_resolve);
 // 2: both (one launch after the chunked kernels)
+__device__ __forceinline__ void inflate_image(InflateSmem &sm, ImageDesc &im);
+
+// mode 1 runs on a few workgroups that walk the whole list: the images the
+// chunked path gave up on are rare (none in the configs[4] pool), and a
+// workgroup per image -- each asking for ~74 KiB of LDS while the chunk
+// decode and the unfilter hold most of it -- kept 3-10 ms of mostly empty
+// workgroups waiting to be dispatched on every batch's critical path.
+// The wave raises its issue priority: one wave's serial chain per image, on
+// the batch's critical path, sharing its SIMD with the throughput kernels of
+// the other batches in flight (a 33 ms mask took 83 ms among them).
 __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
-                                                    int mode) {
+                                                    uint32_t n, int mode) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   InflateSmem &sm = *reinterpret_cast<InflateSmem *>(smem_raw);
-  const WgItem it = list[blockIdx.x];
-  ImageDesc &im = imgs[it.image];
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t stride = mode == 1 ? gridDim.x : n;  // modes 0 / 2: one image per workgroup
+  for (uint32_t i = blockIdx.x; i < n; i += stride) {
+    ImageDesc &im = imgs[list[i].image];
+    const PngDesc &pd = im.png;
+    const bool take = mode == 0 ? pd.nchunks == 0 : mode == 1 ? (pd.nchunks && pd.serial) : !(pd.nchunks && !pd.serial);
+    if (!take) continue;
+    inflate_image(sm, im);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void inflate_image(InflateSmem &sm, ImageDesc &im) {
   const PngDesc &pd = im.png;
-  if (mode == 0 ? pd.nchunks != 0 : mode == 1 ? !(pd.nchunks && pd.serial) : (pd.nchunks && !pd.serial)) return;
   const uint32_t lane = threadIdx.x;
   const DG_GLOBAL uint32_t *z = gp<const uint32_t>(pd.zs);
   DG_GLOBAL uint8_t *out = gp<uint8_t>(pd.raw);
@@ -293,7 +302,7 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
   HTab tl{sm.lut_l, sm.sym_l, sm.cnt[0], sm.first[0], sm.off[0], kLitBits};
   HTab td{sm.lut_d, sm.sym_d, sm.cnt[1], sm.first[1], sm.off[1], kDistBits};
   HTab tc{sm.lut_c, sm.sym_c, sm.cnt[2], sm.first[2], sm.off[2], kClBits};
-  uint32_t op = 0, fp = 0;  // output produced / flushed to HBM
+  uint32_t op = 0;  // output produced (in HBM and the window)
   uint32_t nlit = 0;        // literals stashed in lanes [0, nlit) (positions op - nlit + lane)
   uint32_t litv = 0;
   int status = 0;
@@ -301,16 +310,12 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
   auto consumed = [&]() -> uint64_t { return (uint64_t)br.wnext * 32u - br.nb; };
   auto stash_flush = [&]() {
     if (nlit) {
-      if (lane < nlit) sm.ring[(op - nlit + lane) & kRingMask] = (uint8_t)litv;
+      if (lane < nlit) {
+        const uint32_t o = op - nlit + lane;
+        sm.ring[o & kRingMask] = (uint8_t)litv;
+        if (o < want) out[o] = (uint8_t)litv;
+      }
       nlit = 0;
-    }
-  };
-  auto maybe_flush = [&]() {
-    if (op - fp >= kFlush) {
-      stash_flush();
-      __syncthreads();
-      flush_ring(sm, out, fp, kFlush, want);
-      fp += kFlush;
     }
   };
   refill(sm, br, z);
@@ -322,7 +327,6 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
   while (!status && !last && op < want) {
     br_uni(br);
     op = uni(op);
-    fp = uni(fp);
     refill(sm, br, z);
     last = getbits(br, 1) != 0;
     const uint32_t type = getbits(br, 2);
@@ -345,21 +349,15 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
       }
       stash_flush();
       const DG_GLOBAL uint8_t *zb = (const DG_GLOBAL uint8_t *)z;
-      uint32_t done = 0;
-      while (done < len && op < want) {
-        uint32_t n = len - done;
-        const uint32_t room = fp + kFlush + kFlush / 2 - op;  // keep op - fp below the ring's reach
-        if (n > room) n = room;
-        for (uint32_t j = lane; j < n; j += 64) sm.ring[(op + j) & kRingMask] = zb[pos + done + j];
-        op += n;
-        done += n;
-        __syncthreads();
-        while (op - fp >= kFlush) {
-          flush_ring(sm, out, fp, kFlush, want);
-          fp += kFlush;
-          __syncthreads();
-        }
+      // (a later byte of a block longer than the window lands in its slot
+      // after the earlier one: same lane, later iteration)
+      for (uint32_t j = lane; j < len; j += 64) {
+        const uint8_t v = zb[pos + j];
+        sm.ring[(op + j) & kRingMask] = v;
+        if (op + j < want) out[op + j] = v;
       }
+      op += len;
+      __syncthreads();
       // reposition the reader after the block
       const uint32_t np = pos + len;
       br.bb = 0;
@@ -459,7 +457,6 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
     for (;;) {
       br_uni(br);
       op = uni(op);
-      fp = uni(fp);
       nlit = uni(nlit);
       refill(sm, br, z);
       const uint32_t s = decode_sym(br, tl);
@@ -469,7 +466,6 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
         op++;
         if (nlit == 64) stash_flush();
         if (op >= want) break;
-        maybe_flush();
         continue;
       }
       if (s == 256) break;
@@ -501,7 +497,10 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
         const uint32_t b = sm.ring[src0 & kRingMask];
         for (uint32_t r = 0; r < rounds; r++) {
           const uint32_t j = lane + 64u * r;
-          if (j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)b;
+          if (j < len) {
+            sm.ring[(q + j) & kRingMask] = (uint8_t)b;
+            if (q + j < want) out[q + j] = (uint8_t)b;
+          }
         }
       } else {  // every read before the writes: one LDS round trip (len <= 258)
         const float rcp = 1.0f / (float)dist;
@@ -521,7 +520,10 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
 #pragma unroll
         for (uint32_t r = 0; r < 5; r++) {
           const uint32_t j = lane + 64u * r;
-          if (r < rounds && j < len) sm.ring[(q + j) & kRingMask] = (uint8_t)v[r];
+          if (r < rounds && j < len) {
+            sm.ring[(q + j) & kRingMask] = (uint8_t)v[r];
+            if (q + j < want) out[q + j] = (uint8_t)v[r];
+          }
         }
       }
       op += len;
@@ -530,19 +532,12 @@ __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs
         status = 2;
         break;
       }
-      maybe_flush();
     }
     if (consumed() > limit_bits + 64) status = 2;
   }
   if (!status && op < want) status = 2;  // stream ended before the last scanline
   stash_flush();
   __syncthreads();
-  // final flush: [fp, min(op, want))
-  while (fp < op && fp < want) {
-    const uint32_t n = op - fp < kFlush ? op - fp : kFlush;
-    flush_ring(sm, out, fp, n, want);
-    fp += n;
-  }
   if (status && lane == 0) im.status = status;
 }
 
@@ -1539,6 +1534,9 @@ __global__ __launch_bounds__(64) void k_png_unfilter(ImageDesc *__restrict__ img
                                                      uint32_t *__restrict__ ticket, uint32_t dbg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t uf_smem[];  // uf_smem_bytes(batch's widest unit, U)
   __shared__ uint32_t s_ticket;
+  // a band is a serial wavefront on its image's critical path, as the serial
+  // inflate (k_png_inflate): issue priority over the other batches' waves
+  __builtin_amdgcn_s_setprio(2);
   DG_GLOBAL uint32_t *flags = gp<uint32_t>((uint64_t)(uintptr_t)flags_);
   for (;;) {
     if (threadIdx.x == 0) s_ticket = atomicAdd(ticket, 1u);
@@ -1699,8 +1697,9 @@ void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
                               (int)sizeof(InflateSmem));
     attr = true;
   }
-  if (nwg)
-    hipLaunchKernelGGL(k_png_inflate, dim3(nwg), dim3(64), sizeof(InflateSmem), st, imgs, list, mode);
+  const uint32_t grid = mode == 1 ? std::min<uint32_t>(nwg, 4u) : nwg;
+  if (grid)
+    hipLaunchKernelGGL(k_png_inflate, dim3(grid), dim3(64), sizeof(InflateSmem), st, imgs, list, nwg, mode);
 }
 void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_inf_find, dim3(nwg), dim3(64), 0, st, imgs, ch, list);
@@ -1749,7 +1748,7 @@ void launch_inf_resolve(hipStream_t st, ImageDesc *imgs, const InfChunk *ch, con
   if (nwg) hipLaunchKernelGGL(k_inf_resolve, dim3(nwg), dim3(1024), 0, st, imgs, ch, list);
 }
 template <uint32_t U>
-static void launch_png_unfilter_t(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks,
+static void launch_png_unfilter_t(uint32_t max_per_cu, hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks,
                                   uint32_t *flags, uint32_t ncu, uint32_t maxbpp, uint32_t dbg) {
   // flags: ntasks progress words + the ticket counter, zeroed by the caller
   static bool attr = false;  // > 64 KiB of dynamic LDS
@@ -1759,7 +1758,8 @@ static void launch_png_unfilter_t(hipStream_t st, ImageDesc *imgs, const WgItem 
     attr = true;
   }
   const uint32_t bpp = maxbpp < 1 ? 1u : maxbpp > 4 ? 4u : maxbpp, lds = uf_smem_bytes(bpp, U);
-  const uint32_t per_cu = std::max<uint32_t>(1u, (160u * 1024u - 64u) / (lds + 64u));  // workers resident per CU
+  uint32_t per_cu = std::max<uint32_t>(1u, (160u * 1024u - 64u) / (lds + 64u));  // workers resident per CU
+  if (max_per_cu && per_cu > max_per_cu) per_cu = max_per_cu;
   const uint32_t g = std::min(ntasks, ncu * per_cu);
   if (g)
     hipLaunchKernelGGL(k_png_unfilter<U>, dim3(g), dim3(64), lds, st, imgs, tasks, ntasks, flags, flags + ntasks, dbg);
@@ -1767,11 +1767,11 @@ static void launch_png_unfilter_t(hipStream_t st, ImageDesc *imgs, const WgItem 
 // units: filter units per lane per diagonal step (tiles of 64 * units columns;
 // 1 halves the LDS per worker, 2 halves the shuffle round trips per unit)
 void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
-                         uint32_t ncu, uint32_t maxbpp, uint32_t dbg, uint32_t units) {
+                         uint32_t ncu, uint32_t maxbpp, uint32_t dbg, uint32_t units, uint32_t max_per_cu) {
   if (units == 1)
-    launch_png_unfilter_t<1>(st, imgs, tasks, ntasks, flags, ncu, maxbpp, dbg);
+    launch_png_unfilter_t<1>(max_per_cu, st, imgs, tasks, ntasks, flags, ncu, maxbpp, dbg);
   else
-    launch_png_unfilter_t<2>(st, imgs, tasks, ntasks, flags, ncu, maxbpp, dbg);
+    launch_png_unfilter_t<2>(max_per_cu, st, imgs, tasks, ntasks, flags, ncu, maxbpp, dbg);
 }
 void launch_png_expand(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_png_expand, dim3(nwg), dim3(256), 0, st, imgs, list);

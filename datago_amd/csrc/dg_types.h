@@ -386,7 +386,7 @@ struct BatchFlags {
   uint32_t debug;           // test switches (kDbg*), kept across resync rounds
   uint64_t idct_list;       // fused IDCT: uint32 {image, block} pairs, idct_cap of them
   uint32_t idct_cap;
-  uint32_t pad1;
+  uint32_t prio;            // option "entropy_prio": wave issue priority of k_huff_sync / k_huff_write (0-3)
 };
 // The counters a resync round clears (everything before `wgtime`).
 constexpr size_t kFlagCounters = 24;

@@ -428,6 +428,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     d_ccache_.cap = 0;
     return DG_OK;
   }
+  if (k == "entropy_prio") {  // wave issue priority (s_setprio) of the entropy kernels, 0-3
+    if (v < 0 || v > 3) return DG_ERR_INVALID;
+    entropy_prio_ = (int)v;
+    return DG_OK;
+  }
   if (k == "max_device_mb") {  // device memory budget of the context (0: none)
     if (v < 0) return DG_ERR_INVALID;
     max_dev_bytes_ = (size_t)v << 20;
@@ -661,6 +666,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
   if (k == "sub_density") {  // bits-per-block threshold for shorter subsequences (0 = off)
     if (v < 0 || v > 4096) return DG_ERR_INVALID;
     sub_density_ = (double)v;
+    return DG_OK;
+  }
+  if (k == "uf_per_cu") {  // PNG unfilter: persistent workers per CU at most (0: as many as the LDS holds)
+    if (v < 0 || v > 16) return DG_ERR_INVALID;
+    uf_per_cu_ = (int)v;
     return DG_OK;
   }
   if (k == "uf_units") {  // PNG unfilter: filter units per lane per step (1: half the LDS per worker)
@@ -2381,6 +2391,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     bf->wgtime_write = (uint32_t)b.lists[L_SYNC].size();
   }
   ((BatchFlags *)(P + b.flags_off))->debug = (uint32_t)(debug_flags_ >> 16) & 3u;
+  ((BatchFlags *)(P + b.flags_off))->prio = (uint32_t)entropy_prio_;
   ((BatchFlags *)(P + b.flags_off))->idct_list = (uint64_t)(uintptr_t)((char *)sl.scratch.p + idct_list_off);
   ((BatchFlags *)(P + b.flags_off))->idct_cap = b.idct_cap;
   memcpy(P + b.desc_off, b.descs.data(), b.descs.size() * sizeof(ImageDesc));
@@ -2659,7 +2670,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
       uint32_t *uf = (uint32_t *)((char *)sl.scratch.p + b.uf_flags_off);
       HIPCHK(hipMemsetAsync(uf, 0, (size_t)(b.uf_n + 1) * 4, sl.st));
       launch_png_unfilter(sl.st, dm, lst(L_UNF), cnt(L_UNF), uf, ncu_, b.uf_maxbpp, (uint32_t)(debug_flags_ >> 18) & 1u,
-                          uf_units_);
+                          uf_units_, (uint32_t)uf_per_cu_);
     }
     launch_png_expand(sl.st, dd, lst(L_EXPAND), cnt(L_EXPAND));
   }

@@ -404,6 +404,8 @@ class Context {
 
   Slot slots_[kAllSlots];  // [0, kMaxInflight): baseline batches; then kProgSlots progressive ones
   uint32_t ncu_ = 256;  // compute units: persistent-worker grids
+  int entropy_prio_ = 0;  // option "entropy_prio"
+  int uf_per_cu_ = 0;     // option "uf_per_cu"
   int nslots_ = 4;  // option "slots": batches in flight (each slot: own streams + scratch; 4 measured +2% over 3 with own queues)
   int next_slot_ = 0;
   uint64_t next_ticket_ = 1;

@@ -93,7 +93,7 @@ void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
 // dbg bit 0: band 1 of every plane times out on its first wait (test switch)
 void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,
                          uint32_t ncu, uint32_t maxbpp, uint32_t dbg,
-                         uint32_t units);
+                         uint32_t units, uint32_t max_per_cu);  // max_per_cu: workers per CU cap (0: LDS-bound)
 // 256 pixels per workgroup
 void launch_png_expand(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg);
 // alpha program at `point` (0 before call 1, 1 between the calls, 2 after call 2): 256 pixels per workgroup

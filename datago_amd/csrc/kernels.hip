@@ -433,6 +433,14 @@ __device__ __forceinline__ void store_sub(SubState &o, uint32_t in, uint32_t out
   }
 }
 
+// BatchFlags::prio (option "entropy_prio") as the wave's issue priority
+__device__ __forceinline__ void entropy_setprio(const BatchFlags *flags) {
+  const uint32_t p = __builtin_amdgcn_readfirstlane(flags->prio);
+  if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 3) __builtin_amdgcn_s_setprio(3);
+}
+
 template <bool STAGE>
 __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__ imgs,
                                                    const WgItem *__restrict__ list,
@@ -443,6 +451,7 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   HuffTable *tabs = (HuffTable *)huff_dyn;
   __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
   const uint64_t t_start = wg_clock();
+  entropy_setprio(flags);
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
   load_tables(tabs, pool, im);
@@ -658,6 +667,7 @@ __global__ __launch_bounds__(256) void k_huff_write(ImageDesc *__restrict__ imgs
   __shared__ int32_t qt[3 * 64];                  // fused IDCT: quantisation tables, natural order
   __shared__ uint8_t n2z[64];                     // fused IDCT: natural -> zigzag index
   const uint64_t t_start = wg_clock();
+  entropy_setprio(flags);
   const WgItem it = list[blockIdx.x];
   const ImageDesc &im = imgs[it.image];
   load_tables(tabs, pool, im);

@@ -282,10 +282,13 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *                 staging and streams; progressive batches use two slots of their own
  *   "hb_bands"    band H kernel: 8-row bands per workgroup, 1..64 (default 16)
  *   "entropy_lpt" 1 = dispatch the slowest entropy workgroups first (default 1)
+ *   "entropy_prio" 0-3: wave issue priority (s_setprio) of k_huff_sync / k_huff_write over the other
+ *                 batches' pixel kernels sharing their SIMDs (default 0)
  *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)
  *   "png_chunked" 0 = inflate every PNG with the serial kernel (test switch; default 1)
  *   "inf_chunk"   chunk-parallel inflate: compressed bytes per chunk (power of two, 4096..65536; default 32768)
  *   "uf_units"    1 or 2 (default 2): PNG unfilter filter units per lane per diagonal step (1: half the LDS)
+ *   "uf_per_cu"   PNG unfilter: persistent workers per CU at most (default 0: as many as the LDS holds)
  *   "inf_decode"  0..5: chunk-parallel inflate lookup bits (literal/length, distance) per lane in LDS:
  *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (24 KiB), 3 7/5, 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
  *                 the next 8 stream words of every lane in registers, refilled wave-wide; 8 / 9 / 11 = 7/6, 6/5,
