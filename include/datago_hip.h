@@ -287,7 +287,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)
  *   "png_chunked" 0 = inflate every PNG with the serial kernel (test switch; default 1)
  *   "inf_chunk"   chunk-parallel inflate: compressed bytes per chunk (power of two, 4096..65536; default 32768)
- *   "uf_units"    1 or 2 (default 2): PNG unfilter filter units per lane per diagonal step (1: half the LDS)
+ *   "uf_units"    1 or 2 (default 1): PNG unfilter filter units per lane per diagonal step (1: half the LDS
+ *                 per worker, twice the workers per CU: configs[4] 18.5 -> 19.4 Gpx/s, unfilter 17.5 -> 13.7 ms)
  *   "uf_per_cu"   PNG unfilter: persistent workers per CU at most (default 0: as many as the LDS holds)
  *   "inf_decode"  0..5: chunk-parallel inflate lookup bits (literal/length, distance) per lane in LDS:
  *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (24 KiB), 3 7/5, 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
