@@ -1,11 +1,11 @@
 #!/bin/bash
 # dg_decode_one latency: small-batch entropy options (OPTS via tools/gpu_one.sh),
 # then the default under a kernel trace with the per-batch chain and a timeline
-# of every stream around one batch (tools/one_chain.py).  OUT=gpurun_out/r5i
+# of every stream around one batch (tools/one_chain.py).  OUT=gpurun_out/one_trace
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=${OUT:-gpurun_out/r5i}
+OUT=${OUT:-gpurun_out/one_trace}
 mkdir -p $OUT
 python -c "import datago_amd._lib as L; L.load()" || exit 3
 OUT=$OUT/one ONE_IMAGES=2048 THREADS=32 OPTS="${ONE_OPTS:-;small_coded=33554432 sub_small=512 lead_small=1024;small_coded=33554432 sub_small=1024 lead_small=2048}" tools/gpu_one.sh || exit $?

@@ -1,11 +1,11 @@
 #!/bin/bash
 # configs[4] PNG investigation: the PNG tests, the bench line over inflate-decode
 # variants (VARIANTS: inf_decode values), a rocprof kernel trace (per-kernel spans,
-# timeline) and SQ counter passes per kernel (one batch in flight).  OUT=gpurun_out/png5
+# timeline) and SQ counter passes per kernel (one batch in flight).  OUT=gpurun_out/png
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=${OUT:-gpurun_out/png5}
+OUT=${OUT:-gpurun_out/png}
 mkdir -p $OUT
 python -c "import datago_amd._lib as L; L.load()" || exit 3
 if [ "${TESTS:-1}" = 1 ]; then
