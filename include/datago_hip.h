@@ -291,7 +291,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *                 per worker, twice the workers per CU: configs[4] 18.5 -> 19.4 Gpx/s, unfilter 17.5 -> 13.7 ms)
  *   "uf_per_cu"   PNG unfilter: persistent workers per CU at most (default 0: as many as the LDS holds)
  *   "inf_decode"  0..5: chunk-parallel inflate lookup bits (literal/length, distance) per lane in LDS:
- *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (24 KiB), 3 7/5, 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
+ *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (24 KiB), 3 7/5 (20 KiB, default since round 5:
+ *                 configs[4] 19.1-19.4 -> 20.1-20.3 Gpx/s), 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
  *                 the next 8 stream words of every lane in registers, refilled wave-wide; 8 / 9 / 11 = 7/6, 6/5,
  *                 8/6 bits with the symbol tables of longer codes in LDS too (64 / 52 / 96 KiB per wave); 12 / 13 =
  *                 8 / 9 with the register buffer; 14 = 0 with it; 15 = 11 with it
