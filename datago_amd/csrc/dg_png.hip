@@ -597,6 +597,24 @@ __device__ __forceinline__ uint64_t inf_header_fast(uint64_t lo, uint64_t hi) {
   return bad ? 0ull : hist | 1ull;  // bit 0 set: field 0 (length-0 count) is never read
 }
 
+// Stage 2 of the finder: the code-length code is complete (Kraft sum of its
+// lengths exactly 1), in 32-bit arithmetic -- what inf_header_fast's
+// per-level check amounts to (an over-subscribed level makes the sum exceed
+// 1, an incomplete code leaves it short), without the 64-bit histogram
+// (~6 instead of ~9 operations per length).  The header fields were stage 1's.
+__device__ __forceinline__ bool inf_kraft_fast(uint64_t lo, uint64_t hi) {
+  const uint32_t ncode = (((uint32_t)lo >> 13) & 15u) + 4u;
+  const uint64_t clbits = (lo >> 17) | (hi << 47);  // 19 3-bit lengths from bit 0
+  const uint32_t c0 = (uint32_t)clbits, c1 = (uint32_t)(clbits >> 30);  // c1: lengths 10.. at bit 0
+  uint32_t k = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 19; i++) {
+    const uint32_t l = i < 10 ? (c0 >> (3 * i)) & 7u : (c1 >> (3 * (i - 10))) & 7u;
+    k += (i < ncode && l) ? 128u >> l : 0u;
+  }
+  return k == 128u;
+}
+
 __device__ bool inf_header_full(const DG_GLOBAL uint32_t *z, uint32_t zwords, uint32_t pos, uint64_t lo, uint64_t hi,
                                 uint64_t hist) {
   const uint32_t h = (uint32_t)lo & 0x1FFFFu;
@@ -711,7 +729,7 @@ __device__ __forceinline__ bool inf_candidate(const DG_GLOBAL uint32_t *z, uint3
 //     positions; ~11% of random positions pass.  (Round 5: one position per
 //     lane per step, ~20 instructions for 64 positions, made the finder ~60%
 //     of a configs[4] batch's VALU work -- more than the decode it feeds.)
-//  2. inf_header_fast (the code-length code's Kraft sum) on the step's
+//  2. the code-length code's Kraft sum (inf_kraft_fast) on the step's
 //     survivors, 64 at a time, their stream words read from the step's words
 //     in LDS; ~0.4% of those pass;
 //  3. inf_header_full on the Kraft survivors, once kInfStage3 of them have
@@ -798,7 +816,7 @@ __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ i
         for (uint32_t j = 0; j < 4; j++) qw[j] = win[(pos >> 5) - W + j];
         uint64_t lo, hi;
         inf_bits96(qw, pos & 31u, lo, hi);
-        const bool pass = lane < nb && inf_header_fast(lo, hi) != 0;
+        const bool pass = lane < nb && inf_kraft_fast(lo, hi);
         const uint64_t mp = __ballot(pass);
         if (pass) qpos[qn + (uint32_t)__popcll(mp & below)] = pos;
         qn += (uint32_t)__popcll(mp);
