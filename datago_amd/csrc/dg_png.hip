@@ -898,14 +898,15 @@ __device__ bool lane_build(const DG_GLOBAL uint8_t *lens, uint32_t n, LaneTab<B,
   return true;
 }
 
-constexpr uint32_t kLbBuf = 8;  // Q: stream words buffered in registers per lane
+constexpr uint32_t kLbBuf = 8;  // Q: stream words buffered in registers per lane (default)
 
+template <uint32_t NB = kLbBuf>
 struct LaneBits {
   uint64_t bb;
   uint32_t nb, wp, zwords;  // wp: index of the next stream word to shift into bb
   uint32_t w1;              // Q = false: that word, loaded one refill ahead
   uint32_t nbuf;            // Q = true: words wp .. wp + nbuf - 1 held in buf
-  uint32_t buf[kLbBuf];
+  uint32_t buf[NB];
 };
 
 // Q: the next kLbBuf stream words of every lane sit in registers, refilled
@@ -914,11 +915,13 @@ struct LaneBits {
 // compiler waits for it where the branches join: every fourth symbol of a
 // literal-heavy stream paid a full memory latency.
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
-__device__ __forceinline__ void lb_fill(LaneBits &r, const DG_GLOBAL uint32_t *z) {
+template <uint32_t NB>
+__device__ __forceinline__ void lb_fill(LaneBits<NB> &r, const DG_GLOBAL uint32_t *z) {
+  static_assert(NB % 4 == 0, "whole 16-byte loads");
   const uint32_t i = r.wp;
-  if (i + kLbBuf <= r.zwords) {
+  if (i + NB <= r.zwords) {
 #pragma unroll
-    for (uint32_t k = 0; k < kLbBuf; k += 4) {
+    for (uint32_t k = 0; k < NB; k += 4) {
       const u32x4a q = *(const DG_GLOBAL u32x4a *)(z + i + k);
       r.buf[k] = q.x;
       r.buf[k + 1] = q.y;
@@ -927,13 +930,13 @@ __device__ __forceinline__ void lb_fill(LaneBits &r, const DG_GLOBAL uint32_t *z
     }
   } else {
 #pragma unroll
-    for (uint32_t k = 0; k < kLbBuf; k++) r.buf[k] = i + k < r.zwords ? z[i + k] : 0u;
+    for (uint32_t k = 0; k < NB; k++) r.buf[k] = i + k < r.zwords ? z[i + k] : 0u;
   }
-  r.nbuf = kLbBuf;
+  r.nbuf = NB;
 }
 
-template <bool Q>
-__device__ __forceinline__ void lb_seek(LaneBits &r, const DG_GLOBAL uint32_t *z, uint32_t wp) {
+template <bool Q, uint32_t NB>
+__device__ __forceinline__ void lb_seek(LaneBits<NB> &r, const DG_GLOBAL uint32_t *z, uint32_t wp) {
   r.wp = wp;
   if (Q) {
     lb_fill(r, z);
@@ -945,13 +948,13 @@ __device__ __forceinline__ void lb_seek(LaneBits &r, const DG_GLOBAL uint32_t *z
 // Q: at a point every lane of the wave reaches: refill all lanes' buffers
 // together once any lane holds fewer words than a symbol step can take (a
 // length/distance pair is at most 48 bits: two words)
-template <bool Q>
-__device__ __forceinline__ void lb_top(LaneBits &r, const DG_GLOBAL uint32_t *z) {
+template <bool Q, uint32_t NB>
+__device__ __forceinline__ void lb_top(LaneBits<NB> &r, const DG_GLOBAL uint32_t *z) {
   if (Q && __ballot(r.nbuf < 3u)) lb_fill(r, z);
 }
 
-template <bool Q = false>
-__device__ __forceinline__ void lb_refill(LaneBits &r, const DG_GLOBAL uint32_t *z) {
+template <bool Q, uint32_t NB>
+__device__ __forceinline__ void lb_refill(LaneBits<NB> &r, const DG_GLOBAL uint32_t *z) {
   if (r.nb < 32) {
     if (Q) {
       if (r.nbuf == 0) lb_fill(r, z);  // off the symbol loop (headers, stored blocks)
@@ -960,7 +963,7 @@ __device__ __forceinline__ void lb_refill(LaneBits &r, const DG_GLOBAL uint32_t 
       r.wp++;
       r.nbuf--;
 #pragma unroll
-      for (uint32_t k = 0; k + 1 < kLbBuf; k++) r.buf[k] = r.buf[k + 1];
+      for (uint32_t k = 0; k + 1 < NB; k++) r.buf[k] = r.buf[k + 1];
     } else {
       r.bb |= (uint64_t)r.w1 << r.nb;
       r.nb += 32;
@@ -969,17 +972,19 @@ __device__ __forceinline__ void lb_refill(LaneBits &r, const DG_GLOBAL uint32_t 
     }
   }
 }
-__device__ __forceinline__ uint32_t lb_get(LaneBits &r, uint32_t k) {
+template <uint32_t NB>
+__device__ __forceinline__ uint32_t lb_get(LaneBits<NB> &r, uint32_t k) {
   const uint32_t v = (uint32_t)r.bb & ((1u << k) - 1u);
   r.bb >>= k;
   r.nb -= k;
   return v;
 }
 // consumed bit position: wp counts the word held in w1
-__device__ __forceinline__ uint32_t lb_pos(const LaneBits &r) { return r.wp * 32u - r.nb; }
+template <uint32_t NB>
+__device__ __forceinline__ uint32_t lb_pos(const LaneBits<NB> &r) { return r.wp * 32u - r.nb; }
 
-template <uint32_t B, typename LutPtr, typename SymPtr>
-__device__ __forceinline__ uint32_t lane_sym(LaneBits &r, const LaneTab<B, LutPtr, SymPtr> &t) {
+template <uint32_t B, typename LutPtr, typename SymPtr, uint32_t NB>
+__device__ __forceinline__ uint32_t lane_sym(LaneBits<NB> &r, const LaneTab<B, LutPtr, SymPtr> &t) {
   const uint32_t peek = (uint32_t)r.bb;
   const uint32_t e = t.lut[peek & ((1u << B) - 1u)];
   if (e & 15u) {
@@ -1023,7 +1028,7 @@ constexpr uint32_t inf_lds_per_lane() {
 // lie before the chunk (resolved by k_inf_resolve). WG lanes per workgroup;
 // the lookups take WG * inf_lds_per_lane<LB, DB>() bytes of LDS (64 lanes,
 // 9/7 bits: 80 KiB, two workgroups per CU).
-template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false, bool SL = false>
+template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false, bool SL = false, uint32_t NB = kLbBuf>
 __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
                                                    uint32_t nch) {
   constexpr uint32_t kInfLdsPerLane = inf_lds_per_lane<LB, DB, SL>();
@@ -1059,7 +1064,7 @@ __global__ __launch_bounds__(WG) void k_inf_decode(const ImageDesc *__restrict__
   LaneTab<6, DG_GLOBAL uint16_t *> tc{(DG_GLOBAL uint16_t *)(tb + 3328), (DG_GLOBAL uint16_t *)(tb + 3520), 0, 0,
                                       {0, 0, 0}};
   const uint32_t zbits_total = pd.zlen * 8u;
-  LaneBits r;
+  LaneBits<NB> r;
   r.zwords = (pd.zlen + 3) / 4;
   {
     const uint32_t p = c.start;
@@ -1722,17 +1727,17 @@ void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
 void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_inf_find, dim3(nwg), dim3(64), 0, st, imgs, ch, list);
 }
-template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false, bool SL = false>
+template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false, bool SL = false, uint32_t NB = kLbBuf>
 static void launch_inf_decode_t(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch) {
   constexpr uint32_t lds = WG * inf_lds_per_lane<LB, DB, SL>();
   static bool attr = false;  // > 64 KiB of dynamic LDS
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_inf_decode<WG, LB, DB, Q, SL>,
+    (void)hipFuncSetAttribute((const void *)k_inf_decode<WG, LB, DB, Q, SL, NB>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   if (nch)
-    hipLaunchKernelGGL((k_inf_decode<WG, LB, DB, Q, SL>), dim3((nch + WG - 1) / WG), dim3(WG), lds, st, imgs, ch,
+    hipLaunchKernelGGL((k_inf_decode<WG, LB, DB, Q, SL, NB>), dim3((nch + WG - 1) / WG), dim3(WG), lds, st, imgs, ch,
                        nch);
 }
 // variant: 64-lane workgroups with 0 = 9/7-bit lookups (80 KiB, 2 per CU);
@@ -1759,6 +1764,19 @@ void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint
     case 13: launch_inf_decode_t<64, 6, 5, true, true>(st, imgs, ch, nch); break;
     case 14: launch_inf_decode_t<64, 9, 7, true>(st, imgs, ch, nch); break;
     case 15: launch_inf_decode_t<64, 8, 6, true, true>(st, imgs, ch, nch); break;
+    case 16: launch_inf_decode_t<64, 7, 5, true>(st, imgs, ch, nch); break;   // 3 + register buffer
+    case 17: launch_inf_decode_t<64, 7, 4>(st, imgs, ch, nch); break;         // 18 KiB
+    case 18: launch_inf_decode_t<64, 8, 5>(st, imgs, ch, nch); break;         // 36 KiB
+    case 19: launch_inf_decode_t<64, 8, 4>(st, imgs, ch, nch); break;         // 34 KiB
+    case 20: launch_inf_decode_t<64, 7, 4, true>(st, imgs, ch, nch); break;   // 17 + register buffer
+    case 21: launch_inf_decode_t<64, 6, 5, true>(st, imgs, ch, nch); break;   // 4 + register buffer
+    case 22: launch_inf_decode_t<64, 6, 4, true>(st, imgs, ch, nch); break;   // 5 + register buffer
+    case 23: launch_inf_decode_t<64, 7, 5, true, false, 4>(st, imgs, ch, nch); break;   // 16, 4 words
+    case 24: launch_inf_decode_t<64, 7, 5, true, false, 12>(st, imgs, ch, nch); break;  // 16, 12 words
+    case 25: launch_inf_decode_t<64, 7, 5, true, false, 16>(st, imgs, ch, nch); break;  // 16, 16 words
+    case 26: launch_inf_decode_t<64, 7, 5, true, false, 24>(st, imgs, ch, nch); break;  // 16, 24 words
+    case 27: launch_inf_decode_t<64, 7, 5, true, false, 32>(st, imgs, ch, nch); break;  // 16, 32 words
+    case 28: launch_inf_decode_t<64, 7, 4, true, false, 16>(st, imgs, ch, nch); break;  // 20, 16 words
     default: launch_inf_decode_t<64, 9, 7>(st, imgs, ch, nch); break;
   }
 }

@@ -681,8 +681,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
   if (k == "inf_decode") {  // k_inf_decode lookup bits (literal/length, distance): 0 9/7, 1 8/6, 2 7/6, 3 7/5, 4 6/5,
                             // 5 6/4; 6, 7 = 2, 1 with the wave-batched register stream buffer; 8 / 9 / 11 =
                             // 7/6, 6/5, 8/6 with the canonical walk's symbol tables in LDS; 12 / 13 = 8 / 9
-                            // with the register buffer; 14 = 0 with it, 15 = 11 with it
-    if (v < 0 || v > 15 || v == 10) return DG_ERR_INVALID;
+                            // with the register buffer; 14 = 0 with it, 15 = 11 with it; 16 = 3 with it;
+                            // 17 7/4, 18 8/5, 19 8/4; 20 / 21 / 22 = 17 / 4 / 5 with the register buffer;
+                            // 23 / 24 / 25 / 26 / 27 = 16 with a 4 / 12 / 16 / 24 / 32-word buffer;
+                            // 28 = 20 with a 16-word buffer
+    if (v < 0 || v > 28 || v == 10) return DG_ERR_INVALID;
     inf_decode_ = (uint32_t)v;
     return DG_OK;
   }

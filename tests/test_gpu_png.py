@@ -196,7 +196,7 @@ def test_png_large_full_size_properties(ctx512):
     assert st == 0 and (arr.shape[1], arr.shape[0]) == t.target_size(1800, 1200)
 
 
-@pytest.mark.parametrize("inf_decode,inf_chunk", [(d, 32768) for d in range(16) if d != 10] + [(2, 4096), (2, 8192), (2, 16384),
+@pytest.mark.parametrize("inf_decode,inf_chunk", [(d, 32768) for d in range(29) if d != 10] + [(2, 4096), (2, 8192), (2, 16384),
                                                                                      (3, 65536), (9, 16384)])
 def test_chunked_inflate_matches_serial_and_oracle(inf_decode, inf_chunk):
     """Large streams take the chunk-parallel inflate (block-header search,
