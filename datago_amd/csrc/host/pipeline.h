@@ -447,7 +447,8 @@ class Context {
   bool chroma_rec_ = true;              // option "chroma_rec": half-rate chroma planes as 8-byte records (dg_plane.h)
   bool band_dec_ = false;               // option "band_dec": IDCT + colour + first H pass in k_band_dec
   uint32_t uf_units_ = 1;               // option "uf_units": PNG unfilter units per lane per step (1 or 2; round 5: 1)
-  uint32_t inf_decode_ = 3;             // option "inf_decode": k_inf_decode lookup bits (3 = 7/5, 20 KiB LDS per wave)
+  uint32_t inf_decode_ = 25;            // option "inf_decode": k_inf_decode shape (25 = 7/5 lookup bits, 20 KiB LDS
+                                        // per wave, 16 stream words per lane in registers)
   bool h_mfma_ = false;                 // option "h_mfma": band H passes on the matrix cores (k_resize_hm; measured slower: off)
   double sub_density_ = 0;              // option "sub_density": bits per block below which subsequences shrink
   bool lead_density_ = false;           // option "lead_density": their lead-in shrinks by the same factor

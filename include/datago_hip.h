@@ -290,14 +290,15 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "uf_units"    1 or 2 (default 1): PNG unfilter filter units per lane per diagonal step (1: half the LDS
  *                 per worker, twice the workers per CU: configs[4] 18.5 -> 19.4 Gpx/s, unfilter 17.5 -> 13.7 ms)
  *   "uf_per_cu"   PNG unfilter: persistent workers per CU at most (default 0: as many as the LDS holds)
- *   "inf_decode"  0..5: chunk-parallel inflate lookup bits (literal/length, distance) per lane in LDS:
- *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (24 KiB), 3 7/5 (20 KiB, default since round 5:
- *                 configs[4] 19.1-19.4 -> 20.1-20.3 Gpx/s), 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
+ *   "inf_decode"  0..28 (not 10): chunk-parallel inflate lookup bits (literal/length, distance) per lane in LDS:
+ *                 0 9/7 (80 KiB per wave), 1 8/6, 2 7/6 (24 KiB), 3 7/5 (20 KiB; round 5: configs[4]
+ *                 19.1-19.4 -> 20.1-20.3 Gpx/s), 4 6/5, 5 6/4; 6 / 7 = 2 / 1 with
  *                 the next 8 stream words of every lane in registers, refilled wave-wide; 8 / 9 / 11 = 7/6, 6/5,
  *                 8/6 bits with the symbol tables of longer codes in LDS too (64 / 52 / 96 KiB per wave); 12 / 13 =
  *                 8 / 9 with the register buffer; 14 = 0 with it; 15 = 11 with it; 16 = 3 with it;
  *                 17 7/4, 18 8/5, 19 8/4 bits; 20 / 21 / 22 = 17 / 4 / 5 with the register buffer;
- *                 23 / 24 / 25 / 26 / 27 = 16 with a 4 / 12 / 16 / 24 / 32-word buffer; 28 = 20 with 16 words
+ *                 23 / 24 / 25 / 26 / 27 = 16 with a 4 / 12 / 16 / 24 / 32-word buffer; 28 = 20 with 16 words.
+ *                 Default 25 (7/5 bits, 16 words: configs[4] 20.5 -> 22.5-22.8 Gpx/s)
  *   "copy_threads" host threads copying a host-out batch's outputs to the caller's buffers (default 8)
  *   "write_split" 1 = k_huff_write decodes each entropy range as two halves split at the sync pass's
  *                 half-way checkpoint (images without restart markers; default); 0 = one lane per range
