@@ -734,11 +734,11 @@ __device__ __forceinline__ bool inf_candidate(const DG_GLOBAL uint32_t *z, uint3
 //     in LDS; ~0.4% of those pass;
 //  3. inf_header_full on the Kraft survivors, once kInfStage3 of them have
 //     queued (a round costs its longest lane's decode: batching more
-//     positions per round scans further past the first real header).
+//     positions per round scans further past the first real header;
+//     template S3, option "inf_stage3").
 // Every stage keeps position order, so the first position passing stage 3 is
 // the first candidate of the chunk.
-constexpr uint32_t kInfStage3 = 32;
-
+template <uint32_t kInfStage3>
 __global__ __launch_bounds__(64) void k_inf_find(const ImageDesc *__restrict__ imgs, InfChunk *__restrict__ ch,
                                                  const WgItem *__restrict__ list) {
   __shared__ uint32_t q1pos[2048];  // stage-2 queue: the step's header-field survivors, in order
@@ -1724,8 +1724,15 @@ void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
   if (grid)
     hipLaunchKernelGGL(k_png_inflate, dim3(grid), dim3(64), sizeof(InflateSmem), st, imgs, list, nwg, mode);
 }
-void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg) {
-  if (nwg) hipLaunchKernelGGL(k_inf_find, dim3(nwg), dim3(64), 0, st, imgs, ch, list);
+void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg,
+                     uint32_t stage3) {
+  if (!nwg) return;
+  switch (stage3) {
+    case 8: hipLaunchKernelGGL(k_inf_find<8>, dim3(nwg), dim3(64), 0, st, imgs, ch, list); break;
+    case 16: hipLaunchKernelGGL(k_inf_find<16>, dim3(nwg), dim3(64), 0, st, imgs, ch, list); break;
+    case 64: hipLaunchKernelGGL(k_inf_find<64>, dim3(nwg), dim3(64), 0, st, imgs, ch, list); break;
+    default: hipLaunchKernelGGL(k_inf_find<32>, dim3(nwg), dim3(64), 0, st, imgs, ch, list); break;
+  }
 }
 template <uint32_t WG, uint32_t LB, uint32_t DB, bool Q = false, bool SL = false, uint32_t NB = kLbBuf>
 static void launch_inf_decode_t(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch) {

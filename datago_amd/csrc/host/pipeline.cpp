@@ -650,6 +650,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     plan_threads_ = (int)v;
     return DG_OK;
   }
+  if (k == "inf_stage3") {  // k_inf_find: Kraft survivors queued per full header check round
+    if (v != 8 && v != 16 && v != 32 && v != 64) return DG_ERR_INVALID;
+    inf_stage3_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "inf_chunk") {  // compressed bytes per chunk of the chunk-parallel inflate
     if (v < 4096 || v > 65536 || (v & (v - 1))) return DG_ERR_INVALID;
     inf_chunk_ = (uint32_t)v;
@@ -2658,7 +2663,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
         HIPCHK(hipEventRecord(sl.ev_png1, sl.side));
       }
       InfChunk *ich = (InfChunk *)(M + b.ichunk_off);
-      launch_inf_find(sl.st, dd, ich, lst(L_INF_FIND), cnt(L_INF_FIND));
+      launch_inf_find(sl.st, dd, ich, lst(L_INF_FIND), cnt(L_INF_FIND), inf_stage3_);
       launch_inf_decode(sl.st, dd, ich, (uint32_t)b.ichunks.size(), inf_decode_);
       launch_inf_resolve(sl.st, dm, ich, lst(L_INF_RES), cnt(L_INF_RES));
       launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG), beside ? 1 : 2);

@@ -420,6 +420,7 @@ class Context {
   bool wg_timing_ = false;
   bool chunked_off_ = false;  // option "png_chunked" = 0
   uint32_t inf_chunk_ = kInfChunk;  // option "inf_chunk"
+  uint32_t inf_stage3_ = 32;        // option "inf_stage3"
   int plan_threads_ = 4;            // option "plan_threads"
   int meta_pull_ = 1;               // option "meta_pull"
   size_t list_hint_[L_COUNT] = {};  // work-list sizes of the previous batch (reserve)

@@ -101,7 +101,9 @@ void launch_alpha(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uin
 size_t png_inflate_smem();
 // chunk-parallel inflate (see InfChunk): find = one wave per chunk > 0 (list item.image = chunk),
 // decode = one lane per chunk, resolve = one 1024-thread workgroup per chunked image
-void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg);
+// stage3: Kraft survivors queued before a full header check round (8, 16, 32 or 64)
+void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg,
+                     uint32_t stage3);
 void launch_inf_decode(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, uint32_t nch, uint32_t variant);
 void launch_inf_resolve(hipStream_t st, ImageDesc *imgs, const InfChunk *ch, const WgItem *list, uint32_t nwg);
 }  // namespace dg

@@ -287,6 +287,8 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "entropy_once" 1 = decode-once staging + scatter instead of a second decode (default 0; slower)
  *   "png_chunked" 0 = inflate every PNG with the serial kernel (test switch; default 1)
  *   "inf_chunk"   chunk-parallel inflate: compressed bytes per chunk (power of two, 4096..65536; default 32768)
+ *   "inf_stage3"  8, 16, 32 or 64 (default 32): PNG block finder, Kraft survivors queued before each round
+ *                 of full header checks
  *   "uf_units"    1 or 2 (default 1): PNG unfilter filter units per lane per diagonal step (1: half the LDS
  *                 per worker, twice the workers per CU: configs[4] 18.5 -> 19.4 Gpx/s, unfilter 17.5 -> 13.7 ms)
  *   "uf_per_cu"   PNG unfilter: persistent workers per CU at most (default 0: as many as the LDS holds)

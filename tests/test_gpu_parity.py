@@ -260,7 +260,7 @@ def test_band_and_slot_options_validated():
     ctx = L.Context(0)
     for k, v in (("hb_bands", 0), ("hb_bands", 65), ("slots", 0), ("slots", 7), ("inf_decode", -1),
                  ("inf_decode", 10), ("inf_decode", 29), ("uf_units", 0), ("uf_units", 3), ("plan_threads", 0), ("inf_chunk", 1000),
-                 ("inf_chunk", 2048), ("sub_auto", 3000), ("meta_pull", 3)):
+                 ("inf_chunk", 2048), ("inf_stage3", 12), ("sub_auto", 3000), ("meta_pull", 3)):
         with pytest.raises(Exception):
             ctx.set_option(k, v)
 

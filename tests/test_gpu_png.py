@@ -196,14 +196,17 @@ def test_png_large_full_size_properties(ctx512):
     assert st == 0 and (arr.shape[1], arr.shape[0]) == t.target_size(1800, 1200)
 
 
-@pytest.mark.parametrize("inf_decode,inf_chunk", [(d, 32768) for d in range(29) if d != 10] + [(2, 4096), (2, 8192), (2, 16384),
-                                                                                     (3, 65536), (9, 16384)])
-def test_chunked_inflate_matches_serial_and_oracle(inf_decode, inf_chunk):
+@pytest.mark.parametrize("inf_decode,inf_chunk,stage3",
+                         [(d, 32768, 32) for d in range(29) if d != 10] +
+                         [(2, 4096, 32), (2, 8192, 32), (2, 16384, 32), (3, 65536, 32), (9, 16384, 32)] +
+                         [(25, 32768, s) for s in (8, 16, 64)])
+def test_chunked_inflate_matches_serial_and_oracle(inf_decode, inf_chunk, stage3):
     """Large streams take the chunk-parallel inflate (block-header search,
     one lane per chunk, window markers); it must equal the oracle and the
     serial kernel (option png_chunked=0) byte for byte, for every
     k_inf_decode shape (option inf_decode: lanes per workgroup, lookup bits)
-    and chunk size (option inf_chunk: compressed bytes per chunk)."""
+    and chunk size (option inf_chunk: compressed bytes per chunk), and the
+    block finder's round size (option inf_stage3)."""
     L = _lib()
     rng = np.random.default_rng(31)
     datas = []
@@ -217,6 +220,7 @@ def test_chunked_inflate_matches_serial_and_oracle(inf_decode, inf_chunk):
     a = L.Context(0)
     a.set_option("inf_decode", inf_decode)
     a.set_option("inf_chunk", inf_chunk)
+    a.set_option("inf_stage3", stage3)
     b = L.Context(0)
     b.set_option("png_chunked", 0)
     ra, rb = a.decode_batch(datas), b.decode_batch(datas)
