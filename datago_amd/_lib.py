@@ -291,8 +291,17 @@ def close_all() -> None:
 
 
 def _close_all_at_exit() -> None:
-    if os.environ.get("DG_NO_ATEXIT_CLOSE") != "1":
-        close_all()
+    # dg_ctx_destroy waits for exclusive use of the context.  At interpreter
+    # exit only daemon threads are left, and one of them may be inside a long
+    # dg_wait / dg_decode_one: then the contexts are left to the
+    # library's exit hook, which skips a context that is still in use
+    # (try-lock) instead of blocking the exit.
+    import threading
+    if os.environ.get("DG_NO_ATEXIT_CLOSE") == "1":
+        return
+    if any(t.is_alive() and t is not threading.current_thread() for t in threading.enumerate()):
+        return
+    close_all()
 
 
 atexit.register(_close_all_at_exit)

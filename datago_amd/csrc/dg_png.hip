@@ -261,25 +261,40 @@ __device__ __forceinline__ uint32_t decode_sym(BitReader &br, const HTab &t) {
 // 2: both (one launch after the chunked kernels)
 __device__ __forceinline__ void inflate_image(InflateSmem &sm, ImageDesc &im);
 
-// mode 1 runs on a few workgroups that walk the whole list: the images the
-// chunked path gave up on are rare (none in the configs[4] pool), and a
-// workgroup per image -- each asking for ~74 KiB of LDS while the chunk
-// decode and the unfilter hold most of it -- kept 3-10 ms of mostly empty
-// workgroups waiting to be dispatched on every batch's critical path.
+// mode 1 runs on up to one workgroup per CU that claim list entries from a
+// work counter (BatchFlags::png_next) until the list is exhausted: the
+// images the chunked path gave up on are rare (none in the configs[4] pool),
+// and a workgroup per image -- each asking for ~41 KiB of LDS while the
+// chunk decode and the unfilter hold most of it -- kept 3-10 ms of mostly
+// empty workgroups waiting to be dispatched on every batch's critical path.
+// A batch whose streams the chunked path cannot start in (stored or
+// fixed-Huffman blocks only) still gets one workgroup per fallback image, up
+// to one per CU (a fixed 4 workgroups serialised such batches).
 // The wave raises its issue priority: one wave's serial chain per image, on
 // the batch's critical path, sharing its SIMD with the throughput kernels of
 // the other batches in flight (a 33 ms mask took 83 ms among them).
 __global__ __launch_bounds__(64) void k_png_inflate(ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list,
-                                                    uint32_t n, int mode) {
+                                                    uint32_t n, int mode, BatchFlags *flags) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
   InflateSmem &sm = *reinterpret_cast<InflateSmem *>(smem_raw);
+  __shared__ uint32_t claim;
   __builtin_amdgcn_s_setprio(3);
-  const uint32_t stride = mode == 1 ? gridDim.x : n;  // modes 0 / 2: one image per workgroup
-  for (uint32_t i = blockIdx.x; i < n; i += stride) {
+  if (mode != 1) {  // modes 0 / 2: one image per workgroup
+    ImageDesc &im = imgs[list[blockIdx.x].image];
+    const PngDesc &pd = im.png;
+    const bool take = mode == 0 ? pd.nchunks == 0 : !(pd.nchunks && !pd.serial);
+    if (take) inflate_image(sm, im);
+    return;
+  }
+  for (;;) {  // every workgroup exits once the counter passes n
+    if (threadIdx.x == 0) claim = atomicAdd(&flags->png_next, 1u);
+    __syncthreads();
+    const uint32_t i = claim;
+    __syncthreads();
+    if (i >= n) return;
     ImageDesc &im = imgs[list[i].image];
     const PngDesc &pd = im.png;
-    const bool take = mode == 0 ? pd.nchunks == 0 : mode == 1 ? (pd.nchunks && pd.serial) : !(pd.nchunks && !pd.serial);
-    if (!take) continue;
+    if (!(pd.nchunks && pd.serial)) continue;
     inflate_image(sm, im);
     __syncthreads();
   }
@@ -1713,16 +1728,17 @@ __global__ __launch_bounds__(256) void k_alpha(const ImageDesc *__restrict__ img
 void launch_png_gather(hipStream_t st, const GatherJob *jobs, const WgItem *list, uint32_t nwg) {
   if (nwg) hipLaunchKernelGGL(k_png_gather, dim3(nwg), dim3(256), 0, st, jobs, list);
 }
-void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, int mode) {
+void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, int mode,
+                        BatchFlags *flags, uint32_t ncu) {
   static bool attr = false;  // > 64 KiB of dynamic LDS
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)k_png_inflate, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)sizeof(InflateSmem));
     attr = true;
   }
-  const uint32_t grid = mode == 1 ? std::min<uint32_t>(nwg, 4u) : nwg;
+  const uint32_t grid = mode == 1 ? std::min<uint32_t>(nwg, ncu) : nwg;
   if (grid)
-    hipLaunchKernelGGL(k_png_inflate, dim3(grid), dim3(64), sizeof(InflateSmem), st, imgs, list, nwg, mode);
+    hipLaunchKernelGGL(k_png_inflate, dim3(grid), dim3(64), sizeof(InflateSmem), st, imgs, list, nwg, mode, flags);
 }
 void launch_inf_find(hipStream_t st, const ImageDesc *imgs, InfChunk *ch, const WgItem *list, uint32_t nwg,
                      uint32_t stage3) {

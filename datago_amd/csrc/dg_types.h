@@ -380,7 +380,7 @@ struct BatchFlags {
   uint32_t write_mismatch;  // k_huff_write exit != next subsequence's input
   uint32_t sync_iters_max;  // longest intra-workgroup sync loop
   uint32_t idct_late;       // fused IDCT: blocks k_huff_write left to k_idct_list (entries in idct_list)
-  uint32_t pad0;
+  uint32_t png_next;        // k_png_inflate mode 1: next list entry a workgroup claims
   uint64_t wgtime;          // debug: device array of {start, end} s_memrealtime per workgroup, 0 = off
   uint32_t wgtime_write;    // first record of k_huff_write's workgroups
   uint32_t debug;           // test switches (kDbg*), kept across resync rounds

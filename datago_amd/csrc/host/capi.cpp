@@ -130,9 +130,12 @@ struct CtxUse {
 
 }  // namespace
 
-#define DG_USE(ctx, fail)  \
-  CtxUse use_(ctx);        \
-  if (!use_.ok) return fail
+#define DG_USE(ctx, fail)                                             \
+  CtxUse use_(ctx);                                                   \
+  if (!use_.ok) {                                                     \
+    dg::set_error(ctx ? "context already destroyed" : "null context"); \
+    return fail;                                                      \
+  }
 
 extern "C" {
 
@@ -386,13 +389,19 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
 }
 
 dg_status dg_ctx_set_option(dg_ctx *ctx, const char *key, int64_t value) {
-  if (!key) return DG_ERR_INVALID;
+  if (!key) {
+    dg::set_error("dg_ctx_set_option: null key");
+    return DG_ERR_INVALID;
+  }
   DG_USE(ctx, DG_ERR_INVALID);
   return ctx->c->set_option(key, value);
 }
 
 int64_t dg_ctx_get_stat(dg_ctx *ctx, const char *key) {
-  if (!key) return -1;
+  if (!key) {
+    dg::set_error("dg_ctx_get_stat: null key");
+    return -1;
+  }
   DG_USE(ctx, -1);
   return ctx->c->get_stat(key);
 }

@@ -367,36 +367,43 @@ static uint32_t h_mfma_steps(const ResizePass &ps) {
   return window <= 64.0 ? 1u : (window <= 128.0 ? 2u : 0u);
 }
 
+// A rejected option names itself, the value and the accepted range in
+// dg_last_error (the range as the condition that rejects it).
+static dg_status opt_error(const std::string &k, int64_t v, const std::string &why) {
+  set_error("dg_ctx_set_option(\"" + k + "\", " + std::to_string(v) + "): " + why);
+  return DG_ERR_INVALID;
+}
+
 dg_status Context::set_option(const std::string &k, int64_t v) {
   if (k == "sub_bits") {
-    if (v != 0 && (v < 64 || v > 65536 || (v & (v - 1)))) return DG_ERR_INVALID;  // power of two
+    if (v != 0 && (v < 64 || v > 65536 || (v & (v - 1)))) return opt_error(k, v, "valid unless v != 0 && (v < 64 || v > 65536 || (v & (v - 1)))");  // power of two
     sub_bits_ = (uint32_t)v;
     return DG_OK;
   }
   if (k == "sub_auto") {
-    if (v < 1024 || v > 65536 || (v & (v - 1))) return DG_ERR_INVALID;
+    if (v < 1024 || v > 65536 || (v & (v - 1))) return opt_error(k, v, "valid unless v < 1024 || v > 65536 || (v & (v - 1))");
     sub_auto_ = (uint32_t)v;
     return DG_OK;
   }
   if (k == "lead_bits") {
-    if (v < -1 || v > (1 << 20)) return DG_ERR_INVALID;
+    if (v < -1 || v > (1 << 20)) return opt_error(k, v, "valid unless v < -1 || v > (1 << 20)");
     lead_bits_ = v;
     return DG_OK;
   }
   if (k == "coalesce_max") {
-    if (v < 1 || v > 4096) return DG_ERR_INVALID;
+    if (v < 1 || v > 4096) return opt_error(k, v, "valid unless v < 1 || v > 4096");
     std::lock_guard<std::mutex> lk(cmu_);
     coalesce_max_ = (int)v;
     return DG_OK;
   }
   if (k == "coalesce_inflight") {  // dg_decode_one: coalesced baseline batches in flight (0 = "slots")
-    if (v < 0 || v > kMaxInflight) return DG_ERR_INVALID;
+    if (v < 0 || v > kMaxInflight) return opt_error(k, v, "valid unless v < 0 || v > " + std::to_string(kMaxInflight));
     std::lock_guard<std::mutex> lk(cmu_);
     coalesce_inflight_ = (int)v;
     return DG_OK;
   }
   if (k == "coalesce_us") {
-    if (v < 0 || v > 1000000) return DG_ERR_INVALID;
+    if (v < 0 || v > 1000000) return opt_error(k, v, "valid unless v < 0 || v > 1000000");
     std::lock_guard<std::mutex> lk(cmu_);
     coalesce_us_ = (int)v;
     return DG_OK;
@@ -414,10 +421,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "coef_cache_mb") {  // Lanczos table cache arena (0: off); takes effect at the next reset
-    if (v < 0 || v > 65536) return DG_ERR_INVALID;
+    if (v < 0 || v > 65536) return opt_error(k, v, "valid unless v < 0 || v > 65536");
     std::lock_guard<std::mutex> lk(mu_);
     for (const Slot &o : slots_)
-      if (o.batch && !o.batch->done && o.batch->uses_ccache) return DG_ERR_INVALID;  // not while tables are in use
+      if (o.batch && !o.batch->done && o.batch->uses_ccache) return opt_error(k, v, "not while a batch in flight uses the table cache");  // not while tables are in use
     ccache_cap_ = (size_t)v << 20;
     ccache_index_clear();
     ccache_.clear();
@@ -429,18 +436,18 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "entropy_prio") {  // wave issue priority (s_setprio) of the entropy kernels, 0-3
-    if (v < 0 || v > 3) return DG_ERR_INVALID;
+    if (v < 0 || v > 3) return opt_error(k, v, "valid unless v < 0 || v > 3");
     entropy_prio_ = (int)v;
     return DG_OK;
   }
   if (k == "max_device_mb") {  // device memory budget of the context (0: none)
-    if (v < 0) return DG_ERR_INVALID;
+    if (v < 0) return opt_error(k, v, "valid unless v < 0");
     max_dev_bytes_ = (size_t)v << 20;
     budget_slots_ = kMaxInflight;
     return DG_OK;
   }
   if (k == "slots") {
-    if (v < 1 || v > (int64_t)kMaxInflight) return DG_ERR_INVALID;
+    if (v < 1 || v > (int64_t)kMaxInflight) return opt_error(k, v, "valid unless v < 1 || v > " + std::to_string(kMaxInflight));
     nslots_ = (int)v;
     next_slot_ %= nslots_;
     return DG_OK;
@@ -455,12 +462,12 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "prog_lanes") {  // dg_decode_one: progressive batches in flight on the progressive slots; 0: mixed in
-    if (v < 0 || v > kProgSlots) return DG_ERR_INVALID;
+    if (v < 0 || v > kProgSlots) return opt_error(k, v, "valid unless v < 0 || v > " + std::to_string(kProgSlots));
     prog_lanes_ = (int)v;
     return DG_OK;
   }
   if (k == "prog_queue") {  // progressive slots' streams: 0 plain, 1 high / 2 low priority, 3 CU-masked
-    if (v < 0 || v > 3) return DG_ERR_INVALID;
+    if (v < 0 || v > 3) return opt_error(k, v, "valid unless v < 0 || v > 3");
     {
       std::lock_guard<std::mutex> lk(pmu_);
       if (!pagg_.empty()) flush_pagg_locked();
@@ -477,7 +484,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return make_prog_streams();
   }
   if (k == "slot_queue") {  // baseline slots' streams: 0 plain, 1 high / 2 low priority, 3 CU-masked (own queues)
-    if (v < 0 || v > 3) return DG_ERR_INVALID;
+    if (v < 0 || v > 3) return opt_error(k, v, "valid unless v < 0 || v > 3");
     std::lock_guard<std::mutex> lk(mu_);
     for (int j = 0; j < kMaxInflight; j++) {
       Slot &sl = slots_[j];
@@ -490,7 +497,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return make_streams(0, kMaxInflight, slot_queue_, 0, side_queue_);
   }
   if (k == "side_queue") {  // the baseline slots' side streams: -1 as slot_queue, else a slot_queue mode
-    if (v < -1 || v > 3) return DG_ERR_INVALID;
+    if (v < -1 || v > 3) return opt_error(k, v, "valid unless v < -1 || v > 3");
     std::lock_guard<std::mutex> lk(mu_);
     for (int j = 0; j < kMaxInflight; j++) {
       Slot &sl = slots_[j];
@@ -503,7 +510,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return make_streams(0, kMaxInflight, slot_queue_, 0, side_queue_);
   }
   if (k == "prog_cus") {  // prog_queue 3: CUs the progressive streams may use (0 = all); set before prog_queue
-    if (v < 0 || v > 4096) return DG_ERR_INVALID;
+    if (v < 0 || v > 4096) return opt_error(k, v, "valid unless v < 0 || v > 4096");
     prog_cus_ = (int)v;
     return DG_OK;
   }
@@ -512,12 +519,12 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "prog_batch") {  // progressive aggregate: launched once it holds this many images
-    if (v < 1 || v > 65536) return DG_ERR_INVALID;
+    if (v < 1 || v > 65536) return opt_error(k, v, "valid unless v < 1 || v > 65536");
     prog_batch_ = (int)v;
     return DG_OK;
   }
   if (k == "prog_flush_us") {  // ... or once it is this old at a submit / poll / wait_ready
-    if (v < 0 || v > 100000000) return DG_ERR_INVALID;
+    if (v < 0 || v > 100000000) return opt_error(k, v, "valid unless v < 0 || v > 100000000");
     prog_flush_us_ = (int)v;
     return DG_OK;
   }
@@ -526,7 +533,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "write_pair") {  // k_huff_write: up to v more AC symbols per step from the same peek (0..3)
-    if (v < 0 || v > 3) return DG_ERR_INVALID;
+    if (v < 0 || v > 3) return opt_error(k, v, "valid unless v < 0 || v > 3");
     write_pair_ = (int)v;
     return DG_OK;
   }
@@ -539,7 +546,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "prog_chain") {  // chain dependency groups costing <= this % of the batch's longest scan (0: off)
-    if (v < 0 || v > 100000) return DG_ERR_INVALID;
+    if (v < 0 || v > 100000) return opt_error(k, v, "valid unless v < 0 || v > 100000");
     prog_chain_ = (int)v;
     return DG_OK;
   }
@@ -560,7 +567,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "hb_bands") {  // band H kernel: 8-row bands per workgroup
-    if (v < 1 || v > 64) return DG_ERR_INVALID;
+    if (v < 1 || v > 64) return opt_error(k, v, "valid unless v < 1 || v > 64");
     hb_bands_ = (uint32_t)v;
     return DG_OK;
   }
@@ -598,7 +605,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "copy_threads") {  // host threads for the output copies of a host-out batch (default 8)
-    if (v < 1 || v > 64) return DG_ERR_INVALID;
+    if (v < 1 || v > 64) return opt_error(k, v, "valid unless v < 1 || v > 64");
     copy_threads_ = (int)v;
     return DG_OK;
   }
@@ -607,32 +614,37 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "decode_semantics") {  // 0: libjpeg-turbo (pinned), 1: zune-jpeg 0.5.12 restated (unpinned)
-    if (v != 0 && v != 1) return DG_ERR_INVALID;
+    if (v != 0 && v != 1) return opt_error(k, v, "valid unless v != 0 && v != 1");
     decode_sem_ = (int)v;
     return DG_OK;
   }
   if (k == "small_coded") {  // batches under this many coded bytes take sub_small / lead_small (0 = off)
-    if (v < 0) return DG_ERR_INVALID;
+    if (v < 0) return opt_error(k, v, "valid unless v < 0");
     small_coded_ = (uint64_t)v;
     return DG_OK;
   }
   if (k == "sub_small") {
-    if (v < 64 || v > 65536 || (v & (v - 1))) return DG_ERR_INVALID;
+    if (v < 64 || v > 65536 || (v & (v - 1))) return opt_error(k, v, "valid unless v < 64 || v > 65536 || (v & (v - 1))");
     sub_small_ = (uint32_t)v;
     return DG_OK;
   }
   if (k == "lead_small") {
-    if (v < 0 || v > (1 << 16)) return DG_ERR_INVALID;
+    if (v < 0 || v > (1 << 16)) return opt_error(k, v, "valid unless v < 0 || v > (1 << 16)");
     lead_small_ = (uint32_t)v;
     return DG_OK;
   }
+  if (k == "v_tile") {  // V pass output rows per column tile (k_resize_vt); 0: one thread per 16 output bytes
+    if (v != 0 && v != 2 && v != 4 && v != 8) return opt_error(k, v, "valid: 0, 2, 4, 8");
+    v_tile_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "v_units") {  // k_resize_v: 256-unit strides per workgroup item
-    if (v < 1 || v > 8) return DG_ERR_INVALID;
+    if (v < 1 || v > 8) return opt_error(k, v, "valid unless v < 1 || v > 8");
     v_units_ = (uint32_t)v;
     return DG_OK;
   }
   if (k == "lead_big") {  // auto lead-in of images with >= 4-block MCUs (4:2:0), bits
-    if (v < 0 || v > (1 << 16)) return DG_ERR_INVALID;
+    if (v < 0 || v > (1 << 16)) return opt_error(k, v, "valid unless v < 0 || v > (1 << 16)");
     lead_big_ = (uint32_t)v;
     return DG_OK;
   }
@@ -641,22 +653,22 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "meta_pull") {  // the GPU reads from page-locked staging: 1 the descriptors, 2 also host inputs
-    if (v < 0 || v > 2) return DG_ERR_INVALID;
+    if (v < 0 || v > 2) return opt_error(k, v, "valid unless v < 0 || v > 2");
     meta_pull_ = (int)v;
     return DG_OK;
   }
   if (k == "plan_threads") {  // host threads parsing a submission's headers (1 = the caller only)
-    if (v < 1 || v > 64) return DG_ERR_INVALID;
+    if (v < 1 || v > 64) return opt_error(k, v, "valid unless v < 1 || v > 64");
     plan_threads_ = (int)v;
     return DG_OK;
   }
   if (k == "inf_stage3") {  // k_inf_find: Kraft survivors queued per full header check round
-    if (v != 8 && v != 16 && v != 32 && v != 64) return DG_ERR_INVALID;
+    if (v != 8 && v != 16 && v != 32 && v != 64) return opt_error(k, v, "valid unless v != 8 && v != 16 && v != 32 && v != 64");
     inf_stage3_ = (uint32_t)v;
     return DG_OK;
   }
   if (k == "inf_chunk") {  // compressed bytes per chunk of the chunk-parallel inflate
-    if (v < 4096 || v > 65536 || (v & (v - 1))) return DG_ERR_INVALID;
+    if (v < 4096 || v > 65536 || (v & (v - 1))) return opt_error(k, v, "valid unless v < 4096 || v > 65536 || (v & (v - 1))");
     inf_chunk_ = (uint32_t)v;
     return DG_OK;
   }
@@ -669,17 +681,17 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "sub_density") {  // bits-per-block threshold for shorter subsequences (0 = off)
-    if (v < 0 || v > 4096) return DG_ERR_INVALID;
+    if (v < 0 || v > 4096) return opt_error(k, v, "valid unless v < 0 || v > 4096");
     sub_density_ = (double)v;
     return DG_OK;
   }
   if (k == "uf_per_cu") {  // PNG unfilter: persistent workers per CU at most (0: as many as the LDS holds)
-    if (v < 0 || v > 16) return DG_ERR_INVALID;
+    if (v < 0 || v > 16) return opt_error(k, v, "valid unless v < 0 || v > 16");
     uf_per_cu_ = (int)v;
     return DG_OK;
   }
   if (k == "uf_units") {  // PNG unfilter: filter units per lane per step (1: half the LDS per worker)
-    if (v < 1 || v > 2) return DG_ERR_INVALID;
+    if (v < 1 || v > 2) return opt_error(k, v, "valid unless v < 1 || v > 2");
     uf_units_ = (uint32_t)v;
     return DG_OK;
   }
@@ -690,7 +702,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
                             // 17 7/4, 18 8/5, 19 8/4; 20 / 21 / 22 = 17 / 4 / 5 with the register buffer;
                             // 23 / 24 / 25 / 26 / 27 = 16 with a 4 / 12 / 16 / 24 / 32-word buffer;
                             // 28 = 20 with a 16-word buffer
-    if (v < 0 || v > 28 || v == 10) return DG_ERR_INVALID;
+    if (v < 0 || v > 28 || v == 10) return opt_error(k, v, "valid unless v < 0 || v > 28 || v == 10");
     inf_decode_ = (uint32_t)v;
     return DG_OK;
   }
@@ -707,7 +719,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     return DG_OK;
   }
   if (k == "dec_strips") {
-    if (v < 1 || v > 4096) return DG_ERR_INVALID;
+    if (v < 1 || v > 4096) return opt_error(k, v, "valid unless v < 1 || v > 4096");
     dec_strips_ = (uint32_t)v;
     return DG_OK;
   }
@@ -715,7 +727,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     debug_flags_ = (int)v;
     return DG_OK;
   }
-  return DG_ERR_INVALID;
+  return opt_error(k, v, "unknown option");
 }
 
 int64_t Context::get_stat(const std::string &k) {
@@ -775,6 +787,7 @@ int64_t Context::get_stat(const std::string &k) {
   }
   if (k == "hpool") return (int64_t)hpool_.size();
   if (k == "qpool") return (int64_t)qpool_.size();
+  set_error("dg_ctx_get_stat(\"" + k + "\"): unknown statistic");
   return -1;
 }
 
@@ -2036,6 +2049,20 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       if (o.batch && !o.batch->done && finish(o)) continue;
       free_slot_buffers(o);
     }
+    // the Lanczos table arena counts too (256 MiB by default): with every
+    // other batch finished only this one could read it
+    bool cache_busy = b.uses_ccache;
+    for (const Slot &o : slots_)
+      if (&o != &sl && o.batch && !o.batch->done && o.batch->uses_ccache) cache_busy = true;
+    if (!cache_busy && d_ccache_.p) {
+      ccache_index_clear();
+      ccache_.clear();
+      ccache_off_ = 0;
+      ccache_full_ = false;
+      hipFree(d_ccache_.p);
+      d_ccache_.p = nullptr;
+      d_ccache_.cap = 0;
+    }
   }
   if (st) return st;
   sl.coef_bytes = CO.off;
@@ -2262,6 +2289,11 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
           for (uint32_t it = 0; it < cnt; it++) hm[s / 2][fused][ks - 1].push_back({I, it});
         else
           for (uint32_t it = 0; it < cnt; it++) hb[s / 2][fused][cls].push_back({I, it});
+      } else if (v_tile_ && (ps.src_stride & 15) == 0) {  // k_resize_vt: 4 waves of (R rows x 1 KiB) tiles
+        const uint32_t units = (ps.width * ps.C + 15) / 16;
+        const uint32_t tiles = (units + 63) / 64 * ((ps.rows + v_tile_ - 1) / v_tile_);
+        for (uint32_t it = 0; it < tiles; it += 4) b.lists[s == 1 ? L_RVT1 : L_RVT3].push_back({I, it});
+        b.v_tile = v_tile_;
       } else {
         uint32_t cnt = (ps.width * ps.C + 15) / 16 * ps.rows;
         for (uint32_t it = 0; it < cnt; it += 256 * v_units_) b.lists[L_RH0 + s].push_back({I, it});
@@ -2659,17 +2691,17 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
       if (beside) {
         HIPCHK(hipEventRecord(sl.ev_png0, sl.st));
         HIPCHK(hipStreamWaitEvent(sl.side, sl.ev_png0, 0));
-        launch_png_inflate(sl.side, dm, lst(L_PNG), cnt(L_PNG), 0);
+        launch_png_inflate(sl.side, dm, lst(L_PNG), cnt(L_PNG), 0, fl, ncu_);
         HIPCHK(hipEventRecord(sl.ev_png1, sl.side));
       }
       InfChunk *ich = (InfChunk *)(M + b.ichunk_off);
       launch_inf_find(sl.st, dd, ich, lst(L_INF_FIND), cnt(L_INF_FIND), inf_stage3_);
       launch_inf_decode(sl.st, dd, ich, (uint32_t)b.ichunks.size(), inf_decode_);
       launch_inf_resolve(sl.st, dm, ich, lst(L_INF_RES), cnt(L_INF_RES));
-      launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG), beside ? 1 : 2);
+      launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG), beside ? 1 : 2, fl, ncu_);
       if (beside) HIPCHK(hipStreamWaitEvent(sl.st, sl.ev_png1, 0));
     } else {
-      launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG), 2);  // serial: every stream
+      launch_png_inflate(sl.st, dm, lst(L_PNG), cnt(L_PNG), 2, fl, ncu_);  // serial: every stream
     }
   }
   if (next()) return DG_ERR_DEVICE;
@@ -2775,6 +2807,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV1), cnt(L_RV1), 1, v_units_);
+  launch_resize_vt(sl.st, dd, lst(L_RVT1), cnt(L_RVT1), 1, b.v_tile);
   launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_hm(sl.st, dd, lst(L_RM2), b.hmclass[1], 2);
@@ -2782,6 +2815,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3, v_units_);
+  launch_resize_vt(sl.st, dd, lst(L_RVT3), cnt(L_RVT3), 3, b.v_tile);
   launch_alpha(sl.st, dd, lst(L_ALPHA2), cnt(L_ALPHA2), 2 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_copy(sl.st, dd, lst(L_COPY), cnt(L_COPY));
@@ -2843,6 +2877,15 @@ void Context::fail_batch(Slot &sl, dg_status st) {
   for (int i = 0; i < b.n && i < (int)b.mptr.size(); i++)
     if (b.mptr[i] && b.mptr[i]->status == DG_OK) b.mptr[i]->status = st;
   for (size_t i = 0; i < b.pub.size(); i++) *b.pub[i] = b.local_meta[i];
+  // Lanczos tables this batch was producing never become ready: retire their
+  // keys (the index slot stays as a tombstone, probes pass it) so that a later
+  // batch produces them again instead of recomputing its own copy every time
+  // until the arena starts over
+  for (const Batch::CProd &pr : b.ccache_prod)
+    if (pr.entry < (int)ccache_.size() && !ccache_[pr.entry].ready) {
+      ccache_[pr.entry].key.ksize = 0xFFFFFFFFu;
+      ccache_[pr.entry].key.in_size = 0;
+    }
   b.done = true;
 }
 
@@ -3178,18 +3221,21 @@ bool Context::pagg_stale_locked() {
 dg_status Context::submit_split(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs,
                                 const size_t *lens, const int32_t *forced, uint8_t *const *outs,
                                 const uint64_t *caps, dg_payload_meta *const *mptrs, bool host_io,
-                                std::vector<uint64_t> &tickets, bool prog, bool defer_meta) {
+                                std::vector<uint64_t> &tickets, bool prog, bool defer_meta, bool whole_failed) {
   if (n <= 0) return DG_OK;
   int slot = -1;
   if (prog) {
     std::lock_guard<std::mutex> lk(mu_);
     slot = pick_prog_slot();
   }
-  uint64_t t = 0;
-  dg_status st = submit(n, h_srcs, d_srcs, lens, forced, outs, caps, nullptr, host_io, &t, mptrs, slot, defer_meta);
-  if (st != kNeedSplit) {
-    if (!st) tickets.push_back(t);
-    return st;
+  dg_status st = kNeedSplit;
+  if (!whole_failed) {  // (the caller already planned the whole submission and saw kNeedSplit)
+    uint64_t t = 0;
+    st = submit(n, h_srcs, d_srcs, lens, forced, outs, caps, nullptr, host_io, &t, mptrs, slot, defer_meta);
+    if (st != kNeedSplit) {
+      if (!st) tickets.push_back(t);
+      return st;
+    }
   }
   if (n == 1) {  // one image larger than the device budget: that sample fails, not the worker
     dg_payload_meta &m = *mptrs[0];
@@ -3204,6 +3250,10 @@ dg_status Context::submit_split(int n, const uint8_t *const *h_srcs, const uint8
   const int h = n / 2;
   st = submit_split(h, h_srcs, d_srcs, lens, forced, outs, caps, mptrs, host_io, tickets, prog, defer_meta);
   if (st) return st;
+  if (debug_flags_ & (1 << 24)) {  // test switch: the second part fails after the first launched
+    set_error("forced failure of a split submission's second part (debug_flags bit 24)");
+    return DG_ERR_DEVICE;
+  }
   return submit_split(n - h, h_srcs + h, d_srcs ? d_srcs + h : nullptr, lens + h, forced ? forced + h : nullptr,
                       outs + h, caps + h, mptrs + h, host_io, tickets, prog, defer_meta);
 }
@@ -3243,6 +3293,17 @@ dg_status Context::flush_pagg_locked() {
   return st;
 }
 
+// A split submission failed part-way: the parts that launched
+// before the failure still write into the caller's outputs (and a host-out
+// part copies to them at its finish), so they complete before the error is
+// returned -- the caller may free its buffers as soon as this call fails.
+dg_status Context::fail_split_parts(const std::vector<uint64_t> &launched, dg_status st) {
+  const std::string why = g_last_error;
+  for (uint64_t t : launched) wait(t);
+  set_error(why);
+  return st;
+}
+
 dg_status Context::submit_user(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
                                const int32_t *forced, uint8_t *const *outs, const uint64_t *caps,
                                dg_payload_meta *metas, bool host_io, uint64_t *ticket) {
@@ -3260,8 +3321,8 @@ dg_status Context::submit_user(int n, const uint8_t *const *h_srcs, const uint8_
       std::vector<dg_payload_meta *> mp(n);
       for (int i = 0; i < n; i++) mp[i] = &metas[i];
       SplitRec rec;
-      st = submit_split(n, h_srcs, d_srcs, lens, forced, outs, caps, mp.data(), host_io, rec.tbs, false, false);
-      if (st) return st;
+      st = submit_split(n, h_srcs, d_srcs, lens, forced, outs, caps, mp.data(), host_io, rec.tbs, false, false, true);
+      if (st) return fail_split_parts(rec.tbs, st);
       std::lock_guard<std::mutex> lk(pmu_);
       {
         std::lock_guard<std::mutex> lk2(mu_);
@@ -3297,7 +3358,7 @@ dg_status Context::submit_user(int n, const uint8_t *const *h_srcs, const uint8_
     }
     dg_status st = submit_split((int)h.size(), h.data(), host_io ? nullptr : d.data(), ln.data(), fb.data(),
                                 ou.data(), cp.data(), mp.data(), host_io, rec.tbs, false, false);
-    if (st) return st;
+    if (st) return fail_split_parts(rec.tbs, st);
   }
   std::lock_guard<std::mutex> lk(pmu_);
   if (!pagg_.empty() && pagg_host_ != host_io) flush_pagg_locked();  // an aggregate is host- or device-fed

@@ -85,6 +85,7 @@ struct Batch {
   bool any_png = false, any_alpha = false, any_enc = false;
   bool any_fused = false;  // some image's IDCT runs inside k_huff_write
   uint32_t idct_cap = 0;   // entries of BatchFlags::idct_list
+  uint32_t v_tile = 0;     // rows per k_resize_vt tile the V lists were built for
   bool stage_on = false;  // decode-once staging (option "entropy_once")
   uint32_t max_slots = 1; // largest Huffman table count of an image (dynamic LDS of k_huff_sync/fix)
   uint32_t max_ac = 0;    // most distinct AC tables of a baseline JPEG (k_huff_sync multi-symbol lookups)
@@ -170,6 +171,7 @@ enum ListId {
   L_RHV,                                                    // fused first H + V pass (k_resize_hv)
   L_DEC,                                                    // IDCT + colour + first H pass (k_band_dec)
   L_RM0, L_RM2,                                             // band H passes on the matrix cores (k_resize_hm)
+  L_RVT1, L_RVT3,                                           // V passes on column tiles (k_resize_vt)
   L_COUNT
 };
 static_assert((int)L_COUNT <= 40, "Batch::lists");
@@ -248,11 +250,13 @@ class Context {
   bool pagg_stale_locked();       // the open aggregate is older than prog_flush_us
   // submit(), split into halves while a part's plan exceeds the device
   // budget (option "max_device_mb"); tickets of the parts that run are
-  // appended.  prog: the parts go to progressive slots.
+  // appended.  prog: the parts go to progressive slots.  whole_failed: the
+  // caller planned all n already and got kNeedSplit (start with the halves).
   dg_status submit_split(int n, const uint8_t *const *h_srcs, const uint8_t *const *d_srcs, const size_t *lens,
                          const int32_t *forced, uint8_t *const *outs, const uint64_t *caps,
                          dg_payload_meta *const *mptrs, bool host_io, std::vector<uint64_t> &tickets, bool prog,
-                         bool defer_meta);
+                         bool defer_meta, bool whole_failed = false);
+  dg_status fail_split_parts(const std::vector<uint64_t> &launched, dg_status st);
   size_t dev_footprint(const Slot *except = nullptr) const;  // device bytes this context holds
   bool budget_fit(Slot &self, size_t rs, size_t rc, size_t ri);  // mu_ held: room for self's next batch
   void free_slot_buffers(Slot &o);
@@ -428,6 +432,7 @@ class Context {
   uint32_t lead_big_ = 4096;        // option "lead_big" (6144 -> 4096 with 8192-bit ranges: +1.3%, profiles/r04/lead_big)
   uint64_t small_coded_ = 0;        // option "small_coded" (0: off)
   uint32_t sub_small_ = 512, lead_small_ = 1024;  // options "sub_small", "lead_small"
+  uint32_t v_tile_ = 4;             // option "v_tile": V pass on R-row column tiles (k_resize_vt<R>; 0 = k_resize_v)
   uint32_t v_units_ = 2;            // option "v_units" (profiles/r04/v_units: 1 / 2 / 4 -> V traffic 1.95 / ? / 3.91 GB per batch)
   static constexpr int kPlanGrain = 32;  // images per planning work piece
   std::unique_ptr<HostPool> plan_pool_;

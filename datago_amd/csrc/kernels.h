@@ -59,6 +59,8 @@ void launch_resize_hm(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
 void launch_resize_hv(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2]);
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage,
                      uint32_t vunits);
+void launch_resize_vt(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage,
+                      uint32_t rows);
 // k_band_dec (dg_band.hip): IDCT + upsampling + colour + the first H pass of images with pass[0].mode &
 // kHDecode; list = ncls[0] items of the 320-pixel class, then ncls[1] of the 640-pixel class
 void launch_band_dec(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2],
@@ -88,7 +90,8 @@ namespace dg {
 void launch_png_gather(hipStream_t st, const GatherJob *jobs, const WgItem *list, uint32_t nwg);
 // one 64-thread workgroup (one wave) per image
 // mode: 0 unchunked streams only, 1 chunked-path fallbacks only, 2 both
-void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, int mode);
+void launch_png_inflate(hipStream_t st, ImageDesc *imgs, const WgItem *list, uint32_t nwg, int mode,
+                        BatchFlags *flags, uint32_t ncu);
 // tasks: (image, pass << 24 | band) in ticket order; flags: ntasks + 1 zeroed words;
 // dbg bit 0: band 1 of every plane times out on its first wait (test switch)
 void launch_png_unfilter(hipStream_t st, ImageDesc *imgs, const WgItem *tasks, uint32_t ntasks, uint32_t *flags,

@@ -2593,6 +2593,126 @@ __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ 
   }
 }
 
+// Vertical pass on column tiles (option "v_tile" = R).
+// One wave owns R consecutive output rows x 64 16-byte units (1 KiB) of one
+// pass and walks the source rows their windows span once, in pairs: each
+// source row is loaded once per tile instead of once per output row that
+// uses it (k_resize_v re-loads all n taps for every output row and left the
+// overlap to L2), and the byte-pair perms of a source-row pair are shared by
+// the R outputs.  The R x pairs weight table (two i16 taps per dword, zero
+// outside an output's window) is built per wave in LDS, in windows of
+// kVtWCap / R pairs; a pair whose weights are both zero for an output is a
+// scalar branch (the rows are wave-uniform).  Same arithmetic as k_resize_v
+// (bias, v_dot2_i32_i16 over (row i, row i + 1) pairs, clip_shift), so the
+// bytes are identical: a tap pair's zero weight adds exactly 0.
+constexpr uint32_t kVtWCap = 256;  // packed weight pairs per wave in LDS
+
+template <int R>
+__global__ __launch_bounds__(256) void k_resize_vt(const ImageDesc *__restrict__ imgs,
+                                                   const WgItem *__restrict__ list, int stage) {
+  __shared__ uint32_t wtab[4][kVtWCap];
+  const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
+  const ResizePass &ps = imgs[it.image].pass[stage];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t rowbytes = ps.width * ps.C;
+  const uint32_t units = (rowbytes + 15) / 16;
+  const uint32_t chunks = (units + 63) / 64;
+  const uint32_t groups = (ps.rows + R - 1) / R;
+  const uint32_t w = it.item0 + wv;  // this wave's tile
+  if (w >= chunks * groups) return;  // (wave-uniform)
+  const uint32_t g = w / chunks, c = w - g * chunks;
+  const uint32_t y0 = g * R;
+  const uint32_t nr = ps.rows - y0 < (uint32_t)R ? ps.rows - y0 : (uint32_t)R;
+  const uint32_t u = c * 64 + lane;
+  const uint32_t b0 = (u < units ? u : units - 1) * 16;  // lanes past the row load a valid unit, store nothing
+  const uint32_t yc0 = y0 + ps.out0;                      // coefficient row of output row y0
+  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds);
+  const DG_GLOBAL int16_t *kbase = gp<const int16_t>(ps.coef);
+  const int32_t prec = ps.precision, bias = 1 << (prec - 1);
+  // the span of source rows the tile's windows cover
+  int32_t lo = 0x7FFFFFFF, hi = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if ((uint32_t)r < nr) {
+      const int32_t s = bounds[2 * (yc0 + r)], n = bounds[2 * (yc0 + r) + 1];
+      lo = s < lo ? s : lo;
+      hi = s + n > hi ? s + n : hi;
+    }
+  }
+  const uint32_t npair = (uint32_t)(hi - lo + 1) >> 1;
+  const uint32_t pwin = kVtWCap / R;  // pairs per weight-table window
+  int32_t a[R][16];
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int j = 0; j < 16; j++) a[r][j] = bias;
+  const size_t sstride = ps.src_stride;
+  const DG_GLOBAL uint8_t *src = gp<const uint8_t>(ps.src) + (size_t)(lo - (int32_t)ps.row0) * sstride + b0;
+  uint32_t *wt = wtab[wv];
+  for (uint32_t p0 = 0; p0 < npair; p0 += pwin) {
+    const uint32_t pn = npair - p0 < pwin ? npair - p0 : pwin;
+    __builtin_amdgcn_wave_barrier();  // the previous window's reads are issued (one wave: LDS in order)
+    for (uint32_t e = lane; e < (uint32_t)R * pn; e += 64) {
+      const uint32_t r = e / pn, p = e - r * pn;
+      uint32_t pk = 0;
+      if (r < nr) {
+        const int32_t s = bounds[2 * (yc0 + r)], n = bounds[2 * (yc0 + r) + 1];
+        const int32_t j = lo + 2 * (int32_t)(p0 + p) - s;  // tap index of the pair's first row
+        const DG_GLOBAL int16_t *k = kbase + (size_t)(yc0 + r) * ps.ksize;
+        const uint32_t w0 = (j >= 0 && j < n) ? (uint32_t)(uint16_t)k[j] : 0u;
+        const uint32_t w1 = (j + 1 >= 0 && j + 1 < n) ? (uint32_t)(uint16_t)k[j + 1] : 0u;
+        pk = w0 | (w1 << 16);
+      }
+      wt[r * pn + p] = pk;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t p = 0; p < pn; p++) {
+      const uint32_t i = 2 * (p0 + p);  // source row lo + i (and lo + i + 1)
+      const u32x4 v0 = *(const DG_GLOBAL u32x4 *)(src + (size_t)i * sstride);
+      const u32x4 v1 = (int32_t)i + 1 < hi - lo ? *(const DG_GLOBAL u32x4 *)(src + (size_t)(i + 1) * sstride)
+                                                : u32x4{0u, 0u, 0u, 0u};
+      uint32_t pr[16];
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+          pr[4 * j + b] = __builtin_amdgcn_perm(v1[j], v0[j], 0x0C000C00u | ((4u + (uint32_t)b) << 16) | (uint32_t)b);
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const uint32_t wp = __builtin_amdgcn_readfirstlane(wt[r * pn + p]);
+        if (wp == 0u) continue;  // both taps outside output r's window (scalar branch)
+        const s16x2 wv2 = __builtin_bit_cast(s16x2, wp);
+#pragma unroll
+        for (int q = 0; q < 16; q++) a[r][q] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pr[q]), wv2, a[r][q], false);
+      }
+    }
+  }
+  if (u >= units) return;
+  const uint32_t nb = rowbytes - u * 16 < 16 ? rowbytes - u * 16 : 16;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if ((uint32_t)r >= nr) break;
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      o[j] = pack4(clip_shift(a[r][4 * j], prec), clip_shift(a[r][4 * j + 1], prec), clip_shift(a[r][4 * j + 2], prec),
+                   clip_shift(a[r][4 * j + 3], prec));
+    DG_GLOBAL uint8_t *dst = gp<uint8_t>(ps.dst) + (size_t)(y0 + r) * ps.dst_stride + u * 16;
+    if (nb == 16 && (ps.dst_stride & 15) == 0) {
+      *(DG_GLOBAL u32x4 *)dst = u32x4{o[0], o[1], o[2], o[3]};
+    } else if (nb == 16 && (ps.dst_stride & 3) == 0) {
+      DG_GLOBAL uint32_t *d = (DG_GLOBAL uint32_t *)dst;
+      d[0] = o[0];
+      d[1] = o[1];
+      d[2] = o[2];
+      d[3] = o[3];
+    } else {
+      for (uint32_t j = 0; j < nb; j++) dst[j] = (uint8_t)(o[j >> 2] >> (8 * (j & 3)));
+    }
+  }
+}
+
 // image 0.25 Rgba<u8>::blend of `f` over an opaque (128,128,128,255) pixel,
 // then its RGB: f32 arithmetic in the crate's order, truncating casts.
 // hipcc's f32 division is IEEE correctly rounded and contraction is off, so
@@ -2778,6 +2898,15 @@ void launch_resize_hv(hipStream_t st, const ImageDesc *imgs, const WgItem *list,
 void launch_resize_v(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage,
                      uint32_t vunits) {
   DG_LAUNCH(k_resize_v, nwg, st, imgs, list, stage | (int)(vunits << 8));
+}
+void launch_resize_vt(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg, int stage,
+                      uint32_t rows) {
+  if (rows == 8)
+    DG_LAUNCH(k_resize_vt<8>, nwg, st, imgs, list, stage);
+  else if (rows == 2)
+    DG_LAUNCH(k_resize_vt<2>, nwg, st, imgs, list, stage);
+  else
+    DG_LAUNCH(k_resize_vt<4>, nwg, st, imgs, list, stage);
 }
 void launch_copy(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg) {
   DG_LAUNCH(k_copy, nwg, st, imgs, list);

@@ -115,3 +115,15 @@ def test_probe_accepts_more_than_64_progressive_scans(L):
     info = _lib.ProbeInfo()
     assert L.dg_probe(d, len(d), ctypes.byref(info)) == 0
     assert info.progressive == 1 and info.gpu_supported == 1
+
+
+def test_failing_calls_set_last_error(L):
+    """dg_last_error names the failure of the call that just failed (VERDICT r5
+    item 8), also for calls that need no GPU: a null context or key."""
+    assert L.dg_ctx_set_option(None, b"slots", 4) == _lib.DG_ERR_INVALID
+    assert _lib.last_error() == "null context"
+    h = ctypes.c_void_p()
+    assert L.dg_bucket_table_build(224, 0, 0.5, 2.0, ctypes.byref(h)) == _lib.DG_ERR_INVALID
+    assert _lib.last_error() == "invalid bucket parameters"
+    assert L.dg_ctx_get_stat(None, b"batches") == -1
+    assert _lib.last_error() == "null context"

@@ -142,3 +142,29 @@ def test_budget_settles_on_fewer_slots():
     assert c.stat("budget_oom") == 0
     assert c.stat("peak_device_mb") <= budget + 16, (c.stat("peak_device_mb"), budget)
     c.close()
+
+
+def test_split_failure_waits_for_launched_parts():
+    """a budget split whose second part fails after the first
+    launched returns the error only once the launched part has finished
+    writing the caller's outputs (host-out: copied back), so the caller may
+    free its buffers as soon as the call fails; the context stays usable."""
+    datas = synth.mixed_corpus(78, 24, 256, 1200)
+    ref = _ref_ctx()
+    ref.decode_batch(datas)
+    peak = ref.stat("peak_device_mb")
+    ref.close()
+    base = _base_mb()
+    c = _ctx()
+    c.set_option("max_device_mb", base + max(8, (peak - base) // 3))
+    c.set_option("debug_flags", 1 << 24)
+    outs = [np.empty(max(c.output_size(d)[1], 1), np.uint8) for d in datas]
+    with pytest.raises(L.DgError) as e:
+        c.submit_host(datas, outs)
+    assert "second part" in str(e.value)
+    assert c.stat("budget_splits") > 0
+    del outs  # the launched part is finished: freeing the outputs is safe
+    c.set_option("debug_flags", 0)
+    got = c.decode_batch(datas)
+    assert all(s == 0 for s, _, _ in got)
+    c.close()

@@ -312,3 +312,32 @@ def test_unfilter_wait_timeout_is_unsupported_not_corrupt():
     for d, (st, arr, _) in zip(tall, ctx.decode_batch(tall)):  # switch off: decoded again
         assert st == 0
         assert np.array_equal(arr.reshape(O.png_decode(d)[1].shape), O.png_decode(d)[1])
+
+
+def test_many_serial_fallbacks_bit_exact_and_timed():
+    """streams the chunked inflate cannot start in (zlib level 0 =
+    stored blocks, Z_FIXED = fixed-Huffman blocks: the block finder looks for
+    dynamic-Huffman headers) fall back to the serial kernel, which now claims
+    images from a work counter on up to one workgroup per CU instead of 4
+    fixed workgroups walking the list.  Every image bit-exact; the batch's
+    time is printed (tools/gpu_png.sh: compare before / after)."""
+    import time
+    L = _lib()
+    rng = np.random.default_rng(41)
+    datas = []
+    for i in range(48):
+        px = synth.synth_pixels(rng, 300 + 7 * i, 260 + 5 * i)
+        datas.append(synth.pil_png(px, compress_level=0) if i % 2 == 0 else
+                     synth.make_png(500 + i, 300 + 7 * i, 260 + 5 * i, "RGB", strategy=zlib.Z_FIXED))
+    a = L.Context(0)
+    a.decode_batch(datas[:2])
+    f0 = a.stat("png_serial_fallbacks")
+    t0 = time.perf_counter()
+    ra = a.decode_batch(datas)
+    dt = time.perf_counter() - t0
+    nfb = a.stat("png_serial_fallbacks") - f0
+    print(f"{len(datas)} images, {nfb} serial fallbacks, {dt * 1e3:.1f} ms")
+    for d, (sa, xa, _) in zip(datas, ra):
+        _, ref = O.png_decode(d)
+        assert sa == 0 and np.array_equal(xa, ref)
+    assert nfb + a.stat("png_small_streams") > 0

@@ -14,6 +14,7 @@
   decoder takes the image -- never as DG_OK with wrong pixels.  Forced with
   the context's debug switches.
 """
+import ctypes
 import io
 
 import numpy as np
@@ -210,3 +211,24 @@ def test_unsettled_resync_is_a_per_image_status():
     ctx.set_option("debug_flags", 0)
     res = ctx.decode_batch(jpgs)
     assert all(r[0] == 0 and np.array_equal(r[1], O.jpeg_decode(d)[1]) for d, r in zip(jpgs, res))
+
+
+@pytest.mark.parametrize("key,value", [("inf_decode", 99), ("slots", 0), ("coalesce_max", 0), ("sub_bits", 100),
+                                       ("decode_semantics", 2), ("no_such_option", 1)])
+def test_rejected_option_names_itself_in_last_error(key, value):
+    """a failing dg_ctx_set_option sets dg_last_error to a
+    message naming the option, the value and the accepted range (a stale
+    message from an earlier failure -- round 5's "truncated PNG chunk" after
+    an out-of-range inf_decode -- must not survive)."""
+    L = _lib()
+    ctx = L.Context(0)
+    ctx.set_option("slots", 4)
+    h = ctypes.c_void_p()
+    assert L.load().dg_bucket_table_build(224, 0, 0.5, 2.0, ctypes.byref(h)) == L.DG_ERR_INVALID  # a stale message
+    assert L.load().dg_ctx_set_option(ctx._h, key.encode(), value) == L.DG_ERR_INVALID
+    msg = L.last_error()
+    assert key in msg and str(value) in msg, msg
+    assert ("unknown option" in msg) if key == "no_such_option" else ("valid unless" in msg), msg
+    assert L.load().dg_ctx_get_stat(ctx._h, b"no_such_stat") == -1
+    assert "no_such_stat" in L.last_error()
+    ctx.close()

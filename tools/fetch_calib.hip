@@ -1,0 +1,184 @@
+// fetch_calib.hip -- known-byte microkernels for calibrating rocprofv3's
+// FETCH_SIZE / WRITE_SIZE on gfx950.
+//
+// The MI355X guide calibrates FETCH_SIZE only for wide coalesced streaming
+// reads (16 B per lane: it reports half the bytes).  The datago_amd kernels
+// also read 4-byte words (entropy streams), 8-byte records (chroma fill),
+// and 16-byte parts of 128-byte coefficient blocks, one block per lane
+// (k_idct_t's sparse loads).  Each kernel below moves a known number of
+// bytes in one of those shapes over a 2 GiB buffer (far past the 256 MiB
+// Infinity Cache), once per dispatch; tools/fetch_calib.py joins the PMC
+// passes with the byte counts this program prints (one JSON line per
+// dispatch, in dispatch order) and derives a correction factor per shape.
+//
+//   hipcc -O3 --offload-arch=gfx950 -o tools/fetch_calib tools/fetch_calib.hip
+//   rocprofv3 --pmc FETCH_SIZE --output-format csv -d OUT/fetch -o run -- tools/fetch_calib > OUT/fetch.jsonl
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+#define CHK(x)                                                                  \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(2);                                                                  \
+    }                                                                           \
+  } while (0)
+
+// a sink that the compiler cannot drop and that is (almost) never written
+__device__ __forceinline__ void sink(unsigned *out, unsigned acc) {
+  if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+// coalesced streaming reads of W bytes per lane
+template <int W>
+__global__ __launch_bounds__(256) void rd(const unsigned char *__restrict__ p, size_t n, unsigned *out) {
+  unsigned acc = 0;
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n / W; i += stride) {
+    if constexpr (W == 16) {
+      const u32x4 v = ((const u32x4 *)p)[i];
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    } else if constexpr (W == 8) {
+      const u32x2 v = ((const u32x2 *)p)[i];
+      acc ^= v.x ^ v.y;
+    } else if constexpr (W == 4) {
+      acc ^= ((const unsigned *)p)[i];
+    } else if constexpr (W == 2) {
+      acc ^= ((const unsigned short *)p)[i];
+    } else {
+      acc ^= p[i];
+    }
+  }
+  sink(out, acc);
+}
+
+// one 128-byte line per lane, K of its eight 16-byte parts read (the first K;
+// k_idct_t's sparse coefficient loads: low zigzag parts of each block)
+template <int K>
+__global__ __launch_bounds__(256) void rd_part(const unsigned char *__restrict__ p, size_t n, unsigned *out) {
+  unsigned acc = 0;
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t l = (size_t)blockIdx.x * 256 + threadIdx.x; l < n / 128; l += stride) {
+    const u32x4 *q = (const u32x4 *)(p + l * 128);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const u32x4 v = q[k];
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  }
+  sink(out, acc);
+}
+
+// 64 lanes reading the same 64-byte-aligned 8-byte record pattern as the
+// chroma-record fill: lane l reads 8 bytes at 8 * l + 16 * (l / 8) -- half of
+// each 32-byte sector pair touched (a strided 8-byte gather, 50% useful)
+__global__ __launch_bounds__(256) void rd8_half(const unsigned char *__restrict__ p, size_t n, unsigned *out) {
+  unsigned acc = 0;
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n / 16; i += stride) {
+    const u32x2 v = *(const u32x2 *)(p + i * 16);  // 8 of every 16 bytes
+    acc ^= v.x ^ v.y;
+  }
+  sink(out, acc);
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void wr(unsigned char *__restrict__ p, size_t n) {
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n / W; i += stride) {
+    const unsigned v = (unsigned)i * 2654435761u;
+    if constexpr (W == 16) ((u32x4 *)p)[i] = u32x4{v, v + 1, v + 2, v + 3};
+    else if constexpr (W == 8) ((u32x2 *)p)[i] = u32x2{v, v + 1};
+    else if constexpr (W == 4) ((unsigned *)p)[i] = v;
+    else p[i] = (unsigned char)v;
+  }
+}
+
+// one 128-byte line per lane, K of its 16-byte parts written (k_huff_write's
+// sparse flush stores the nonzero parts of a block)
+template <int K>
+__global__ __launch_bounds__(256) void wr_part(unsigned char *__restrict__ p, size_t n) {
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t l = (size_t)blockIdx.x * 256 + threadIdx.x; l < n / 128; l += stride) {
+    u32x4 *q = (u32x4 *)(p + l * 128);
+    const unsigned v = (unsigned)l * 2654435761u;
+#pragma unroll
+    for (int k = 0; k < K; k++) q[k] = u32x4{v, v + k, v, v};
+  }
+}
+
+// 8 lanes per 128-byte line, all 8 parts written by the 8 lanes (the
+// cooperative flush of k_huff_write: one 16-byte part per lane, 128 B
+// contiguous per 8 lanes, 8 lines per wave-instruction)
+__global__ __launch_bounds__(256) void wr_coop(unsigned char *__restrict__ p, size_t n) {
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n / 16; i += stride) {
+    // lane group g of a wave writes line (i / 8) scattered: lines 4 KiB apart
+    const size_t line = i / 8, part = i % 8;
+    const size_t nl = n / 128;
+    const size_t sl = (line * 32 + line / (nl / 32)) % nl;  // a permutation of the lines when 32 | nl
+    const unsigned v = (unsigned)i;
+    *(u32x4 *)(p + sl * 128 + part * 16) = u32x4{v, v, v, v};
+  }
+}
+
+int main(int argc, char **argv) {
+  const size_t N = (argc > 1 ? strtoull(argv[1], nullptr, 10) : 2048ull) << 20;  // MiB
+  unsigned char *buf;
+  unsigned *out;
+  CHK(hipMalloc(&buf, N));
+  CHK(hipMalloc(&out, 64));
+  CHK(hipMemset(buf, 1, N));
+  int ncu = 0;
+  CHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  const dim3 grid(ncu * 16), blk(256);
+  hipEvent_t e0, e1;
+  CHK(hipEventCreate(&e0));
+  CHK(hipEventCreate(&e1));
+  CHK(hipDeviceSynchronize());
+  int seq = 0;
+  auto run = [&](const char *name, const char *dir, double bytes, auto launch) {
+    for (int rep = 0; rep < 2; rep++) {  // rep 0 warms the code object; both are in the PMC trace
+      CHK(hipEventRecord(e0, 0));
+      launch();
+      CHK(hipEventRecord(e1, 0));
+      CHK(hipEventSynchronize(e1));
+      float ms = 0;
+      CHK(hipEventElapsedTime(&ms, e0, e1));
+      printf("{\"seq\": %d, \"kernel\": \"%s\", \"rep\": %d, \"dir\": \"%s\", \"bytes\": %.0f, \"ms\": %.4f, "
+             "\"GBs\": %.1f}\n",
+             seq++, name, rep, dir, bytes, ms, bytes / (ms * 1e-3) / 1e9);
+      fflush(stdout);
+    }
+  };
+  const double n = (double)N;
+  run("rd16", "read", n, [&] { rd<16><<<grid, blk>>>(buf, N, out); });
+  run("rd8", "read", n, [&] { rd<8><<<grid, blk>>>(buf, N, out); });
+  run("rd4", "read", n, [&] { rd<4><<<grid, blk>>>(buf, N, out); });
+  run("rd2", "read", n, [&] { rd<2><<<grid, blk>>>(buf, N, out); });
+  run("rd1", "read", n, [&] { rd<1><<<grid, blk>>>(buf, N, out); });
+  run("rd_part1", "read", n / 8, [&] { rd_part<1><<<grid, blk>>>(buf, N, out); });
+  run("rd_part2", "read", n / 4, [&] { rd_part<2><<<grid, blk>>>(buf, N, out); });
+  run("rd_part4", "read", n / 2, [&] { rd_part<4><<<grid, blk>>>(buf, N, out); });
+  run("rd_part8", "read", n, [&] { rd_part<8><<<grid, blk>>>(buf, N, out); });
+  run("rd8_half", "read", n / 2, [&] { rd8_half<<<grid, blk>>>(buf, N, out); });
+  run("wr16", "write", n, [&] { wr<16><<<grid, blk>>>(buf, N); });
+  run("wr8", "write", n, [&] { wr<8><<<grid, blk>>>(buf, N); });
+  run("wr4", "write", n, [&] { wr<4><<<grid, blk>>>(buf, N); });
+  run("wr1", "write", n, [&] { wr<1><<<grid, blk>>>(buf, N); });
+  run("wr_part1", "write", n / 8, [&] { wr_part<1><<<grid, blk>>>(buf, N); });
+  run("wr_part4", "write", n / 2, [&] { wr_part<4><<<grid, blk>>>(buf, N); });
+  run("wr_part8", "write", n, [&] { wr_part<8><<<grid, blk>>>(buf, N); });
+  run("wr_coop", "write", n, [&] { wr_coop<<<grid, blk>>>(buf, N); });
+  CHK(hipGetLastError());
+  CHK(hipDeviceSynchronize());
+  CHK(hipFree(buf));
+  CHK(hipFree(out));
+  return 0;
+}
