@@ -444,6 +444,33 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     if (v < 0) return opt_error(k, v, "valid unless v < 0");
     max_dev_bytes_ = (size_t)v << 20;
     budget_slots_ = kMaxInflight;
+    budget_planned_ = false;
+    // Contexts under a budget are the ones that share a device (several
+    // ranks, or a loader beside training): their slot streams share the
+    // process's hardware queues instead of taking two of their own each --
+    // 8 ranks x 4 slots x 2 own queues oversubscribed the device's queues
+    // (profiles/r05/ranks: 6-9 Gpx/s at 4 slots, 104 at 2).  An explicit
+    // slot_queue / side_queue wins.
+    if (v > 0 && !queue_set_ && (slot_queue_ != 0 || side_queue_ != -1)) {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (int j = 0; j < kMaxInflight; j++) {
+        Slot &sl = slots_[j];
+        if (sl.batch && !sl.batch->done) {
+          dg_status st = finish(sl);
+          if (st) return st;
+        }
+      }
+      slot_queue_ = 0;
+      side_queue_ = -1;
+      bool any = false;
+      for (int j = 0; j < kMaxInflight; j++) any = any || slots_[j].st;
+      if (any) return make_streams(0, kMaxInflight, slot_queue_, 0, side_queue_);
+    }
+    return DG_OK;
+  }
+  if (k == "budget_plan") {  // 1: the first batch under a budget sizes every slot (no growth later); 0: grow and trade
+    budget_plan_ = v != 0;
+    budget_planned_ = false;
     return DG_OK;
   }
   if (k == "slots") {
@@ -485,6 +512,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
   }
   if (k == "slot_queue") {  // baseline slots' streams: 0 plain, 1 high / 2 low priority, 3 CU-masked (own queues)
     if (v < 0 || v > 3) return opt_error(k, v, "valid unless v < 0 || v > 3");
+    queue_set_ = true;
     std::lock_guard<std::mutex> lk(mu_);
     for (int j = 0; j < kMaxInflight; j++) {
       Slot &sl = slots_[j];
@@ -498,6 +526,7 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
   }
   if (k == "side_queue") {  // the baseline slots' side streams: -1 as slot_queue, else a slot_queue mode
     if (v < -1 || v > 3) return opt_error(k, v, "valid unless v < -1 || v > 3");
+    queue_set_ = true;
     std::lock_guard<std::mutex> lk(mu_);
     for (int j = 0; j < kMaxInflight; j++) {
       Slot &sl = slots_[j];
@@ -1030,6 +1059,78 @@ void Context::free_slot_buffers(Slot &o) {
   }
 }
 
+// mu_ held.  Planned budget (option "budget_plan"): the first baseline batch
+// under the budget decides how many batches fit in flight and sizes every
+// slot then -- an even share of the budget left after the table pools, the
+// Lanczos cache and a 1/32 reserve for the descriptor buffers, split over
+// scratch / coefficients / input in the first batch's proportions, at least
+// 1.25x what that batch needs -- so that a loader sharing its GPU (ranks, or
+// training) allocates and frees nothing after its first batch: hipMalloc took
+// ~170 ms and hipFree synchronised the device inside the timed window of the
+// 8-ranks-on-one-GPU rehearsal.  A later batch that does
+// not fit its slot is split (kNeedSplit), never grown; its input arena
+// (host-in submissions after device-in ones) is the one buffer added later.
+dg_status Context::budget_planned_fit(Slot &sl, size_t rs, size_t rc, size_t ri) {
+  const size_t MB = (size_t)1 << 20;
+  budget_room_ = 0;
+  if (budget_planned_) {
+    if (rs <= sl.scratch.cap && rc <= sl.coef.cap && ri <= sl.input.cap) {
+      const size_t fp = dev_footprint();
+      budget_room_ = fp < max_dev_bytes_ ? (max_dev_bytes_ - fp) / 2 : 0;
+      return DG_OK;
+    }
+    // a planned slot without buffers (a progressive batch took them back), or
+    // the first host-in batch: allocate, if the budget has room
+    const size_t want_s = std::max(plan_cs_, rs), want_c = std::max(plan_cc_, rc);
+    const size_t want_i = ri ? std::max(plan_ci_, align_up(ri + ri / 4, MB)) : 0;
+    if (rs > plan_cs_ || rc > plan_cc_ || (ri && plan_ci_ && ri > plan_ci_)) return kNeedSplit;
+    const size_t add = (sl.scratch.cap < want_s ? want_s : 0) + (sl.coef.cap < want_c ? want_c : 0) +
+                       (sl.input.cap < want_i ? want_i : 0);
+    if (dev_footprint() + add > max_dev_bytes_) return kNeedSplit;
+    if (sl.scratch.cap < want_s && ensure(sl.scratch, want_s, sl.st, true)) return kNeedSplit;
+    if (sl.coef.cap < want_c && ensure(sl.coef, want_c, sl.st, true)) return kNeedSplit;
+    if (sl.input.cap < want_i && ensure(sl.input, want_i, sl.st, true)) return kNeedSplit;
+    if (ri && !plan_ci_) plan_ci_ = want_i;
+    return DG_OK;
+  }
+  // first sizing: every other slot gives its buffers back (a budget set on a
+  // context that ran without one), then the plan
+  for (int j = 0; j < kAllSlots; j++) {
+    Slot &o = slots_[j];
+    if (&o == &sl) continue;
+    if (o.batch && !o.batch->done && finish(o)) return DG_ERR_DEVICE;
+    free_slot_buffers(o);
+  }
+  free_slot_buffers(sl);
+  if (!retired_dev_.empty() && sync_all() == DG_OK) free_retired();
+  const size_t others = dev_footprint(&sl) + sl.meta.cap + sl.wgt.cap;
+  const size_t reserve = std::max<size_t>(max_dev_bytes_ / 32, 64 * MB);
+  if (others + reserve >= max_dev_bytes_) return kNeedSplit;
+  size_t avail = max_dev_bytes_ - others - reserve;
+  {  // a budget above what the device has free plans for what it has (less 1/8 for the others on it)
+    size_t dfree = 0, dtotal = 0;
+    if (hipMemGetInfo(&dfree, &dtotal) == hipSuccess) avail = std::min(avail, dfree - std::min(dfree, dtotal / 8));
+  }
+  const size_t need = rs + rc + ri;
+  if (need + need / 4 > avail) return kNeedSplit;  // the halves plan the budget
+  const int ns = (int)std::max<size_t>(1, std::min<size_t>((size_t)nslots_, avail / (need + need / 4)));
+  const double f = (double)(avail / (size_t)ns) / (double)need;
+  plan_cs_ = (size_t)((double)rs * f) & ~(MB - 1);
+  plan_cc_ = (size_t)((double)rc * f) & ~(MB - 1);
+  plan_ci_ = ri ? (size_t)((double)ri * f) & ~(MB - 1) : 0;
+  if (ensure(sl.scratch, plan_cs_, sl.st, true) || ensure(sl.coef, plan_cc_, sl.st, true) ||
+      (plan_ci_ && ensure(sl.input, plan_ci_, sl.st, true))) {
+    free_slot_buffers(sl);
+    set_error("device allocation of the planned budget failed");
+    return DG_ERR_OOM;
+  }
+  budget_slots_ = ns;
+  stat_budget_slots_min_ = std::min<int64_t>(stat_budget_slots_min_, ns);
+  budget_planned_ = true;
+  budget_room_ = reserve / 2;
+  return DG_OK;
+}
+
 // mu_ held.  The device budget (option "max_device_mb"): make room for a
 // batch of `self` whose scratch / coefficient / input arenas need rs / rc /
 // ri bytes.  In order: keep self's buffers if they already fit; free the
@@ -1059,6 +1160,18 @@ bool Context::budget_fit(Slot &self, size_t rs, size_t rc, size_t ri) {
   };
   auto has_buffers = [](const Slot &o) { return o.scratch.p || o.coef.p || o.input.p; };
   if (others() + keep > max_dev_bytes_ && !retired_dev_.empty() && sync_all() == DG_OK) free_retired();
+  if (budget_planned_) {  // (a progressive slot) the planned baseline slots keep their buffers
+    for (int j = kMaxInflight; j < kAllSlots && others() + keep > max_dev_bytes_; j++)
+      if (j != si) give_back(slots_[j]);
+    if (others() + keep <= max_dev_bytes_) {
+      budget_room_ = max_dev_bytes_ - others() - keep;
+      return true;
+    }
+    if (others() + tight > max_dev_bytes_) return false;
+    free_slot_buffers(self);
+    budget_room_ = max_dev_bytes_ - others() - tight;
+    return true;
+  }
   for (int j = std::max(1, budget_slots_); j < kMaxInflight && others() + keep > max_dev_bytes_; j++)
     if (j != si && has_buffers(slots_[j])) give_back(slots_[j]);
   while (others() + keep > max_dev_bytes_) {
@@ -2037,8 +2150,14 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   // to be split (submit_split); without one, a failed allocation first
   // finishes the other slots' batches and frees their buffers, then splits.
   const size_t rs = L.off + 256, rc = CO.off + 256, ri = host_io ? IN.off + 64 : 0;
-  if (!budget_fit(sl, rs, rc, ri)) return kNeedSplit;
-  for (int attempt = 0;; attempt++) {
+  const bool planned = max_dev_bytes_ && budget_plan_ && &sl - slots_ < kMaxInflight;
+  if (planned) {
+    st = budget_planned_fit(sl, rs, rc, ri);
+    if (st) return st;
+  } else if (!budget_fit(sl, rs, rc, ri)) {
+    return kNeedSplit;
+  }
+  for (int attempt = 0; !planned; attempt++) {
     st = ensure(sl.scratch, rs, sl.st);
     if (!st) st = ensure(sl.coef, rc, sl.st);
     if (!st && host_io) st = ensure(sl.input, ri, sl.st);
@@ -2487,7 +2606,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   phase(6);
   stat_batches_++;
   *ticket = sl.batch->ticket;
-  if (!max_dev_bytes_ && stat_batches_ <= 2 * kMaxInflight) prewarm_slots(sl);
+  if ((!max_dev_bytes_ || budget_planned_) && stat_batches_ <= 2 * kMaxInflight) prewarm_slots(sl);
   return DG_OK;
 }
 
@@ -2498,7 +2617,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
 // first timed window: 110 vs 115-117 Gpx/s in the other four windows).
 void Context::prewarm_slots(const Slot &self) {
   if (&self - slots_ >= kMaxInflight) return;
-  for (int j = 0; j < nslots_; j++) {
+  const int ns = max_dev_bytes_ ? std::max(1, std::min(nslots_, budget_slots_)) : nslots_;
+  for (int j = 0; j < ns; j++) {
     Slot &o = slots_[j];
     if (&o == &self || (o.batch && !o.batch->done)) continue;
     if (slot_streams(o)) return;

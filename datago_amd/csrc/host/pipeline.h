@@ -306,6 +306,15 @@ class Context {
   size_t budget_room_ = 0;          // headroom the current submit's growth may take under the budget
   int budget_slots_ = kMaxInflight;  // baseline slots in turn under the budget (budget_fit lowers it)
   int64_t stat_budget_slots_min_ = kMaxInflight;
+  // Planned budget (option "budget_plan", default 1): the
+  // first baseline batch under a budget decides the slot count and each
+  // slot's buffer sizes from the budget, and every planned slot is sized
+  // then; later batches that do not fit their slot are split, never grown.
+  bool budget_plan_ = true;
+  bool budget_planned_ = false;
+  size_t plan_cs_ = 0, plan_cc_ = 0, plan_ci_ = 0;  // planned scratch / coefficient / input bytes per slot
+  bool queue_set_ = false;  // slot_queue / side_queue set explicitly (else a budget shares the process queues)
+  dg_status budget_planned_fit(Slot &sl, size_t rs, size_t rc, size_t ri);
   int64_t stat_peak_dev_ = 0, stat_budget_splits_ = 0, stat_budget_frees_ = 0, stat_budget_oom_ = 0;
   dg_status finish(Slot &sl);       // finish_body, or fail_batch on its error
   dg_status finish_body(Slot &sl);

@@ -27,8 +27,10 @@ def _ctx():
 
 def _base_mb():
     """Device MB of a context after one tiny image: table pools + tiny arenas
-    (allocated as a budgeted context does: exact sizes, no growth headroom)."""
+    (allocated as a budgeted context does: exact sizes, no growth headroom;
+    budget_plan 0: a huge budget would otherwise be planned for)."""
     c = _ctx()
+    c.set_option("budget_plan", 0)
     c.set_option("max_device_mb", 1 << 20)
     st, _, _ = c.decode_batch([synth.make_jpeg(1, 32, 32, 90)])[0]
     assert st == 0
@@ -41,6 +43,7 @@ def _ref_ctx():
     """Unbudgeted outputs, footprint as one slot's exact-size buffers (a huge
     budget: no growth headroom, no prewarmed idle slots)."""
     c = _ctx()
+    c.set_option("budget_plan", 0)
     c.set_option("max_device_mb", 1 << 20)
     return c
 
@@ -120,6 +123,7 @@ def test_budget_settles_on_fewer_slots():
     ref.close()
     base = _base_mb()
     one = _ctx()
+    one.set_option("budget_plan", 0)
     one.set_option("max_device_mb", 1 << 20)  # exact sizes, as under a budget
     one.decode_batch(datas)
     per_slot = one.stat("device_mb") - base
@@ -167,4 +171,47 @@ def test_split_failure_waits_for_launched_parts():
     c.set_option("debug_flags", 0)
     got = c.decode_batch(datas)
     assert all(s == 0 for s, _, _ in got)
+    c.close()
+
+
+def test_planned_budget_allocates_nothing_after_first_batch():
+    """under a budget the first batch decides the slot count
+    and sizes every slot it will use (option budget_plan, default on); later
+    batches -- several in flight, cycling over the slots -- allocate and free
+    nothing (stats allocs / budget_frees unchanged), stay within the budget
+    and bit-exact against an unbudgeted context."""
+    # the first batch holds the largest files: every later batch fits the
+    # pinned staging and descriptor buffers it sized (their growth would be an
+    # allocation too)
+    datas = sorted(synth.mixed_corpus(79, 48, 256, 1100), key=len, reverse=True)
+    batches = [datas[i:i + 8] for i in range(0, 48, 8)]
+    ref = _ref_ctx()
+    want = [ref.decode_batch(b) for b in batches]
+    one = ref.stat("peak_device_mb")
+    ref.close()
+    base = _base_mb()
+    budget = base + 3 * max(8, one - base)
+    c = _ctx()
+    c.set_option("max_device_mb", budget)
+    outs = [[np.empty(max(c.output_size(d)[1], 1), np.uint8) for d in b] for b in batches]
+    tk, metas, keep = c.submit_host(batches[0], outs[0])
+    c.wait(tk)
+    a0, f0 = c.stat("allocs"), c.stat("budget_frees")
+    assert c.stat("budget_slots") >= 2, (c.stat("budget_slots"), budget, one, base)
+    for rep in range(2):
+        pend = []
+        for k, b in enumerate(batches):
+            pend.append((k, c.submit_host(b, outs[k])))
+            if len(pend) >= 3:
+                k0, (t0, m0, _) = pend.pop(0)
+                c.wait(t0)
+        for k0, (t0, m0, _) in pend:
+            c.wait(t0)
+        for k, b in enumerate(batches):
+            for j, (st, arr, _) in enumerate(want[k]):
+                assert st == 0 and np.array_equal(outs[k][j][:arr.size].reshape(arr.shape), arr), (rep, k, j)
+    assert c.stat("allocs") == a0, (a0, c.stat("allocs"))
+    assert c.stat("budget_frees") == f0
+    assert c.stat("budget_splits") == 0
+    assert c.stat("peak_device_mb") <= budget, (c.stat("peak_device_mb"), budget)
     c.close()

@@ -46,6 +46,33 @@ def main(root):
             if (ln["dir"] == "read") == (counter == "FETCH_SIZE"):
                 s["factor"] = round(ln["bytes"] / cb, 4) if cb else None
                 s["GBs"] = ln["GBs"]
+    # request-size passes: bytes = 32 n32 + 64 n64 + 128 n128 (reads), 32 (n - n64) + 64 n64 (writes)
+    for sub, ctrs in (("req", ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum",
+                                "TCC_EA0_RDREQ_128B_sum")),
+                      ("wreq", ("TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"))):
+        path = os.path.join(root, sub + ".jsonl")
+        if not os.path.exists(path):
+            continue
+        lines = [json.loads(x) for x in open(path) if x.startswith("{")]
+        cols = {c: _rows(root, sub, c)[0] for c in ctrs}
+        if any(len(v) != len(lines) for v in cols.values()):
+            raise SystemExit(f"{sub}: dispatch count mismatch")
+        for j, ln in enumerate(lines):
+            if ln["rep"] != 1:
+                continue
+            s = out["shapes"][ln["kernel"]]
+            v = {c: cols[c][j] for c in ctrs}
+            if sub == "req":
+                s["rdreq"] = {"all": round(v[ctrs[0]]), "32B": round(v[ctrs[1]]), "64B": round(v[ctrs[2]]),
+                              "128B": round(v[ctrs[3]])}
+                rb = 32 * v[ctrs[1]] + 64 * v[ctrs[2]] + 128 * v[ctrs[3]]
+                s["read_bytes_by_request_size"] = round(rb)
+                if ln["dir"] == "read":
+                    s["factor_by_request_size"] = round(ln["bytes"] / rb, 4) if rb else None
+            else:
+                s["wrreq"] = {"all": round(v[ctrs[0]]), "64B": round(v[ctrs[1]])}
+                wb = 32 * (v[ctrs[0]] - v[ctrs[1]]) + 64 * v[ctrs[1]]
+                s["write_bytes_by_request_size"] = round(wb)
     json.dump(out, sys.stdout, indent=1)
     print()
 

@@ -10,10 +10,12 @@ OUT=${OUT:-gpurun_out/calib}
 mkdir -p $OUT
 if [ "${CALIB:-1}" = 1 ]; then
   timeout -k 10 60 rocprofv3 -L > $OUT/counters_avail.txt 2>&1 || echo "counter list rc $?"
-  for pass in fetch:FETCH_SIZE write:WRITE_SIZE; do
+  for pass in fetch:FETCH_SIZE write:WRITE_SIZE \
+      req:TCC_EA0_RDREQ_sum,TCC_EA0_RDREQ_32B_sum,TCC_EA0_RDREQ_64B_sum,TCC_EA0_RDREQ_128B_sum \
+      wreq:TCC_EA0_WRREQ_sum,TCC_EA0_WRREQ_64B_sum; do
     sub=${pass%%:*}; ctr=${pass#*:}
     echo "=== pmc $ctr"
-    timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d $OUT/$sub -o run -- tools/fetch_calib \
+    timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d $OUT/$sub -o run -- tools/fetch_calib \
       > $OUT/$sub.jsonl 2> $OUT/$sub.err
     rc=$?; echo "exit $rc"; [ $rc -eq 0 ] || { tail -5 $OUT/$sub.err; exit $rc; }
   done

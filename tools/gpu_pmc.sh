@@ -21,7 +21,9 @@ run() {  # name counters...
 run sq SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS &&
 run sq2 SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR &&
 run fetch FETCH_SIZE &&
-run write WRITE_SIZE
+run write WRITE_SIZE &&
+run req TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum &&
+run wreq TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum
 rc=$?
 [ $rc -eq 0 ] || exit $rc
 python tools/pmc_traffic.py $OUT "batch=${BATCH:-256} pool=${POOL:-4096} size=1024/32 short=256-2048" ${BATCH:-256} \

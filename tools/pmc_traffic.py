@@ -77,14 +77,38 @@ def main(root, config=None, images_per_batch=None):
         valu = {k: v / max(nbv, 1) for k, v in valu.items()}
     fetch, nb = res["FETCH_SIZE"]
     write, _ = res["WRITE_SIZE"]
+    # request-size passes (tools/gpu_calib.sh calibrated them against known byte counts):
+    # read bytes = 32 n32 + 64 n64 + 128 n128, write bytes = 32 (n - n64) + 64 n64
+    def per_stage(sub, weights):
+        files = glob.glob(os.path.join(root, sub, "**", "*counter_collection.csv"), recursive=True)
+        rows = [r for f in files for r in csv.DictReader(open(f)) if r["Counter_Name"] in weights]
+        if not rows:
+            return None
+        seq = dict(stage_sequence(rows))
+        nbq = len({int(r["Dispatch_Id"]) for r in rows if "k_huff_sync" in r["Kernel_Name"]})
+        acc = defaultdict(float)
+        for r in rows:
+            d = int(r["Dispatch_Id"])
+            if d in seq:
+                acc[seq[d]] += weights[r["Counter_Name"]] * float(r["Counter_Value"])
+        return {k: v / max(nbq, 1) for k, v in acc.items()}
+    rd_req = per_stage("req", {"TCC_EA0_RDREQ_32B_sum": 32.0, "TCC_EA0_RDREQ_64B_sum": 64.0,
+                               "TCC_EA0_RDREQ_128B_sum": 128.0})
+    wr_req = per_stage("wreq", {"TCC_EA0_WRREQ_sum": 32.0, "TCC_EA0_WRREQ_64B_sum": 32.0})
     stages = sorted(set(fetch) | set(write))
     out = {
         "config": config,
         "images_per_batch": int(images_per_batch) if images_per_batch else None,
         "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (tools/gpu_pmc.sh)",
         "batches": nb,
-        "correction": "FETCH_SIZE x2 (gfx950 reports half of wide reads; uncalibrated for narrower accesses)",
-        "bytes_per_batch": {s: round(2.0 * fetch.get(s, 0.0) + write.get(s, 0.0)) for s in stages},
+        "correction": ("reads: request-size counters (32 n32 + 64 n64 + 128 n128), writes: WRITE_SIZE; "
+                       "calibrated on known bytes (profiles/r06/calib/fetch_calib.json: FETCH_SIZE x2 = the bytes "
+                       "for 4/8/16-B and partial-line 16-B reads; a partial 128-B line is fetched whole)"
+                       if rd_req else "FETCH_SIZE x2 (calibrated: profiles/r06/calib/fetch_calib.json)"),
+        "bytes_per_batch": {s: round((rd_req.get(s, 0.0) if rd_req else 2.0 * fetch.get(s, 0.0)) + write.get(s, 0.0))
+                            for s in stages},
+        "read_bytes_by_request_size": {s: round(v) for s, v in sorted(rd_req.items())} if rd_req else None,
+        "write_bytes_by_request_size": {s: round(v) for s, v in sorted(wr_req.items())} if wr_req else None,
         "fetch_bytes_per_batch_x2": {s: round(2.0 * fetch.get(s, 0.0)) for s in stages},
         "write_bytes_per_batch": {s: round(write.get(s, 0.0)) for s in stages},
         "valu_wave_insts_per_batch": {s: round(v) for s, v in sorted(valu.items())},
