@@ -845,6 +845,250 @@ DG_HD void decode_range(const ImageDesc &im, const TAB *tabs, const DG_GLOBAL ui
   }
 }
 
+// ---- two state-only chains per lane (k_huff_sync2)
+//
+// k_huff_sync's per-lane work -- the lead-in of subsequence s (lead_in) and
+// then its range (decode_range<false>: counts, DC sums, checkpoints, exit
+// state) -- is one serial chain of dependent table lookups.  With few waves
+// per SIMD (a configs[1] batch has ~3 per SIMD, dg_decode_one's small
+// batches one) nothing hides a lookup's LDS latency.
+// SyncChain is that chain as a resumable state machine, so that a lane can
+// advance two independent chains (subsequences s and s + 128) in lockstep
+// and both chains' lookups are in flight together.  The step is
+// decode_range's state-only step with multi-symbol AC runs; the rare events
+// (restart markers, checkpoints, the end of the lead-in and of the range)
+// run in a per-chain branch, in decode_range's order.  A finished chain
+// keeps stepping with its position frozen -- only the position and the
+// counts are guarded per step -- and its results were fixed when it finished.
+// tests/native/emu.cpp checks every pair against lead_in + decode_range.
+template <class TAB>
+struct SyncChain {
+  BitWin b;
+  uint32_t pos, r, z, comp, mi, ev;
+  uint32_t phase;  // 0 lead-in, 1 range, 2 done
+  uint32_t a0, a1, mpos, midx, k, cpos, nck;
+  uint32_t in;     // entry state of the range (the lead-in's exit)
+  const TAB *tdc, *tac;
+  RangeAcc acc;    // the range's accumulators (final once phase == 2)
+  DG_GLOBAL Ckpt *ck;
+};
+
+template <class TAB>
+DG_HD void schain_tables(SyncChain<TAB> &c, const ImageDesc &im, const TAB *tabs, const uint16_t *mt, uint32_t acm) {
+  c.tdc = &tabs[(im.slotmap >> ((c.comp << 1) << 2)) & 15u];
+  c.tac = &tabs[(im.slotmap >> (((c.comp << 1) | 1u) << 2)) & 15u];
+  c.mi = mt ? (acm >> (2u * c.comp)) & 3u : 3u;
+}
+
+// range phase from entry state c.in (decode_range's prologue); `fresh`: the
+// bit window is not positioned yet (no lead-in ran)
+template <class TAB>
+DG_HD void schain_range(SyncChain<TAB> &c, const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uint8_t *stream,
+                        const DG_GLOBAL uint32_t *mk, const uint16_t *mt, uint32_t acm, bool fresh) {
+  c.phase = 1;
+  c.acc.m = 0;
+  c.acc.n = 0;
+  c.acc.dc[0] = c.acc.dc[1] = c.acc.dc[2] = 0;
+  c.r = st_r(c.in);
+  c.z = st_z(c.in);
+  if (c.a0 >= im.ds_bits) {  // empty trailing subsequence: constant exit
+    c.acc.out = pack_state(0, 0, 0);
+    c.phase = 2;
+    c.ev = kInf;
+    if (fresh) {  // a valid window for the frozen steps
+      c.pos = 0;
+      bw_init(c.b, stream, im.ds_lsw, 0);
+    }
+    return;
+  }
+  c.pos = c.a0 + st_rel(c.in);
+  c.mpos = im.nmk ? first_marker(mk, im.nmk, c.a0, c.midx) : kInf;
+  if (fresh) bw_init(c.b, stream, im.ds_lsw, c.pos < c.a1 ? c.pos : c.a0);
+  c.comp = (im.comp_bits >> (2 * c.r)) & 3u;
+  schain_tables(c, im, tabs, mt, acm);
+  c.k = 0;
+  c.cpos = c.a0 + kCkptBits;
+  const uint32_t e = c.a1 < c.mpos ? c.a1 : c.mpos;
+  c.ev = (c.k < c.nck && c.cpos < e) ? c.cpos : e;
+}
+
+template <class TAB>
+DG_HD void schain_begin(SyncChain<TAB> &c, const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uint8_t *stream,
+                        const DG_GLOBAL uint32_t *mk, uint32_t s, uint32_t lead, bool active, DG_GLOBAL Ckpt *ck,
+                        const uint16_t *mt, uint32_t acm) {
+  const uint32_t S = im.sub_bits, total = im.ds_bits;
+  c.ck = ck;
+  c.nck = ck ? num_ckpt(S) : 0u;
+  c.a0 = s * S;
+  c.a1 = c.a0 + S < total ? c.a0 + S : total;
+  c.k = 0;
+  c.cpos = 0;
+  c.midx = 0;
+  c.mpos = kInf;
+  c.in = pack_state(0, 0, 0);
+  c.acc.out = pack_state(0, 0, 0);
+  c.acc.m = c.acc.n = 0;
+  c.acc.dc[0] = c.acc.dc[1] = c.acc.dc[2] = 0;
+  c.r = c.z = 0;
+  c.comp = im.comp_bits & 3u;
+  if (!active) {  // no subsequence: a finished chain on a valid window
+    c.phase = 2;
+    c.ev = kInf;
+    c.pos = 0;
+    bw_init(c.b, stream, im.ds_lsw, 0);
+    schain_tables(c, im, tabs, mt, acm);
+    return;
+  }
+  if (s == 0 || lead == 0 || c.a0 >= total) {  // lead_in's exact / constant entry
+    schain_range(c, im, tabs, stream, mk, mt, acm, true);
+    return;
+  }
+  c.phase = 0;
+  c.pos = c.a0 > lead ? c.a0 - lead : 0u;
+  c.mpos = im.nmk ? first_marker(mk, im.nmk, c.pos, c.midx) : kInf;
+  schain_tables(c, im, tabs, mt, acm);
+  bw_init(c.b, stream, im.ds_lsw, c.pos);
+  c.ev = c.a0 < c.mpos ? c.a0 : c.mpos;
+}
+
+// pos >= ev: the lead-in's loop head (marker, end of the lead-in), then, in
+// the range, decode_range's event block (marker, checkpoint, end)
+template <class TAB>
+DG_HD void schain_event(SyncChain<TAB> &c, const ImageDesc &im, const TAB *tabs, const DG_GLOBAL uint8_t *stream,
+                        const DG_GLOBAL uint32_t *mk, const uint16_t *mt, uint32_t acm) {
+  const uint32_t cbits = im.comp_bits;
+  if (c.phase == 0) {
+    if (c.pos >= c.mpos) {  // restart marker before the start: exact state from here
+      c.pos = c.mpos;
+      c.r = 0;
+      c.z = 0;
+      c.comp = cbits & 3u;
+      schain_tables(c, im, tabs, mt, acm);
+      c.midx++;
+      c.mpos = c.midx < im.nmk ? mk[c.midx] : kInf;
+      bw_seek(c.b, c.pos);
+    }
+    if (c.pos < c.a0) {
+      c.ev = c.a0 < c.mpos ? c.a0 : c.mpos;
+      return;
+    }
+    const uint32_t rel = c.pos - c.a0;
+    c.in = pack_state(rel > 255 ? 255 : rel, c.r, c.z);
+    schain_range(c, im, tabs, stream, mk, mt, acm, false);
+    if (c.phase != 1 || c.pos < c.ev) return;
+  }
+  if (c.phase != 1) return;
+  if (c.pos >= c.mpos) {  // restart marker: hard resync
+    const bool owned = c.mpos < c.a1;
+    c.pos = c.mpos;
+    c.r = 0;
+    c.z = 0;
+    c.comp = cbits & 3u;
+    schain_tables(c, im, tabs, mt, acm);
+    if (owned) {
+      c.acc.m++;
+      c.acc.n = 0;
+      c.acc.dc[0] = c.acc.dc[1] = c.acc.dc[2] = 0;
+    }
+    c.midx++;
+    c.mpos = c.midx < im.nmk ? mk[c.midx] : kInf;
+    bw_seek(c.b, c.pos);
+  }
+  if (c.k < c.nck && c.cpos < c.a1 && c.pos >= c.cpos) {  // first boundary at/after checkpoint k
+    const uint32_t rel = c.pos - c.cpos;
+    DG_GLOBAL Ckpt &ck = c.ck[c.k];
+    ck.st = pack_state(rel > 255 ? 255 : rel, c.r, c.z);
+    ck.m = c.acc.m;
+    ck.n = c.acc.n;
+    ck.dc[0] = c.acc.dc[0];
+    ck.dc[1] = c.acc.dc[1];
+    ck.dc[2] = c.acc.dc[2];
+    c.k++;
+    c.cpos += kCkptBits;
+  }
+  if (c.pos >= c.a1) {  // the range's end: exit state, checkpoint prefixes -> tails
+    const uint32_t rel = c.pos - c.a1;
+    c.acc.out = pack_state(rel > 255 ? 255 : rel, c.r, c.z);
+    for (uint32_t j = 0; j < c.k; j++) {
+      DG_GLOBAL Ckpt &ck = c.ck[j];
+      if (c.acc.m > ck.m) {
+        ck.m = c.acc.m - ck.m;
+        ck.n = c.acc.n;
+        ck.dc[0] = c.acc.dc[0];
+        ck.dc[1] = c.acc.dc[1];
+        ck.dc[2] = c.acc.dc[2];
+      } else {
+        ck.m = 0;
+        ck.n = c.acc.n - ck.n;
+        ck.dc[0] = c.acc.dc[0] - ck.dc[0];
+        ck.dc[1] = c.acc.dc[1] - ck.dc[1];
+        ck.dc[2] = c.acc.dc[2] - ck.dc[2];
+      }
+    }
+    c.phase = 2;
+    c.ev = kInf;
+    return;
+  }
+  const uint32_t e = c.a1 < c.mpos ? c.a1 : c.mpos;
+  c.ev = (c.k < c.nck && c.cpos < e) ? c.cpos : e;
+}
+
+// The per-symbol step of two chains, written as their table reads first
+// (four independent LDS lookups) and their state updates after.
+template <class TAB>
+DG_HD void schain_commit(SyncChain<TAB> &c, const ImageDesc &im, const TAB *tabs, const uint16_t *mt, uint32_t acm,
+                         uint32_t bits, uint32_t e, uint32_t m) {
+  const bool isdc = c.z == 0u;
+  const bool live = c.phase != 2u;
+  const uint32_t len = e >> 8, sym = e & 0xFFu;
+  const uint32_t size = sym & 15u;
+  const int32_t v = huff_value(bits, len, size);
+  const uint32_t mc = m & 15u;
+  const uint32_t zm = c.pos + mc <= c.ev ? multi_next_z(m, c.z) : 0xFFFFFFFFu;
+  const bool take_m = zm != 0xFFFFFFFFu;
+  const uint32_t np = c.pos + (take_m ? mc : len + size);
+  c.pos = live ? np : c.pos;
+  const bool cnt = isdc && live;
+  c.acc.n += cnt ? 1u : 0u;
+  add3(c.acc.dc, c.comp, cnt ? v : 0);
+  const uint32_t zn = take_m ? zm : huff_next_z(c.z, sym);
+  bw_shift(c.b, c.pos);
+  const bool bend = zn >= 64u;
+  c.z = bend ? 0u : zn;
+  c.r = bend ? (c.r + 1u == im.bpm ? 0u : c.r + 1u) : c.r;
+  c.comp = (im.comp_bits >> (2u * c.r)) & 3u;
+  schain_tables(c, im, tabs, mt, acm);
+}
+
+template <class TAB>
+DG_HD void schain_step2(SyncChain<TAB> &A, SyncChain<TAB> &B, const ImageDesc &im, const TAB *tabs,
+                        const uint16_t *mt, uint32_t acm) {
+  bw_refill(A.b);
+  bw_refill(B.b);
+  const uint32_t ba = bw_peek(A.b, A.pos), bb = bw_peek(B.b, B.pos);
+  const TAB &ta = *(A.z == 0u ? A.tdc : A.tac), &tb = *(B.z == 0u ? B.tdc : B.tac);
+  uint32_t ea = ta.lut[ba >> (32 - kLutBits)], eb = tb.lut[bb >> (32 - kLutBits)];
+  const uint32_t ma = (A.mi != 3u && A.z != 0u) ? (uint32_t)mt[(A.mi << kMultiBits) | (ba >> (32u - kMultiBits))] : 0u;
+  const uint32_t mb = (B.mi != 3u && B.z != 0u) ? (uint32_t)mt[(B.mi << kMultiBits) | (bb >> (32u - kMultiBits))] : 0u;
+  if (ea == 0u || (ea & 0x8000u)) ea = huff_lookup(ta, ba);  // codes longer than the first level
+  if (eb == 0u || (eb & 0x8000u)) eb = huff_lookup(tb, bb);
+  schain_commit(A, im, tabs, mt, acm, ba, ea, ma);
+  schain_commit(B, im, tabs, mt, acm, bb, eb, mb);
+}
+
+// Both chains to their ends (lead-in + range each).
+template <class TAB>
+DG_HD void schain_run2(SyncChain<TAB> &A, SyncChain<TAB> &B, const ImageDesc &im, const TAB *tabs,
+                       const DG_GLOBAL uint8_t *stream, const DG_GLOBAL uint32_t *mk, const uint16_t *mt,
+                       uint32_t acm) {
+  for (;;) {
+    if (A.pos >= A.ev) schain_event(A, im, tabs, stream, mk, mt, acm);
+    if (B.pos >= B.ev) schain_event(B, im, tabs, stream, mk, mt, acm);
+    if (A.phase == 2u && B.phase == 2u) break;
+    schain_step2(A, B, im, tabs, mt, acm);
+  }
+}
+
 // ------------------------------------------------------------ destuffing
 
 // Classify raw byte i of a scan: returns 1 if it carries entropy-coded data,

@@ -557,6 +557,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     prog_flush_us_ = (int)v;
     return DG_OK;
   }
+  if (k == "sync2") {  // k_huff_sync2: two lead-in + range chains per lane (0: one, k_huff_sync)
+    sync2_ = v != 0;
+    return DG_OK;
+  }
   if (k == "sync_pair") {  // k_huff_sync: a second AC symbol per single step from the same peek (A/B)
     sync_pair_ = v != 0;
     return DG_OK;
@@ -794,6 +798,7 @@ int64_t Context::get_stat(const std::string &k) {
   }
   if (k == "max_device_mb") return (int64_t)(max_dev_bytes_ >> 20);
   if (k == "budget_splits") return stat_budget_splits_;
+  if (k == "budget_plan_mb") return (int64_t)((plan_cs_ + plan_cc_ + plan_ci_) >> 20);  // planned bytes per slot
   if (k == "budget_slots") return max_dev_bytes_ ? std::min<int64_t>(nslots_, stat_budget_slots_min_) : nslots_;
   if (k == "coef_cache_hits") return stat_ccache_hits_;
   if (k == "coef_cache_new") return stat_ccache_new_;
@@ -2897,7 +2902,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   Ckpt *ck = (Ckpt *)((char *)sl.scratch.p + sl.ckpt_off);
   if (!from_fix)
     launch_huff_sync(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on, b.max_slots,
-                     multi_lead_ ? b.max_ac : 0u, sync_pair_);
+                     multi_lead_ ? b.max_ac : 0u, sync_pair_, sync2_);
   if (next()) return DG_ERR_DEVICE;
   launch_huff_fix(sl.st, dd, lst(L_SYNC), cnt(L_SYNC), hp, subs, ck, fl, b.stage_on, b.max_slots);
   if (next()) return DG_ERR_DEVICE;

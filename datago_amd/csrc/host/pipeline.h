@@ -390,6 +390,7 @@ class Context {
   int64_t stat_prog_aggs_ = 0, stat_prog_agg_images_ = 0;
   bool multi_lead_ = true;   // option "multi_lead": multi-symbol AC steps in k_huff_sync's state-only decodes
   int write_pair_ = 3;       // option "write_pair": up to this many more AC symbols per k_huff_write step from one peek
+  bool sync2_ = false;       // option "sync2": k_huff_sync with two chains per lane (k_huff_sync2)
   bool sync_pair_ = false;   // option "sync_pair": the same in k_huff_sync (measured slower beside multi_lead: off)
   bool prog_side_ = false;  // option "prog_side": progressive scans on the side stream (measured slower: off)
   int coalesce_max_ = 64, coalesce_us_ = 500;

@@ -19,7 +19,7 @@ struct Ckpt;
 // max_ac: the most distinct AC tables of an image (multi-symbol lead-in lookups, 0 = off)
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                       const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
-                      uint32_t max_slots, uint32_t max_ac, bool pair);
+                      uint32_t max_slots, uint32_t max_ac, bool pair, bool two = false);
 void launch_huff_fix(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                      const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
                      uint32_t max_slots);

@@ -529,6 +529,110 @@ __global__ __launch_bounds__(256) void k_huff_sync(const ImageDesc *__restrict__
   wg_time_store(flags, blockIdx.x, t_start);
 }
 
+// k_huff_sync with two chains per lane (option "sync2"):
+// the same 256 slots per workgroup (slot 0 the lead-in slot, 255 useful
+// subsequences, so k_huff_fix, k_huff_scan and the work lists are unchanged)
+// on 128 threads, thread t owning slots t and t + 128.  Each thread runs both
+// slots' lead-in + range decodes in lockstep (SyncChain, dg_entropy.h): two
+// independent lookup chains per lane instead of one.  The verification loop
+// is k_huff_sync's over the 256 slots; its rare re-decodes run per slot.
+__global__ __launch_bounds__(128) void k_huff_sync2(const ImageDesc *__restrict__ imgs,
+                                                    const WgItem *__restrict__ list,
+                                                    const HuffTable *__restrict__ pool,
+                                                    SubState *__restrict__ subs, Ckpt *__restrict__ ckpt,
+                                                    BatchFlags *flags, uint32_t multi) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t huff_dyn[];
+  HuffTable *tabs = (HuffTable *)huff_dyn;
+  __shared__ uint32_t ex[kSubPerWg], ins[kSubPerWg];
+  const uint64_t t_start = wg_clock();
+  entropy_setprio(flags);
+  const WgItem it = list[blockIdx.x];
+  const ImageDesc &im = imgs[it.image];
+  load_tables(tabs, pool, im);
+  uint16_t *mt = (uint16_t *)(huff_dyn + (size_t)im.nslots * sizeof(HuffTable));
+  uint32_t acm = 0xFFu, nac = 0, acs[kMultiLuts] = {0, 0, 0};
+  for (uint32_t c = 0; c < im.ncomp && c < 4; c++) {
+    const uint32_t sl = (im.slotmap >> ((2 * c + 1) * 4)) & 15u;
+    uint32_t a = 3;
+    for (uint32_t q = 0; q < nac; q++)
+      if (acs[q] == sl) a = q;
+    if (a == 3 && nac < kMultiLuts) {
+      acs[nac] = sl;
+      a = nac++;
+    }
+    acm = (acm & ~(3u << (2 * c))) | (a << (2 * c));
+  }
+  __syncthreads();
+  if (multi & 1u) {
+    for (uint32_t i = threadIdx.x; i < (nac << kMultiBits); i += blockDim.x) {
+      const uint32_t q = i >> kMultiBits;
+      const uint32_t sl = q == 0 ? acs[0] : q == 1 ? acs[1] : acs[2];
+      mt[i] = (uint16_t)multi_entry(tabs[sl], i & ((1u << kMultiBits) - 1u));
+    }
+  }
+  __syncthreads();
+  const uint16_t *mtp = (multi & 1u) ? mt : nullptr;
+  const int t = threadIdx.x;
+  const uint32_t s0 = it.item0;  // first useful subsequence
+  const uint32_t nck = num_ckpt(im.sub_bits);
+  const DG_GLOBAL uint8_t *scan = gp<const uint8_t>(im.ds);
+  const DG_GLOBAL uint32_t *mkp = gp<const uint32_t>(im.mk);
+  bool active[2], head[2];
+  uint32_t sv[2];
+  DG_GLOBAL Ckpt *ckv[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int q = t + 128 * h;                      // slot
+    const int64_t si = (int64_t)s0 + q - 1;         // its subsequence (q = 0: lead-in)
+    active[h] = si >= 0 && si < (int64_t)im.nsub;
+    head[h] = (q == 0) || (s0 == 0 && q == 1);
+    sv[h] = active[h] ? (uint32_t)si : 0u;
+    ckv[h] = (q > 0 && active[h] && nck && im.ckpt) ? (DG_GLOBAL Ckpt *)ckpt + im.ckpt_base + (size_t)sv[h] * nck
+                                                   : nullptr;
+  }
+  SyncChain<HuffTable> A, B;
+  schain_begin(A, im, tabs, scan, mkp, sv[0], im.lead_bits, active[0], ckv[0], mtp, acm);
+  schain_begin(B, im, tabs, scan, mkp, sv[1], im.lead_bits, active[1], ckv[1], mtp, acm);
+  schain_run2(A, B, im, tabs, scan, mkp, mtp, acm);
+  RangeAcc acc[2] = {A.acc, B.acc};
+  ex[t] = active[0] ? A.acc.out : 0u;
+  ins[t] = A.in;
+  ex[t + 128] = active[1] ? B.acc.out : 0u;
+  ins[t + 128] = B.in;
+  __syncthreads();
+  uint32_t iters = 0;
+  for (;;) {
+    bool redo[2];
+    uint32_t pin[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int q = t + 128 * h;
+      redo[h] = active[h] && !head[h] && ins[q] != ex[q - 1];
+      pin[h] = redo[h] ? ex[q - 1] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int q = t + 128 * h;
+      if (redo[h]) {
+        decode_range<false>(im, tabs, scan, mkp, sv[h], pin[h], acc[h], nullptr, ckv[h], true, ex[q], nullptr, mtp,
+                            acm, 0u);
+        ex[q] = acc[h].out;
+        ins[q] = pin[h];
+      }
+    }
+    iters++;
+    if (!__syncthreads_or(redo[0] || redo[1])) break;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int q = t + 128 * h;
+    if (active[h] && q > 0) store_sub(subs[im.sub_base + sv[h]], ins[q], ex[q], acc[h]);
+  }
+  if (t == 0) atomicMax(&flags->sync_iters_max, iters);
+  wg_time_store(flags, blockIdx.x, t_start);
+}
+
 template <bool STAGE>
 __global__ __launch_bounds__(256) void k_huff_fix(const ImageDesc *__restrict__ imgs,
                                                   const WgItem *__restrict__ list,
@@ -2808,11 +2912,13 @@ void launch_destuff_one(hipStream_t st, ImageDesc *imgs, const WgItem *list, uin
 // per workgroup, 8 resident workgroups per CU instead of 6
 void launch_huff_sync(hipStream_t st, const ImageDesc *imgs, const WgItem *list, uint32_t nwg,
                       const HuffTable *pool, SubState *subs, Ckpt *ck, BatchFlags *flags, bool stage,
-                      uint32_t max_slots, uint32_t max_ac, bool pair) {
+                      uint32_t max_slots, uint32_t max_ac, bool pair, bool two) {
   if (!nwg) return;
   const size_t lds = (size_t)max_slots * sizeof(HuffTable) + ((size_t)max_ac << kMultiBits) * 2;
   const uint32_t multi = (max_ac ? 1u : 0u) | (pair ? 2u : 0u);  // bit 0: multi-symbol lookups, bit 1: pair steps
-  if (stage)
+  if (two && !stage && !pair)  // two chains per lane (k_huff_sync2: no staging, no pair steps)
+    hipLaunchKernelGGL(k_huff_sync2, dim3(nwg), dim3(128), lds, st, imgs, list, pool, subs, ck, flags, multi);
+  else if (stage)
     hipLaunchKernelGGL(k_huff_sync<true>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags, multi);
   else
     hipLaunchKernelGGL(k_huff_sync<false>, dim3(nwg), dim3(256), lds, st, imgs, list, pool, subs, ck, flags, multi);

@@ -20,6 +20,11 @@ extern "C" void emu_set_lead(uint32_t lead) { g_lead = lead; }
 static int64_t g_multi_mismatch = 0, g_multi_checked = 0;
 extern "C" int64_t emu_multi_mismatch() { return g_multi_mismatch; }
 extern "C" int64_t emu_multi_checked() { return g_multi_checked; }
+// k_huff_sync2's two-chain SyncChain decode vs lead_in + decode_range per slot
+// (entry state, accumulators, exit state and every checkpoint record)
+static int64_t g_two_mismatch = 0, g_two_checked = 0;
+extern "C" int64_t emu_two_mismatch() { return g_two_mismatch; }
+extern "C" int64_t emu_two_checked() { return g_two_checked; }
 
 extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bits, int16_t *out,
                                 size_t cap_blocks, size_t *nblocks, int64_t *stats) {
@@ -106,6 +111,47 @@ extern "C" int emu_decode_coefs(const uint8_t *data, size_t len, uint32_t sub_bi
   const uint32_t NW = (d.nsub + U - 1) / U;
   int64_t redo_total = 0, iters_max = 0, fix_wgs = 0, rounds = 0;
   auto ckp = [&](uint32_t s) { return NCK ? &ck[(size_t)s * NCK] : (Ckpt *)nullptr; };
+  // ---- k_huff_sync2's chains: slots t and t + 128 of a workgroup on one lane
+  {
+    std::vector<Ckpt> ck1((size_t)d.nsub * (NCK ? NCK : 1)), ck2((size_t)d.nsub * (NCK ? NCK : 1));
+    for (uint32_t wg = 0; wg < NW; wg++) {
+      const uint32_t s0 = wg * U;
+      for (uint32_t t = 0; t < 128; t++) {
+        SyncChain<HuffTable> ch[2];
+        uint32_t sv[2];
+        bool act[2];
+        for (int hh = 0; hh < 2; hh++) {
+          const uint32_t q = t + 128 * hh;
+          const int64_t si = (int64_t)s0 + q - 1;
+          act[hh] = si >= 0 && si < (int64_t)d.nsub;
+          sv[hh] = act[hh] ? (uint32_t)si : 0u;
+          schain_begin(ch[hh], d, tabs.data(), scan, mkp, sv[hh], d.lead_bits, act[hh],
+                       (q > 0 && act[hh] && NCK) ? &ck2[(size_t)sv[hh] * NCK] : (Ckpt *)nullptr, mt.data(), acm);
+        }
+        schain_run2(ch[0], ch[1], d, tabs.data(), scan, mkp, mt.data(), acm);
+        for (int hh = 0; hh < 2; hh++) {
+          if (!act[hh]) continue;
+          const uint32_t q = t + 128 * hh;
+          const uint32_t in = lead_in(d, tabs.data(), scan, mkp, sv[hh], d.lead_bits, mt.data(), acm, false);
+          RangeAcc a;
+          Ckpt *c1 = (q > 0 && NCK) ? &ck1[(size_t)sv[hh] * NCK] : (Ckpt *)nullptr;
+          decode_range<false>(d, tabs.data(), scan, mkp, sv[hh], in, a, nullptr, c1, false, 0, nullptr, mt.data(), acm,
+                              0u);
+          const RangeAcc &b = ch[hh].acc;
+          bool bad = in != ch[hh].in || a.out != b.out || a.m != b.m || a.n != b.n || a.dc[0] != b.dc[0] ||
+                     a.dc[1] != b.dc[1] || a.dc[2] != b.dc[2];
+          if (c1)
+            for (uint32_t j = 0; j < NCK; j++) {
+              const Ckpt &x = c1[j], &y = ck2[(size_t)sv[hh] * NCK + j];
+              bad = bad || x.st != y.st || x.m != y.m || x.n != y.n || x.dc[0] != y.dc[0] || x.dc[1] != y.dc[1] ||
+                    x.dc[2] != y.dc[2];
+            }
+          g_two_checked++;
+          g_two_mismatch += bad ? 1 : 0;
+        }
+      }
+    }
+  }
   // ---- k_huff_sync (mirrors the kernel: threads in lockstep phases)
   for (uint32_t wg = 0; wg < NW; wg++) {
     const uint32_t s0 = wg * U;

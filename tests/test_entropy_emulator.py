@@ -36,10 +36,13 @@ def emu():
 
     E.emu_multi_mismatch.restype = ctypes.c_int64
     E.emu_multi_checked.restype = ctypes.c_int64
+    E.emu_two_mismatch.restype = ctypes.c_int64
+    E.emu_two_checked.restype = ctypes.c_int64
 
     def run(data, sub_bits, lead=0):
         E.emu_set_lead(lead)
         run.multi0 = (E.emu_multi_mismatch(), E.emu_multi_checked())
+        run.two0 = (E.emu_two_mismatch(), E.emu_two_checked())
         cap = 1 << 18
         out = np.zeros((cap, 64), np.int16)
         nb = ctypes.c_size_t()
@@ -47,6 +50,7 @@ def emu():
         r = E.emu_decode_coefs(data, len(data), sub_bits, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),
                                cap, ctypes.byref(nb), st)
         run.multi = (E.emu_multi_mismatch() - run.multi0[0], E.emu_multi_checked() - run.multi0[1])
+        run.two = (E.emu_two_mismatch() - run.two0[0], E.emu_two_checked() - run.two0[1])
         return r, out[: nb.value], list(st)
     return run
 
@@ -68,6 +72,8 @@ def test_emulated_parallel_decode_matches_oracle(emu, seed, sub_bits, lead):
     assert stats[5] == 0  # write pass exit == next subsequence's entry everywhere
     # k_huff_sync's multi-symbol lead-in (kMultiBits lookups) ends in the same state as single steps
     assert emu.multi[0] == 0, emu.multi
+    # k_huff_sync2: two chains per lane in lockstep equal lead_in + decode_range per slot
+    assert emu.two[0] == 0 and emu.two[1] > 0, emu.two
 
 
 def test_truncated_stream_is_detected(emu):

@@ -601,3 +601,34 @@ def test_v_tile_bit_exact(v_tile):
                 continue  # (the PNG suites pin PNG resizes to the oracle; here: equal to v_tile 0)
             _, dec = O.jpeg_decode(d)
             assert np.array_equal(a1, O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR))
+
+
+@pytest.mark.parametrize("sub_bits,lead", [(0, -1), (1024, -1), (4096, 0), (8192, -1), (2048, 6144)])
+def test_sync2_bit_exact(sub_bits, lead):
+    """Option sync2: k_huff_sync2 runs two lead-in + range chains per lane
+    (SyncChain, dg_entropy.h; tests/native/emu.cpp checks each pair against
+    lead_in + decode_range).  Bit-exact against the oracle and against the
+    one-chain kernel -- with restart markers, gray, 4:2:2 / 4:4:4, images of
+    fewer subsequences than a workgroup and of many workgroups -- with no
+    write mismatch."""
+    L = _lib()
+    datas = _rand_jpegs(14, 12, maxdim=1400) + _rand_jpegs(15, 4, maxdim=900, rst=True)
+    datas.append(synth.make_jpeg(91, 2400, 1600, 92, "4:2:0", False))
+    datas.append(synth.make_jpeg(92, 1800, 1200, 60, "4:4:4", False))
+    datas.append(synth.make_jpeg(93, 3000, 2000, 95, "4:2:0", False, restart_marker_rows=2))
+    outs = {}
+    for two in (0, 1):
+        ctx = L.Context(0)
+        ctx.set_option("sync2", two)
+        if sub_bits:
+            ctx.set_option("sub_bits", sub_bits)
+        if lead >= 0:
+            ctx.set_option("lead_bits", lead)
+        outs[two] = ctx.decode_batch(datas)
+        assert ctx.stat("write_mismatch") == 0
+        ctx.close()
+    for i, (d, (s0, a0, _), (s1, a1, _)) in enumerate(zip(datas, outs[0], outs[1])):
+        assert s0 == 0 and s1 == 0, i
+        assert np.array_equal(a0, a1), (i, sub_bits)
+        ost, ref = O.jpeg_decode(d)
+        assert np.array_equal(a1.reshape(ref.shape), ref), (i, sub_bits)
