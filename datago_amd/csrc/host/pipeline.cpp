@@ -125,12 +125,13 @@ Context::~Context() {
     if (sl.done) hipEventDestroy(sl.done);
     for (hipEvent_t e : {sl.ev_meta, sl.ev_coef, sl.ev_zero, sl.ev_prog, sl.ev_png0, sl.ev_png1})
       if (e) hipEventDestroy(e);
-    if (sl.coef.p) hipFree(sl.coef.p);
+    if (sl.coef.p && !sl.views) hipFree(sl.coef.p);
     for (hipStream_t q : {sl.st, sl.side})
       if (q) hipStreamDestroy(q);
     if (sl.wgt.p) hipFree(sl.wgt.p);
     for (DevBuf *b : {&sl.scratch, &sl.meta, &sl.input})
-      if (b->p) hipFree(b->p);
+      if (b->p && (b == &sl.meta || !sl.views)) hipFree(b->p);
+    if (sl.arena.p) hipFree(sl.arena.p);
     for (PinBuf *b : {&sl.stage, &sl.out})
       if (b->p) hipHostFree(b->p);
   }
@@ -700,6 +701,11 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     inf_stage3_ = (uint32_t)v;
     return DG_OK;
   }
+  if (k == "inf_cap") {  // chunk-parallel inflate: entries per chunk, in tenths of the image's expansion of a span
+    if (v < 10 || v > 100) return opt_error(k, v, "valid unless v < 10 || v > 100");
+    inf_cap_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "inf_chunk") {  // compressed bytes per chunk of the chunk-parallel inflate
     if (v < 4096 || v > 65536 || (v & (v - 1))) return opt_error(k, v, "valid unless v < 4096 || v > 65536 || (v & (v - 1))");
     inf_chunk_ = (uint32_t)v;
@@ -798,7 +804,7 @@ int64_t Context::get_stat(const std::string &k) {
   }
   if (k == "max_device_mb") return (int64_t)(max_dev_bytes_ >> 20);
   if (k == "budget_splits") return stat_budget_splits_;
-  if (k == "budget_plan_mb") return (int64_t)((plan_cs_ + plan_cc_ + plan_ci_) >> 20);  // planned bytes per slot
+  if (k == "budget_plan_mb") return (int64_t)(plan_arena_ >> 20);  // planned bytes per slot
   if (k == "budget_slots") return max_dev_bytes_ ? std::min<int64_t>(nslots_, stat_budget_slots_min_) : nslots_;
   if (k == "coef_cache_hits") return stat_ccache_hits_;
   if (k == "coef_cache_new") return stat_ccache_new_;
@@ -963,7 +969,9 @@ size_t Context::dev_footprint(const Slot *except) const {
   size_t t = retired_dev_bytes_;
   for (const Slot &o : slots_) {
     if (&o == except) continue;
-    for (const DevBuf *b : {&o.scratch, &o.meta, &o.input, &o.coef, &o.wgt}) t += b->cap;
+    for (const DevBuf *b : {&o.meta, &o.wgt, &o.arena}) t += b->cap;
+    if (!o.views)
+      for (const DevBuf *b : {&o.scratch, &o.input, &o.coef}) t += b->cap;
   }
   for (int g = 0; g < kPoolGens; g++) t += d_hpool_[g].cap + d_qpool_[g].cap;
   return t + d_ccache_.cap;
@@ -1055,7 +1063,14 @@ int Context::ccache_lookup(const ResizePass &ps, Batch &b, bool &hit) {
 
 // An idle slot's device buffers (no batch, or its batch finished).
 void Context::free_slot_buffers(Slot &o) {
-  for (DevBuf *b : {&o.scratch, &o.meta, &o.input, &o.coef}) {
+  if (o.views) {  // carved from the arena
+    for (DevBuf *b : {&o.scratch, &o.input, &o.coef}) {
+      b->p = nullptr;
+      b->cap = 0;
+    }
+    o.views = false;
+  }
+  for (DevBuf *b : {&o.scratch, &o.meta, &o.input, &o.coef, &o.arena}) {
     if (!b->p) continue;
     hipFree(b->p);
     b->p = nullptr;
@@ -1078,24 +1093,25 @@ void Context::free_slot_buffers(Slot &o) {
 dg_status Context::budget_planned_fit(Slot &sl, size_t rs, size_t rc, size_t ri) {
   const size_t MB = (size_t)1 << 20;
   budget_room_ = 0;
+  // this batch's scratch / coefficient / input views of the slot's arena
+  const size_t os = 0, oc = align_up(rs, 256), oi = oc + align_up(rc, 256), need = oi + ri;
+  auto carve = [&]() {
+    char *a = (char *)sl.arena.p;
+    sl.scratch = DevBuf{a + os, rs};
+    sl.coef = DevBuf{a + oc, rc};
+    sl.input = DevBuf{ri ? a + oi : nullptr, ri};
+    sl.views = true;
+    const size_t fp = dev_footprint();
+    budget_room_ = fp < max_dev_bytes_ ? (max_dev_bytes_ - fp) / 2 : 0;
+  };
   if (budget_planned_) {
-    if (rs <= sl.scratch.cap && rc <= sl.coef.cap && ri <= sl.input.cap) {
-      const size_t fp = dev_footprint();
-      budget_room_ = fp < max_dev_bytes_ ? (max_dev_bytes_ - fp) / 2 : 0;
-      return DG_OK;
+    if (need > plan_arena_) return kNeedSplit;
+    if (!sl.arena.p) {  // a planned slot without its arena (a progressive batch took the room): take it back
+      if (sl.scratch.p || sl.coef.p || sl.input.p) free_slot_buffers(sl);
+      if (dev_footprint() + plan_arena_ > max_dev_bytes_ || ensure(sl.arena, plan_arena_, sl.st, true))
+        return kNeedSplit;
     }
-    // a planned slot without buffers (a progressive batch took them back), or
-    // the first host-in batch: allocate, if the budget has room
-    const size_t want_s = std::max(plan_cs_, rs), want_c = std::max(plan_cc_, rc);
-    const size_t want_i = ri ? std::max(plan_ci_, align_up(ri + ri / 4, MB)) : 0;
-    if (rs > plan_cs_ || rc > plan_cc_ || (ri && plan_ci_ && ri > plan_ci_)) return kNeedSplit;
-    const size_t add = (sl.scratch.cap < want_s ? want_s : 0) + (sl.coef.cap < want_c ? want_c : 0) +
-                       (sl.input.cap < want_i ? want_i : 0);
-    if (dev_footprint() + add > max_dev_bytes_) return kNeedSplit;
-    if (sl.scratch.cap < want_s && ensure(sl.scratch, want_s, sl.st, true)) return kNeedSplit;
-    if (sl.coef.cap < want_c && ensure(sl.coef, want_c, sl.st, true)) return kNeedSplit;
-    if (sl.input.cap < want_i && ensure(sl.input, want_i, sl.st, true)) return kNeedSplit;
-    if (ri && !plan_ci_) plan_ci_ = want_i;
+    carve();
     return DG_OK;
   }
   // first sizing: every other slot gives its buffers back (a budget set on a
@@ -1109,29 +1125,27 @@ dg_status Context::budget_planned_fit(Slot &sl, size_t rs, size_t rc, size_t ri)
   free_slot_buffers(sl);
   if (!retired_dev_.empty() && sync_all() == DG_OK) free_retired();
   const size_t others = dev_footprint(&sl) + sl.meta.cap + sl.wgt.cap;
-  const size_t reserve = std::max<size_t>(max_dev_bytes_ / 32, 64 * MB);
-  if (others + reserve >= max_dev_bytes_) return kNeedSplit;
+  if (others >= max_dev_bytes_) return kNeedSplit;
+  // descriptor / weight buffers of the planned slots grow into the reserve
+  const size_t reserve =
+      std::min<size_t>(std::max<size_t>(max_dev_bytes_ / 32, 64 * MB), (max_dev_bytes_ - others) / 4);
   size_t avail = max_dev_bytes_ - others - reserve;
   {  // a budget above what the device has free plans for what it has (less 1/8 for the others on it)
     size_t dfree = 0, dtotal = 0;
     if (hipMemGetInfo(&dfree, &dtotal) == hipSuccess) avail = std::min(avail, dfree - std::min(dfree, dtotal / 8));
   }
-  const size_t need = rs + rc + ri;
   if (need + need / 4 > avail) return kNeedSplit;  // the halves plan the budget
   const int ns = (int)std::max<size_t>(1, std::min<size_t>((size_t)nslots_, avail / (need + need / 4)));
-  const double f = (double)(avail / (size_t)ns) / (double)need;
-  plan_cs_ = (size_t)((double)rs * f) & ~(MB - 1);
-  plan_cc_ = (size_t)((double)rc * f) & ~(MB - 1);
-  plan_ci_ = ri ? (size_t)((double)ri * f) & ~(MB - 1) : 0;
-  if (ensure(sl.scratch, plan_cs_, sl.st, true) || ensure(sl.coef, plan_cc_, sl.st, true) ||
-      (plan_ci_ && ensure(sl.input, plan_ci_, sl.st, true))) {
-    free_slot_buffers(sl);
+  plan_arena_ = (avail / (size_t)ns) & ~(MB - 1);
+  if (ensure(sl.arena, plan_arena_, sl.st, true)) {
     set_error("device allocation of the planned budget failed");
     return DG_ERR_OOM;
   }
   budget_slots_ = ns;
   stat_budget_slots_min_ = std::min<int64_t>(stat_budget_slots_min_, ns);
   budget_planned_ = true;
+  next_slot_ = 1 % ns;
+  carve();
   budget_room_ = reserve / 2;
   return DG_OK;
 }
@@ -1163,7 +1177,7 @@ bool Context::budget_fit(Slot &self, size_t rs, size_t rc, size_t ri) {
     if (o.batch && !o.batch->done && finish(o)) return;
     free_slot_buffers(o);
   };
-  auto has_buffers = [](const Slot &o) { return o.scratch.p || o.coef.p || o.input.p; };
+  auto has_buffers = [](const Slot &o) { return o.scratch.p || o.coef.p || o.input.p || o.arena.p; };
   if (others() + keep > max_dev_bytes_ && !retired_dev_.empty() && sync_all() == DG_OK) free_retired();
   if (budget_planned_) {  // (a progressive slot) the planned baseline slots keep their buffers
     for (int j = kMaxInflight; j < kAllSlots && others() + keep > max_dev_bytes_; j++)
@@ -1711,10 +1725,12 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         if (nch >= 2 && !chunked_off_) {
           pd.chunk0 = (uint32_t)b.ichunks.size();
           pd.nchunks = nch;
-          // entries per chunk: 3x the image's average expansion (+64 Ki), at most the whole image;
-          // a chunk that needs more sends the image to the serial kernel
+          // entries per chunk: inf_cap / 10 times the image's average expansion of a span (+64 Ki), at
+          // most the whole image; a chunk that needs more sends the image to the serial kernel.  The
+          // entries (2 bytes per output byte) are most of a PNG batch's device memory: 3x made them
+          // 6x the raw image
           const double ratio = (double)want / (double)g.zlen;
-          const uint64_t cap = std::min<uint64_t>(want, (uint64_t)(3.0 * ratio * span) + 65536);
+          const uint64_t cap = std::min<uint64_t>(want, (uint64_t)(0.1 * inf_cap_ * ratio * span) + 65536);
           for (uint32_t k = 0; k < nch; k++) {
             InfChunk c;
             memset(&c, 0, sizeof(c));
@@ -2159,8 +2175,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   if (planned) {
     st = budget_planned_fit(sl, rs, rc, ri);
     if (st) return st;
-  } else if (!budget_fit(sl, rs, rc, ri)) {
-    return kNeedSplit;
+  } else {
+    if (sl.views) free_slot_buffers(sl);  // (the budget plan was switched off)
+    if (!budget_fit(sl, rs, rc, ri)) return kNeedSplit;
   }
   for (int attempt = 0; !planned; attempt++) {
     st = ensure(sl.scratch, rs, sl.st);
@@ -2627,9 +2644,17 @@ void Context::prewarm_slots(const Slot &self) {
     Slot &o = slots_[j];
     if (&o == &self || (o.batch && !o.batch->done)) continue;
     if (slot_streams(o)) return;
+    if (self.views) {  // planned budget: the slot's arena
+      if (ensure(o.arena, self.arena.cap, nullptr, true) || ensure(o.meta, self.meta.cap, nullptr, true) ||
+          ensure(o.wgt, self.wgt.cap, nullptr, true) || ensure_pinned(o.stage, self.stage.cap, nullptr, true) ||
+          ensure_pinned(o.out, self.out.cap, nullptr, true))
+        return;
+      continue;
+    }
     if (ensure(o.scratch, self.scratch.cap, nullptr, true) || ensure(o.coef, self.coef.cap, nullptr, true) ||
         ensure(o.input, self.input.cap, nullptr, true) || ensure(o.meta, self.meta.cap, nullptr, true) ||
-        ensure(o.wgt, self.wgt.cap, nullptr, true) || ensure_pinned(o.stage, self.stage.cap, nullptr, true))
+        ensure(o.wgt, self.wgt.cap, nullptr, true) || ensure_pinned(o.stage, self.stage.cap, nullptr, true) ||
+        ensure_pinned(o.out, self.out.cap, nullptr, true))
       return;
   }
 }
@@ -2638,6 +2663,12 @@ void Context::prewarm_slots(const Slot &self) {
 // finishes first.  Progressive batches have slots of their own
 // (pick_prog_slot), so every baseline slot cycles at the baseline pace.
 int Context::pick_slot() {
+  // the planned budget's first sizing runs on slot 0 (budget_planned_fit sizes
+  // slots [0, budget_slots_)); submissions split before it keep that slot
+  if (max_dev_bytes_ && budget_plan_ && !budget_planned_) {
+    next_slot_ = 0;
+    return 0;
+  }
   const int ns = max_dev_bytes_ ? std::max(1, std::min(nslots_, budget_slots_)) : nslots_;
   const int i = next_slot_ % ns;
   next_slot_ = (i + 1) % ns;

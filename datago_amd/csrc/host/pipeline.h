@@ -145,6 +145,10 @@ struct Slot {
   DevBuf scratch, meta, input;
   DevBuf wgt;  // debug: per-workgroup timestamps of the entropy kernels (option "wg_timing")
   DevBuf coef;  // coefficient arena of the batch (k_huff_write -> k_idct)
+  // planned budget: one allocation per slot, scratch / coef / input carved
+  // from it per batch (views: never allocated or freed on their own)
+  DevBuf arena;
+  bool views = false;
   size_t coef_bytes = 0;
   PinBuf stage, out;
   std::vector<hipEvent_t> ev;  // per-stage timing events
@@ -312,7 +316,7 @@ class Context {
   // then; later batches that do not fit their slot are split, never grown.
   bool budget_plan_ = true;
   bool budget_planned_ = false;
-  size_t plan_cs_ = 0, plan_cc_ = 0, plan_ci_ = 0;  // planned scratch / coefficient / input bytes per slot
+  size_t plan_arena_ = 0;  // planned bytes per slot (scratch + coefficients + input, one allocation)
   bool queue_set_ = false;  // slot_queue / side_queue set explicitly (else a budget shares the process queues)
   dg_status budget_planned_fit(Slot &sl, size_t rs, size_t rc, size_t ri);
   int64_t stat_peak_dev_ = 0, stat_budget_splits_ = 0, stat_budget_frees_ = 0, stat_budget_oom_ = 0;
@@ -434,6 +438,7 @@ class Context {
   bool wg_timing_ = false;
   bool chunked_off_ = false;  // option "png_chunked" = 0
   uint32_t inf_chunk_ = kInfChunk;  // option "inf_chunk"
+  uint32_t inf_cap_ = 30;           // option "inf_cap": chunk entries, tenths of the expansion of a span
   uint32_t inf_stage3_ = 32;        // option "inf_stage3"
   int plan_threads_ = 4;            // option "plan_threads"
   int meta_pull_ = 1;               // option "meta_pull"
