@@ -509,13 +509,31 @@ __device__ __forceinline__ void inflate_image(InflateSmem &sm, ImageDesc &im) {
       // Branches are wave-uniform.
       const uint32_t q = op, src0 = op - dist, rounds = (len + 63u) >> 6;
       if (dist == 1u) {  // run of one byte (masks, flat rows): one broadcast read
+        // The aligned body as dwords (<= 65 of them: one or two stores per lane
+        // instead of up to five byte stores), the unaligned head and tail bytes
+        // by lanes of their own.  (A 5.4 MB mask is 22 K such runs, mean length
+        // 243: the serial mask inflate's copies.)
         const uint32_t b = sm.ring[src0 & kRingMask];
-        for (uint32_t r = 0; r < rounds; r++) {
-          const uint32_t j = lane + 64u * r;
-          if (j < len) {
-            sm.ring[(q + j) & kRingMask] = (uint8_t)b;
-            if (q + j < want) out[q + j] = (uint8_t)b;
+        const uint32_t e = q + len, a0 = (q + 3u) & ~3u, a1 = e & ~3u;
+        const uint32_t hb = (a0 < e ? a0 : e) - q;           // head bytes before the first aligned dword
+        const uint32_t nd = a1 > a0 ? (a1 - a0) >> 2 : 0u;   // whole dwords
+        const uint32_t ts = a1 > a0 ? a1 : a0;                // tail: [ts, e)
+        const uint32_t tb = e > ts ? e - ts : 0u;
+        const uint32_t w4 = b * 0x01010101u;
+        for (uint32_t k = lane; k < nd; k += 64) {
+          const uint32_t p = a0 + 4u * k;
+          *(uint32_t *)&sm.ring[p & kRingMask] = w4;
+          if (p + 4u <= want) {
+            *(DG_GLOBAL uint32_t *)(out + p) = w4;
+          } else {
+            for (uint32_t x = 0; x < 4u; x++)
+              if (p + x < want) out[p + x] = (uint8_t)b;
           }
+        }
+        if (lane < hb + tb) {
+          const uint32_t p = lane < hb ? q + lane : ts + (lane - hb);
+          sm.ring[p & kRingMask] = (uint8_t)b;
+          if (p < want) out[p] = (uint8_t)b;
         }
       } else {  // every read before the writes: one LDS round trip (len <= 258)
         const float rcp = 1.0f / (float)dist;

@@ -706,6 +706,15 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     inf_cap_ = (uint32_t)v;
     return DG_OK;
   }
+  if (k == "png_alias") {  // PNG chunk entries share device memory with the later stages' buffers
+    png_alias_ = v != 0;
+    return DG_OK;
+  }
+  if (k == "inf_pad") {  // chunk-parallel inflate: entries per chunk on top of inf_cap's
+    if (v < 0 || v > (1 << 20)) return opt_error(k, v, "valid unless v < 0 || v > 2^20");
+    inf_pad_ = (uint32_t)v;
+    return DG_OK;
+  }
   if (k == "inf_chunk") {  // compressed bytes per chunk of the chunk-parallel inflate
     if (v < 4096 || v > 65536 || (v & (v - 1))) return opt_error(k, v, "valid unless v < 4096 || v > 65536 || (v & (v - 1))");
     inf_chunk_ = (uint32_t)v;
@@ -1663,6 +1672,13 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
   Layout L;        // scratch arena
   Layout CO;       // coefficient arena (zero-filled per batch)
   Layout IN;       // input arena (host path)
+  // The chunk-parallel inflate's entries (CH, 2 bytes per output byte, most
+  // of a PNG batch's memory) are dead once k_inf_resolve has turned them into
+  // raw bytes, before anything writes the buffers of the unfilter / expand /
+  // resize stages (LT).  Both regions are laid out from 0 and placed at the
+  // same offset of the scratch arena (option "png_alias", default on).
+  Layout LT, CH;
+  const bool alias = png_alias_;
   std::vector<size_t> in_off(n, 0);
   size_t out_total = 0;
   uint64_t ckpt_total = 0;  // checkpoint records of the batch (per-image sub_bits)
@@ -1681,6 +1697,9 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     // alpha programs: buffer = dst of pass `stage` (-1: the decoded image), byte offset
     int aop_stage[kAlphaPoints];
     size_t aop_off[kAlphaPoints];
+    // offsets taken from the late region (LT): bit 0 unf, 1 pix, 2 out, 3 + s pass_dst[s]
+    uint32_t late = 0;
+    int img = -1;
   };
   std::vector<Offs> offs;
   for (int i = 0; i < n; i++) {
@@ -1690,6 +1709,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     memset(&d, 0, sizeof(d));
     Offs o;
     memset(&o, 0, sizeof(o));
+    o.late = 0;
+    o.img = i;
     for (int s_ = 0; s_ < kStages; s_++) o.pass_cache[s_] = -1;
     uint32_t W, H, C;
     size_t cur_stride;
@@ -1730,7 +1751,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
           // entries (2 bytes per output byte) are most of a PNG batch's device memory: 3x made them
           // 6x the raw image
           const double ratio = (double)want / (double)g.zlen;
-          const uint64_t cap = std::min<uint64_t>(want, (uint64_t)(0.1 * inf_cap_ * ratio * span) + 65536);
+          const uint64_t cap = std::min<uint64_t>(want, (uint64_t)(0.1 * inf_cap_ * ratio * span) + inf_pad_);
           for (uint32_t k = 0; k < nch; k++) {
             InfChunk c;
             memset(&c, 0, sizeof(c));
@@ -1739,17 +1760,19 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
             c.span = span;
             c.cap = (uint32_t)cap;
             c.start = k == 0 ? 16u : kInfNone;  // chunk 0: first block after the 2-byte zlib header
-            c.out = L.take(cap * 2, 256);       // offsets: made absolute below
-            c.tab = L.take(kInfTabBytes, 256);
+            c.out = (alias ? CH : L).take(cap * 2, 256);  // offsets: made absolute below
+            c.tab = (alias ? CH : L).take(kInfTabBytes, 256);
             b.ichunks.push_back(c);
           }
         }
       }
       o.raw = L.take((size_t)g.rawlen + 16, 256);
-      o.unf = L.take(g.interlace ? (size_t)g.unflen + 16 : (size_t)H * pd.ustride, 256);
+      o.unf = (alias ? LT : L).take(g.interlace ? (size_t)g.unflen + 16 : (size_t)H * pd.ustride, 256);
+      o.late |= alias ? 1u : 0u;
       if (pd.expand) {
         d.pix_stride = (uint32_t)align_up((size_t)W * C, 16);
-        o.pix = L.take((size_t)d.pix_stride * H);
+        o.pix = (alias ? LT : L).take((size_t)d.pix_stride * H);
+        o.late |= alias ? 2u : 0u;
       } else {
         d.pix_stride = pd.ustride;
       }
@@ -1937,7 +1960,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
       ps.C = C;
       ps.dst_stride = (uint32_t)align_up((size_t)width * C, 16);
       o.pass_srcoff[stage] = (size_t)xoff * C;  // column window of the source (V passes)
-      o.pass_dst[stage] = L.take((size_t)ps.dst_stride * ps.rows);
+      o.pass_dst[stage] = (alias ? LT : L).take((size_t)ps.dst_stride * ps.rows);
+      o.late |= alias ? 8u << stage : 0u;
       o.pass_cache[stage] = ccache_lookup(ps, b, o.pass_hit[stage]);
       if (o.pass_cache[stage] < 0) {
         o.pass_coef[stage] = L.take((size_t)out_size * ps.ksize * 2);
@@ -2060,7 +2084,8 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
         d.copy_mode = (has_cfg_ && !(W == p.out_w && H == p.out_h)) ? 3 : 4;
     }
     if (host_io) {
-      o.out = L.take(p.out_bytes, 16);
+      o.out = (alias ? LT : L).take(p.out_bytes, 16);
+      o.late |= alias ? 4u : 0u;
       b.out_dev_off[i] = o.out;
       out_total += p.out_bytes;
     }
@@ -2114,6 +2139,24 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
     b.descs.push_back(d);
     offs.push_back(o);
     (void)last_stage;
+  }
+  if (alias) {  // the late buffers and the chunk entries share one region after the early ones
+    const size_t r0 = align_up(L.off, 256);
+    L.off = r0 + std::max(LT.off, CH.off);
+    for (Offs &o : offs) {
+      if (o.late & 1u) o.unf += r0;
+      if (o.late & 2u) o.pix += r0;
+      if (o.late & 4u) {
+        o.out += r0;
+        b.out_dev_off[o.img] = o.out;
+      }
+      for (int s = 0; s < kStages; s++)
+        if ((o.late & (8u << s)) && o.pass_dst[s] != (size_t)-1) o.pass_dst[s] += r0;
+    }
+    for (InfChunk &c : b.ichunks) {
+      c.out += r0;
+      c.tab += r0;
+    }
   }
   b.total_subs = sub_base;
   if (b.any_enc) {  // encoder bit buffers: one contiguous region, zeroed with one memset per batch
