@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--serial-steps", type=int, default=3,
                     help="untimed batches run one at a time after the timed region: per-kernel times without "
                          "the overlap of consecutive batches (roofline_isolated)")
-    ap.add_argument("--pmc-json", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05",
+    ap.add_argument("--pmc-json", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06",
                                                        "pmc", "pmc_traffic.json"),
                     help="per-stage HBM bytes from a PMC run of this configuration (tools/pmc_traffic.py)")
     ap.add_argument("--wg-timing", action="store_true", help="debug: per-workgroup timing of the entropy kernels")
