@@ -84,7 +84,8 @@ def main(root, config=None, images_per_batch=None):
         rows = [r for f in files for r in csv.DictReader(open(f)) if r["Counter_Name"] in weights]
         if not rows:
             return None
-        seq = dict(stage_sequence(rows))
+        first = next(iter(weights))  # one row per dispatch for the stage sequence (it counts launches)
+        seq = dict(stage_sequence([r for r in rows if r["Counter_Name"] == first]))
         nbq = len({int(r["Dispatch_Id"]) for r in rows if "k_huff_sync" in r["Kernel_Name"]})
         acc = defaultdict(float)
         for r in rows:
