@@ -438,7 +438,7 @@ class Context {
   bool wg_timing_ = false;
   bool chunked_off_ = false;  // option "png_chunked" = 0
   uint32_t inf_chunk_ = kInfChunk;  // option "inf_chunk"
-  uint32_t inf_cap_ = 15;           // option "inf_cap": chunk entries, tenths of the expansion of a span
+  uint32_t inf_cap_ = 30;           // option "inf_cap": chunk entries, tenths of the expansion of a span
   bool png_alias_ = true;           // option "png_alias": chunk entries alias the unfilter/resize buffers
   uint32_t inf_pad_ = 65536;        // option "inf_pad": chunk entries on top of inf_cap's
   uint32_t inf_stage3_ = 32;        // option "inf_stage3"
