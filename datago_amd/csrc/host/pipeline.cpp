@@ -621,6 +621,10 @@ dg_status Context::set_option(const std::string &k, int64_t v) {
     h_prefetch_ = v != 0;
     return DG_OK;
   }
+  if (k == "h_planar") {
+    h_planar_ = v != 0;
+    return DG_OK;
+  }
   if (k == "destuff_one") {
     destuff_one_ = v != 0;
     return DG_OK;
@@ -3001,7 +3005,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
   launch_band_dec(sl.st, dd, lst(L_DEC), b.decclass, qp, dec_strips_ | (dec_dbg_ << 16));
   launch_resize_hm(sl.st, dd, lst(L_RM0), b.hmclass[0], 0);
-  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0, h_prefetch_);
+  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0, h_prefetch_, h_planar_);
   launch_resize_hv(sl.st, dd, lst(L_RHV), b.hvclass);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
@@ -3010,7 +3014,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_hm(sl.st, dd, lst(L_RM2), b.hmclass[1], 2);
-  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2, h_prefetch_);
+  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2, h_prefetch_, h_planar_);
   launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3, v_units_);

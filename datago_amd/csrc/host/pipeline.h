@@ -465,6 +465,7 @@ class Context {
   bool sparse_coef_ = true;             // option "sparse_coef": k_huff_write stores, k_idct_t loads, only the
                                         // 16-byte parts through each block's last nonzero (ImageDesc::ccnt)
   bool h_prefetch_ = true;              // option "h_prefetch": specialised fused fills load the next band before the convolution
+  bool h_planar_ = true;                // option "h_planar": fused 8/16-tap band passes over planar u16-pair segments (k_resize_hbp)
   bool destuff_one_ = false;            // option "destuff_one": single-pass destuff with decoupled look-back
                                         // (configs[1] 0.66 vs 0.43 ms three-pass: off)
   bool chroma_rec_ = true;              // option "chroma_rec": half-rate chroma planes as 8-byte records (dg_plane.h)

@@ -1993,6 +1993,14 @@ __device__ __forceinline__ void hfill_bytes4(const DG_GLOBAL uint8_t *row, uint3
 }
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
+// tap pairs read per step of the band convolutions (k_resize_hb: DG_HB_STEP,
+// k_resize_hbp: DG_HPL_STEP); build-time, for A/B builds
+#ifndef DG_HB_STEP
+#define DG_HB_STEP 2
+#endif
+#ifndef DG_HPL_STEP
+#define DG_HPL_STEP 2
+#endif
 
 template <int KMAX, int C, uint32_t SEGSTRIDE = kHSegStride, bool RING = false>
 __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, const uint32_t *kw2,
@@ -2015,20 +2023,33 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
     // starts), so each pair is one 8-byte-aligned ds_read_b64: half the LDS
     // instructions, and banked over 64 dwords instead of 32, so the lanes'
     // stride-s reads (s = the downscale factor) stop conflicting up to s = 2.
+    // Two pairs per step (a second pair past the window has zero weights):
+    // a step's reads issue together instead of each pair's being waited for
+    // before the next pair's issue (the per-pair exit splits the blocks).
     const uint32_t offe = off & ~1u;
+    constexpr int NP = KMAX > 0 ? (KMAX + 1) / 2 : 1, S = DG_HB_STEP;
 #pragma unroll
-    for (int j = 0; j < (KMAX > 0 ? (KMAX + 1) / 2 : 1); j++) {
+    for (int j = 0; j < NP; j += S) {
       if ((uint32_t)(2 * j) >= ksize + 1) break;
-      const s16x2 w = __builtin_bit_cast(s16x2, kw2[j]);
+      u32x2 vv[S][R];
 #pragma unroll
-      for (uint32_t r = 0; r < R; r++) {
-        const u32x2 vv = *(const u32x2 *)(seg + (r0 + 2 * r) * SEGSTRIDE + offe + 2 * j);
-        const uint32_t v0 = vv.x, v1 = vv.y;
+      for (int h = 0; h < S; h++)
 #pragma unroll
-        for (int c = 0; c < C; c++) {
-          const uint32_t sel = 0x0C000C00u | ((4u + (uint32_t)c) << 16) | (uint32_t)c;  // [v0.c, 0, v1.c, 0]
-          const uint32_t pr = __builtin_amdgcn_perm(v1, v0, sel);
-          a[r][c] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pr), w, a[r][c], false);
+        for (uint32_t r = 0; r < R; r++)
+          vv[h][r] = j + h < NP ? *(const u32x2 *)(seg + (r0 + 2 * r) * SEGSTRIDE + offe + 2 * (j + h)) : u32x2{0, 0};
+#pragma unroll
+      for (int h = 0; h < S; h++) {
+        if (j + h >= NP) break;
+        const s16x2 w = __builtin_bit_cast(s16x2, kw2[j + h]);
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+          const uint32_t v0 = vv[h][r].x, v1 = vv[h][r].y;
+#pragma unroll
+          for (int c = 0; c < C; c++) {
+            const uint32_t sel = 0x0C000C00u | ((4u + (uint32_t)c) << 16) | (uint32_t)c;  // [v0.c, 0, v1.c, 0]
+            const uint32_t pr = __builtin_amdgcn_perm(v1, v0, sel);
+            a[r][c] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pr), w, a[r][c], false);
+          }
         }
       }
     }
@@ -2237,6 +2258,280 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX == 8 ?
     }
   }
   hband<KMAX, FUSED, FC_GENERIC, false>(im, ps, it.item0, seg, ob, ext);
+}
+
+// ---- band H pass over a planar segment (option "h_planar", k_resize_hbp)
+//
+// The first pass of a colour JPEG with up to 16 taps, as k_resize_hb<K,
+// true> computes it (same work items, fill jobs, weights and sums: the
+// bytes are equal), but the band's LDS segment holds each row's channels
+// as planes of u16 pixel pairs -- pixel 2i in the low half of dword i, 2i + 1
+// in the high half, the v_dot2_i32_i16 operand as it is -- instead of one
+// dword per pixel.  The convolution then reads one dword per tap pair and
+// channel and feeds it to the dot2 unchanged (k_resize_hb spends a v_perm
+// per tap pair and channel building that operand from pixel dwords), and
+// the 4:2:0 zune fill (the configs[1] headline's layout) upsamples and
+// colour-converts two pixels per instruction in packed 16-bit arithmetic,
+// its results already in that layout.  Other fill classes convert their
+// pixel dwords (three v_perm per pixel pair).
+//   A measured split of k_resize_hb<16> (round 6, resize_h1 1.80 ms per
+// configs[1] batch): without the fill arithmetic 1.28 ms, without the
+// convolution 1.24, without the plane loads 1.68 -- the kernel follows its
+// VALU work, not its loads.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+template <class T, class S>
+__device__ __forceinline__ T bcast(S v) {
+  return __builtin_bit_cast(T, v);
+}
+constexpr uint32_t hpl_stride(int kmax) { return hseg_px(kmax) / 2 + 4; }  // dwords per row-channel plane
+
+// One octet of the 4:2:0 zune fill (hcolor_fc8<FC_420_Z>'s arithmetic) as
+// u16 pairs per channel: R[i] = (pixel 2i, pixel 2i + 1) of the octet.
+__device__ __forceinline__ void hpl_420z(const ImageDesc &im, const FillRaw &f, uint32_t x0, uint32_t R[4],
+                                         uint32_t G[4], uint32_t B[4]) {
+  // the 6 samples of a chroma record (load_crec6's order: left neighbour,
+  // 4 samples, right neighbour) as 3 pairs
+  auto rec3 = [](u32x2 w, u16x2 c[3]) {
+    c[0] = bcast<u16x2>(__builtin_amdgcn_perm(w.x, w.y, 0x0C040C00u));
+    c[1] = bcast<u16x2>(__builtin_amdgcn_perm(0u, w.x, 0x0C020C01u));
+    c[2] = bcast<u16x2>(__builtin_amdgcn_perm(w.y, w.x, 0x0C050C03u));
+  };
+  const bool edge = (x0 >> 1) + 4u == im.cbw[1] * 8u;  // the padded chroma row's last 4 samples: zune's quirk
+  const u16x2 two = {2, 2}, three = {3, 3};
+  u16x2 Cp[2][4];  // Cb, Cr: pixel pairs (0,1), (2,3), (4,5), (6,7)
+#pragma unroll
+  for (int pl = 0; pl < 2; pl++) {
+    u16x2 n[3], fa[3], c[3];
+    rec3(pl ? f.r0 : f.b0, n);
+    rec3(pl ? f.r1 : f.b1, fa);
+#pragma unroll
+    for (int i = 0; i < 3; i++) c[i] = (n[i] * three + fa[i] + two) >> 2;  // vertical: (3 near + far + 2) >> 2
+    // horizontal: even_k = (3 c[k+1] + 2 + c[k]) >> 2, odd_k = (3 c[k+1] + 2 + c[k+2]) >> 2
+    const u16x2 s12 = bcast<u16x2>(__builtin_amdgcn_perm(bcast<uint32_t>(c[1]), bcast<uint32_t>(c[0]), 0x05040302u));
+    const u16x2 s34 = bcast<u16x2>(__builtin_amdgcn_perm(bcast<uint32_t>(c[2]), bcast<uint32_t>(c[1]), 0x05040302u));
+    const u16x2 t12 = s12 * three + two, t34 = s34 * three + two;
+    const uint32_t e01 = bcast<uint32_t>((t12 + c[0]) >> 2), o01 = bcast<uint32_t>((t12 + c[1]) >> 2);
+    uint32_t e23 = bcast<uint32_t>((t34 + c[1]) >> 2), o23 = bcast<uint32_t>((t34 + c[2]) >> 2);
+    if (edge) {  // even_3 = (3 c[3] + c[4] + 2) >> 2 (= odd_2), odd_3 = c[4]
+      e23 = __builtin_amdgcn_perm(o23, e23, 0x05040100u);
+      o23 = __builtin_amdgcn_perm(bcast<uint32_t>(c[2]), o23, 0x05040100u);
+    }
+    Cp[pl][0] = bcast<u16x2>(__builtin_amdgcn_perm(o01, e01, 0x05040100u));
+    Cp[pl][1] = bcast<u16x2>(__builtin_amdgcn_perm(o01, e01, 0x07060302u));
+    Cp[pl][2] = bcast<u16x2>(__builtin_amdgcn_perm(o23, e23, 0x05040100u));
+    Cp[pl][3] = bcast<u16x2>(__builtin_amdgcn_perm(o23, e23, 0x07060302u));
+  }
+  const s16x2 c128 = {128, 128}, zero = {0, 0}, c255 = {255, 255};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t yw = i < 2 ? f.y.x : f.y.y;
+    const s16x2 y = bcast<s16x2>(__builtin_amdgcn_perm(0u, yw, (i & 1) ? 0x0C030C02u : 0x0C010C00u));
+    const s16x2 xcb = bcast<s16x2>(Cp[0][i]) - c128, xcr = bcast<s16x2>(Cp[1][i]) - c128;
+    // ycc_to_rgb_zune in 16 bits: every product and sum fits (|x| <= 128)
+    s16x2 r = y + ((xcr * (s16x2){45, 45}) >> 5);
+    s16x2 g = y - ((xcb * (s16x2){11, 11} + xcr * (s16x2){23, 23}) >> 5);
+    s16x2 b = y + ((xcb * (s16x2){113, 113}) >> 6);
+    r = __builtin_elementwise_min(__builtin_elementwise_max(r, zero), c255);
+    g = __builtin_elementwise_min(__builtin_elementwise_max(g, zero), c255);
+    b = __builtin_elementwise_min(__builtin_elementwise_max(b, zero), c255);
+    R[i] = bcast<uint32_t>(r);
+    G[i] = bcast<uint32_t>(g);
+    B[i] = bcast<uint32_t>(b);
+  }
+}
+
+// pixel dwords (RGB in bytes 0..2) -> u16 pairs per channel
+__device__ __forceinline__ void hpl_split(const uint32_t v[8], uint32_t R[4], uint32_t G[4], uint32_t B[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    R[i] = __builtin_amdgcn_perm(v[2 * i + 1], v[2 * i], 0x0C040C00u);
+    G[i] = __builtin_amdgcn_perm(v[2 * i + 1], v[2 * i], 0x0C050C01u);
+    B[i] = __builtin_amdgcn_perm(v[2 * i + 1], v[2 * i], 0x0C060C02u);
+  }
+}
+
+template <int KMAX, uint32_t SPS>
+__device__ __forceinline__ void hconv_rows_pl(const uint32_t *segp, uint32_t pb, const uint32_t *kw2, uint32_t ksize,
+                                              uint32_t r0, uint32_t nrows, int32_t prec, uint8_t *ob, uint32_t col) {
+  constexpr uint32_t R = kHBandRows / 2;  // rows r0, r0 + 2, ...
+  const int32_t bias = 1 << (prec - 1);
+  int32_t a[R][3];
+#pragma unroll
+  for (uint32_t r = 0; r < R; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) a[r][c] = bias;
+  // Two pairs per step (a second pair past this pass's window has zero
+  // weights, kw2): each step's 24 reads are issued together.  One pair per
+  // step (k_resize_hb's loop) waits for each pair's reads to lgkmcnt(0)
+  // before the next -- 8 exposed LDS round trips per band at 16 taps; all
+  // pairs in one straight-line block hoisted every read and spilled.
+  constexpr int NP = (KMAX + 1) / 2, S = DG_HPL_STEP;
+  static_assert(NP % S == 0, "whole steps");
+  const uint32_t *base = segp + r0 * 3 * SPS + pb;
+#pragma unroll
+  for (int j = 0; j < NP; j += S) {
+    if ((uint32_t)(2 * j) >= ksize + 1) break;
+    uint32_t v[S][R][3];
+#pragma unroll
+    for (int h = 0; h < S; h++)
+#pragma unroll
+      for (uint32_t r = 0; r < R; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) v[h][r][c] = base[(2 * r * 3 + c) * SPS + j + h];
+#pragma unroll
+    for (int h = 0; h < S; h++) {
+      const s16x2 w = bcast<s16x2>(kw2[j + h]);
+#pragma unroll
+      for (uint32_t r = 0; r < R; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) a[r][c] = __builtin_amdgcn_sdot2(bcast<s16x2>(v[h][r][c]), w, a[r][c], false);
+    }
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < R; r++)
+    if (r0 + 2 * r < nrows) {
+      uint8_t *o = ob + (r0 + 2 * r) * (kHBandCols * 4) + col * 3;
+#pragma unroll
+      for (int c = 0; c < 3; c++) o[c] = clip_shift(a[r][c], prec);
+    }
+}
+
+template <int KMAX, int FC, bool PF>
+__device__ __forceinline__ void hband_pl(const ImageDesc &im, const ResizePass &ps, uint32_t item, uint32_t *segp,
+                                         uint8_t *ob, uint32_t *ext) {
+  static_assert(KMAX == 8 || KMAX == 16, "planar segments for the 8- and 16-tap classes");
+  constexpr uint32_t SEGPX = hseg_px(KMAX), SPS = hpl_stride(KMAX);
+  const uint32_t tiles = (ps.width + kHBandCols - 1) / kHBandCols;
+  const uint32_t group = item / tiles, tile = item - group * tiles;
+  const uint32_t x0 = tile * kHBandCols;
+  const uint32_t x1 = x0 + kHBandCols < ps.width ? x0 + kHBandCols : ps.width;
+  const DG_GLOBAL int32_t *bounds = gp<const int32_t>(ps.bounds) + 2 * ps.out0;
+  const uint32_t ksize = ps.ksize;
+  const DG_GLOBAL int16_t *coef = gp<const int16_t>(ps.coef) + (size_t)ps.out0 * ksize;
+  const uint32_t t = threadIdx.x, col = t & (kHBandCols - 1), x = x0 + col;
+  const bool valid = x < x1;
+  uint32_t st = 0, n = 0;
+  if (valid) {
+    st = (uint32_t)bounds[2 * x];
+    n = (uint32_t)bounds[2 * x + 1];
+  }
+  if (t == 0) {
+    ext[0] = 0xFFFFFFFFu;
+    ext[1] = 0;
+  }
+  __syncthreads();
+  if (valid && t < kHBandCols) {
+    atomicMin(&ext[0], st);
+    atomicMax(&ext[1], st + ksize);
+  }
+  __syncthreads();
+  const uint32_t p0 = ext[0] & ~7u;
+  uint32_t p1 = ext[1];
+  if (p1 - p0 > SEGPX) p1 = p0 + SEGPX;  // host sizing guarantees this never triggers
+  const uint32_t pe = p1 < ps.in_size ? p1 : ps.in_size;
+  uint32_t kw2[(KMAX + 1) / 2];  // weights (w_2j, w_2j+1) as i16 x 2
+  const DG_GLOBAL int16_t *kp = coef + (size_t)(valid ? x : x0) * ksize;
+  {
+    const uint32_t sh = (st - p0) & 1u;
+#pragma unroll
+    for (int j = 0; j < (KMAX + 1) / 2; j++) {
+      const int32_t tl = 2 * j - (int32_t)sh, th = tl + 1;
+      const uint32_t lo = (valid && tl >= 0 && (uint32_t)tl < n) ? (uint16_t)kp[tl] : 0u;
+      const uint32_t hi = (valid && (uint32_t)th < n) ? (uint16_t)kp[th] : 0u;
+      kw2[j] = lo | (hi << 16);
+    }
+  }
+  const uint32_t fr = t >> 5, fl = t & 31;  // store: 32 threads per row
+  const uint32_t pb = (st - p0) >> 1, r0 = t / kHBandCols;  // pair index of the window's first pair
+  const uint32_t njob_row = (pe - p0 + 7) >> 3;
+  const uint32_t inv_row = ((1u << 20) - 1u + njob_row) / (njob_row ? njob_row : 1u);
+  const int32_t prec = ps.precision;
+  const uint32_t rb = (x1 - x0) * 3;
+  const uint32_t ybeg = group * kHBandRows * ps.bands;
+  constexpr bool PREFETCH = FC != FC_GENERIC && PF;
+  FillRaw pre;
+  if (PREFETCH && ybeg < ps.rows) {
+    const uint32_t nr0 = ps.rows - ybeg < kHBandRows ? ps.rows - ybeg : kHBandRows;
+    if (t < nr0 * njob_row) {
+      const uint32_t r = __umul24(t, inv_row) >> 20, q = t - r * njob_row;
+      pre = hload_fc8<FC>(im, ps.row0 + ybeg + r, p0 + 8 * q);
+    }
+  }
+  for (uint32_t bi = 0; bi < ps.bands; bi++) {
+    const uint32_t y0 = ybeg + bi * kHBandRows;
+    if (y0 >= ps.rows) break;
+    const uint32_t nrows = ps.rows - y0 < kHBandRows ? ps.rows - y0 : kHBandRows;
+    const uint32_t njob = nrows * njob_row;
+    for (uint32_t j = t; j < njob; j += 256) {
+      const uint32_t r = __umul24(j, inv_row) >> 20, q = j - r * njob_row;
+      uint32_t Rw[4], Gw[4], Bw[4];
+      if (FC == FC_GENERIC) {
+        uint32_t v[8];
+        hcolor8(im, ps.row0 + y0 + r, p0 + 8 * q, v);
+        hpl_split(v, Rw, Gw, Bw);
+      } else {
+        const FillRaw f = (PREFETCH && j == t) ? pre : hload_fc8<FC>(im, ps.row0 + y0 + r, p0 + 8 * q);
+        if (FC == FC_420_Z) {
+          hpl_420z(im, f, p0 + 8 * q, Rw, Gw, Bw);
+        } else {
+          uint32_t v[8];
+          hcolor_fc8<FC>(im, f, p0 + 8 * q, v);
+          hpl_split(v, Rw, Gw, Bw);
+        }
+      }
+      uint32_t *d = segp + r * 3 * SPS + 4 * q;
+      *(u32x4 *)d = u32x4{Rw[0], Rw[1], Rw[2], Rw[3]};
+      *(u32x4 *)(d + SPS) = u32x4{Gw[0], Gw[1], Gw[2], Gw[3]};
+      *(u32x4 *)(d + 2 * SPS) = u32x4{Bw[0], Bw[1], Bw[2], Bw[3]};
+    }
+    __syncthreads();
+    if (PREFETCH) {
+      const uint32_t y1 = y0 + kHBandRows;
+      if (bi + 1 < ps.bands && y1 < ps.rows) {
+        const uint32_t nr1 = ps.rows - y1 < kHBandRows ? ps.rows - y1 : kHBandRows;
+        if (t < nr1 * njob_row) {
+          const uint32_t r = __umul24(t, inv_row) >> 20, q = t - r * njob_row;
+          pre = hload_fc8<FC>(im, ps.row0 + y1 + r, p0 + 8 * q);
+        }
+      }
+    }
+    if (valid) hconv_rows_pl<KMAX, SPS>(segp, pb, kw2, ksize, r0, nrows, prec, ob, col);
+    __syncthreads();
+    DG_GLOBAL uint8_t *dst = gp<uint8_t>(ps.dst) + (size_t)y0 * ps.dst_stride + (size_t)x0 * 3;
+    if (fr < nrows && fl * 16 < rb) {
+      const uint32_t r = fr, b = fl * 16;
+      DG_GLOBAL uint8_t *d = dst + (size_t)r * ps.dst_stride + b;
+      const uint8_t *o = ob + r * (kHBandCols * 4) + b;
+      if (b + 16 <= rb && (((uintptr_t)d) & 15) == 0) {
+        *(DG_GLOBAL u32x4 *)d = *(const u32x4 *)o;
+      } else {
+        const uint32_t e = b + 16 < rb ? 16 : rb - b;
+        for (uint32_t i = 0; i < e; i++) d[i] = o[i];
+      }
+    }
+  }
+}
+
+// 6 waves per SIMD for 8 taps (80 VGPRs: without the next-band prefetch,
+// which would spill there -- measured level with it, round 6), 5 for 16.
+template <int KMAX, bool PF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX == 8 ? 6 : 5))) void k_resize_hbp(
+    const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list, int stage) {
+  __shared__ __attribute__((aligned(16))) uint32_t segp[kHBandRows * 3 * hpl_stride(KMAX)];
+  __shared__ __attribute__((aligned(16))) uint8_t ob[kHBandRows * kHBandCols * 4];
+  __shared__ uint32_t ext[2];
+  const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
+  const ImageDesc &im = imgs[it.image];
+  const ResizePass &ps = im.pass[stage];
+  switch (fill_class(im)) {
+    case FC_420: hband_pl<KMAX, FC_420, PF>(im, ps, it.item0, segp, ob, ext); return;
+    case FC_420_Z: hband_pl<KMAX, FC_420_Z, PF>(im, ps, it.item0, segp, ob, ext); return;
+    case FC_422: hband_pl<KMAX, FC_422, PF>(im, ps, it.item0, segp, ob, ext); return;
+    case FC_422_Z: hband_pl<KMAX, FC_422_Z, PF>(im, ps, it.item0, segp, ob, ext); return;
+    case FC_444: hband_pl<KMAX, FC_444, PF>(im, ps, it.item0, segp, ob, ext); return;
+    case FC_444_Z: hband_pl<KMAX, FC_444_Z, PF>(im, ps, it.item0, segp, ob, ext); return;
+    default: hband_pl<KMAX, FC_GENERIC, false>(im, ps, it.item0, segp, ob, ext); return;
+  }
 }
 
 // ---- band H pass on the matrix cores (k_resize_hm)
@@ -2979,9 +3274,28 @@ static void launch_hb_classes(hipStream_t st, const ImageDesc *imgs, const WgIte
   DG_LAUNCH((k_resize_hb<0, FUSED>), ncls[3], st, imgs, list, stage);
   list += ncls[3];
 }
+// The fused classes with a planar segment (h_planar): 8 and 16 taps on
+// k_resize_hbp, the wider ones on k_resize_hb (their planar segment would
+// cost a resident workgroup per CU)
+template <bool PF>
+static void launch_hb_fused_planar(hipStream_t st, const ImageDesc *imgs, const WgItem *&list, const uint32_t ncls[4],
+                                   int stage) {
+  DG_LAUNCH((k_resize_hbp<8, false>), ncls[0], st, imgs, list, stage);
+  list += ncls[0];
+  DG_LAUNCH((k_resize_hbp<16, PF>), ncls[1], st, imgs, list, stage);
+  list += ncls[1];
+  DG_LAUNCH((k_resize_hb<32, true, PF>), ncls[2], st, imgs, list, stage);
+  list += ncls[2];
+  DG_LAUNCH((k_resize_hb<0, true>), ncls[3], st, imgs, list, stage);
+  list += ncls[3];
+}
 void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][4],
-                      int stage, bool prefetch) {
-  if (prefetch)
+                      int stage, bool prefetch, bool planar) {
+  if (planar && prefetch)
+    launch_hb_fused_planar<true>(st, imgs, list, ncls[1], stage);
+  else if (planar)
+    launch_hb_fused_planar<false>(st, imgs, list, ncls[1], stage);
+  else if (prefetch)
     launch_hb_classes<true, true>(st, imgs, list, ncls[1], stage);
   else
     launch_hb_classes<true, false>(st, imgs, list, ncls[1], stage);

@@ -603,6 +603,48 @@ def test_v_tile_bit_exact(v_tile):
             assert np.array_equal(a1, O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]), O.MODE_FIR))
 
 
+@pytest.mark.parametrize("sem", SEMS, ids=SEM_IDS)
+def test_h_planar_bit_exact(sem):
+    """Option h_planar: the fused 8- and 16-tap band H passes over planar
+    u16-pair segments (k_resize_hbp; the 4:2:0 zune fill in packed 16-bit
+    arithmetic) equal k_resize_hb (h_planar 0) and the oracle byte for byte:
+    every fill class (4:2:0 / 4:2:2 / 4:4:4, gray, an RGB-transform JPEG on
+    the generic fill), widths whose padded chroma row ends inside the
+    segment (zune's last-pair quirk) or past it, odd window starts, 1x-2.5x
+    downscales (both planar classes) and wider ones (k_resize_hb's 32-tap
+    class beside them), upscales, x.5 crops, with and without the next-band
+    prefetch."""
+    from datago_amd import _lib as L
+    dims = [(1100, 1500), (2048, 1536), (333, 777), (1300, 700), (1024, 1024), (1040, 1568), (2600, 1100),
+            (777, 2048), (1536, 1536), (903, 1601), (2304, 1296), (3000, 1000)]
+    subs = ["4:2:0", "4:2:0", "4:2:2", "4:4:4", "4:2:0", "4:2:0", "4:2:0", "4:2:2", "4:4:4", "4:2:0", "4:2:0",
+            "4:2:0"]
+    datas = [synth.make_jpeg(1950 + i, w, h, 80 + i, subs[i], gray=i == 6) for i, (w, h) in enumerate(dims)]
+    rgb = io.BytesIO()
+    Image.fromarray(synth.synth_pixels(np.random.default_rng(3), 1200, 900, False)).save(
+        rgb, "JPEG", quality=90, keep_rgb=True)
+    datas.append(rgb.getvalue())
+    for size, ratio in ((1024, 32), (512, 16)):
+        t = B.ARAwareTransform(size, ratio, 0.5, 2.0)
+        outs = {}
+        for hp, pf in ((0, 1), (1, 1), (1, 0)):
+            ctx = L.Context(0, crop_and_resize=True, default_image_size=size, downsampling_ratio=ratio,
+                            min_aspect_ratio=0.5, max_aspect_ratio=2.0, decode_semantics=sem)
+            ctx.set_option("h_planar", hp)
+            ctx.set_option("h_prefetch", pf)
+            outs[(hp, pf)] = ctx.decode_batch(datas)
+            ctx.close()
+        for k, d in enumerate(datas):
+            s0, a0, _ = outs[(0, 1)][k]
+            assert s0 == 0
+            for key in ((1, 1), (1, 0)):
+                s1, a1, _ = outs[key][k]
+                assert s1 == 0 and a1.shape == a0.shape and np.array_equal(a0, a1), (size, k, key)
+            dec = _oracle_decoded(d, sem)
+            assert np.array_equal(a0, O.crop_and_resize(dec, *t.target_size(dec.shape[1], dec.shape[0]),
+                                                        O.MODE_FIR)), (size, k)
+
+
 @pytest.mark.parametrize("sub_bits,lead", [(0, -1), (1024, -1), (4096, 0), (8192, -1), (2048, 6144)])
 def test_sync2_bit_exact(sub_bits, lead):
     """Option sync2: k_huff_sync2 runs two lead-in + range chains per lane
