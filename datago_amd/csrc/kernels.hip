@@ -1993,14 +1993,6 @@ __device__ __forceinline__ void hfill_bytes4(const DG_GLOBAL uint8_t *row, uint3
 }
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
-// tap pairs read per step of the band convolutions (k_resize_hb: DG_HB_STEP,
-// k_resize_hbp: DG_HPL_STEP); build-time, for A/B builds
-#ifndef DG_HB_STEP
-#define DG_HB_STEP 2
-#endif
-#ifndef DG_HPL_STEP
-#define DG_HPL_STEP 2
-#endif
 
 template <int KMAX, int C, uint32_t SEGSTRIDE = kHSegStride, bool RING = false>
 __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, const uint32_t *kw2,
@@ -2023,33 +2015,20 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
     // starts), so each pair is one 8-byte-aligned ds_read_b64: half the LDS
     // instructions, and banked over 64 dwords instead of 32, so the lanes'
     // stride-s reads (s = the downscale factor) stop conflicting up to s = 2.
-    // Two pairs per step (a second pair past the window has zero weights):
-    // a step's reads issue together instead of each pair's being waited for
-    // before the next pair's issue (the per-pair exit splits the blocks).
     const uint32_t offe = off & ~1u;
-    constexpr int NP = KMAX > 0 ? (KMAX + 1) / 2 : 1, S = DG_HB_STEP;
 #pragma unroll
-    for (int j = 0; j < NP; j += S) {
+    for (int j = 0; j < (KMAX > 0 ? (KMAX + 1) / 2 : 1); j++) {
       if ((uint32_t)(2 * j) >= ksize + 1) break;
-      u32x2 vv[S][R];
+      const s16x2 w = __builtin_bit_cast(s16x2, kw2[j]);
 #pragma unroll
-      for (int h = 0; h < S; h++)
+      for (uint32_t r = 0; r < R; r++) {
+        const u32x2 vv = *(const u32x2 *)(seg + (r0 + 2 * r) * SEGSTRIDE + offe + 2 * j);
+        const uint32_t v0 = vv.x, v1 = vv.y;
 #pragma unroll
-        for (uint32_t r = 0; r < R; r++)
-          vv[h][r] = j + h < NP ? *(const u32x2 *)(seg + (r0 + 2 * r) * SEGSTRIDE + offe + 2 * (j + h)) : u32x2{0, 0};
-#pragma unroll
-      for (int h = 0; h < S; h++) {
-        if (j + h >= NP) break;
-        const s16x2 w = __builtin_bit_cast(s16x2, kw2[j + h]);
-#pragma unroll
-        for (uint32_t r = 0; r < R; r++) {
-          const uint32_t v0 = vv[h][r].x, v1 = vv[h][r].y;
-#pragma unroll
-          for (int c = 0; c < C; c++) {
-            const uint32_t sel = 0x0C000C00u | ((4u + (uint32_t)c) << 16) | (uint32_t)c;  // [v0.c, 0, v1.c, 0]
-            const uint32_t pr = __builtin_amdgcn_perm(v1, v0, sel);
-            a[r][c] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pr), w, a[r][c], false);
-          }
+        for (int c = 0; c < C; c++) {
+          const uint32_t sel = 0x0C000C00u | ((4u + (uint32_t)c) << 16) | (uint32_t)c;  // [v0.c, 0, v1.c, 0]
+          const uint32_t pr = __builtin_amdgcn_perm(v1, v0, sel);
+          a[r][c] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, pr), w, a[r][c], false);
         }
       }
     }
@@ -2360,32 +2339,19 @@ __device__ __forceinline__ void hconv_rows_pl(const uint32_t *segp, uint32_t pb,
   for (uint32_t r = 0; r < R; r++)
 #pragma unroll
     for (int c = 0; c < 3; c++) a[r][c] = bias;
-  // Two pairs per step (a second pair past this pass's window has zero
-  // weights, kw2): each step's 24 reads are issued together.  One pair per
-  // step (k_resize_hb's loop) waits for each pair's reads to lgkmcnt(0)
-  // before the next -- 8 exposed LDS round trips per band at 16 taps; all
-  // pairs in one straight-line block hoisted every read and spilled.
-  constexpr int NP = (KMAX + 1) / 2, S = DG_HPL_STEP;
-  static_assert(NP % S == 0, "whole steps");
-  const uint32_t *base = segp + r0 * 3 * SPS + pb;
+  // (Two pairs per step, their 24 reads issued together, measured slower:
+  // resize_h1 1.69-1.72 vs 1.65-1.70 ms, round 6.)
 #pragma unroll
-  for (int j = 0; j < NP; j += S) {
+  for (int j = 0; j < (KMAX + 1) / 2; j++) {
     if ((uint32_t)(2 * j) >= ksize + 1) break;
-    uint32_t v[S][R][3];
+    const s16x2 w = bcast<s16x2>(kw2[j]);
 #pragma unroll
-    for (int h = 0; h < S; h++)
+    for (uint32_t r = 0; r < R; r++)
 #pragma unroll
-      for (uint32_t r = 0; r < R; r++)
-#pragma unroll
-        for (int c = 0; c < 3; c++) v[h][r][c] = base[(2 * r * 3 + c) * SPS + j + h];
-#pragma unroll
-    for (int h = 0; h < S; h++) {
-      const s16x2 w = bcast<s16x2>(kw2[j + h]);
-#pragma unroll
-      for (uint32_t r = 0; r < R; r++)
-#pragma unroll
-        for (int c = 0; c < 3; c++) a[r][c] = __builtin_amdgcn_sdot2(bcast<s16x2>(v[h][r][c]), w, a[r][c], false);
-    }
+      for (int c = 0; c < 3; c++) {
+        const uint32_t pr = segp[((r0 + 2 * r) * 3 + c) * SPS + pb + j];
+        a[r][c] = __builtin_amdgcn_sdot2(bcast<s16x2>(pr), w, a[r][c], false);
+      }
   }
 #pragma unroll
   for (uint32_t r = 0; r < R; r++)
