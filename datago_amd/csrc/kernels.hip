@@ -2251,8 +2251,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX == 8 ?
 // per tap pair and channel building that operand from pixel dwords), and
 // the 4:2:0 zune fill (the configs[1] headline's layout) upsamples and
 // colour-converts two pixels per instruction in packed 16-bit arithmetic,
-// its results already in that layout.  Other fill classes convert their
-// pixel dwords (three v_perm per pixel pair).
+// its results already in that layout (4:2:2 and 4:4:4 zune fills too).
+// The libjpeg-mode and generic fills convert their pixel dwords (three
+// v_perm per pixel pair).
 //   A measured split of k_resize_hb<16> (round 6, resize_h1 1.80 ms per
 // configs[1] batch): without the fill arithmetic 1.28 ms, without the
 // convolution 1.24, without the plane loads 1.68 -- the kernel follows its
@@ -2264,41 +2265,58 @@ __device__ __forceinline__ T bcast(S v) {
 }
 constexpr uint32_t hpl_stride(int kmax) { return hseg_px(kmax) / 2 + 4; }  // dwords per row-channel plane
 
-// One octet of the 4:2:0 zune fill (hcolor_fc8<FC_420_Z>'s arithmetic) as
-// u16 pairs per channel: R[i] = (pixel 2i, pixel 2i + 1) of the octet.
-__device__ __forceinline__ void hpl_420z(const ImageDesc &im, const FillRaw &f, uint32_t x0, uint32_t R[4],
+// One octet of a zune fill (hcolor_fc8<FC_4xx_Z>'s arithmetic; SS = 2
+// 4:2:0, 1 4:2:2, 0 4:4:4) as u16 pairs per channel: R[i] = (pixel 2i,
+// pixel 2i + 1) of the octet.
+template <int SS>
+__device__ __forceinline__ void hpl_zune(const ImageDesc &im, const FillRaw &f, uint32_t x0, uint32_t R[4],
                                          uint32_t G[4], uint32_t B[4]) {
-  // the 6 samples of a chroma record (load_crec6's order: left neighbour,
-  // 4 samples, right neighbour) as 3 pairs
-  auto rec3 = [](u32x2 w, u16x2 c[3]) {
-    c[0] = bcast<u16x2>(__builtin_amdgcn_perm(w.x, w.y, 0x0C040C00u));
-    c[1] = bcast<u16x2>(__builtin_amdgcn_perm(0u, w.x, 0x0C020C01u));
-    c[2] = bcast<u16x2>(__builtin_amdgcn_perm(w.y, w.x, 0x0C050C03u));
-  };
-  const bool edge = (x0 >> 1) + 4u == im.cbw[1] * 8u;  // the padded chroma row's last 4 samples: zune's quirk
-  const u16x2 two = {2, 2}, three = {3, 3};
   u16x2 Cp[2][4];  // Cb, Cr: pixel pairs (0,1), (2,3), (4,5), (6,7)
+  if (SS == 0) {  // full-rate chroma: the plane bytes as they are
 #pragma unroll
-  for (int pl = 0; pl < 2; pl++) {
-    u16x2 n[3], fa[3], c[3];
-    rec3(pl ? f.r0 : f.b0, n);
-    rec3(pl ? f.r1 : f.b1, fa);
+    for (int pl = 0; pl < 2; pl++) {
+      const u32x2 w = pl ? f.r0 : f.b0;
 #pragma unroll
-    for (int i = 0; i < 3; i++) c[i] = (n[i] * three + fa[i] + two) >> 2;  // vertical: (3 near + far + 2) >> 2
-    // horizontal: even_k = (3 c[k+1] + 2 + c[k]) >> 2, odd_k = (3 c[k+1] + 2 + c[k+2]) >> 2
-    const u16x2 s12 = bcast<u16x2>(__builtin_amdgcn_perm(bcast<uint32_t>(c[1]), bcast<uint32_t>(c[0]), 0x05040302u));
-    const u16x2 s34 = bcast<u16x2>(__builtin_amdgcn_perm(bcast<uint32_t>(c[2]), bcast<uint32_t>(c[1]), 0x05040302u));
-    const u16x2 t12 = s12 * three + two, t34 = s34 * three + two;
-    const uint32_t e01 = bcast<uint32_t>((t12 + c[0]) >> 2), o01 = bcast<uint32_t>((t12 + c[1]) >> 2);
-    uint32_t e23 = bcast<uint32_t>((t34 + c[1]) >> 2), o23 = bcast<uint32_t>((t34 + c[2]) >> 2);
-    if (edge) {  // even_3 = (3 c[3] + c[4] + 2) >> 2 (= odd_2), odd_3 = c[4]
-      e23 = __builtin_amdgcn_perm(o23, e23, 0x05040100u);
-      o23 = __builtin_amdgcn_perm(bcast<uint32_t>(c[2]), o23, 0x05040100u);
+      for (int i = 0; i < 4; i++)
+        Cp[pl][i] = bcast<u16x2>(__builtin_amdgcn_perm(0u, i < 2 ? w.x : w.y, (i & 1) ? 0x0C030C02u : 0x0C010C00u));
     }
-    Cp[pl][0] = bcast<u16x2>(__builtin_amdgcn_perm(o01, e01, 0x05040100u));
-    Cp[pl][1] = bcast<u16x2>(__builtin_amdgcn_perm(o01, e01, 0x07060302u));
-    Cp[pl][2] = bcast<u16x2>(__builtin_amdgcn_perm(o23, e23, 0x05040100u));
-    Cp[pl][3] = bcast<u16x2>(__builtin_amdgcn_perm(o23, e23, 0x07060302u));
+  } else {
+    // the 6 samples of a chroma record (load_crec6's order: left neighbour,
+    // 4 samples, right neighbour) as 3 pairs
+    auto rec3 = [](u32x2 w, u16x2 c[3]) {
+      c[0] = bcast<u16x2>(__builtin_amdgcn_perm(w.x, w.y, 0x0C040C00u));
+      c[1] = bcast<u16x2>(__builtin_amdgcn_perm(0u, w.x, 0x0C020C01u));
+      c[2] = bcast<u16x2>(__builtin_amdgcn_perm(w.y, w.x, 0x0C050C03u));
+    };
+    const bool edge = (x0 >> 1) + 4u == im.cbw[1] * 8u;  // the padded chroma row's last 4 samples: zune's quirk
+    const u16x2 two = {2, 2}, three = {3, 3};
+#pragma unroll
+    for (int pl = 0; pl < 2; pl++) {
+      u16x2 c[3];
+      rec3(pl ? f.r0 : f.b0, c);
+      if (SS == 2) {  // vertical: (3 near + far + 2) >> 2
+        u16x2 fa[3];
+        rec3(pl ? f.r1 : f.b1, fa);
+#pragma unroll
+        for (int i = 0; i < 3; i++) c[i] = (c[i] * three + fa[i] + two) >> 2;
+      }
+      // horizontal: even_k = (3 c[k+1] + 2 + c[k]) >> 2, odd_k = (3 c[k+1] + 2 + c[k+2]) >> 2
+      const u16x2 s12 =
+          bcast<u16x2>(__builtin_amdgcn_perm(bcast<uint32_t>(c[1]), bcast<uint32_t>(c[0]), 0x05040302u));
+      const u16x2 s34 =
+          bcast<u16x2>(__builtin_amdgcn_perm(bcast<uint32_t>(c[2]), bcast<uint32_t>(c[1]), 0x05040302u));
+      const u16x2 t12 = s12 * three + two, t34 = s34 * three + two;
+      const uint32_t e01 = bcast<uint32_t>((t12 + c[0]) >> 2), o01 = bcast<uint32_t>((t12 + c[1]) >> 2);
+      uint32_t e23 = bcast<uint32_t>((t34 + c[1]) >> 2), o23 = bcast<uint32_t>((t34 + c[2]) >> 2);
+      if (edge) {  // even_3 = (3 c[3] + c[4] + 2) >> 2 (= odd_2), odd_3 = c[4]
+        e23 = __builtin_amdgcn_perm(o23, e23, 0x05040100u);
+        o23 = __builtin_amdgcn_perm(bcast<uint32_t>(c[2]), o23, 0x05040100u);
+      }
+      Cp[pl][0] = bcast<u16x2>(__builtin_amdgcn_perm(o01, e01, 0x05040100u));
+      Cp[pl][1] = bcast<u16x2>(__builtin_amdgcn_perm(o01, e01, 0x07060302u));
+      Cp[pl][2] = bcast<u16x2>(__builtin_amdgcn_perm(o23, e23, 0x05040100u));
+      Cp[pl][3] = bcast<u16x2>(__builtin_amdgcn_perm(o23, e23, 0x07060302u));
+    }
   }
   const s16x2 c128 = {128, 128}, zero = {0, 0}, c255 = {255, 255};
 #pragma unroll
@@ -2437,8 +2455,8 @@ __device__ __forceinline__ void hband_pl(const ImageDesc &im, const ResizePass &
         hpl_split(v, Rw, Gw, Bw);
       } else {
         const FillRaw f = (PREFETCH && j == t) ? pre : hload_fc8<FC>(im, ps.row0 + y0 + r, p0 + 8 * q);
-        if (FC == FC_420_Z) {
-          hpl_420z(im, f, p0 + 8 * q, Rw, Gw, Bw);
+        if (FC == FC_420_Z || FC == FC_422_Z || FC == FC_444_Z) {
+          hpl_zune<FC == FC_420_Z ? 2 : FC == FC_422_Z ? 1 : 0>(im, f, p0 + 8 * q, Rw, Gw, Bw);
         } else {
           uint32_t v[8];
           hcolor_fc8<FC>(im, f, p0 + 8 * q, v);
