@@ -2383,7 +2383,7 @@ __device__ __forceinline__ void hconv_rows_pl(const uint32_t *segp, uint32_t pb,
 template <int KMAX, int FC, bool PF>
 __device__ __forceinline__ void hband_pl(const ImageDesc &im, const ResizePass &ps, uint32_t item, uint32_t *segp,
                                          uint8_t *ob, uint32_t *ext) {
-  static_assert(KMAX == 8 || KMAX == 16 || KMAX == 32, "planar segments for the 8- to 32-tap classes");
+  static_assert(KMAX == 8 || KMAX == 16, "planar segments for the 8- and 16-tap classes");
   constexpr uint32_t SEGPX = hseg_px(KMAX), SPS = hpl_stride(KMAX);
   const uint32_t tiles = (ps.width + kHBandCols - 1) / kHBandCols;
   const uint32_t group = item / tiles, tile = item - group * tiles;
@@ -2499,7 +2499,7 @@ __device__ __forceinline__ void hband_pl(const ImageDesc &im, const ResizePass &
 // 6 waves per SIMD for 8 taps (80 VGPRs: without the next-band prefetch,
 // which would spill there -- measured level with it, round 6), 5 for 16.
 template <int KMAX, bool PF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX == 8 ? 6 : KMAX == 16 ? 5 : 4))) void k_resize_hbp(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX == 8 ? 6 : 5))) void k_resize_hbp(
     const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list, int stage) {
   __shared__ __attribute__((aligned(16))) uint32_t segp[kHBandRows * 3 * hpl_stride(KMAX)];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kHBandRows * kHBandCols * 4];
@@ -3259,8 +3259,9 @@ static void launch_hb_classes(hipStream_t st, const ImageDesc *imgs, const WgIte
   list += ncls[3];
 }
 // The fused classes with a planar segment (h_planar): 8 and 16 taps on
-// k_resize_hbp, the wider ones on k_resize_hb (their planar segment would
-// cost a resident workgroup per CU)
+// k_resize_hbp, the wider ones on k_resize_hb (a planar 32-tap class, 35 KiB
+// of LDS: 4 workgroups per CU instead of 5, measured level -- resize_h1
+// 1.60-1.63 vs 1.62-1.64 ms, round 6 -- and was not kept)
 template <bool PF>
 static void launch_hb_fused_planar(hipStream_t st, const ImageDesc *imgs, const WgItem *&list, const uint32_t ncls[4],
                                    int stage) {
@@ -3268,11 +3269,7 @@ static void launch_hb_fused_planar(hipStream_t st, const ImageDesc *imgs, const 
   list += ncls[0];
   DG_LAUNCH((k_resize_hbp<16, PF>), ncls[1], st, imgs, list, stage);
   list += ncls[1];
-#if DG_HBP32
-  DG_LAUNCH((k_resize_hbp<32, PF>), ncls[2], st, imgs, list, stage);
-#else
   DG_LAUNCH((k_resize_hb<32, true, PF>), ncls[2], st, imgs, list, stage);
-#endif
   list += ncls[2];
   DG_LAUNCH((k_resize_hb<0, true>), ncls[3], st, imgs, list, stage);
   list += ncls[3];
