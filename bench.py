@@ -1029,7 +1029,10 @@ def main() -> int:
         iso = None
         if ser_n:
             skern = {k: v / ser_n for k, v in ser_tot.items() if k not in ("upload", "download")}
-            sdom = max(skern, key=skern.get)
+            # the dominant kernel is the one with the largest share of the timed region's stage spans
+            # (resize_h1: ~6 of 18 ms per step); its duration is the isolated pass's (the entropy sync
+            # kernel's isolated time is as long, but it keeps its speed beside the other batches)
+            sdom = dom if dom in skern else max(skern, key=skern.get)
             sach = (ser_alg.get(sdom, 0.0) / ser_n) / (skern[sdom] / 1e3) / 1e9 if skern[sdom] > 0 else 0.0
             iso = {"kernel": sdom, "kernel_ms_per_launch": round(skern[sdom], 4), "achieved": round(sach, 2),
                    "unit": "GB/s", "frac": round(sach / HBM_PEAK_GBS, 5), "batches": ser_n,
@@ -1128,7 +1131,8 @@ def main() -> int:
                           "peak_measured_copy": copy_gbs,
                           "frac_of_measured_copy": round(iso["achieved"] / copy_gbs, 5) if copy_gbs else None,
                           "note": f"per launch = one {B_}-image batch; kernel time from HIP events with the batch "
-                                  "alone on the GPU (roofline_isolated)"} if iso else
+                                  "alone on the GPU (roofline_isolated); kernel = the largest share of the timed "
+                                  "region's stage spans (roofline_overlapped_span)"} if iso else
                          {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                           "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,

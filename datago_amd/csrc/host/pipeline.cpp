@@ -2477,6 +2477,7 @@ dg_status Context::submit(int n, const uint8_t *const *h_srcs, const uint8_t *co
           for (uint32_t it = 0; it < cnt; it++) hm[s / 2][fused][ks - 1].push_back({I, it});
         else
           for (uint32_t it = 0; it < cnt; it++) hb[s / 2][fused][cls].push_back({I, it});
+        if (fused && d.sem) b.h_zune = 1;  // the planar fused kernels of the zune fill classes
       } else if (v_tile_ && (ps.src_stride & 15) == 0) {  // k_resize_vt: 4 waves of (R rows x 1 KiB) tiles
         const uint32_t units = (ps.width * ps.C + 15) / 16;
         const uint32_t tiles = (units + 63) / 64 * ((ps.rows + v_tile_ - 1) / v_tile_);
@@ -3005,7 +3006,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_alpha(sl.st, dd, lst(L_ALPHA0), cnt(L_ALPHA0), 0 | (alpha_flags << 8));
   launch_band_dec(sl.st, dd, lst(L_DEC), b.decclass, qp, dec_strips_ | (dec_dbg_ << 16));
   launch_resize_hm(sl.st, dd, lst(L_RM0), b.hmclass[0], 0);
-  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0, h_prefetch_, h_planar_);
+  launch_resize_hb(sl.st, dd, lst(L_RH0), b.hclass[0], 0, h_prefetch_, h_planar_, b.h_zune != 0);
   launch_resize_hv(sl.st, dd, lst(L_RHV), b.hvclass);
   launch_resize_h(sl.st, dd, lst(L_RHX0), cnt(L_RHX0), 0 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
@@ -3014,7 +3015,7 @@ dg_status Context::launch_all(Slot &sl, bool from_fix) {
   launch_alpha(sl.st, dd, lst(L_ALPHA1), cnt(L_ALPHA1), 1 | (alpha_flags << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_hm(sl.st, dd, lst(L_RM2), b.hmclass[1], 2);
-  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2, h_prefetch_, h_planar_);
+  launch_resize_hb(sl.st, dd, lst(L_RH2), b.hclass[1], 2, h_prefetch_, h_planar_, b.h_zune != 0);
   launch_resize_h(sl.st, dd, lst(L_RHX2), cnt(L_RHX2), 2 | ((debug_flags_ & 0xFF) << 8));
   if (next()) return DG_ERR_DEVICE;
   launch_resize_v(sl.st, dd, lst(L_RV3), cnt(L_RV3), 3, v_units_);

@@ -86,6 +86,7 @@ struct Batch {
   bool any_fused = false;  // some image's IDCT runs inside k_huff_write
   uint32_t idct_cap = 0;   // entries of BatchFlags::idct_list
   uint32_t v_tile = 0;     // rows per k_resize_vt tile the V lists were built for
+  uint32_t h_zune = 0;     // fused H items in zune decode semantics: k_resize_hbp's zune-class kernels
   bool stage_on = false;  // decode-once staging (option "entropy_once")
   uint32_t max_slots = 1; // largest Huffman table count of an image (dynamic LDS of k_huff_sync/fix)
   uint32_t max_ac = 0;    // most distinct AC tables of a baseline JPEG (k_huff_sync multi-symbol lookups)

@@ -50,7 +50,7 @@ void launch_resize_h(hipStream_t st, const ImageDesc *imgs, const WgItem *list, 
 // each ordered by weight-count class (<= 8, 16, 32 taps, more)
 void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][4],
                       int stage,
-                      bool prefetch, bool planar);
+                      bool prefetch, bool planar, bool zune);
 // band H pass on the matrix cores (k_resize_hm): ncls[fused][ks - 1] items, launched fused KS 1, fused KS 2,
 // byte-fill KS 1, byte-fill KS 2 (KS = 64-wide K steps of a 16-column subtile's window)
 void launch_resize_hm(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][2],

@@ -2496,10 +2496,16 @@ __device__ __forceinline__ void hband_pl(const ImageDesc &im, const ResizePass &
   }
 }
 
-// 6 waves per SIMD for 8 taps (80 VGPRs: without the next-band prefetch,
-// which would spill there -- measured level with it, round 6), 5 for 16.
-template <int KMAX, bool PF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX == 8 ? 6 : 5))) void k_resize_hbp(
+// Z: the zune fill classes (the drop-in's decode semantics), else the
+// libjpeg ones; an image of the other semantics in the batch takes the
+// generic fill (bit-exact, slower).  Split so that each kernel holds only its
+// own fills' registers: the zune 16-tap kernel fits 6 waves per SIMD (80
+// VGPRs; its zune paths spill nothing -- only the rare generic fill reloads a
+// few words per band), +2% headline over 5 waves (round 6); the libjpeg one
+// keeps 5.  8 taps: 6 waves, without the next-band prefetch (which would
+// spill there; measured level with it).
+template <int KMAX, bool PF, bool Z>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX == 8 || Z ? 6 : 5))) void k_resize_hbp(
     const ImageDesc *__restrict__ imgs, const WgItem *__restrict__ list, int stage) {
   __shared__ __attribute__((aligned(16))) uint32_t segp[kHBandRows * 3 * hpl_stride(KMAX)];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kHBandRows * kHBandCols * 4];
@@ -2507,15 +2513,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX == 8 ?
   const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
   const ImageDesc &im = imgs[it.image];
   const ResizePass &ps = im.pass[stage];
-  switch (fill_class(im)) {
-    case FC_420: hband_pl<KMAX, FC_420, PF>(im, ps, it.item0, segp, ob, ext); return;
-    case FC_420_Z: hband_pl<KMAX, FC_420_Z, PF>(im, ps, it.item0, segp, ob, ext); return;
-    case FC_422: hband_pl<KMAX, FC_422, PF>(im, ps, it.item0, segp, ob, ext); return;
-    case FC_422_Z: hband_pl<KMAX, FC_422_Z, PF>(im, ps, it.item0, segp, ob, ext); return;
-    case FC_444: hband_pl<KMAX, FC_444, PF>(im, ps, it.item0, segp, ob, ext); return;
-    case FC_444_Z: hband_pl<KMAX, FC_444_Z, PF>(im, ps, it.item0, segp, ob, ext); return;
-    default: hband_pl<KMAX, FC_GENERIC, false>(im, ps, it.item0, segp, ob, ext); return;
+  const int fc = fill_class(im);
+  if (Z) {
+    switch (fc) {
+      case FC_420_Z: hband_pl<KMAX, FC_420_Z, PF>(im, ps, it.item0, segp, ob, ext); return;
+      case FC_422_Z: hband_pl<KMAX, FC_422_Z, PF>(im, ps, it.item0, segp, ob, ext); return;
+      case FC_444_Z: hband_pl<KMAX, FC_444_Z, PF>(im, ps, it.item0, segp, ob, ext); return;
+      default: break;
+    }
+  } else {
+    switch (fc) {
+      case FC_420: hband_pl<KMAX, FC_420, PF>(im, ps, it.item0, segp, ob, ext); return;
+      case FC_422: hband_pl<KMAX, FC_422, PF>(im, ps, it.item0, segp, ob, ext); return;
+      case FC_444: hband_pl<KMAX, FC_444, PF>(im, ps, it.item0, segp, ob, ext); return;
+      default: break;
+    }
   }
+  hband_pl<KMAX, FC_GENERIC, false>(im, ps, it.item0, segp, ob, ext);
 }
 
 // ---- band H pass on the matrix cores (k_resize_hm)
@@ -3262,12 +3276,12 @@ static void launch_hb_classes(hipStream_t st, const ImageDesc *imgs, const WgIte
 // k_resize_hbp, the wider ones on k_resize_hb (a planar 32-tap class, 35 KiB
 // of LDS: 4 workgroups per CU instead of 5, measured level -- resize_h1
 // 1.60-1.63 vs 1.62-1.64 ms, round 6 -- and was not kept)
-template <bool PF>
+template <bool PF, bool Z>
 static void launch_hb_fused_planar(hipStream_t st, const ImageDesc *imgs, const WgItem *&list, const uint32_t ncls[4],
                                    int stage) {
-  DG_LAUNCH((k_resize_hbp<8, false>), ncls[0], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hbp<8, false, Z>), ncls[0], st, imgs, list, stage);
   list += ncls[0];
-  DG_LAUNCH((k_resize_hbp<16, PF>), ncls[1], st, imgs, list, stage);
+  DG_LAUNCH((k_resize_hbp<16, PF, Z>), ncls[1], st, imgs, list, stage);
   list += ncls[1];
   DG_LAUNCH((k_resize_hb<32, true, PF>), ncls[2], st, imgs, list, stage);
   list += ncls[2];
@@ -3275,11 +3289,13 @@ static void launch_hb_fused_planar(hipStream_t st, const ImageDesc *imgs, const 
   list += ncls[3];
 }
 void launch_resize_hb(hipStream_t st, const ImageDesc *imgs, const WgItem *list, const uint32_t ncls[2][4],
-                      int stage, bool prefetch, bool planar) {
-  if (planar && prefetch)
-    launch_hb_fused_planar<true>(st, imgs, list, ncls[1], stage);
+                      int stage, bool prefetch, bool planar, bool zune) {
+  if (planar && zune)
+    prefetch ? launch_hb_fused_planar<true, true>(st, imgs, list, ncls[1], stage)
+             : launch_hb_fused_planar<false, true>(st, imgs, list, ncls[1], stage);
   else if (planar)
-    launch_hb_fused_planar<false>(st, imgs, list, ncls[1], stage);
+    prefetch ? launch_hb_fused_planar<true, false>(st, imgs, list, ncls[1], stage)
+             : launch_hb_fused_planar<false, false>(st, imgs, list, ncls[1], stage);
   else if (prefetch)
     launch_hb_classes<true, true>(st, imgs, list, ncls[1], stage);
   else
