@@ -309,6 +309,9 @@ int32_t dg_last_batch_timings(dg_ctx *ctx, const char **names, float *ms, int32_
  *   "plan_threads" host threads parsing a submission's headers (default 4; 1 = the submitting thread only)
  *   "hv_fused"     1 = fuse the first H and V passes of colour JPEGs where they fit (default 0; slower)
  *   "h_mfma"       1 = band H passes on the matrix cores (k_resize_hm, i8 MFMA; default 0: measured slower); 0 = VALU kernel
+ *   "h_planar"     1 = the first H pass of a colour JPEG with up to 16 taps over a planar LDS segment of u16
+ *                 pixel pairs (k_resize_hbp; zune fills in packed 16-bit arithmetic; default 1: resize_h1
+ *                 1.79 -> 1.60 ms per configs[1] batch); 0 = k_resize_hb for every class.  Same bytes either way
  *   "band_dec"     1 = IDCT + upsampling + colour + the first H pass of a JPEG in one kernel (k_band_dec,
  *                 MFMA convolution; default 0: measured slower); 0 = IDCT to planes + the band H kernel
  *   "dec_strips"   k_band_dec: 16-row strips per workgroup (default 8)
