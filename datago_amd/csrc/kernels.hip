@@ -2059,12 +2059,111 @@ __device__ __forceinline__ void hconv_rows(const uint32_t *seg, uint32_t off, co
     }
 }
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+template <class T, class S>
+__device__ __forceinline__ T bcast(S v) {
+  return __builtin_bit_cast(T, v);
+}
+
+// One octet of a zune fill (hcolor_fc8<FC_4xx_Z>'s arithmetic; SS = 2
+// 4:2:0, 1 4:2:2, 0 4:4:4) as u16 pairs per channel: R[i] = (pixel 2i,
+// pixel 2i + 1) of the octet.
+template <int SS>
+__device__ __forceinline__ void hpl_zune(const ImageDesc &im, const FillRaw &f, uint32_t x0, uint32_t R[4],
+                                         uint32_t G[4], uint32_t B[4]) {
+  u16x2 Cp[2][4];  // Cb, Cr: pixel pairs (0,1), (2,3), (4,5), (6,7)
+  if (SS == 0) {  // full-rate chroma: the plane bytes as they are
+#pragma unroll
+    for (int pl = 0; pl < 2; pl++) {
+      const u32x2 w = pl ? f.r0 : f.b0;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        Cp[pl][i] = bcast<u16x2>(__builtin_amdgcn_perm(0u, i < 2 ? w.x : w.y, (i & 1) ? 0x0C030C02u : 0x0C010C00u));
+    }
+  } else {
+    // the 6 samples of a chroma record (load_crec6's order: left neighbour,
+    // 4 samples, right neighbour) as 3 pairs
+    auto rec3 = [](u32x2 w, u16x2 c[3]) {
+      c[0] = bcast<u16x2>(__builtin_amdgcn_perm(w.x, w.y, 0x0C040C00u));
+      c[1] = bcast<u16x2>(__builtin_amdgcn_perm(0u, w.x, 0x0C020C01u));
+      c[2] = bcast<u16x2>(__builtin_amdgcn_perm(w.y, w.x, 0x0C050C03u));
+    };
+    const bool edge = (x0 >> 1) + 4u == im.cbw[1] * 8u;  // the padded chroma row's last 4 samples: zune's quirk
+    const u16x2 two = {2, 2}, three = {3, 3};
+#pragma unroll
+    for (int pl = 0; pl < 2; pl++) {
+      u16x2 c[3];
+      rec3(pl ? f.r0 : f.b0, c);
+      if (SS == 2) {  // vertical: (3 near + far + 2) >> 2
+        u16x2 fa[3];
+        rec3(pl ? f.r1 : f.b1, fa);
+#pragma unroll
+        for (int i = 0; i < 3; i++) c[i] = (c[i] * three + fa[i] + two) >> 2;
+      }
+      // horizontal: even_k = (3 c[k+1] + 2 + c[k]) >> 2, odd_k = (3 c[k+1] + 2 + c[k+2]) >> 2
+      const u16x2 s12 =
+          bcast<u16x2>(__builtin_amdgcn_perm(bcast<uint32_t>(c[1]), bcast<uint32_t>(c[0]), 0x05040302u));
+      const u16x2 s34 =
+          bcast<u16x2>(__builtin_amdgcn_perm(bcast<uint32_t>(c[2]), bcast<uint32_t>(c[1]), 0x05040302u));
+      const u16x2 t12 = s12 * three + two, t34 = s34 * three + two;
+      const uint32_t e01 = bcast<uint32_t>((t12 + c[0]) >> 2), o01 = bcast<uint32_t>((t12 + c[1]) >> 2);
+      uint32_t e23 = bcast<uint32_t>((t34 + c[1]) >> 2), o23 = bcast<uint32_t>((t34 + c[2]) >> 2);
+      if (edge) {  // even_3 = (3 c[3] + c[4] + 2) >> 2 (= odd_2), odd_3 = c[4]
+        e23 = __builtin_amdgcn_perm(o23, e23, 0x05040100u);
+        o23 = __builtin_amdgcn_perm(bcast<uint32_t>(c[2]), o23, 0x05040100u);
+      }
+      Cp[pl][0] = bcast<u16x2>(__builtin_amdgcn_perm(o01, e01, 0x05040100u));
+      Cp[pl][1] = bcast<u16x2>(__builtin_amdgcn_perm(o01, e01, 0x07060302u));
+      Cp[pl][2] = bcast<u16x2>(__builtin_amdgcn_perm(o23, e23, 0x05040100u));
+      Cp[pl][3] = bcast<u16x2>(__builtin_amdgcn_perm(o23, e23, 0x07060302u));
+    }
+  }
+  const s16x2 c128 = {128, 128}, zero = {0, 0}, c255 = {255, 255};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t yw = i < 2 ? f.y.x : f.y.y;
+    const s16x2 y = bcast<s16x2>(__builtin_amdgcn_perm(0u, yw, (i & 1) ? 0x0C030C02u : 0x0C010C00u));
+    const s16x2 xcb = bcast<s16x2>(Cp[0][i]) - c128, xcr = bcast<s16x2>(Cp[1][i]) - c128;
+    // ycc_to_rgb_zune in 16 bits: every product and sum fits (|x| <= 128)
+    s16x2 r = y + ((xcr * (s16x2){45, 45}) >> 5);
+    s16x2 g = y - ((xcb * (s16x2){11, 11} + xcr * (s16x2){23, 23}) >> 5);
+    s16x2 b = y + ((xcb * (s16x2){113, 113}) >> 6);
+    r = __builtin_elementwise_min(__builtin_elementwise_max(r, zero), c255);
+    g = __builtin_elementwise_min(__builtin_elementwise_max(g, zero), c255);
+    b = __builtin_elementwise_min(__builtin_elementwise_max(b, zero), c255);
+    R[i] = bcast<uint32_t>(r);
+    G[i] = bcast<uint32_t>(g);
+    B[i] = bcast<uint32_t>(b);
+  }
+}
+
+// u16 pairs per channel -> pixel dwords (RGB in bytes 0..2)
+__device__ __forceinline__ void hpl_join(const uint32_t R[4], const uint32_t G[4], const uint32_t B[4], uint32_t v[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t rg = __builtin_amdgcn_perm(G[i], R[i], 0x06020400u);  // r0 g0 r1 g1
+    v[2 * i] = __builtin_amdgcn_perm(B[i], rg, 0x0C040100u);
+    v[2 * i + 1] = __builtin_amdgcn_perm(B[i], rg, 0x0C060302u);
+  }
+}
+
+// pixel dwords (RGB in bytes 0..2) -> u16 pairs per channel
+__device__ __forceinline__ void hpl_split(const uint32_t v[8], uint32_t R[4], uint32_t G[4], uint32_t B[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    R[i] = __builtin_amdgcn_perm(v[2 * i + 1], v[2 * i], 0x0C040C00u);
+    G[i] = __builtin_amdgcn_perm(v[2 * i + 1], v[2 * i], 0x0C050C01u);
+    B[i] = __builtin_amdgcn_perm(v[2 * i + 1], v[2 * i], 0x0C060C02u);
+  }
+}
+
 // LDS source segment (pixels per row) of a band H kernel, per weight class:
 // a window of <= 8 taps means a downscale of at most ~1.2x, <= 16 taps at most
 // ~2.5x, so 128 output columns read at most 192 / 384 source pixels (the host
 // promotes a pass to the next class when h_pass_span says otherwise).  The
 // smaller segments let 8 workgroups share a CU instead of 6 (LDS-bound).
 constexpr uint32_t hseg_px(int kmax) { return kmax == 8 ? 192u : kmax == 16 ? 384u : kHSegPx; }
+constexpr uint32_t hpl_stride(int kmax) { return hseg_px(kmax) / 2 + 4; }  // dwords per row-channel plane
 
 // FUSED: the first pass of a colour JPEG (fill = upsample + colour
 // conversion from the planes, C = 3); otherwise the fill copies interleaved
@@ -2162,7 +2261,13 @@ __device__ __forceinline__ void hband(const ImageDesc &im, const ResizePass &ps,
           // a thread's first job of the band was loaded before the previous
           // band's convolution (pre); later ones load here
           const FillRaw f = (PREFETCH && j == t) ? pre : hload_fc8<FC>(im, ps.row0 + y0 + r, p0 + 8 * q);
-          hcolor_fc8<FC>(im, f, p0 + 8 * q, v);
+          if (FC == FC_420_Z || FC == FC_422_Z || FC == FC_444_Z) {
+            uint32_t Rw[4], Gw[4], Bw[4];  // the planar kernel's packed zune fill, back to pixel dwords
+            hpl_zune<FC == FC_420_Z ? 2 : FC == FC_422_Z ? 1 : 0>(im, f, p0 + 8 * q, Rw, Gw, Bw);
+            hpl_join(Rw, Gw, Bw, v);
+          } else {
+            hcolor_fc8<FC>(im, f, p0 + 8 * q, v);
+          }
         }
         hput8(v, seg + r * SS + 8 * q);
       } else {
@@ -2258,95 +2363,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX == 8 ?
 // configs[1] batch): without the fill arithmetic 1.28 ms, without the
 // convolution 1.24, without the plane loads 1.68 -- the kernel follows its
 // VALU work, not its loads.
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-template <class T, class S>
-__device__ __forceinline__ T bcast(S v) {
-  return __builtin_bit_cast(T, v);
-}
-constexpr uint32_t hpl_stride(int kmax) { return hseg_px(kmax) / 2 + 4; }  // dwords per row-channel plane
-
-// One octet of a zune fill (hcolor_fc8<FC_4xx_Z>'s arithmetic; SS = 2
-// 4:2:0, 1 4:2:2, 0 4:4:4) as u16 pairs per channel: R[i] = (pixel 2i,
-// pixel 2i + 1) of the octet.
-template <int SS>
-__device__ __forceinline__ void hpl_zune(const ImageDesc &im, const FillRaw &f, uint32_t x0, uint32_t R[4],
-                                         uint32_t G[4], uint32_t B[4]) {
-  u16x2 Cp[2][4];  // Cb, Cr: pixel pairs (0,1), (2,3), (4,5), (6,7)
-  if (SS == 0) {  // full-rate chroma: the plane bytes as they are
-#pragma unroll
-    for (int pl = 0; pl < 2; pl++) {
-      const u32x2 w = pl ? f.r0 : f.b0;
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        Cp[pl][i] = bcast<u16x2>(__builtin_amdgcn_perm(0u, i < 2 ? w.x : w.y, (i & 1) ? 0x0C030C02u : 0x0C010C00u));
-    }
-  } else {
-    // the 6 samples of a chroma record (load_crec6's order: left neighbour,
-    // 4 samples, right neighbour) as 3 pairs
-    auto rec3 = [](u32x2 w, u16x2 c[3]) {
-      c[0] = bcast<u16x2>(__builtin_amdgcn_perm(w.x, w.y, 0x0C040C00u));
-      c[1] = bcast<u16x2>(__builtin_amdgcn_perm(0u, w.x, 0x0C020C01u));
-      c[2] = bcast<u16x2>(__builtin_amdgcn_perm(w.y, w.x, 0x0C050C03u));
-    };
-    const bool edge = (x0 >> 1) + 4u == im.cbw[1] * 8u;  // the padded chroma row's last 4 samples: zune's quirk
-    const u16x2 two = {2, 2}, three = {3, 3};
-#pragma unroll
-    for (int pl = 0; pl < 2; pl++) {
-      u16x2 c[3];
-      rec3(pl ? f.r0 : f.b0, c);
-      if (SS == 2) {  // vertical: (3 near + far + 2) >> 2
-        u16x2 fa[3];
-        rec3(pl ? f.r1 : f.b1, fa);
-#pragma unroll
-        for (int i = 0; i < 3; i++) c[i] = (c[i] * three + fa[i] + two) >> 2;
-      }
-      // horizontal: even_k = (3 c[k+1] + 2 + c[k]) >> 2, odd_k = (3 c[k+1] + 2 + c[k+2]) >> 2
-      const u16x2 s12 =
-          bcast<u16x2>(__builtin_amdgcn_perm(bcast<uint32_t>(c[1]), bcast<uint32_t>(c[0]), 0x05040302u));
-      const u16x2 s34 =
-          bcast<u16x2>(__builtin_amdgcn_perm(bcast<uint32_t>(c[2]), bcast<uint32_t>(c[1]), 0x05040302u));
-      const u16x2 t12 = s12 * three + two, t34 = s34 * three + two;
-      const uint32_t e01 = bcast<uint32_t>((t12 + c[0]) >> 2), o01 = bcast<uint32_t>((t12 + c[1]) >> 2);
-      uint32_t e23 = bcast<uint32_t>((t34 + c[1]) >> 2), o23 = bcast<uint32_t>((t34 + c[2]) >> 2);
-      if (edge) {  // even_3 = (3 c[3] + c[4] + 2) >> 2 (= odd_2), odd_3 = c[4]
-        e23 = __builtin_amdgcn_perm(o23, e23, 0x05040100u);
-        o23 = __builtin_amdgcn_perm(bcast<uint32_t>(c[2]), o23, 0x05040100u);
-      }
-      Cp[pl][0] = bcast<u16x2>(__builtin_amdgcn_perm(o01, e01, 0x05040100u));
-      Cp[pl][1] = bcast<u16x2>(__builtin_amdgcn_perm(o01, e01, 0x07060302u));
-      Cp[pl][2] = bcast<u16x2>(__builtin_amdgcn_perm(o23, e23, 0x05040100u));
-      Cp[pl][3] = bcast<u16x2>(__builtin_amdgcn_perm(o23, e23, 0x07060302u));
-    }
-  }
-  const s16x2 c128 = {128, 128}, zero = {0, 0}, c255 = {255, 255};
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t yw = i < 2 ? f.y.x : f.y.y;
-    const s16x2 y = bcast<s16x2>(__builtin_amdgcn_perm(0u, yw, (i & 1) ? 0x0C030C02u : 0x0C010C00u));
-    const s16x2 xcb = bcast<s16x2>(Cp[0][i]) - c128, xcr = bcast<s16x2>(Cp[1][i]) - c128;
-    // ycc_to_rgb_zune in 16 bits: every product and sum fits (|x| <= 128)
-    s16x2 r = y + ((xcr * (s16x2){45, 45}) >> 5);
-    s16x2 g = y - ((xcb * (s16x2){11, 11} + xcr * (s16x2){23, 23}) >> 5);
-    s16x2 b = y + ((xcb * (s16x2){113, 113}) >> 6);
-    r = __builtin_elementwise_min(__builtin_elementwise_max(r, zero), c255);
-    g = __builtin_elementwise_min(__builtin_elementwise_max(g, zero), c255);
-    b = __builtin_elementwise_min(__builtin_elementwise_max(b, zero), c255);
-    R[i] = bcast<uint32_t>(r);
-    G[i] = bcast<uint32_t>(g);
-    B[i] = bcast<uint32_t>(b);
-  }
-}
-
-// pixel dwords (RGB in bytes 0..2) -> u16 pairs per channel
-__device__ __forceinline__ void hpl_split(const uint32_t v[8], uint32_t R[4], uint32_t G[4], uint32_t B[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    R[i] = __builtin_amdgcn_perm(v[2 * i + 1], v[2 * i], 0x0C040C00u);
-    G[i] = __builtin_amdgcn_perm(v[2 * i + 1], v[2 * i], 0x0C050C01u);
-    B[i] = __builtin_amdgcn_perm(v[2 * i + 1], v[2 * i], 0x0C060C02u);
-  }
-}
-
 template <int KMAX, uint32_t SPS>
 __device__ __forceinline__ void hconv_rows_pl(const uint32_t *segp, uint32_t pb, const uint32_t *kw2, uint32_t ksize,
                                               uint32_t r0, uint32_t nrows, int32_t prec, uint8_t *ob, uint32_t col) {
