@@ -3020,8 +3020,12 @@ __global__ __launch_bounds__(256) void k_resize_v(const ImageDesc *__restrict__ 
 // bytes are identical: a tap pair's zero weight adds exactly 0.
 constexpr uint32_t kVtWCap = 256;  // packed weight pairs per wave in LDS
 
+// 5 waves per SIMD for R <= 4: the prefetched pair needs 98 VGPRs
+// unconstrained at R = 4 (4 waves: measured slower than without the
+// prefetch); at 96 the compiler keeps one dword of setup in scratch, outside
+// the row loop.  R = 8 (option value, not the default) is left unconstrained.
 template <int R>
-__global__ __launch_bounds__(256) void k_resize_vt(const ImageDesc *__restrict__ imgs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R <= 4 ? 5 : 1))) void k_resize_vt(const ImageDesc *__restrict__ imgs,
                                                    const WgItem *__restrict__ list, int stage) {
   __shared__ uint32_t wtab[4][kVtWCap];
   const WgItem it = list[xcd_remap(blockIdx.x, gridDim.x)];
@@ -3080,17 +3084,25 @@ __global__ __launch_bounds__(256) void k_resize_vt(const ImageDesc *__restrict__
       wt[r * pn + p] = pk;
     }
     __builtin_amdgcn_wave_barrier();
+    // the next pair's rows are loaded while this pair's dot2s run: one
+    // memory round trip per weight window instead of one per source-row pair
+    // (resize_v1 0.57 -> 0.535 ms per configs[1] batch, round 6)
+    auto ld = [&](uint32_t i, u32x4 &v0, u32x4 &v1) {
+      v0 = *(const DG_GLOBAL u32x4 *)(src + (size_t)i * sstride);
+      v1 = (int32_t)i + 1 < hi - lo ? *(const DG_GLOBAL u32x4 *)(src + (size_t)(i + 1) * sstride) : u32x4{0u, 0u, 0u, 0u};
+    };
+    u32x4 n0, n1;
+    ld(2 * p0, n0, n1);
     for (uint32_t p = 0; p < pn; p++) {
       const uint32_t i = 2 * (p0 + p);  // source row lo + i (and lo + i + 1)
-      const u32x4 v0 = *(const DG_GLOBAL u32x4 *)(src + (size_t)i * sstride);
-      const u32x4 v1 = (int32_t)i + 1 < hi - lo ? *(const DG_GLOBAL u32x4 *)(src + (size_t)(i + 1) * sstride)
-                                                : u32x4{0u, 0u, 0u, 0u};
+      const u32x4 v0 = n0, v1 = n1;
       uint32_t pr[16];
 #pragma unroll
       for (int j = 0; j < 4; j++)
 #pragma unroll
         for (int b = 0; b < 4; b++)
           pr[4 * j + b] = __builtin_amdgcn_perm(v1[j], v0[j], 0x0C000C00u | ((4u + (uint32_t)b) << 16) | (uint32_t)b);
+      if (p + 1 < pn) ld(i + 2, n0, n1);
 #pragma unroll
       for (int r = 0; r < R; r++) {
         const uint32_t wp = __builtin_amdgcn_readfirstlane(wt[r * pn + p]);
