@@ -73,9 +73,11 @@ def parse():
     ap.add_argument("--sub-bits", type=int, default=0)
     ap.add_argument("--workers", type=int, default=0, help="corpus generation processes")
     ap.add_argument("--lead-bits", type=int, default=-1, help="entropy lead-in bits (-1 = library default)")
-    ap.add_argument("--serial-steps", type=int, default=3,
+    ap.add_argument("--serial-steps", type=int, default=5,
                     help="untimed batches run one at a time after the timed region: per-kernel times without "
-                         "the overlap of consecutive batches (roofline_isolated)")
+                         "the overlap of consecutive batches (roofline_isolated); 5, the batches the "
+                         "isolated-pass kernel trace (tools/gpu_calib.sh ISO, SERIAL=5) measures: the entropy "
+                         "stages differ by up to 30% between batches of different images")
     ap.add_argument("--pmc-json", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06",
                                                        "pmc", "pmc_traffic.json"),
                     help="per-stage HBM bytes from a PMC run of this configuration (tools/pmc_traffic.py)")
