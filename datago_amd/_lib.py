@@ -394,15 +394,29 @@ class Context:
     def decode_one(self, data: bytes, forced_bucket: int = -1, out: Optional[np.ndarray] = None):
         """dg_decode_one: one image; concurrent callers (threads) are coalesced
         into shared GPU batches by the library.  `out`: a reused (ideally
-        host_register'ed) uint8 buffer of at least output_size bytes."""
-        st, nb = self.output_size(data, forced_bucket)
-        if st != DG_OK:
-            return st, None, PayloadMeta()
-        if out is None or out.nbytes < nb:
-            out = np.empty(max(nb, 1), np.uint8)
+        host_register'ed) uint8 buffer of at least output_size bytes.  With
+        `out` given the header pass is the library's own: a buffer that turns
+        out too small (DG_ERR_SMALL_BUFFER, meta.nbytes = the size needed) is
+        replaced and the call made once more."""
+        L = load()
         m = PayloadMeta()
-        st = load().dg_decode_one(self._h, data, len(data), forced_bucket, out.ctypes.data, max(nb, 1),
-                                  ctypes.byref(m))
+        if out is not None and out.nbytes > 0:
+            st = L.dg_decode_one(self._h, data, len(data), forced_bucket, out.ctypes.data, out.nbytes,
+                                 ctypes.byref(m))
+            if st != DG_ERR_SMALL_BUFFER:
+                if st != DG_OK:
+                    return st, None, m
+                c = int(m.nbytes // (m.width * m.height)) if m.width and m.height else 0
+                return DG_OK, out[: m.nbytes].reshape(m.height, m.width, c), m
+            nb = int(m.nbytes)
+        else:
+            st, nb = self.output_size(data, forced_bucket)
+            if st != DG_OK:
+                return st, None, PayloadMeta()
+        out = np.empty(max(nb, 1), np.uint8)
+        m = PayloadMeta()
+        st = L.dg_decode_one(self._h, data, len(data), forced_bucket, out.ctypes.data, max(nb, 1),
+                             ctypes.byref(m))
         if st != DG_OK:
             return st, None, m
         c = int(m.nbytes // (m.width * m.height)) if m.width and m.height else 0

@@ -3,6 +3,7 @@ whose buffer lies in a registered range are DMA'd straight from HBM, bypassing
 the pinned staging buffer and the host copy.  Same bytes as the staged path
 and the oracle; pipelined submits reuse the pool; decode_one into a
 registered buffer; unregistering waits for copies in flight."""
+import ctypes
 import numpy as np
 import pytest
 
@@ -52,6 +53,13 @@ def test_registered_pool_direct_dma_bit_exact():
         st, arr, m = ctx.decode_one(datas[0], out=one)
         assert st == 0 and np.array_equal(arr.reshape(-1), staged[0][1].reshape(-1))
         ctx.host_unregister(one)
+        # a caller's buffer too small: the library says so (SMALL_BUFFER, size in the meta), the wrapper retries
+        st, arr, m = ctx.decode_one(datas[0], out=np.zeros(16, np.uint8))
+        assert st == 0 and np.array_equal(arr.reshape(-1), staged[0][1].reshape(-1))
+        m = L.PayloadMeta()
+        st = L.load().dg_decode_one(ctx._h, datas[0], len(datas[0]), -1, np.zeros(16, np.uint8).ctypes.data, 16,
+                                    ctypes.byref(m))
+        assert st == L.DG_ERR_SMALL_BUFFER and m.nbytes == staged[0][1].nbytes
     finally:
         for p in pools:
             ctx.host_unregister(p)
